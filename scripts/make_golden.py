@@ -1,0 +1,152 @@
+"""Generate golden vectors by importing the reference's own Python on CPU.
+
+Run in the build container only (the reference does not exist on the GPU box):
+    python scripts/make_golden.py
+Writes small seeded .npz fixtures into tests/golden/.  The fixtures are data
+(inputs and the reference's outputs); no reference source is copied.
+
+Pinned here:
+  * utils/sh_utils.py:57-112 eval_sh (SH basis constants + sign conventions), deg 0-3
+  * scene/lod_model.py:286-290 set_anchor_mask + scene/basic_model.py:192-210 map_to_int_level
+  * scene/basic_model.py:297-371 generate_neural_gaussians (anchor -> Gaussian decode),
+    RGB (view_dim=3) and SH2 (view_dim=0) variants, MLP shapes of scene/lod_model.py:67-84
+  * utils/loss_utils.py:17-60 l1_loss / ssim and utils/image_utils.py:18-20 psnr
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+
+
+class _Subscriptable:
+    def __class_getitem__(cls, item):
+        return cls
+
+
+def _stub_modules():
+    """Stub third-party imports the reference pulls in but the decode never touches."""
+    for name in ["torch_scatter", "plyfile", "jaxtyping", "cv2", "kornia", "laspy", "colorama",
+                 "simple_knn", "simple_knn._C"]:
+        if name not in sys.modules:
+            m = types.ModuleType(name)
+            m.scatter_max = None
+            m.PlyData = m.PlyElement = object
+            m.Float = m.Int = m.Shaped = _Subscriptable
+            m.Fore = m.Style = types.SimpleNamespace(RED="", GREEN="", RESET_ALL="", RESET="")
+            m.init = lambda *a, **k: None
+            sys.modules[name] = m
+
+
+def golden_sh():
+    from utils.sh_utils import eval_sh
+    g = torch.Generator().manual_seed(11)
+    out = {}
+    for deg in range(4):
+        n = 257
+        K = (deg + 1) ** 2
+        sh = torch.randn(n, 3, K, generator=g)       # reference layout [..., C, K]
+        dirs = torch.randn(n, 3, generator=g)
+        dirs = dirs / dirs.norm(dim=-1, keepdim=True)
+        res = eval_sh(deg, sh, dirs)                   # [n, 3]
+        out[f"deg{deg}_coeffs_nk3"] = sh.permute(0, 2, 1).contiguous().numpy()  # gsplat layout
+        out[f"deg{deg}_dirs"] = dirs.numpy()
+        out[f"deg{deg}_colors"] = res.numpy()
+    np.savez(os.path.join(OUT, "sh_eval.npz"), **out)
+
+
+def _make_lod_model(n_anchor, view_dim, color_attr, seed):
+    import torch.nn as nn
+    from scene.lod_model import GaussianLoDModel
+    feat_dim, n_offsets = 32, 10
+    model = GaussianLoDModel.__new__(GaussianLoDModel)
+    model.feat_dim, model.view_dim, model.n_offsets = feat_dim, view_dim, n_offsets
+    model.appearance_dim = 0
+    model.color_attr = color_attr
+    model.dist2level = "floor"
+    model.standard_dist, model.fork, model.street_levels = 26.686, 2, 8
+    if color_attr == "RGB":
+        model.active_sh_degree, model.color_dim = None, 3
+    else:
+        model.active_sh_degree, model.color_dim = 2, 27
+    model.setup_functions()
+    g = torch.Generator().manual_seed(seed)
+    torch.manual_seed(seed)
+    model.mlp_opacity = nn.Sequential(nn.Linear(feat_dim + view_dim, feat_dim), nn.ReLU(True),
+                                      nn.Linear(feat_dim, n_offsets), nn.Tanh())
+    model.mlp_cov = nn.Sequential(nn.Linear(feat_dim + view_dim, feat_dim), nn.ReLU(True),
+                                  nn.Linear(feat_dim, 7 * n_offsets))
+    model.mlp_color = nn.Sequential(nn.Linear(feat_dim + view_dim, feat_dim), nn.ReLU(True),
+                                    nn.Linear(feat_dim, model.color_dim * n_offsets))
+    model._anchor = torch.rand(n_anchor, 3, generator=g) * 40 - 20
+    model._anchor_feat = torch.randn(n_anchor, feat_dim, generator=g) * 0.5
+    model._offset = torch.randn(n_anchor, n_offsets, 3, generator=g) * 0.1
+    model._scaling = torch.log(torch.full((n_anchor, 6), 0.01)) + torch.randn(n_anchor, 6, generator=g) * 0.1
+    model._rotation = torch.zeros(n_anchor, 4)
+    model._rotation[:, 0] = 1
+    model._level = torch.randint(0, 8, (n_anchor, 1), generator=g, dtype=torch.int32)
+    model._extra_level = torch.randn(n_anchor, generator=g) * 0.2
+    model.smooth_complement = lambda visible_mask: torch.ones((int(visible_mask.sum()), 1))
+    return model
+
+
+def golden_decode():
+    from types import SimpleNamespace
+    for tag, view_dim, color_attr in [("rgb", 3, "RGB"), ("sh2", 0, "SH2")]:
+        model = _make_lod_model(1000, view_dim, color_attr, seed=21 if tag == "rgb" else 22)
+        cam_center = torch.tensor([0.5, -1.0, 2.0])
+        res_scale = 1.0
+        model.set_anchor_mask(cam_center, res_scale)
+        anchor_mask = model._anchor_mask.clone()
+        cam = SimpleNamespace(camera_center=cam_center)
+        with torch.no_grad():
+            xyz, offsets, color, opacity, scaling, rot, sh_degree, mask = model.generate_neural_gaussians(
+                cam, anchor_mask)
+        sd = {}
+        for name, mlp in [("opacity", model.mlp_opacity), ("cov", model.mlp_cov), ("color", model.mlp_color)]:
+            sd[f"{name}_w1"] = mlp[0].weight.detach().numpy()
+            sd[f"{name}_b1"] = mlp[0].bias.detach().numpy()
+            sd[f"{name}_w2"] = mlp[2].weight.detach().numpy()
+            sd[f"{name}_b2"] = mlp[2].bias.detach().numpy()
+        np.savez(os.path.join(OUT, f"decode_{tag}.npz"),
+                 anchor=model._anchor.numpy(), anchor_feat=model._anchor_feat.numpy(),
+                 offset=model._offset.numpy(), scaling=model._scaling.numpy(),
+                 level=model._level.numpy(), extra_level=model._extra_level.numpy(),
+                 cam_center=cam_center.numpy(), res_scale=np.float32(res_scale),
+                 standard_dist=np.float32(model.standard_dist), fork=np.int32(model.fork),
+                 street_levels=np.int32(model.street_levels), view_dim=np.int32(view_dim),
+                 anchor_mask=anchor_mask.numpy(),
+                 out_xyz=xyz.numpy(), out_color=color.numpy(), out_opacity=opacity.numpy(),
+                 out_scaling=scaling.numpy(), out_rot=rot.numpy(), out_mask=mask.numpy(),
+                 **sd)
+
+
+def golden_losses():
+    from utils.image_utils import psnr
+    from utils.loss_utils import l1_loss, ssim
+    g = torch.Generator().manual_seed(31)
+    a = torch.rand(3, 64, 80, generator=g)
+    b = (a + 0.1 * torch.randn(3, 64, 80, generator=g)).clamp(0, 1)
+    np.savez(os.path.join(OUT, "losses.npz"), img=a.numpy(), gt=b.numpy(),
+             l1=np.float32(l1_loss(a, b).item()), ssim=np.float32(ssim(a, b).item()),
+             psnr=psnr(a[None], b[None]).numpy())
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    sys.path.insert(0, REF)
+    _stub_modules()
+    golden_sh()
+    golden_decode()
+    golden_losses()
+    print("wrote", sorted(os.listdir(OUT)))
+
+
+if __name__ == "__main__":
+    main()
