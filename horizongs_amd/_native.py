@@ -1,0 +1,99 @@
+"""ctypes binding of libhgsr.so (the C ABI declared in include/hgsr.h).
+
+The product path has no CPU fallback: if the library is missing, or a tensor is
+not on the HIP device, the call raises.  Device pointers and the current torch
+stream are passed straight through; the library never allocates.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libhgsr.so")
+
+_lock = threading.Lock()
+_lib = None
+
+P = ct.c_void_p
+I = ct.c_int
+I64 = ct.c_int64
+F = ct.c_float
+SZ = ct.c_size_t
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "hgsr_version": (I, []),
+    "hgsr_last_error": (ct.c_char_p, []),
+    "hgsr_project3d_fwd": (I, [I, I, P, P, P, P, P, I, I, F, F, F, F, P, P, P, P, P]),
+    "hgsr_project3d_bwd": (I, [I, I, P, P, P, P, P, I, I, F, P, P, P, P, P, P, P, P, P]),
+    "hgsr_project2d_fwd": (I, [I, I, P, P, P, P, P, I, I, F, F, F, P, P, P, P, P, P]),
+    "hgsr_project2d_bwd": (I, [I, I, P, P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P]),
+    "hgsr_sh_fwd": (I, [I, I, I64, P, P, P, P, P]),
+    "hgsr_sh_bwd": (I, [I, I, I64, P, P, P, P, P, P, P]),
+    "hgsr_isect_ws1_bytes": (SZ, [I, I, I, I]),
+    "hgsr_isect_ws2_bytes": (SZ, [I64, I64]),
+    "hgsr_isect_count": (I, [I, I, P, P, I, I, I, P, P, P, P, SZ, P]),
+    "hgsr_isect_emit_sorted": (I, [I, I, P, P, P, I, I, I, P, I64, I64, P, P, P, SZ, P, SZ, P]),
+    "hgsr_isect_emit_unsorted": (I, [I, I, P, P, P, I, I, I, P, P, P, P]),
+    "hgsr_isect_offset_encode": (I, [I64, P, I, I, I, P, P]),
+    "hgsr_raster3d_fwd": (I, [I, I, I, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P]),
+    "hgsr_raster3d_bwd_ws_bytes": (SZ, [I, I, I]),
+    "hgsr_raster3d_bwd": (I, [I, I, I, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, P, P,
+                              SZ, P]),
+    "hgsr_raster2d_fwd": (I, [I, I, I, P, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P]),
+    "hgsr_raster2d_bwd_ws_bytes": (SZ, [I, I, I]),
+    "hgsr_raster2d_bwd": (I, [I, I, I, P, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, P,
+                              P, P, P, SZ, P]),
+}
+
+EXPORTED = tuple(n for n in _SIGS)
+
+
+def lib():
+    """Load libhgsr.so once (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"hgsr native library not found at {LIB_PATH}; build it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+            h = ct.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(h, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = h
+    return _lib
+
+
+def call(name, *args):
+    st = getattr(lib(), name)(*args)
+    if st != 0:
+        msg = lib().hgsr_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({st}): {msg}")
+
+
+def size_query(name, *args) -> int:
+    return int(getattr(lib(), name)(*args))
+
+
+def stream(dev=None) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def ptr(t):
+    """Device pointer of a contiguous HIP tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("hgsr: tensor must live on the HIP device (no CPU path)")
+    if not t.is_contiguous():
+        raise RuntimeError("hgsr: tensor must be contiguous")
+    return t.data_ptr()

@@ -1,0 +1,510 @@
+// K5/K6/K7: tile intersection, depth sort and tile offsets.
+//
+// gsplat emits one 64-bit key per (Gaussian, covered tile) in Gaussian-major
+// order, radix-sorts all of them (46 bits at 1080p: 6 HBM passes over 12 B/isect)
+// and then scans the sorted keys for tile boundaries.  Here the tile is known
+// at emission time, so the work is re-shaped as a bucket sort:
+//
+//   1. isect_count  : per-block LDS histogram of (camera, tile) bins, written as
+//                     a dense [blocks][bins] matrix (no global atomics);
+//   2. isect_colscan: per-bin exclusive prefix over blocks (coalesced across bins);
+//   3. isect_binscan: exclusive scan over bins -> isect_offsets (= gsplat
+//                     isect_offset_encode) and {n_isects, largest bin};
+//   4. isect_emit   : each block scatters 8-byte (depth_bits<<32 | flatten_id)
+//                     keys into its pre-reserved slice of every bin (LDS cursors);
+//   5. tile_sort    : one workgroup per bin sorts its keys in LDS (bitonic; bins
+//                     over 2048 keys: LDS-sorted chunks + in-workgroup merge path)
+//                     and writes isect_ids / flatten_ids.
+// Keys inside a bin are unique ((depth, id) pairs), so ANY correct sort yields
+// exactly the order of gsplat's stable radix sort: depth ascending, ties in
+// Gaussian-major emission order.  Integer outputs are bit-identical.
+#include "common.h"
+
+namespace hgsr {
+
+constexpr int kLdsBins = 16384;   // <= 64 KiB of LDS per block for the histogram / cursors
+constexpr int kSortCap = 2048;    // keys sorted entirely in LDS by one 256-lane workgroup
+
+__host__ __device__ inline int nbits64(int64_t v) {
+    int b = 0;
+    while (v > 0) { ++b; v >>= 1; }
+    return b;
+}
+
+// gsplat isect_tiles rectangle; identical float ops to oracle/hgsr_oracle.c tile_rect
+__device__ __forceinline__ void tile_rect(float mx, float my, int32_t radius, int tile_size, int tw,
+                                          int th, int& x0, int& y0, int& x1, int& y1) {
+#pragma clang fp contract(off)
+    const float tr = (float)radius / (float)tile_size;
+    const float tx = mx / (float)tile_size, ty = my / (float)tile_size;
+    const float fx0 = floorf(tx - tr), fy0 = floorf(ty - tr), fx1 = ceilf(tx + tr), fy1 = ceilf(ty + tr);
+    x0 = fx0 <= 0.f ? 0 : (fx0 >= (float)tw ? tw : (int)fx0);
+    y0 = fy0 <= 0.f ? 0 : (fy0 >= (float)th ? th : (int)fy0);
+    x1 = fx1 <= 0.f ? 0 : (fx1 >= (float)tw ? tw : (int)fx1);
+    y1 = fy1 <= 0.f ? 0 : (fy1 >= (float)th ? th : (int)fy1);
+}
+
+struct IsectGeom {
+    int64_t CN;
+    int n_tiles, n_bins;
+    int per_block;  // Gaussians per block (stage 1/4 partition)
+    int n_blocks;
+    bool lds;       // dense per-block histogram path
+};
+
+static IsectGeom isect_geom(int C, int N, int tw, int th) {
+    IsectGeom g;
+    g.CN = (int64_t)C * N;
+    g.n_tiles = tw * th;
+    g.n_bins = C * g.n_tiles;
+    g.lds = g.n_bins <= kLdsBins;
+    // bound the [blocks][bins] matrix to ~16M entries (64 MiB)
+    int64_t per = 2048;
+    if (g.lds) {
+        const int64_t need = (g.CN * (int64_t)g.n_bins + (16ll << 20) - 1) / (16ll << 20);
+        if (need > per) per = (need + 255) / 256 * 256;
+    }
+    g.per_block = (int)per;
+    g.n_blocks = (int)((g.CN + per - 1) / per);
+    if (g.n_blocks < 1) g.n_blocks = 1;
+    return g;
+}
+
+// ---------------------------------------------------------------- stage 1
+__global__ __launch_bounds__(256) void isect_count_lds_kernel(
+    int64_t CN, int N, int per_block, const float2* __restrict__ means2d,
+    const int32_t* __restrict__ radii, int tile_size, int tw, int th, int n_tiles, int n_bins,
+    int32_t* __restrict__ tiles_per_gauss, int32_t* __restrict__ blockhist) {
+    extern __shared__ __attribute__((aligned(16))) int s_hist[];
+    for (int i = threadIdx.x; i < n_bins; i += 256) s_hist[i] = 0;
+    __syncthreads();
+    const int64_t g0 = (int64_t)blockIdx.x * per_block;
+    const int64_t g1 = min(g0 + per_block, CN);
+    for (int64_t o = g0 + threadIdx.x; o < g1; o += 256) {
+        const int32_t r = radii[o];
+        if (r <= 0) {
+            tiles_per_gauss[o] = 0;
+            continue;
+        }
+        const float2 m = means2d[o];
+        int x0, y0, x1, y1;
+        tile_rect(m.x, m.y, r, tile_size, tw, th, x0, y0, x1, y1);
+        tiles_per_gauss[o] = (y1 - y0) * (x1 - x0);
+        const int base = (int)(o / N) * n_tiles;
+        for (int y = y0; y < y1; ++y)
+            for (int x = x0; x < x1; ++x) atomicAdd(&s_hist[base + y * tw + x], 1);
+    }
+    __syncthreads();
+    int32_t* row = blockhist + (int64_t)blockIdx.x * n_bins;
+    for (int i = threadIdx.x; i < n_bins; i += 256) row[i] = s_hist[i];
+}
+
+__global__ __launch_bounds__(256) void isect_count_global_kernel(
+    int64_t CN, int N, const float2* __restrict__ means2d, const int32_t* __restrict__ radii,
+    int tile_size, int tw, int th, int n_tiles, int32_t* __restrict__ tiles_per_gauss,
+    int32_t* __restrict__ totals) {
+    const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (o >= CN) return;
+    const int32_t r = radii[o];
+    if (r <= 0) {
+        tiles_per_gauss[o] = 0;
+        return;
+    }
+    const float2 m = means2d[o];
+    int x0, y0, x1, y1;
+    tile_rect(m.x, m.y, r, tile_size, tw, th, x0, y0, x1, y1);
+    tiles_per_gauss[o] = (y1 - y0) * (x1 - x0);
+    const int base = (int)(o / N) * n_tiles;
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) atomicAdd(&totals[base + y * tw + x], 1);
+}
+
+// ---------------------------------------------------------------- stage 2
+__global__ __launch_bounds__(256) void isect_colscan_kernel(int n_blocks, int n_bins,
+                                                            int32_t* __restrict__ blockhist,
+                                                            int32_t* __restrict__ totals) {
+    const int bin = blockIdx.x * 256 + threadIdx.x;
+    if (bin >= n_bins) return;
+    int32_t run = 0;
+    int b = 0;
+    for (; b + 8 <= n_blocks; b += 8) {
+        int32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = blockhist[(int64_t)(b + k) * n_bins + bin];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            blockhist[(int64_t)(b + k) * n_bins + bin] = run;
+            run += v[k];
+        }
+    }
+    for (; b < n_blocks; ++b) {
+        const int32_t v = blockhist[(int64_t)b * n_bins + bin];
+        blockhist[(int64_t)b * n_bins + bin] = run;
+        run += v;
+    }
+    totals[bin] = run;
+}
+
+// ---------------------------------------------------------------- stage 3
+// single-workgroup exclusive scan over bins (n_bins <= C * tiles; a few 10^4)
+__global__ __launch_bounds__(1024) void isect_binscan_kernel(int n_bins, const int32_t* __restrict__ totals,
+                                                             int32_t* __restrict__ offsets,
+                                                             int64_t* __restrict__ info) {
+    __shared__ int64_t s_sum[1024];
+    __shared__ int s_max[1024];
+    const int tid = threadIdx.x;
+    const int per = (n_bins + 1023) / 1024;
+    const int b0 = tid * per, b1 = min(b0 + per, n_bins);
+    int64_t local = 0;
+    int mx = 0;
+    for (int i = b0; i < b1; ++i) {
+        local += totals[i];
+        mx = max(mx, totals[i]);
+    }
+    s_sum[tid] = local;
+    s_max[tid] = mx;
+    __syncthreads();
+    // Hillis-Steele inclusive scan of 1024 partial sums
+    for (int d = 1; d < 1024; d <<= 1) {
+        int64_t v = tid >= d ? s_sum[tid - d] : 0;
+        int m2 = tid >= d ? s_max[tid - d] : 0;
+        __syncthreads();
+        s_sum[tid] += v;
+        s_max[tid] = max(s_max[tid], m2);
+        __syncthreads();
+    }
+    int64_t run = s_sum[tid] - local;
+    for (int i = b0; i < b1; ++i) {
+        offsets[i] = (int32_t)run;
+        run += totals[i];
+    }
+    if (tid == 1023) {
+        info[0] = s_sum[1023];
+        info[1] = s_max[1023];
+    }
+}
+
+// ---------------------------------------------------------------- stage 4
+__global__ __launch_bounds__(256) void isect_emit_lds_kernel(
+    int64_t CN, int N, int per_block, const float2* __restrict__ means2d,
+    const int32_t* __restrict__ radii, const float* __restrict__ depths, int tile_size, int tw,
+    int th, int n_tiles, int n_bins, const int32_t* __restrict__ offsets,
+    const int32_t* __restrict__ blockhist, uint64_t* __restrict__ keys) {
+    extern __shared__ __attribute__((aligned(16))) int s_cur[];
+    const int32_t* row = blockhist + (int64_t)blockIdx.x * n_bins;
+    for (int i = threadIdx.x; i < n_bins; i += 256) s_cur[i] = offsets[i] + row[i];
+    __syncthreads();
+    const int64_t g0 = (int64_t)blockIdx.x * per_block;
+    const int64_t g1 = min(g0 + per_block, CN);
+    for (int64_t o = g0 + threadIdx.x; o < g1; o += 256) {
+        const int32_t r = radii[o];
+        if (r <= 0) continue;
+        const float2 m = means2d[o];
+        int x0, y0, x1, y1;
+        tile_rect(m.x, m.y, r, tile_size, tw, th, x0, y0, x1, y1);
+        const uint64_t key = ((uint64_t)__float_as_uint(depths[o]) << 32) | (uint32_t)o;
+        const int base = (int)(o / N) * n_tiles;
+        for (int y = y0; y < y1; ++y)
+            for (int x = x0; x < x1; ++x) {
+                const int pos = atomicAdd(&s_cur[base + y * tw + x], 1);
+                keys[pos] = key;
+            }
+    }
+}
+
+__global__ __launch_bounds__(256) void isect_emit_global_kernel(
+    int64_t CN, int N, const float2* __restrict__ means2d, const int32_t* __restrict__ radii,
+    const float* __restrict__ depths, int tile_size, int tw, int th, int n_tiles,
+    int32_t* __restrict__ cursor, uint64_t* __restrict__ keys) {
+    const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (o >= CN) return;
+    const int32_t r = radii[o];
+    if (r <= 0) return;
+    const float2 m = means2d[o];
+    int x0, y0, x1, y1;
+    tile_rect(m.x, m.y, r, tile_size, tw, th, x0, y0, x1, y1);
+    const uint64_t key = ((uint64_t)__float_as_uint(depths[o]) << 32) | (uint32_t)o;
+    const int base = (int)(o / N) * n_tiles;
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) keys[atomicAdd(&cursor[base + y * tw + x], 1)] = key;
+}
+
+// ---------------------------------------------------------------- stage 5
+__device__ __forceinline__ void bitonic_lds(uint64_t* s, int n) {
+    // n: power of two <= kSortCap; 256 lanes
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < (n >> 1); i += 256) {
+                const int lo = 2 * j * (i / j) + (i % j);
+                const int hi = lo + j;
+                const uint64_t a = s[lo], b = s[hi];
+                const bool asc = (lo & k) == 0;
+                if ((a > b) == asc) {
+                    s[lo] = b;
+                    s[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// merge sorted runs A=[0,la), B=[la,la+lb) of src into dst (unique keys)
+__device__ void merge_runs(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, int la, int lb) {
+    constexpr int E = 8;
+    const uint64_t* A = src;
+    const uint64_t* B = src + la;
+    const int total = la + lb;
+    for (int base = threadIdx.x * E; base < total; base += 256 * E) {
+        int lo = max(0, base - lb), hi = min(base, la);
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (A[mid] < B[base - mid - 1]) lo = mid + 1;
+            else hi = mid;
+        }
+        int i = lo, j = base - lo;
+        const int cnt = min(E, total - base);
+        for (int e = 0; e < cnt; ++e) {
+            const bool takeA = j >= lb || (i < la && A[i] < B[j]);
+            dst[base + e] = takeA ? A[i++] : B[j++];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void tile_sort_kernel(int n_bins, int n_tiles, int tile_bits,
+                                                        const int32_t* __restrict__ offsets,
+                                                        int64_t n_isects, uint64_t* __restrict__ keys,
+                                                        uint64_t* __restrict__ tmp,
+                                                        int64_t* __restrict__ isect_ids,
+                                                        int32_t* __restrict__ flatten_ids) {
+    __shared__ uint64_t s_keys[kSortCap];
+    const int bin = blockIdx.x;
+    const int64_t start = offsets[bin];
+    const int64_t end = bin + 1 < n_bins ? (int64_t)offsets[bin + 1] : n_isects;
+    const int n = (int)(end - start);
+    if (n <= 0) return;
+    const int cam = bin / n_tiles, tile = bin - cam * n_tiles;
+    const int64_t hi = ((int64_t)cam << (32 + tile_bits)) | ((int64_t)tile << 32);
+    if (n <= kSortCap) {
+        int npow = 1;
+        while (npow < n) npow <<= 1;
+        for (int i = threadIdx.x; i < npow; i += 256) s_keys[i] = i < n ? keys[start + i] : ~0ull;
+        __syncthreads();
+        bitonic_lds(s_keys, npow);
+        for (int i = threadIdx.x; i < n; i += 256) {
+            const uint64_t k = s_keys[i];
+            isect_ids[start + i] = hi | (int64_t)(k >> 32);
+            flatten_ids[start + i] = (int32_t)(uint32_t)k;
+        }
+        return;
+    }
+    // large bin: LDS-sorted chunks, then merge passes ping-ponging keys <-> tmp
+    uint64_t* a = keys + start;
+    uint64_t* b = tmp + start;
+    for (int c0 = 0; c0 < n; c0 += kSortCap) {
+        const int cn = min(kSortCap, n - c0);
+        for (int i = threadIdx.x; i < kSortCap; i += 256) s_keys[i] = i < cn ? a[c0 + i] : ~0ull;
+        __syncthreads();
+        bitonic_lds(s_keys, kSortCap);
+        for (int i = threadIdx.x; i < cn; i += 256) a[c0 + i] = s_keys[i];
+        __syncthreads();
+    }
+    for (int L = kSortCap; L < n; L <<= 1) {
+        for (int p = 0; p < n; p += 2 * L) {
+            const int la = min(L, n - p);
+            const int lb = max(0, min(L, n - p - la));
+            merge_runs(a + p, b + p, la, lb);
+        }
+        __syncthreads();
+        uint64_t* t = a;
+        a = b;
+        b = t;
+    }
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const uint64_t k = a[i];
+        isect_ids[start + i] = hi | (int64_t)(k >> 32);
+        flatten_ids[start + i] = (int32_t)(uint32_t)k;
+    }
+}
+
+// ---------------------------------------------------------------- gsplat-order emission / offsets
+__global__ __launch_bounds__(256) void isect_emit_unsorted_kernel(
+    int64_t CN, int N, const float2* __restrict__ means2d, const int32_t* __restrict__ radii,
+    const float* __restrict__ depths, int tile_size, int tw, int th, int tile_bits,
+    const int64_t* __restrict__ cum, int64_t* __restrict__ isect_ids, int32_t* __restrict__ flatten_ids) {
+    const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (o >= CN) return;
+    const int32_t r = radii[o];
+    if (r <= 0) return;
+    const float2 m = means2d[o];
+    int x0, y0, x1, y1;
+    tile_rect(m.x, m.y, r, tile_size, tw, th, x0, y0, x1, y1);
+    int64_t cur = o == 0 ? 0 : cum[o - 1];
+    const int64_t cid = o / N;
+    const int64_t denc = (int64_t)(int32_t)__float_as_int(depths[o]) & 0xFFFFFFFFll;
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) {
+            const int64_t tile_id = (int64_t)y * tw + x;
+            isect_ids[cur] = (cid << (32 + tile_bits)) | (tile_id << 32) | denc;
+            flatten_ids[cur] = (int32_t)o;
+            ++cur;
+        }
+}
+
+__global__ __launch_bounds__(256) void offset_encode_kernel(int64_t n_isects, const int64_t* __restrict__ ids,
+                                                            int C, int n_tiles, int tile_bits,
+                                                            int32_t* __restrict__ offsets) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n_isects) return;
+    const int64_t mask = (1ll << tile_bits) - 1;
+    const int64_t cur = ids[idx] >> 32;
+    const int64_t id_cur = (cur >> tile_bits) * n_tiles + (cur & mask);
+    if (idx == 0)
+        for (int64_t i = 0; i < id_cur + 1; ++i) offsets[i] = 0;
+    if (idx == n_isects - 1)
+        for (int64_t i = id_cur + 1; i < (int64_t)C * n_tiles; ++i) offsets[i] = (int32_t)n_isects;
+    if (idx > 0) {
+        const int64_t prev = ids[idx - 1] >> 32;
+        const int64_t id_prev = (prev >> tile_bits) * n_tiles + (prev & mask);
+        if (id_prev == id_cur) return;
+        for (int64_t i = id_prev + 1; i < id_cur + 1; ++i) offsets[i] = (int32_t)idx;
+    }
+}
+
+__global__ void copy_i32_kernel(int n, const int32_t* __restrict__ a, int32_t* __restrict__ b) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) b[i] = a[i];
+}
+
+}  // namespace hgsr
+
+using namespace hgsr;
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+extern "C" size_t hgsr_isect_ws1_bytes(int C, int N, int tile_w, int tile_h) {
+    const IsectGeom g = isect_geom(C, N, tile_w, tile_h);
+    size_t b = align256((size_t)g.n_bins * 4);  // totals (or global counters)
+    b += align256((size_t)g.n_bins * 4);        // cursors (global path)
+    if (g.lds) b += align256((size_t)g.n_blocks * g.n_bins * 4);
+    return b;
+}
+
+extern "C" size_t hgsr_isect_ws2_bytes(int64_t n_isects, int64_t max_bin) {
+    size_t b = align256((size_t)n_isects * 8);
+    if (max_bin > kSortCap) b += align256((size_t)n_isects * 8);
+    return b;
+}
+
+struct Ws1 {
+    int32_t* totals;
+    int32_t* cursor;
+    int32_t* blockhist;
+};
+static Ws1 carve_ws1(const IsectGeom& g, void* ws) {
+    Ws1 w;
+    char* p = (char*)ws;
+    w.totals = (int32_t*)p;
+    p += align256((size_t)g.n_bins * 4);
+    w.cursor = (int32_t*)p;
+    p += align256((size_t)g.n_bins * 4);
+    w.blockhist = g.lds ? (int32_t*)p : nullptr;
+    return w;
+}
+
+extern "C" int hgsr_isect_count(int C, int N, const float* means2d, const int32_t* radii, int tile_size,
+                                int tile_w, int tile_h, int32_t* tiles_per_gauss, int32_t* isect_offsets,
+                                int64_t* info, void* ws1, size_t ws1_bytes, hgsr_stream_t stream) {
+    HGSR_REQUIRE(C >= 1 && N >= 0 && tile_size > 0 && tile_w > 0 && tile_h > 0, "bad dims");
+    HGSR_REQUIRE((int64_t)C * tile_w * tile_h < (1ll << 30), "too many tiles");
+    HGSR_REQUIRE((int64_t)C * N < (1ll << 31), "C*N exceeds int32 flatten ids");
+    HGSR_REQUIRE(ws1_bytes >= hgsr_isect_ws1_bytes(C, N, tile_w, tile_h), "isect ws1 too small");
+    HGSR_REQUIRE(isect_offsets && info && ws1 && (N == 0 || (means2d && radii && tiles_per_gauss)), "null pointer");
+    const IsectGeom g = isect_geom(C, N, tile_w, tile_h);
+    const Ws1 w = carve_ws1(g, ws1);
+    hipStream_t s = as_stream(stream);
+    if (g.lds) {
+        if (g.CN > 0) {
+            hipLaunchKernelGGL(isect_count_lds_kernel, dim3(g.n_blocks), dim3(256), g.n_bins * 4, s, g.CN, N,
+                               g.per_block, reinterpret_cast<const float2*>(means2d), radii, tile_size, tile_w,
+                               tile_h, g.n_tiles, g.n_bins, tiles_per_gauss, w.blockhist);
+            if (int st = check_launch("isect_count")) return st;
+            hipLaunchKernelGGL(isect_colscan_kernel, dim3((g.n_bins + 255) / 256), dim3(256), 0, s,
+                               g.n_blocks, g.n_bins, w.blockhist, w.totals);
+        } else {
+            if (int st = memset_async(w.totals, (size_t)g.n_bins * 4, s, "isect_count")) return st;
+        }
+    } else {
+        if (int st = memset_async(w.totals, (size_t)g.n_bins * 4, s, "isect_count")) return st;
+        if (g.CN > 0)
+            hipLaunchKernelGGL(isect_count_global_kernel, dim3((unsigned)((g.CN + 255) / 256)), dim3(256), 0, s,
+                               g.CN, N, reinterpret_cast<const float2*>(means2d), radii, tile_size, tile_w,
+                               tile_h, g.n_tiles, tiles_per_gauss, w.totals);
+    }
+    if (int st = check_launch("isect_count")) return st;
+    hipLaunchKernelGGL(isect_binscan_kernel, dim3(1), dim3(1024), 0, s, g.n_bins, w.totals, isect_offsets, info);
+    return check_launch("isect_binscan");
+}
+
+extern "C" int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const int32_t* radii,
+                                      const float* depths, int tile_size, int tile_w, int tile_h,
+                                      const int32_t* isect_offsets, int64_t n_isects, int64_t max_bin,
+                                      int64_t* isect_ids, int32_t* flatten_ids, void* ws1, size_t ws1_bytes,
+                                      void* ws2, size_t ws2_bytes, hgsr_stream_t stream) {
+    HGSR_REQUIRE(C >= 1 && N >= 0 && tile_size > 0 && tile_w > 0 && tile_h > 0, "bad dims");
+    HGSR_REQUIRE(ws1_bytes >= hgsr_isect_ws1_bytes(C, N, tile_w, tile_h), "isect ws1 too small");
+    HGSR_REQUIRE(ws2_bytes >= hgsr_isect_ws2_bytes(n_isects, max_bin), "isect ws2 too small");
+    if (n_isects == 0) return HGSR_OK;
+    HGSR_REQUIRE(means2d && radii && depths && isect_offsets && isect_ids && flatten_ids && ws1 && ws2,
+                 "null pointer");
+    const IsectGeom g = isect_geom(C, N, tile_w, tile_h);
+    const Ws1 w = carve_ws1(g, ws1);
+    uint64_t* keys = (uint64_t*)ws2;
+    uint64_t* tmp = max_bin > kSortCap ? (uint64_t*)((char*)ws2 + align256((size_t)n_isects * 8)) : nullptr;
+    hipStream_t s = as_stream(stream);
+    if (g.lds) {
+        hipLaunchKernelGGL(isect_emit_lds_kernel, dim3(g.n_blocks), dim3(256), g.n_bins * 4, s, g.CN, N,
+                           g.per_block, reinterpret_cast<const float2*>(means2d), radii, depths, tile_size,
+                           tile_w, tile_h, g.n_tiles, g.n_bins, isect_offsets, w.blockhist, keys);
+    } else {
+        hipLaunchKernelGGL(copy_i32_kernel, dim3((g.n_bins + 255) / 256), dim3(256), 0, s, g.n_bins,
+                           isect_offsets, w.cursor);
+        hipLaunchKernelGGL(isect_emit_global_kernel, dim3((unsigned)((g.CN + 255) / 256)), dim3(256), 0, s, g.CN,
+                           N, reinterpret_cast<const float2*>(means2d), radii, depths, tile_size, tile_w, tile_h,
+                           g.n_tiles, w.cursor, keys);
+    }
+    if (int st = check_launch("isect_emit")) return st;
+    hipLaunchKernelGGL(tile_sort_kernel, dim3(g.n_bins), dim3(256), 0, s, g.n_bins, g.n_tiles,
+                       nbits64(g.n_tiles), isect_offsets, n_isects, keys, tmp, isect_ids, flatten_ids);
+    return check_launch("tile_sort");
+}
+
+extern "C" int hgsr_isect_emit_unsorted(int C, int N, const float* means2d, const int32_t* radii,
+                                        const float* depths, int tile_size, int tile_w, int tile_h,
+                                        const int64_t* cum_tiles, int64_t* isect_ids, int32_t* flatten_ids,
+                                        hgsr_stream_t stream) {
+    HGSR_REQUIRE(C >= 1 && N >= 0 && tile_size > 0 && tile_w > 0 && tile_h > 0, "bad dims");
+    const int64_t CN = (int64_t)C * N;
+    if (CN == 0) return HGSR_OK;
+    HGSR_REQUIRE(means2d && radii && depths && cum_tiles && isect_ids && flatten_ids, "null pointer");
+    hipLaunchKernelGGL(isect_emit_unsorted_kernel, dim3((unsigned)((CN + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), CN, N, reinterpret_cast<const float2*>(means2d), radii, depths,
+                       tile_size, tile_w, tile_h, nbits64((int64_t)tile_w * tile_h), cum_tiles, isect_ids,
+                       flatten_ids);
+    return check_launch("isect_emit_unsorted");
+}
+
+extern "C" int hgsr_isect_offset_encode(int64_t n_isects, const int64_t* isect_ids, int C, int tile_w,
+                                        int tile_h, int32_t* offsets, hgsr_stream_t stream) {
+    HGSR_REQUIRE(C >= 1 && tile_w > 0 && tile_h > 0 && offsets, "bad args");
+    hipStream_t s = as_stream(stream);
+    const int n_tiles = tile_w * tile_h;
+    if (n_isects == 0) {
+        if (int st = memset_async(offsets, (size_t)C * n_tiles * 4, s, "offset_encode")) return st;
+        return check_launch("offset_encode");
+    }
+    HGSR_REQUIRE(isect_ids, "null pointer");
+    hipLaunchKernelGGL(offset_encode_kernel, dim3((unsigned)((n_isects + 255) / 256)), dim3(256), 0, s, n_isects,
+                       isect_ids, C, n_tiles, nbits64(n_tiles), offsets);
+    return check_launch("offset_encode");
+}

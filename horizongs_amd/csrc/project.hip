@@ -1,0 +1,585 @@
+// K1/K2/K10: Gaussian projection, 3DGS (EWA) and 2DGS (surfel ray transform),
+// forward and backward.  One lane per (camera, Gaussian); HBM-bound.
+//
+// Compiled with -ffp-contract=off: radii, means2d and depths feed the integer
+// tile/intersection keys, which must be bit-identical to the CPU restatement
+// (oracle/hgsr_oracle.c), so every expression keeps the oracle's operation
+// order and rounding (correctly rounded divide/sqrt, no FMA contraction).
+//
+// Semantics: gsplat fully_fused_projection / fully_fused_projection_2dgs as
+// called at reference gaussian_renderer/render.py:149-186 and inside
+// gsplat.rasterization[_2dgs] (render.py:40-76).
+#include "common.h"
+
+namespace hgsr {
+
+struct Mat3 {
+    float m[3][3];
+};
+
+__device__ __forceinline__ Mat3 mm3(const Mat3& a, const Mat3& b) {
+    Mat3 o;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) o.m[i][j] = a.m[i][0] * b.m[0][j] + a.m[i][1] * b.m[1][j] + a.m[i][2] * b.m[2][j];
+    return o;
+}
+// a * b^T
+__device__ __forceinline__ Mat3 mm3_bt(const Mat3& a, const Mat3& b) {
+    Mat3 o;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) o.m[i][j] = a.m[i][0] * b.m[j][0] + a.m[i][1] * b.m[j][1] + a.m[i][2] * b.m[j][2];
+    return o;
+}
+// a^T * b
+__device__ __forceinline__ Mat3 mm3_at(const Mat3& a, const Mat3& b) {
+    Mat3 o;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) o.m[i][j] = a.m[0][i] * b.m[0][j] + a.m[1][i] * b.m[1][j] + a.m[2][i] * b.m[2][j];
+    return o;
+}
+
+struct View {
+    Mat3 R;
+    float t[3];
+    float fx, fy, cx, cy;
+};
+
+__device__ __forceinline__ View load_view(const float* __restrict__ vm, const float* __restrict__ K) {
+    View v;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) v.R.m[i][j] = vm[i * 4 + j];
+        v.t[i] = vm[i * 4 + 3];
+    }
+    v.fx = K[0];
+    v.cx = K[2];
+    v.fy = K[4];
+    v.cy = K[5];
+    return v;
+}
+
+__device__ __forceinline__ void to_camera(const View& v, const float* m, float mc[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) mc[i] = v.R.m[i][0] * m[0] + v.R.m[i][1] * m[1] + v.R.m[i][2] * m[2] + v.t[i];
+}
+
+__device__ __forceinline__ Mat3 quat_to_rotmat(float4 q) {
+    float w = q.x, x = q.y, y = q.z, z = q.w;
+    float n2 = x * x + y * y + z * z + w * w;
+    float inv = 1.0f / sqrtf(n2);
+    x = x * inv; y = y * inv; z = z * inv; w = w * inv;
+    float x2 = x * x, y2 = y * y, z2 = z * z;
+    float xy = x * y, xz = x * z, yz = y * z;
+    float wx = w * x, wy = w * y, wz = w * z;
+    Mat3 R;
+    R.m[0][0] = 1.0f - 2.0f * (y2 + z2);
+    R.m[0][1] = 2.0f * (xy - wz);
+    R.m[0][2] = 2.0f * (xz + wy);
+    R.m[1][0] = 2.0f * (xy + wz);
+    R.m[1][1] = 1.0f - 2.0f * (x2 + z2);
+    R.m[1][2] = 2.0f * (yz - wx);
+    R.m[2][0] = 2.0f * (xz - wy);
+    R.m[2][1] = 2.0f * (yz + wx);
+    R.m[2][2] = 1.0f - 2.0f * (x2 + y2);
+    return R;
+}
+
+__device__ __forceinline__ float4 quat_to_rotmat_vjp(float4 q, const Mat3& vR) {
+    float w = q.x, x = q.y, y = q.z, z = q.w;
+    float n2 = x * x + y * y + z * z + w * w;
+    float inv = 1.0f / sqrtf(n2);
+    x = x * inv; y = y * inv; z = z * inv; w = w * inv;
+    const float(*v)[3] = vR.m;
+    float gw = 2.0f * (x * (v[2][1] - v[1][2]) + y * (v[0][2] - v[2][0]) + z * (v[1][0] - v[0][1]));
+    float gx = 2.0f * (-2.0f * x * (v[1][1] + v[2][2]) + y * (v[1][0] + v[0][1]) + z * (v[2][0] + v[0][2]) + w * (v[2][1] - v[1][2]));
+    float gy = 2.0f * (x * (v[1][0] + v[0][1]) - 2.0f * y * (v[0][0] + v[2][2]) + z * (v[2][1] + v[1][2]) + w * (v[0][2] - v[2][0]));
+    float gz = 2.0f * (x * (v[2][0] + v[0][2]) + y * (v[2][1] + v[1][2]) - 2.0f * z * (v[0][0] + v[1][1]) + w * (v[1][0] - v[0][1]));
+    float dot = gw * w + gx * x + gy * y + gz * z;
+    return make_float4((gw - dot * w) * inv, (gx - dot * x) * inv, (gy - dot * y) * inv, (gz - dot * z) * inv);
+}
+
+struct Lims {
+    float xp, xn, yp, yn;
+};
+
+__device__ __forceinline__ Lims make_lims(const View& v, int W, int H) {
+    Lims l;
+    float tan_fovx = 0.5f * (float)W / v.fx;
+    float tan_fovy = 0.5f * (float)H / v.fy;
+    l.xp = ((float)W - v.cx) / v.fx + 0.3f * tan_fovx;
+    l.xn = v.cx / v.fx + 0.3f * tan_fovx;
+    l.yp = ((float)H - v.cy) / v.fy + 0.3f * tan_fovy;
+    l.yn = v.cy / v.fy + 0.3f * tan_fovy;
+    return l;
+}
+
+__device__ __forceinline__ float3 ld3(const float* p) { return make_float3(p[0], p[1], p[2]); }
+
+__device__ __forceinline__ Mat3 covar_from_qs(float4 q, float3 s, Mat3& Rq) {
+    Rq = quat_to_rotmat(q);
+    Mat3 M;
+    const float sv[3] = {s.x, s.y, s.z};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) M.m[i][j] = Rq.m[i][j] * sv[j];
+    return mm3_bt(M, M);
+}
+
+// ---------------------------------------------------------------- 3DGS fwd
+__global__ __launch_bounds__(256) void project3d_fwd_kernel(
+    int N, const float* __restrict__ means, const float4* __restrict__ quats,
+    const float* __restrict__ scales, const float* __restrict__ viewmats,
+    const float* __restrict__ Ks, int W, int H, float eps2d, float near_plane, float far_plane,
+    float radius_clip, int32_t* __restrict__ radii, float2* __restrict__ means2d,
+    float* __restrict__ depths, float* __restrict__ conics) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y;
+    if (g >= N) return;
+    const int64_t o = (int64_t)c * N + g;
+    const View v = load_view(viewmats + c * 16, Ks + c * 9);
+    const Lims L = make_lims(v, W, H);
+    const float m[3] = {means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2]};
+    float mc[3];
+    to_camera(v, m, mc);
+    int32_t rad = 0;
+    float2 m2 = make_float2(0.f, 0.f);
+    float dep = 0.f, ca = 0.f, cb = 0.f, cc = 0.f;
+    if (!(mc[2] < near_plane || mc[2] > far_plane)) {
+        Mat3 Rq;
+        const Mat3 cov = covar_from_qs(quats[g], ld3(scales + (int64_t)g * 3), Rq);
+        const Mat3 covc = mm3_bt(mm3(v.R, cov), v.R);
+        const float x = mc[0], y = mc[1], z = mc[2];
+        const float rz = 1.0f / z;
+        const float rz2 = rz * rz;
+        const float tx = z * fminf(L.xp, fmaxf(-L.xn, x * rz));
+        const float ty = z * fminf(L.yp, fmaxf(-L.yn, y * rz));
+        const float J[2][3] = {{v.fx * rz, 0.f, -v.fx * tx * rz2}, {0.f, v.fy * rz, -v.fy * ty * rz2}};
+        float JS[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) JS[i][j] = J[i][0] * covc.m[0][j] + J[i][1] * covc.m[1][j] + J[i][2] * covc.m[2][j];
+        float c2[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) c2[i][j] = JS[i][0] * J[j][0] + JS[i][1] * J[j][1] + JS[i][2] * J[j][2];
+        const float mx = v.fx * x * rz + v.cx;
+        const float my = v.fy * y * rz + v.cy;
+        c2[0][0] = c2[0][0] + eps2d;
+        c2[1][1] = c2[1][1] + eps2d;
+        const float det = c2[0][0] * c2[1][1] - c2[0][1] * c2[1][0];
+        if (det > 0.f) {
+            const float idet = 1.0f / det;
+            const float b = 0.5f * (c2[0][0] + c2[1][1]);
+            const float v1 = b + sqrtf(fmaxf(0.01f, b * b - det));
+            const float radius = ceilf(3.0f * sqrtf(v1));
+            if (radius > radius_clip && !(mx + radius <= 0.f || mx - radius >= (float)W ||
+                                          my + radius <= 0.f || my - radius >= (float)H)) {
+                rad = (int32_t)radius;
+                m2 = make_float2(mx, my);
+                dep = z;
+                ca = c2[1][1] * idet;
+                cb = -c2[0][1] * idet;
+                cc = c2[0][0] * idet;
+            }
+        }
+    }
+    radii[o] = rad;
+    means2d[o] = m2;
+    depths[o] = dep;
+    conics[o * 3 + 0] = ca;
+    conics[o * 3 + 1] = cb;
+    conics[o * 3 + 2] = cc;
+}
+
+// ---------------------------------------------------------------- 3DGS bwd
+// One lane per Gaussian, looping over cameras: deterministic accumulation.
+__global__ __launch_bounds__(256) void project3d_bwd_kernel(
+    int C, int N, const float* __restrict__ means, const float4* __restrict__ quats,
+    const float* __restrict__ scales, const float* __restrict__ viewmats,
+    const float* __restrict__ Ks, int W, int H, const int32_t* __restrict__ radii,
+    const float* __restrict__ conics, const float2* __restrict__ v_means2d,
+    const float* __restrict__ v_depths, const float* __restrict__ v_conics,
+    float* __restrict__ v_means, float4* __restrict__ v_quats, float* __restrict__ v_scales) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= N) return;
+    const float m[3] = {means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2]};
+    const float4 q = quats[g];
+    const float3 s3 = ld3(scales + (int64_t)g * 3);
+    const float s[3] = {s3.x, s3.y, s3.z};
+    float vm_acc[3] = {0.f, 0.f, 0.f};
+    float vs_acc[3] = {0.f, 0.f, 0.f};
+    float4 vq_acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool any = false;
+    Mat3 Rq, cov;
+    for (int c = 0; c < C; ++c) {
+        const int64_t o = (int64_t)c * N + g;
+        if (radii[o] <= 0) continue;
+        if (!any) {
+            cov = covar_from_qs(q, s3, Rq);
+            any = true;
+        }
+        const View v = load_view(viewmats + c * 16, Ks + c * 9);
+        const Lims L = make_lims(v, W, H);
+        const float Ci[2][2] = {{conics[o * 3], conics[o * 3 + 1]}, {conics[o * 3 + 1], conics[o * 3 + 2]}};
+        const float vCi[2][2] = {{v_conics[o * 3], 0.5f * v_conics[o * 3 + 1]},
+                                 {0.5f * v_conics[o * 3 + 1], v_conics[o * 3 + 2]}};
+        float T1[2][2], vc2[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) T1[i][j] = Ci[i][0] * vCi[0][j] + Ci[i][1] * vCi[1][j];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) vc2[i][j] = -(T1[i][0] * Ci[0][j] + T1[i][1] * Ci[1][j]);
+        float mc[3];
+        to_camera(v, m, mc);
+        const Mat3 covc = mm3_bt(mm3(v.R, cov), v.R);
+        const float x = mc[0], y = mc[1], z = mc[2];
+        const float rz = 1.0f / z, rz2 = rz * rz, rz3 = rz2 * rz;
+        const float ux = x * rz, uy = y * rz;
+        const float tx = z * fminf(L.xp, fmaxf(-L.xn, ux));
+        const float ty = z * fminf(L.yp, fmaxf(-L.yn, uy));
+        const float J[2][3] = {{v.fx * rz, 0.f, -v.fx * tx * rz2}, {0.f, v.fy * rz, -v.fy * ty * rz2}};
+        Mat3 vcovc;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                float acc = 0.f;
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b2 = 0; b2 < 2; ++b2) acc += J[a][i] * vc2[a][b2] * J[b2][j];
+                vcovc.m[i][j] = acc;
+            }
+        float vJ[2][3];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                float acc = 0.f;
+#pragma unroll
+                for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) acc += (vc2[a][b2] + vc2[b2][a]) * J[b2][k] * covc.m[k][j];
+                vJ[a][j] = acc;
+            }
+        const float2 vm2 = v_means2d[o];
+        float vmc[3];
+        vmc[0] = v.fx * rz * vm2.x;
+        vmc[1] = v.fy * rz * vm2.y;
+        vmc[2] = -(v.fx * x * vm2.x + v.fy * y * vm2.y) * rz2;
+        vmc[2] += -v.fx * rz2 * vJ[0][0] - v.fy * rz2 * vJ[1][1];
+        if (ux <= L.xp && ux >= -L.xn) {
+            vmc[0] += -v.fx * rz2 * vJ[0][2];
+            vmc[2] += 2.0f * v.fx * tx * rz3 * vJ[0][2];
+        } else {
+            vmc[2] += v.fx * tx * rz3 * vJ[0][2];
+        }
+        if (uy <= L.yp && uy >= -L.yn) {
+            vmc[1] += -v.fy * rz2 * vJ[1][2];
+            vmc[2] += 2.0f * v.fy * ty * rz3 * vJ[1][2];
+        } else {
+            vmc[2] += v.fy * ty * rz3 * vJ[1][2];
+        }
+        vmc[2] += v_depths[o];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) vm_acc[j] += v.R.m[0][j] * vmc[0] + v.R.m[1][j] * vmc[1] + v.R.m[2][j] * vmc[2];
+        const Mat3 vcov = mm3(mm3_at(v.R, vcovc), v.R);
+        Mat3 Mm, vsym;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                Mm.m[i][j] = Rq.m[i][j] * s[j];
+                vsym.m[i][j] = vcov.m[i][j] + vcov.m[j][i];
+            }
+        const Mat3 vM = mm3(vsym, Mm);
+        Mat3 vRq;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) vRq.m[i][j] = vM.m[i][j] * s[j];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) vs_acc[j] += Rq.m[0][j] * vM.m[0][j] + Rq.m[1][j] * vM.m[1][j] + Rq.m[2][j] * vM.m[2][j];
+        const float4 vq = quat_to_rotmat_vjp(q, vRq);
+        vq_acc.x += vq.x; vq_acc.y += vq.y; vq_acc.z += vq.z; vq_acc.w += vq.w;
+    }
+    if (!any) return;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        v_means[(int64_t)g * 3 + j] += vm_acc[j];
+        v_scales[(int64_t)g * 3 + j] += vs_acc[j];
+    }
+    float4 t = v_quats[g];
+    t.x += vq_acc.x; t.y += vq_acc.y; t.z += vq_acc.z; t.w += vq_acc.w;
+    v_quats[g] = t;
+}
+
+// ---------------------------------------------------------------- 2DGS fwd
+struct Surfel {
+    Mat3 RRq, Rq;
+    float RS[3][3];
+    float mc[3];
+};
+
+__device__ __forceinline__ Surfel surfel_frame(const View& v, const float* m, float4 q, float3 s) {
+    Surfel f;
+    to_camera(v, m, f.mc);
+    f.Rq = quat_to_rotmat(q);
+    f.RRq = mm3(v.R, f.Rq);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        f.RS[i][0] = f.RRq.m[i][0] * s.x;
+        f.RS[i][1] = f.RRq.m[i][1] * s.y;
+        f.RS[i][2] = f.RRq.m[i][2];
+    }
+    return f;
+}
+
+__global__ __launch_bounds__(256) void project2d_fwd_kernel(
+    int N, const float* __restrict__ means, const float4* __restrict__ quats,
+    const float* __restrict__ scales, const float* __restrict__ viewmats,
+    const float* __restrict__ Ks, int W, int H, float near_plane, float far_plane,
+    float radius_clip, int32_t* __restrict__ radii, float2* __restrict__ means2d,
+    float* __restrict__ depths, float* __restrict__ ray_transforms, float* __restrict__ normals) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y;
+    if (g >= N) return;
+    const int64_t o = (int64_t)c * N + g;
+    const View v = load_view(viewmats + c * 16, Ks + c * 9);
+    const float m[3] = {means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2]};
+    const Surfel f = surfel_frame(v, m, quats[g], ld3(scales + (int64_t)g * 3));
+    float M[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    float nrm[3] = {0.f, 0.f, 0.f};
+    int32_t rad = 0;
+    float2 m2 = make_float2(0.f, 0.f);
+    float dep = 0.f;
+    if (!(f.mc[2] < near_plane || f.mc[2] > far_plane)) {
+        float WH[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            WH[i][0] = f.RS[i][0];
+            WH[i][1] = f.RS[i][1];
+            WH[i][2] = f.mc[i];
+        }
+        float Mt[3][3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            Mt[0][j] = v.fx * WH[0][j] + v.cx * WH[2][j];
+            Mt[1][j] = v.fy * WH[1][j] + v.cy * WH[2][j];
+            Mt[2][j] = WH[2][j];
+        }
+        const float dist = Mt[2][0] * Mt[2][0] + Mt[2][1] * Mt[2][1] - Mt[2][2] * Mt[2][2];
+        if (dist != 0.f) {
+            const float f0 = 1.0f / dist, f2 = -(1.0f / dist);
+            const float mx = f0 * Mt[0][0] * Mt[2][0] + f0 * Mt[0][1] * Mt[2][1] + f2 * Mt[0][2] * Mt[2][2];
+            const float my = f0 * Mt[1][0] * Mt[2][0] + f0 * Mt[1][1] * Mt[2][1] + f2 * Mt[1][2] * Mt[2][2];
+            const float tpx = f0 * Mt[0][0] * Mt[0][0] + f0 * Mt[0][1] * Mt[0][1] + f2 * Mt[0][2] * Mt[0][2];
+            const float tpy = f0 * Mt[1][0] * Mt[1][0] + f0 * Mt[1][1] * Mt[1][1] + f2 * Mt[1][2] * Mt[1][2];
+            const float hx = mx * mx - tpx, hy = my * my - tpy;
+            const float radius = ceilf(3.33f * sqrtf(fmaxf(1e-4f, fmaxf(hx, hy))));
+            if (radius > radius_clip && !(mx + radius <= 0.f || mx - radius >= (float)W ||
+                                          my + radius <= 0.f || my - radius >= (float)H)) {
+                const float n0 = f.RS[0][2], n1 = f.RS[1][2], n2 = f.RS[2][2];
+                const float d = -n0 * f.mc[0] + -n1 * f.mc[1] + -n2 * f.mc[2];
+                const float sgn = d > 0.f ? 1.0f : -1.0f;
+                rad = (int32_t)radius;
+                m2 = make_float2(mx, my);
+                dep = f.mc[2];
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) M[i][j] = Mt[i][j];
+                nrm[0] = n0 * sgn;
+                nrm[1] = n1 * sgn;
+                nrm[2] = n2 * sgn;
+            }
+        }
+    }
+    radii[o] = rad;
+    means2d[o] = m2;
+    depths[o] = dep;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) ray_transforms[o * 9 + i * 3 + j] = M[i][j];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) normals[o * 3 + i] = nrm[i];
+}
+
+// ---------------------------------------------------------------- 2DGS bwd
+__global__ __launch_bounds__(256) void project2d_bwd_kernel(
+    int C, int N, const float* __restrict__ means, const float4* __restrict__ quats,
+    const float* __restrict__ scales, const float* __restrict__ viewmats,
+    const float* __restrict__ Ks, const int32_t* __restrict__ radii,
+    const float* __restrict__ ray_transforms, const float2* __restrict__ v_means2d,
+    const float* __restrict__ v_depths, const float* __restrict__ v_ray_transforms,
+    const float* __restrict__ v_normals, float* __restrict__ v_means, float4* __restrict__ v_quats,
+    float* __restrict__ v_scales) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= N) return;
+    const float m[3] = {means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2]};
+    const float4 q = quats[g];
+    const float3 s = ld3(scales + (int64_t)g * 3);
+    float vm_acc[3] = {0.f, 0.f, 0.f};
+    float vs0 = 0.f, vs1 = 0.f;
+    float4 vq_acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool any = false;
+    for (int c = 0; c < C; ++c) {
+        const int64_t o = (int64_t)c * N + g;
+        if (radii[o] <= 0) continue;
+        any = true;
+        const View v = load_view(viewmats + c * 16, Ks + c * 9);
+        const Surfel f = surfel_frame(v, m, q, s);
+        const float* M = ray_transforms + o * 9;
+        float vM[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) vM[i][j] = v_ray_transforms[o * 9 + i * 3 + j];
+        const float2 vm2 = v_means2d[o];
+        const float dist = M[6] * M[6] + M[7] * M[7] - M[8] * M[8];
+        const float id = 1.0f / dist;
+        const float e[3] = {1.f, 1.f, -1.f};
+        const float mx = (M[0] * M[6] + M[1] * M[7] - M[2] * M[8]) * id;
+        const float my = (M[3] * M[6] + M[4] * M[7] - M[5] * M[8]) * id;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            vM[0][j] += vm2.x * e[j] * M[6 + j] * id;
+            vM[1][j] += vm2.y * e[j] * M[6 + j] * id;
+            vM[2][j] += (vm2.x * e[j] * M[j] + vm2.y * e[j] * M[3 + j]) * id -
+                        (vm2.x * mx + vm2.y * my) * 2.0f * e[j] * M[6 + j] * id;
+        }
+        float vWH[3][3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            vWH[0][j] = v.fx * vM[0][j];
+            vWH[1][j] = v.fy * vM[1][j];
+            vWH[2][j] = v.cx * vM[0][j] + v.cy * vM[1][j] + vM[2][j];
+        }
+        const float vmc[3] = {vWH[0][2], vWH[1][2], vWH[2][2] + v_depths[o]};
+        const float n0 = f.RS[0][2], n1 = f.RS[1][2], n2 = f.RS[2][2];
+        const float d = -n0 * f.mc[0] + -n1 * f.mc[1] + -n2 * f.mc[2];
+        const float sgn = d > 0.f ? 1.0f : -1.0f;
+        Mat3 vRRq;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            vRRq.m[i][0] = vWH[i][0] * s.x;
+            vRRq.m[i][1] = vWH[i][1] * s.y;
+            vRRq.m[i][2] = sgn * v_normals[o * 3 + i];
+            vs0 += vWH[i][0] * f.RRq.m[i][0];
+            vs1 += vWH[i][1] * f.RRq.m[i][1];
+        }
+        const Mat3 vRq = mm3_at(v.R, vRRq);
+        const float4 vq = quat_to_rotmat_vjp(q, vRq);
+        vq_acc.x += vq.x; vq_acc.y += vq.y; vq_acc.z += vq.z; vq_acc.w += vq.w;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) vm_acc[j] += v.R.m[0][j] * vmc[0] + v.R.m[1][j] * vmc[1] + v.R.m[2][j] * vmc[2];
+    }
+    if (!any) return;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) v_means[(int64_t)g * 3 + j] += vm_acc[j];
+    v_scales[(int64_t)g * 3 + 0] += vs0;
+    v_scales[(int64_t)g * 3 + 1] += vs1;
+    float4 t = v_quats[g];
+    t.x += vq_acc.x; t.y += vq_acc.y; t.z += vq_acc.z; t.w += vq_acc.w;
+    v_quats[g] = t;
+}
+
+}  // namespace hgsr
+
+using namespace hgsr;
+
+static int check_common(int C, int N, const void* means, const void* quats, const void* scales,
+                        const void* viewmats, const void* Ks, int W, int H) {
+    HGSR_REQUIRE(C >= 1 && N >= 0 && W > 0 && H > 0, "bad dims C=%d N=%d W=%d H=%d", C, N, W, H);
+    HGSR_REQUIRE(C <= 65535, "too many cameras (%d)", C);
+    HGSR_REQUIRE(N == 0 || (means && quats && scales && viewmats && Ks), "null input pointer");
+    return HGSR_OK;
+}
+
+extern "C" int hgsr_project3d_fwd(int C, int N, const float* means, const float* quats,
+                                  const float* scales, const float* viewmats, const float* Ks,
+                                  int width, int height, float eps2d, float near_plane,
+                                  float far_plane, float radius_clip, int32_t* radii,
+                                  float* means2d, float* depths, float* conics,
+                                  hgsr_stream_t stream) {
+    int st = check_common(C, N, means, quats, scales, viewmats, Ks, width, height);
+    if (st) return st;
+    HGSR_REQUIRE(N == 0 || (radii && means2d && depths && conics), "null output pointer");
+    if (N == 0) return HGSR_OK;
+    dim3 grid((N + 255) / 256, C);
+    hipLaunchKernelGGL(project3d_fwd_kernel, grid, dim3(256), 0, as_stream(stream), N, means,
+                       reinterpret_cast<const float4*>(quats), scales, viewmats, Ks, width, height,
+                       eps2d, near_plane, far_plane, radius_clip, radii,
+                       reinterpret_cast<float2*>(means2d), depths, conics);
+    return check_launch("project3d_fwd");
+}
+
+extern "C" int hgsr_project3d_bwd(int C, int N, const float* means, const float* quats,
+                                  const float* scales, const float* viewmats, const float* Ks,
+                                  int width, int height, float eps2d, const int32_t* radii,
+                                  const float* conics, const float* v_means2d,
+                                  const float* v_depths, const float* v_conics, float* v_means,
+                                  float* v_quats, float* v_scales, hgsr_stream_t stream) {
+    (void)eps2d;
+    int st = check_common(C, N, means, quats, scales, viewmats, Ks, width, height);
+    if (st) return st;
+    HGSR_REQUIRE(N == 0 || (radii && conics && v_means2d && v_depths && v_conics && v_means && v_quats && v_scales),
+                 "null pointer");
+    if (N == 0) return HGSR_OK;
+    hipLaunchKernelGGL(project3d_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, as_stream(stream), C, N,
+                       means, reinterpret_cast<const float4*>(quats), scales, viewmats, Ks, width,
+                       height, radii, conics, reinterpret_cast<const float2*>(v_means2d), v_depths,
+                       v_conics, v_means, reinterpret_cast<float4*>(v_quats), v_scales);
+    return check_launch("project3d_bwd");
+}
+
+extern "C" int hgsr_project2d_fwd(int C, int N, const float* means, const float* quats,
+                                  const float* scales, const float* viewmats, const float* Ks,
+                                  int width, int height, float near_plane, float far_plane,
+                                  float radius_clip, int32_t* radii, float* means2d, float* depths,
+                                  float* ray_transforms, float* normals, hgsr_stream_t stream) {
+    int st = check_common(C, N, means, quats, scales, viewmats, Ks, width, height);
+    if (st) return st;
+    HGSR_REQUIRE(N == 0 || (radii && means2d && depths && ray_transforms && normals), "null output pointer");
+    if (N == 0) return HGSR_OK;
+    dim3 grid((N + 255) / 256, C);
+    hipLaunchKernelGGL(project2d_fwd_kernel, grid, dim3(256), 0, as_stream(stream), N, means,
+                       reinterpret_cast<const float4*>(quats), scales, viewmats, Ks, width, height,
+                       near_plane, far_plane, radius_clip, radii, reinterpret_cast<float2*>(means2d),
+                       depths, ray_transforms, normals);
+    return check_launch("project2d_fwd");
+}
+
+extern "C" int hgsr_project2d_bwd(int C, int N, const float* means, const float* quats,
+                                  const float* scales, const float* viewmats, const float* Ks,
+                                  int width, int height, const int32_t* radii,
+                                  const float* ray_transforms, const float* v_means2d,
+                                  const float* v_depths, const float* v_ray_transforms,
+                                  const float* v_normals, float* v_means, float* v_quats,
+                                  float* v_scales, hgsr_stream_t stream) {
+    int st = check_common(C, N, means, quats, scales, viewmats, Ks, width, height);
+    if (st) return st;
+    HGSR_REQUIRE(N == 0 || (radii && ray_transforms && v_means2d && v_depths && v_ray_transforms && v_normals &&
+                            v_means && v_quats && v_scales),
+                 "null pointer");
+    if (N == 0) return HGSR_OK;
+    hipLaunchKernelGGL(project2d_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, as_stream(stream), C, N,
+                       means, reinterpret_cast<const float4*>(quats), scales, viewmats, Ks, radii,
+                       ray_transforms, reinterpret_cast<const float2*>(v_means2d), v_depths,
+                       v_ray_transforms, v_normals, v_means, reinterpret_cast<float4*>(v_quats), v_scales);
+    return check_launch("project2d_bwd");
+}

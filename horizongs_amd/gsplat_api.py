@@ -1,0 +1,565 @@
+"""gsplat-compatible call surface backed by the hgsr HIP kernels.
+
+Mirrors the gsplat (< 1.5, FantasticOven2 2DGS fork) functions that Horizon-GS
+calls, so reference gaussian_renderer/render.py runs unchanged through the
+`gsplat` alias package:
+
+  * rasterization()              render.py:40-54  (3DGS, packed=False)
+  * rasterization_2dgs()         render.py:62-76  (2DGS, nested 6-tuple return)
+  * fully_fused_projection()     render.py:149-165 (anchor prefilter)
+  * fully_fused_projection_2dgs() render.py:171-186 (fork signature with densifications)
+plus the lower-level ops gsplat exposes (isect_tiles, isect_offset_encode,
+rasterize_to_pixels[_2dgs], spherical_harmonics).
+
+Argument meaning, shapes, defaults and the returned meta dict follow gsplat;
+unsupported options (packed=True, antialiased mode, covars, tile masks,
+non-pinhole cameras, sparse grads, distributed) raise NotImplementedError
+rather than silently diverging.  Errors from the native layer surface as
+RuntimeError, as gsplat's TORCH_CHECKs do.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import _native as N
+from ._native import ptr
+
+_MAX_CH = 4  # channels per raster kernel call
+
+
+def _f32(t):
+    return t.contiguous() if t.dtype == torch.float32 else t.float().contiguous()
+
+
+def _check_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("hgsr: inputs must be HIP device tensors (no CPU fallback)")
+
+
+def _unsupported(flag, what):
+    if flag:
+        raise NotImplementedError(f"hgsr: {what} is not supported (Horizon-GS never requests it)")
+
+
+# =========================================================================
+# projection
+# =========================================================================
+class _Project3D(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means, quats, scales, viewmats, Ks, width, height, eps2d, near_plane, far_plane,
+                radius_clip):
+        C, Ng = viewmats.shape[0], means.shape[0]
+        dev = means.device
+        radii = torch.empty((C, Ng), dtype=torch.int32, device=dev)
+        means2d = torch.empty((C, Ng, 2), dtype=torch.float32, device=dev)
+        depths = torch.empty((C, Ng), dtype=torch.float32, device=dev)
+        conics = torch.empty((C, Ng, 3), dtype=torch.float32, device=dev)
+        N.call("hgsr_project3d_fwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks),
+               width, height, eps2d, near_plane, far_plane, radius_clip, ptr(radii), ptr(means2d), ptr(depths),
+               ptr(conics), N.stream(dev))
+        ctx.save_for_backward(means, quats, scales, viewmats, Ks, radii, conics)
+        ctx.cfg = (width, height, eps2d)
+        ctx.mark_non_differentiable(radii)
+        return radii, means2d, depths, conics
+
+    @staticmethod
+    def backward(ctx, v_radii, v_means2d, v_depths, v_conics):
+        means, quats, scales, viewmats, Ks, radii, conics = ctx.saved_tensors
+        width, height, eps2d = ctx.cfg
+        C, Ng = viewmats.shape[0], means.shape[0]
+        v_means = torch.zeros_like(means)
+        v_quats = torch.zeros_like(quats)
+        v_scales = torch.zeros_like(scales)
+        N.call("hgsr_project3d_bwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks), width,
+               height, eps2d, ptr(radii), ptr(conics), ptr(_f32(v_means2d)), ptr(_f32(v_depths)),
+               ptr(_f32(v_conics)), ptr(v_means), ptr(v_quats), ptr(v_scales), N.stream(means.device))
+        if ctx.needs_input_grad[3]:
+            raise NotImplementedError("hgsr: gradients w.r.t. viewmats are not supported")
+        return v_means, v_quats, v_scales, None, None, None, None, None, None, None, None
+
+
+def fully_fused_projection(means, covars, quats, scales, viewmats, Ks, width, height, eps2d=0.3,
+                           packed=False, near_plane=0.01, far_plane=1e10, radius_clip=0.0,
+                           sparse_grad=False, calc_compensations=False, camera_model="pinhole"):
+    """gsplat.cuda._wrapper.fully_fused_projection -> (radii, means2d, depths, conics, compensations)."""
+    _unsupported(covars is not None, "covars input")
+    _unsupported(packed, "packed=True")
+    _unsupported(sparse_grad, "sparse_grad")
+    _unsupported(calc_compensations, "calc_compensations")
+    _unsupported(camera_model != "pinhole", f"camera_model={camera_model}")
+    _check_cuda(means, quats, scales, viewmats, Ks)
+    Ng = means.shape[0]
+    assert means.shape == (Ng, 3) and quats.shape == (Ng, 4) and scales.shape == (Ng, 3), "bad Gaussian shapes"
+    assert viewmats.dim() == 3 and viewmats.shape[1:] == (4, 4) and Ks.shape == (viewmats.shape[0], 3, 3)
+    radii, means2d, depths, conics = _Project3D.apply(
+        _f32(means), _f32(quats), _f32(scales), _f32(viewmats), _f32(Ks), int(width), int(height),
+        float(eps2d), float(near_plane), float(far_plane), float(radius_clip))
+    return radii, means2d, depths, conics, None
+
+
+class _Project2D(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means, quats, scales, viewmats, Ks, width, height, near_plane, far_plane, radius_clip):
+        C, Ng = viewmats.shape[0], means.shape[0]
+        dev = means.device
+        radii = torch.empty((C, Ng), dtype=torch.int32, device=dev)
+        means2d = torch.empty((C, Ng, 2), dtype=torch.float32, device=dev)
+        depths = torch.empty((C, Ng), dtype=torch.float32, device=dev)
+        rt = torch.empty((C, Ng, 3, 3), dtype=torch.float32, device=dev)
+        normals = torch.empty((C, Ng, 3), dtype=torch.float32, device=dev)
+        N.call("hgsr_project2d_fwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks),
+               width, height, near_plane, far_plane, radius_clip, ptr(radii), ptr(means2d), ptr(depths), ptr(rt),
+               ptr(normals), N.stream(dev))
+        ctx.save_for_backward(means, quats, scales, viewmats, Ks, radii, rt)
+        ctx.cfg = (width, height)
+        ctx.mark_non_differentiable(radii)
+        return radii, means2d, depths, rt, normals
+
+    @staticmethod
+    def backward(ctx, v_radii, v_means2d, v_depths, v_rt, v_normals):
+        means, quats, scales, viewmats, Ks, radii, rt = ctx.saved_tensors
+        width, height = ctx.cfg
+        C, Ng = viewmats.shape[0], means.shape[0]
+        v_means = torch.zeros_like(means)
+        v_quats = torch.zeros_like(quats)
+        v_scales = torch.zeros_like(scales)
+        N.call("hgsr_project2d_bwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks), width,
+               height, ptr(radii), ptr(rt), ptr(_f32(v_means2d)), ptr(_f32(v_depths)), ptr(_f32(v_rt)),
+               ptr(_f32(v_normals)), ptr(v_means), ptr(v_quats), ptr(v_scales), N.stream(means.device))
+        if ctx.needs_input_grad[3]:
+            raise NotImplementedError("hgsr: gradients w.r.t. viewmats are not supported")
+        return v_means, v_quats, v_scales, None, None, None, None, None, None, None
+
+
+def fully_fused_projection_2dgs(means, quats, scales, viewmats, densifications, Ks, width, height, eps2d=0.3,
+                                packed=False, near_plane=0.01, far_plane=1e10, radius_clip=0.0,
+                                sparse_grad=False):
+    """Fork signature (render.py:171-186): (..., viewmats, densifications, Ks, ...) ->
+    (radii, means2d, depths, ray_transforms, normals).  `densifications` [C,N,2] (zeros)
+    only carries the densification-gradient proxy; the projection values ignore it."""
+    _unsupported(packed, "packed=True")
+    _unsupported(sparse_grad, "sparse_grad")
+    _check_cuda(means, quats, scales, viewmats, Ks)
+    Ng = means.shape[0]
+    assert means.shape == (Ng, 3) and quats.shape == (Ng, 4) and scales.shape == (Ng, 3), "bad Gaussian shapes"
+    return _Project2D.apply(_f32(means), _f32(quats), _f32(scales), _f32(viewmats), _f32(Ks), int(width),
+                            int(height), float(near_plane), float(far_plane), float(radius_clip))
+
+
+# =========================================================================
+# spherical harmonics
+# =========================================================================
+class _SH(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, degree, dirs, coeffs, masks):
+        n = dirs.shape[0]
+        K = coeffs.shape[1]
+        colors = torch.empty((n, 3), dtype=torch.float32, device=dirs.device)
+        N.call("hgsr_sh_fwd", degree, K, n, ptr(dirs), ptr(coeffs), ptr(masks), ptr(colors), N.stream(dirs.device))
+        ctx.save_for_backward(dirs, coeffs, masks)
+        ctx.degree = degree
+        return colors
+
+    @staticmethod
+    def backward(ctx, v_colors):
+        dirs, coeffs, masks = ctx.saved_tensors
+        n, K = coeffs.shape[0], coeffs.shape[1]
+        v_coeffs = torch.empty_like(coeffs)
+        v_dirs = torch.zeros_like(dirs) if ctx.needs_input_grad[1] else None
+        N.call("hgsr_sh_bwd", ctx.degree, K, n, ptr(dirs), ptr(coeffs), ptr(masks), ptr(_f32(v_colors)),
+               ptr(v_coeffs), ptr(v_dirs), N.stream(dirs.device))
+        return None, v_dirs, v_coeffs, None
+
+
+def spherical_harmonics(degrees_to_use: int, dirs: torch.Tensor, coeffs: torch.Tensor,
+                        masks: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """gsplat spherical_harmonics: dirs [..., 3], coeffs [..., K, 3] -> colors [..., 3] (degree <= 3)."""
+    _check_cuda(dirs, coeffs)
+    assert coeffs.shape[-1] == 3 and dirs.shape[-1] == 3
+    K = coeffs.shape[-2]
+    assert (degrees_to_use + 1) ** 2 <= K, "not enough SH coefficients"
+    batch = dirs.shape[:-1]
+    d = _f32(dirs.reshape(-1, 3))
+    c = _f32(coeffs.reshape(-1, K, 3))
+    m = None if masks is None else masks.reshape(-1).to(torch.uint8).contiguous()
+    out = _SH.apply(int(degrees_to_use), d, c, m)
+    return out.reshape(batch + (3,))
+
+
+# =========================================================================
+# tile intersection
+# =========================================================================
+def _tile_grid(width, height, tile_size):
+    return math.ceil(width / tile_size), math.ceil(height / tile_size)
+
+
+@torch.no_grad()
+def _isect_binned(means2d, radii, tile_size, tile_width, tile_height, depths):
+    """Binned tile intersection: (tiles_per_gauss, isect_ids, flatten_ids, isect_offsets)."""
+    C, Ng = radii.shape
+    dev = means2d.device
+    m2 = _f32(means2d.detach())
+    dep = _f32(depths.detach())
+    radii = radii.contiguous()
+    tpg = torch.empty((C, Ng), dtype=torch.int32, device=dev)
+    offsets = torch.empty((C, tile_height, tile_width), dtype=torch.int32, device=dev)
+    info = torch.empty(2, dtype=torch.int64, device=dev)
+    ws1_b = N.size_query("hgsr_isect_ws1_bytes", C, Ng, tile_width, tile_height)
+    ws1 = torch.empty(max(ws1_b, 1), dtype=torch.uint8, device=dev)
+    s = N.stream(dev)
+    N.call("hgsr_isect_count", C, Ng, ptr(m2), ptr(radii), tile_size, tile_width, tile_height, ptr(tpg),
+           ptr(offsets), ptr(info), ptr(ws1), ws1_b, s)
+    n_isects, max_bin = (int(v) for v in info.cpu().tolist())  # the one host sync (gsplat has it too)
+    isect_ids = torch.empty(n_isects, dtype=torch.int64, device=dev)
+    flatten_ids = torch.empty(n_isects, dtype=torch.int32, device=dev)
+    if n_isects > 0:
+        ws2_b = N.size_query("hgsr_isect_ws2_bytes", n_isects, max_bin)
+        ws2 = torch.empty(ws2_b, dtype=torch.uint8, device=dev)
+        N.call("hgsr_isect_emit_sorted", C, Ng, ptr(m2), ptr(radii), ptr(dep), tile_size, tile_width,
+               tile_height, ptr(offsets), n_isects, max_bin, ptr(isect_ids), ptr(flatten_ids), ptr(ws1), ws1_b,
+               ptr(ws2), ws2_b, s)
+    return tpg, isect_ids, flatten_ids, offsets
+
+
+@torch.no_grad()
+def isect_tiles(means2d, radii, depths, tile_size, tile_width, tile_height, sort=True, packed=False,
+                n_cameras=None, camera_ids=None, gaussian_ids=None):
+    """gsplat isect_tiles (non-packed) -> (tiles_per_gauss [C,N], isect_ids [I], flatten_ids [I])."""
+    _unsupported(packed, "packed=True")
+    _check_cuda(means2d, radii, depths)
+    if sort:
+        tpg, ids, fl, _ = _isect_binned(means2d, radii, int(tile_size), int(tile_width), int(tile_height), depths)
+        return tpg, ids, fl
+    C, Ng = radii.shape
+    dev = means2d.device
+    m2, dep, radii = _f32(means2d.detach()), _f32(depths.detach()), radii.contiguous()
+    tpg, _, _, _ = _isect_binned(m2, radii, int(tile_size), int(tile_width), int(tile_height), dep)
+    cum = torch.cumsum(tpg.reshape(-1).to(torch.int64), 0)
+    n = int(cum[-1].item()) if cum.numel() else 0
+    ids = torch.empty(n, dtype=torch.int64, device=dev)
+    fl = torch.empty(n, dtype=torch.int32, device=dev)
+    if n:
+        N.call("hgsr_isect_emit_unsorted", C, Ng, ptr(m2), ptr(radii), ptr(dep), int(tile_size), int(tile_width),
+               int(tile_height), ptr(cum), ptr(ids), ptr(fl), N.stream(dev))
+    return tpg, ids, fl
+
+
+@torch.no_grad()
+def isect_offset_encode(isect_ids, n_cameras, tile_width, tile_height):
+    """gsplat isect_offset_encode -> offsets [C, tile_height, tile_width] int32."""
+    _check_cuda(isect_ids)
+    out = torch.empty((n_cameras, tile_height, tile_width), dtype=torch.int32, device=isect_ids.device)
+    ids = isect_ids.contiguous()
+    N.call("hgsr_isect_offset_encode", ids.numel(), ptr(ids) if ids.numel() else None, int(n_cameras),
+           int(tile_width), int(tile_height), ptr(out), N.stream(isect_ids.device))
+    return out
+
+
+# =========================================================================
+# rasterization (3DGS)
+# =========================================================================
+class _Raster3D(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means2d, conics, colors, opacities, backgrounds, width, height, tile_size, isect_offsets,
+                flatten_ids, absgrad):
+        C = isect_offsets.shape[0]
+        Ng = means2d.shape[1]
+        D = colors.shape[-1]
+        th, tw = isect_offsets.shape[1:]
+        dev = means2d.device
+        rc = torch.empty((C, height, width, D), dtype=torch.float32, device=dev)
+        ra = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
+        last = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        N.call("hgsr_raster3d_fwd", C, Ng, D, ptr(means2d), ptr(conics), ptr(colors), ptr(opacities),
+               ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
+               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), N.stream(dev))
+        ctx.save_for_backward(means2d, conics, colors, opacities, backgrounds, isect_offsets, flatten_ids, ra, last)
+        ctx.cfg = (width, height, tile_size, absgrad)
+        return rc, ra
+
+    @staticmethod
+    def backward(ctx, v_rc, v_ra):
+        means2d, conics, colors, opacities, backgrounds, offsets, flatten_ids, ra, last = ctx.saved_tensors
+        width, height, tile_size, absgrad = ctx.cfg
+        C, Ng, D = means2d.shape[0], means2d.shape[1], colors.shape[-1]
+        th, tw = offsets.shape[1:]
+        dev = means2d.device
+        v_means2d = torch.zeros_like(means2d)
+        v_conics = torch.zeros_like(conics)
+        v_colors = torch.zeros_like(colors)
+        v_opac = torch.zeros_like(opacities)
+        v_abs = torch.zeros_like(means2d) if absgrad else None
+        ws_b = N.size_query("hgsr_raster3d_bwd_ws_bytes", C, Ng, D)
+        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+        v_rc = _f32(v_rc)
+        v_ra = _f32(v_ra)
+        N.call("hgsr_raster3d_bwd", C, Ng, D, ptr(means2d), ptr(conics), ptr(colors), ptr(opacities),
+               ptr(backgrounds), width, height, tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
+               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
+               ptr(v_means2d), ptr(v_conics), ptr(v_colors), ptr(v_opac), ptr(v_abs), ptr(ws), ws_b, N.stream(dev))
+        if absgrad:
+            means2d.absgrad = v_abs
+        v_bg = None
+        if backgrounds is not None and ctx.needs_input_grad[4]:
+            v_bg = (v_rc * (1.0 - ra)).sum(dim=(1, 2))
+        return v_means2d, v_conics, v_colors, v_opac, v_bg, None, None, None, None, None, None
+
+
+def rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_height, tile_size, isect_offsets,
+                        flatten_ids, backgrounds=None, masks=None, packed=False, absgrad=False):
+    """gsplat rasterize_to_pixels (non-packed): colors [C,N,D] -> (render_colors [C,H,W,D], alphas [C,H,W,1])."""
+    _unsupported(masks is not None, "tile masks")
+    _unsupported(packed, "packed=True")
+    _check_cuda(means2d, conics, colors, opacities, isect_offsets, flatten_ids)
+    C, Ng = means2d.shape[:2]
+    D = colors.shape[-1]
+    assert colors.shape[:2] == (C, Ng) and opacities.shape == (C, Ng)
+    args = (_f32(means2d), _f32(conics), None, _f32(opacities))
+    outs, alphas = [], None
+    for c0 in range(0, D, _MAX_CH):
+        c1 = min(D, c0 + _MAX_CH)
+        col = _f32(colors[..., c0:c1])
+        bg = None if backgrounds is None else _f32(backgrounds[..., c0:c1])
+        rc, ra = _Raster3D.apply(args[0], args[1], col, args[3], bg, int(image_width), int(image_height),
+                                 int(tile_size), isect_offsets.contiguous(), flatten_ids.contiguous(), absgrad)
+        outs.append(rc)
+        if alphas is None:
+            alphas = ra
+    render_colors = outs[0] if len(outs) == 1 else torch.cat(outs, dim=-1)
+    return render_colors, alphas
+
+
+# =========================================================================
+# rasterization (2DGS)
+# =========================================================================
+class _Raster2D(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means2d, rt, colors, opacities, normals, densify, backgrounds, width, height, tile_size,
+                isect_offsets, flatten_ids):
+        C = isect_offsets.shape[0]
+        Ng = means2d.shape[1]
+        D = colors.shape[-1]
+        th, tw = isect_offsets.shape[1:]
+        dev = means2d.device
+        rc = torch.empty((C, height, width, D), dtype=torch.float32, device=dev)
+        ra = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
+        rn = torch.empty((C, height, width, 3), dtype=torch.float32, device=dev)
+        rd = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
+        rm = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
+        last = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        med = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        N.call("hgsr_raster2d_fwd", C, Ng, D, ptr(means2d), ptr(rt), ptr(colors), ptr(opacities), ptr(normals),
+               ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
+               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(rn), ptr(rd), ptr(rm),
+               ptr(last), ptr(med), N.stream(dev))
+        ctx.save_for_backward(means2d, rt, colors, opacities, normals, backgrounds, isect_offsets, flatten_ids,
+                              ra, last)
+        ctx.cfg = (width, height, tile_size)
+        ctx.mark_non_differentiable(rd, rm)
+        return rc, ra, rn, rd, rm
+
+    @staticmethod
+    def backward(ctx, v_rc, v_ra, v_rn, v_rd, v_rm):
+        means2d, rt, colors, opacities, normals, backgrounds, offsets, flatten_ids, ra, last = ctx.saved_tensors
+        width, height, tile_size = ctx.cfg
+        C, Ng, D = means2d.shape[0], means2d.shape[1], colors.shape[-1]
+        th, tw = offsets.shape[1:]
+        dev = means2d.device
+        v_means2d = torch.zeros_like(means2d)
+        v_rt = torch.zeros_like(rt)
+        v_colors = torch.zeros_like(colors)
+        v_opac = torch.zeros_like(opacities)
+        v_normals = torch.zeros_like(normals)
+        v_dens = torch.zeros_like(means2d)
+        ws_b = N.size_query("hgsr_raster2d_bwd_ws_bytes", C, Ng, D)
+        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+        v_rc, v_ra, v_rn = _f32(v_rc), _f32(v_ra), _f32(v_rn)
+        N.call("hgsr_raster2d_bwd", C, Ng, D, ptr(means2d), ptr(rt), ptr(colors), ptr(opacities), ptr(normals),
+               ptr(backgrounds), width, height, tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
+               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
+               ptr(v_rn), ptr(v_means2d), ptr(v_rt), ptr(v_colors), ptr(v_opac), ptr(v_normals), ptr(v_dens),
+               ptr(ws), ws_b, N.stream(dev))
+        v_bg = None
+        if backgrounds is not None and ctx.needs_input_grad[6]:
+            v_bg = (v_rc * (1.0 - ra)).sum(dim=(1, 2))
+        return v_means2d, v_rt, v_colors, v_opac, v_normals, v_dens, v_bg, None, None, None, None, None
+
+
+def rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals, densify, image_width,
+                             image_height, tile_size, isect_offsets, flatten_ids, backgrounds=None, masks=None,
+                             packed=False, absgrad=False, distloss=False):
+    """gsplat rasterize_to_pixels_2dgs -> (colors, alphas, normals, distort, median).
+
+    The last colour channel must be the depth (RGB+ED/RGB+D).  The distortion
+    map is computed but, as in gsplat with distloss=False, not differentiated."""
+    _unsupported(masks is not None, "tile masks")
+    _unsupported(packed, "packed=True")
+    _unsupported(absgrad, "absgrad for 2DGS")
+    _unsupported(distloss, "distloss backward")
+    _check_cuda(means2d, ray_transforms, colors, opacities, normals, isect_offsets, flatten_ids)
+    C, Ng = means2d.shape[:2]
+    D = colors.shape[-1]
+    if D > _MAX_CH:
+        raise NotImplementedError("hgsr: 2DGS rasterization supports at most 4 channels (RGB+depth)")
+    if densify is None:
+        densify = torch.zeros_like(means2d)
+    rc, ra, rn, rd, rm = _Raster2D.apply(
+        _f32(means2d), _f32(ray_transforms.reshape(C, Ng, 9)), _f32(colors), _f32(opacities), _f32(normals),
+        densify, None if backgrounds is None else _f32(backgrounds), int(image_width), int(image_height),
+        int(tile_size), isect_offsets.contiguous(), flatten_ids.contiguous())
+    return rc, ra, rn, rd, rm
+
+
+# =========================================================================
+# high-level entry points
+# =========================================================================
+def _camera_centers(viewmats):
+    # c2w translation of a rigid world->camera transform: -R^T t
+    R = viewmats[:, :3, :3]
+    t = viewmats[:, :3, 3]
+    return -(R.transpose(1, 2) @ t[..., None])[..., 0]
+
+
+def _colors_for_raster(means, colors, viewmats, radii, sh_degree, C):
+    if sh_degree is None:
+        if colors.dim() == 2:
+            return colors.expand(C, -1, -1)
+        return colors
+    campos = _camera_centers(viewmats)
+    dirs = means[None, :, :] - campos[:, None, :]
+    shs = colors.expand(C, -1, -1, -1) if colors.dim() == 3 else colors
+    out = spherical_harmonics(sh_degree, dirs, shs, masks=radii > 0)
+    return torch.clamp_min(out + 0.5, 0.0)
+
+
+def _with_depth(colors, backgrounds, depths, render_mode, C):
+    if render_mode in ("RGB+D", "RGB+ED"):
+        colors = torch.cat((colors, depths[..., None]), dim=-1)
+        if backgrounds is not None:
+            backgrounds = torch.cat([backgrounds, torch.zeros(C, 1, device=backgrounds.device)], dim=-1)
+    elif render_mode in ("D", "ED"):
+        colors = depths[..., None]
+        if backgrounds is not None:
+            backgrounds = torch.zeros(C, 1, device=backgrounds.device)
+    return colors, backgrounds
+
+
+def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, height, near_plane=0.01,
+                  far_plane=1e10, radius_clip=0.0, eps2d=0.3, sh_degree=None, packed=True, tile_size=16,
+                  backgrounds=None, render_mode="RGB", sparse_grad=False, absgrad=False,
+                  rasterize_mode="classic", channel_chunk=32, distributed=False, camera_model="pinhole",
+                  covars=None):
+    """gsplat.rasterization (3DGS) -> (render_colors [C,H,W,D], render_alphas [C,H,W,1], meta)."""
+    assert render_mode in ("RGB", "D", "ED", "RGB+D", "RGB+ED"), render_mode
+    _unsupported(packed, "packed=True (pass packed=False as Horizon-GS does)")
+    _unsupported(rasterize_mode != "classic", f"rasterize_mode={rasterize_mode}")
+    _unsupported(distributed, "distributed=True")
+    C = viewmats.shape[0]
+    radii, means2d, depths, conics, _ = fully_fused_projection(
+        means, covars, quats, scales, viewmats, Ks, width, height, eps2d=eps2d, packed=False,
+        near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip, sparse_grad=sparse_grad,
+        calc_compensations=False, camera_model=camera_model)
+    opac = opacities.repeat(C, 1)
+    cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
+    cols, bgs = _with_depth(cols, backgrounds, depths, render_mode, C)
+    tw, th = _tile_grid(width, height, tile_size)
+    tpg, isect_ids, flatten_ids, isect_offsets = _isect_binned(means2d, radii, int(tile_size), tw, th, depths)
+    render_colors, render_alphas = rasterize_to_pixels(
+        means2d, conics, cols, opac, width, height, tile_size, isect_offsets, flatten_ids, backgrounds=bgs,
+        absgrad=absgrad)
+    if render_mode in ("ED", "RGB+ED"):
+        render_colors = torch.cat([render_colors[..., :-1],
+                                   render_colors[..., -1:] / render_alphas.clamp(min=1e-10)], dim=-1)
+    meta = {
+        "camera_ids": None, "gaussian_ids": None, "radii": radii, "means2d": means2d, "depths": depths,
+        "conics": conics, "opacities": opac, "tile_width": tw, "tile_height": th,
+        "tiles_per_gauss": tpg, "isect_ids": isect_ids, "flatten_ids": flatten_ids,
+        "isect_offsets": isect_offsets, "width": width, "height": height, "tile_size": tile_size,
+        "n_cameras": C,
+    }
+    return render_colors, render_alphas, meta
+
+
+def _depth_to_points(depths, camtoworlds, Ks, z_depth=True):
+    height, width = depths.shape[-3:-1]
+    dev = depths.device
+    x, y = torch.meshgrid(torch.arange(width, device=dev), torch.arange(height, device=dev), indexing="xy")
+    fx, fy, cx, cy = Ks[..., 0, 0], Ks[..., 1, 1], Ks[..., 0, 2], Ks[..., 1, 2]
+    camera_dirs = F.pad(torch.stack([(x - cx[..., None, None] + 0.5) / fx[..., None, None],
+                                     (y - cy[..., None, None] + 0.5) / fy[..., None, None]], dim=-1),
+                        (0, 1), value=1.0)
+    directions = torch.einsum("...ij,...hwj->...hwi", camtoworlds[..., :3, :3], camera_dirs)
+    origins = camtoworlds[..., :3, -1]
+    if not z_depth:
+        directions = F.normalize(directions, dim=-1)
+    return origins[..., None, None, :] + depths * directions
+
+
+def depth_to_normal(depths, camtoworlds, Ks, z_depth=True):
+    """K13: central-difference normals of the unprojected depth map [C,H,W,1] -> [C,H,W,3]."""
+    points = _depth_to_points(depths, camtoworlds, Ks, z_depth=z_depth)
+    dx = points[..., 2:, 1:-1, :] - points[..., :-2, 1:-1, :]
+    dy = points[..., 1:-1, 2:, :] - points[..., 1:-1, :-2, :]
+    normals = F.normalize(torch.cross(dx, dy, dim=-1), dim=-1)
+    return F.pad(normals, (0, 0, 1, 1, 1, 1), value=0.0)
+
+
+def _camtoworlds(viewmats):
+    R = viewmats[:, :3, :3]
+    t = viewmats[:, :3, 3]
+    c2w = torch.zeros_like(viewmats)
+    c2w[:, :3, :3] = R.transpose(1, 2)
+    c2w[:, :3, 3] = -(R.transpose(1, 2) @ t[..., None])[..., 0]
+    c2w[:, 3, 3] = 1.0
+    return c2w
+
+
+def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, width, height, near_plane=0.01,
+                       far_plane=1e10, radius_clip=0.0, eps2d=0.3, sh_degree=None, packed=False, tile_size=16,
+                       backgrounds=None, render_mode="RGB", sparse_grad=False, absgrad=False, distloss=False,
+                       depth_mode="expected"):
+    """gsplat.rasterization_2dgs in the fork's nesting (render.py:56-76):
+    ((colors, alphas, normals, normals_from_depth, distort, median), meta).
+
+    Decisions where the fork is unverifiable here: rendered normals
+    and depth normals are in world frame; normals_from_depth uses the expected
+    (or, depth_mode="median", the median) depth; means2d's gradient is the exact
+    chain-rule gradient and the densification proxy goes to meta["gradient_2dgs"].grad."""
+    assert render_mode in ("RGB", "D", "ED", "RGB+D", "RGB+ED"), render_mode
+    _unsupported(packed, "packed=True")
+    C, Ng = viewmats.shape[0], means.shape[0]
+    densifications = torch.zeros((C, Ng, 2), dtype=means.dtype, device=means.device, requires_grad=True)
+    radii, means2d, depths, ray_transforms, normals = fully_fused_projection_2dgs(
+        means, quats, scales, viewmats, densifications, Ks, width, height, eps2d=eps2d, packed=False,
+        near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip, sparse_grad=sparse_grad)
+    opac = opacities.repeat(C, 1)
+    cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
+    cols, bgs = _with_depth(cols, backgrounds, depths, render_mode, C)
+    tw, th = _tile_grid(width, height, tile_size)
+    tpg, isect_ids, flatten_ids, isect_offsets = _isect_binned(means2d, radii, int(tile_size), tw, th, depths)
+    render_colors, render_alphas, render_normals, render_distort, render_median = rasterize_to_pixels_2dgs(
+        means2d, ray_transforms, cols, opac, normals, densifications, width, height, tile_size, isect_offsets,
+        flatten_ids, backgrounds=bgs, absgrad=absgrad, distloss=distloss)
+    if render_mode in ("ED", "RGB+ED"):
+        render_colors = torch.cat([render_colors[..., :-1],
+                                   render_colors[..., -1:] / render_alphas.clamp(min=1e-10)], dim=-1)
+    c2w = _camtoworlds(viewmats)
+    render_normals_from_depth = None
+    if render_mode in ("RGB+ED", "RGB+D"):
+        dmap = render_median if depth_mode == "median" else render_colors[..., -1:]
+        render_normals_from_depth = depth_to_normal(dmap, c2w, Ks)
+    render_normals = torch.einsum("cij,chwj->chwi", c2w[:, :3, :3], render_normals)
+    meta = {
+        "camera_ids": None, "gaussian_ids": None, "radii": radii, "means2d": means2d, "depths": depths,
+        "ray_transforms": ray_transforms, "normals": normals, "opacities": opac, "tile_width": tw,
+        "tile_height": th, "tiles_per_gauss": tpg, "isect_ids": isect_ids, "flatten_ids": flatten_ids,
+        "isect_offsets": isect_offsets, "width": width, "height": height, "tile_size": tile_size,
+        "n_cameras": C, "gradient_2dgs": densifications,
+    }
+    return (render_colors, render_alphas, render_normals, render_normals_from_depth, render_distort,
+            render_median), meta

@@ -1,0 +1,183 @@
+/*
+ * hgsr.h — C ABI of the MI355X (gfx950) differentiable Gaussian rasterizer.
+ *
+ * This is the drop-in boundary for the hot path that Horizon-GS reaches through
+ * gsplat (reference gaussian_renderer/render.py:13-14, :40-76, :149-186).  Each
+ * entry replaces one gsplat CUDA-extension op; the gsplat-compatible Python
+ * surface (horizongs_amd/gsplat_api.py, re-exported by the `gsplat` alias
+ * package) binds them with ctypes.
+ *
+ * Conventions (all entries):
+ *   - every pointer is a DEVICE pointer to row-major contiguous memory, allocated
+ *     by the caller (the library never allocates); fp32 data, int32 ids/radii,
+ *     int64 intersection keys;
+ *   - gradient outputs are zero-initialised by the caller and ACCUMULATED into;
+ *   - work is enqueued on `stream` (a hipStream_t; NULL = default stream) and the
+ *     call returns without synchronising;
+ *   - return 0 (HGSR_OK) or a negative status; hgsr_last_error() then holds a
+ *     thread-local message.  Data values are not validated (NaN propagates).
+ *   - C = cameras, N = Gaussians; per-camera arrays are [C, N, ...]; "flatten ids"
+ *     index the [C*N] flattened arrays (gsplat non-packed mode).
+ */
+#ifndef HGSR_H
+#define HGSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* hgsr_stream_t; /* hipStream_t */
+
+enum {
+    HGSR_OK = 0,
+    HGSR_EINVAL = -1,     /* bad dimensions / unsupported option / null pointer */
+    HGSR_ELAUNCH = -2,    /* kernel launch failed */
+    HGSR_EWORKSPACE = -3  /* workspace too small */
+};
+
+int hgsr_version(void);
+const char* hgsr_last_error(void);
+
+/* ---- K1/K2: 3DGS EWA projection ----------------------------------------
+ * replaces gsplat.cuda._wrapper.fully_fused_projection (packed=False), called at
+ * reference gaussian_renderer/render.py:149-165 and inside gsplat.rasterization
+ * (render.py:40-54).  Outputs [C,N] radii (0 = culled), means2d [C,N,2],
+ * depths [C,N], conics [C,N,3].  Optionally (tile_counts != NULL) nothing else. */
+int hgsr_project3d_fwd(int C, int N, const float* means, const float* quats,
+                       const float* scales, const float* viewmats, const float* Ks,
+                       int width, int height, float eps2d, float near_plane,
+                       float far_plane, float radius_clip, int32_t* radii, float* means2d,
+                       float* depths, float* conics, hgsr_stream_t stream);
+
+/* vjp of the above: accumulates v_means [N,3], v_quats [N,4], v_scales [N,3]. */
+int hgsr_project3d_bwd(int C, int N, const float* means, const float* quats,
+                       const float* scales, const float* viewmats, const float* Ks,
+                       int width, int height, float eps2d, const int32_t* radii,
+                       const float* conics, const float* v_means2d, const float* v_depths,
+                       const float* v_conics, float* v_means, float* v_quats, float* v_scales,
+                       hgsr_stream_t stream);
+
+/* ---- K1'/K10: 2DGS surfel projection -------------------------------------
+ * replaces fully_fused_projection_2dgs (render.py:171-186 and inside
+ * gsplat.rasterization_2dgs).  Outputs radii, means2d, depths,
+ * ray_transforms [C,N,3,3] (row-major K*[R*Rq*diag(sx,sy,1) | t]) and
+ * camera-facing normals [C,N,3]. */
+int hgsr_project2d_fwd(int C, int N, const float* means, const float* quats,
+                       const float* scales, const float* viewmats, const float* Ks,
+                       int width, int height, float near_plane, float far_plane,
+                       float radius_clip, int32_t* radii, float* means2d, float* depths,
+                       float* ray_transforms, float* normals, hgsr_stream_t stream);
+
+int hgsr_project2d_bwd(int C, int N, const float* means, const float* quats,
+                       const float* scales, const float* viewmats, const float* Ks,
+                       int width, int height, const int32_t* radii,
+                       const float* ray_transforms, const float* v_means2d,
+                       const float* v_depths, const float* v_ray_transforms,
+                       const float* v_normals, float* v_means, float* v_quats,
+                       float* v_scales, hgsr_stream_t stream);
+
+/* ---- K3: spherical-harmonics colour --------------------------------------
+ * replaces gsplat spherical_harmonics (used by rasterization when sh_degree is
+ * not None; SH2 configs).  dirs [n,3] (unnormalised), coeffs [n,K,3],
+ * masks [n] (uint8, nullable) -> colors [n,3] (written).  Basis polynomials of
+ * reference utils/sh_utils.py:57-112, degree <= 3. */
+int hgsr_sh_fwd(int degree, int K, int64_t n, const float* dirs, const float* coeffs,
+                const uint8_t* masks, float* colors, hgsr_stream_t stream);
+/* writes v_coeffs [n,K,3]; accumulates v_dirs [n,3] (nullable). */
+int hgsr_sh_bwd(int degree, int K, int64_t n, const float* dirs, const float* coeffs,
+                const uint8_t* masks, const float* v_colors, float* v_coeffs, float* v_dirs,
+                hgsr_stream_t stream);
+
+/* ---- K5/K6/K7: tile intersection, sort, tile offsets ---------------------
+ * Replaces gsplat isect_tiles(sort=True) + cub DeviceRadixSort + isect_offset_encode
+ * with a tile-bucketed binning:
+ *   stage 1 (hgsr_isect_count): tile rectangle per Gaussian -> tiles_per_gauss
+ *     [C,N]; per-block tile histograms; isect_offsets [C, tile_h, tile_w]
+ *     (exclusive scan over (camera, tile) bins = gsplat isect_offset_encode);
+ *     `info` (device, 2 x int64) = {n_isects, largest bin}.
+ *   stage 2 (hgsr_isect_emit_sorted, after the host reads info[0]): scatter
+ *     (depth, id) keys into their bins and sort each bin; writes the SORTED
+ *     isect_ids [n_isects] (cam<<(32+tile_bits) | tile<<32 | depth bits) and
+ *     flatten_ids [n_isects], bit-identical to a stable radix sort of gsplat's
+ *     Gaussian-major emission.
+ * The same `ws1` must be passed to both stages. */
+size_t hgsr_isect_ws1_bytes(int C, int N, int tile_w, int tile_h);
+size_t hgsr_isect_ws2_bytes(int64_t n_isects, int64_t max_bin);
+int hgsr_isect_count(int C, int N, const float* means2d, const int32_t* radii, int tile_size,
+                     int tile_w, int tile_h, int32_t* tiles_per_gauss, int32_t* isect_offsets,
+                     int64_t* info, void* ws1, size_t ws1_bytes, hgsr_stream_t stream);
+int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const int32_t* radii,
+                           const float* depths, int tile_size, int tile_w, int tile_h,
+                           const int32_t* isect_offsets, int64_t n_isects, int64_t max_bin,
+                           int64_t* isect_ids, int32_t* flatten_ids, void* ws1,
+                           size_t ws1_bytes, void* ws2, size_t ws2_bytes,
+                           hgsr_stream_t stream);
+/* gsplat isect_tiles(sort=False): Gaussian-major emission; cum_tiles = inclusive
+ * prefix sum of tiles_per_gauss over the flattened [C*N]. */
+int hgsr_isect_emit_unsorted(int C, int N, const float* means2d, const int32_t* radii,
+                             const float* depths, int tile_size, int tile_w, int tile_h,
+                             const int64_t* cum_tiles, int64_t* isect_ids,
+                             int32_t* flatten_ids, hgsr_stream_t stream);
+/* gsplat isect_offset_encode on already-sorted ids -> offsets [C, tile_h, tile_w]. */
+int hgsr_isect_offset_encode(int64_t n_isects, const int64_t* isect_ids, int C, int tile_w,
+                             int tile_h, int32_t* offsets, hgsr_stream_t stream);
+
+/* ---- K8/K9: 3DGS tile rasterization ---------------------------------------
+ * replaces gsplat rasterize_to_pixels (packed=False, tile_size=16, D <= 4 per
+ * call; callers chunk wider channel counts).  colors [C*N, D], opacities [C*N],
+ * backgrounds [C, D] nullable.  Outputs render_colors [C,H,W,D],
+ * render_alphas [C,H,W,1], last_ids [C,H,W]. */
+int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, const float* conics,
+                      const float* colors, const float* opacities, const float* backgrounds,
+                      int width, int height, int tile_size, int tile_w, int tile_h,
+                      const int32_t* isect_offsets, int64_t n_isects,
+                      const int32_t* flatten_ids, float* render_colors, float* render_alphas,
+                      int32_t* last_ids, hgsr_stream_t stream);
+/* accumulates v_means2d [C*N,2], v_conics [C*N,3], v_colors [C*N,D],
+ * v_opacities [C*N]; v_means2d_abs nullable (gsplat absgrad).  ws: caller
+ * scratch of hgsr_raster3d_bwd_ws_bytes(). */
+size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D);
+int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, const float* conics,
+                      const float* colors, const float* opacities, const float* backgrounds,
+                      int width, int height, int tile_size, int tile_w, int tile_h,
+                      const int32_t* isect_offsets, int64_t n_isects,
+                      const int32_t* flatten_ids, const float* render_alphas,
+                      const int32_t* last_ids, const float* v_render_colors,
+                      const float* v_render_alphas, float* v_means2d, float* v_conics,
+                      float* v_colors, float* v_opacities, float* v_means2d_abs, void* ws,
+                      size_t ws_bytes, hgsr_stream_t stream);
+
+/* ---- K11/K12: 2DGS surfel rasterization -----------------------------------
+ * replaces gsplat rasterize_to_pixels_2dgs.  The LAST colour channel is the
+ * depth (render_mode RGB+ED / RGB+D) used for the median depth and distortion.
+ * Outputs colors [C,H,W,D], alphas [C,H,W,1], normals [C,H,W,3],
+ * distort [C,H,W,1], median [C,H,W,1], last_ids, median_ids [C,H,W]. */
+int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
+                      const float* colors, const float* opacities, const float* normals,
+                      const float* backgrounds, int width, int height, int tile_size,
+                      int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                      const int32_t* flatten_ids, float* render_colors, float* render_alphas,
+                      float* render_normals, float* render_distort, float* render_median,
+                      int32_t* last_ids, int32_t* median_ids, hgsr_stream_t stream);
+/* accumulates v_means2d [C*N,2], v_ray_transforms [C*N,9], v_colors [C*N,D],
+ * v_opacities [C*N], v_normals [C*N,3], v_densify [C*N,2] (d loss / d screen
+ * translation; nullable). */
+size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D);
+int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
+                      const float* colors, const float* opacities, const float* normals,
+                      const float* backgrounds, int width, int height, int tile_size,
+                      int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                      const int32_t* flatten_ids, const float* render_alphas,
+                      const int32_t* last_ids, const float* v_render_colors,
+                      const float* v_render_alphas, const float* v_render_normals,
+                      float* v_means2d, float* v_ray_transforms, float* v_colors,
+                      float* v_opacities, float* v_normals, float* v_densify, void* ws,
+                      size_t ws_bytes, hgsr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HGSR_H */
