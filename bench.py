@@ -1,0 +1,279 @@
+"""North-star benchmark: train-step views/s (fwd+bwd raster) @ 2M Gaussians / 1080p.
+
+One "step" = one training view through the rasterizer path Horizon-GS runs at
+train.py:150-206: gsplat.rasterization(..., packed=False, render_mode="RGB+ED")
+(projection -> tile binning + depth sort -> raster forward), an L1 photometric
+loss plus an alpha term, and loss.backward() (raster backward -> projection
+backward), on a synthetic c2 scene: 2,000,000 Gaussians at
+1920x1080, fp32, inputs resident in HBM.
+
+Multi-GPU: one process per GPU (torchrun); the path shards per chunk (reference
+preprocess/generate_chunks_config.py: one chunk per GPU, no collectives), so each
+rank renders its own seeded scene ("scaling": "weak"); with --mode ddp the ranks
+render different views of ONE scene and all-reduce the Gaussian gradients over
+RCCL after backward (the c5 data-parallel mode).
+
+Prints ONE JSON line (rank 0) with the metric, a roofline object for the dominant
+kernel (HIP-event timed live over the timed region) and a CPU baseline (the C
+oracle on a bounded sample, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from horizongs_amd import _native as NAT  # noqa: E402
+from horizongs_amd import gsplat_api as G  # noqa: E402
+from horizongs_amd.synthetic import make_scene  # noqa: E402
+
+METRIC = "train-step views/sec (fwd+bwd raster) @2M Gaussians/1080p; PSNR delta vs ref"
+FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0      # HBM3E spec
+FLOP_PER_PAIR = {"raster3d_fwd": 20.0, "raster3d_bwd": 60.0, "raster2d_fwd": 40.0, "raster2d_bwd": 120.0}
+KERNELS = ["project3d_fwd", "isect_count", "isect_emit", "tile_sort", "raster3d_fwd", "raster3d_bwd",
+           "project3d_bwd", "project2d_fwd", "raster2d_fwd", "raster2d_bwd", "project2d_bwd", "sh_fwd", "sh_bwd"]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=2_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--gs", choices=["3d", "2d"], default="3d")
+    ap.add_argument("--mode", choices=["chunk", "ddp"], default="chunk")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events (rocprof runs)")
+    return ap.parse_args()
+
+
+class Workload:
+    def __init__(self, args, rank, dev):
+        self.args = args
+        self.dev = dev
+        seed = rank if args.mode == "chunk" else 0
+        sc = make_scene(args.n, args.width, args.height, seed=seed)
+        self.sc = sc
+        self.means = sc.means.to(dev).requires_grad_(True)
+        self.quats = sc.quats.to(dev).requires_grad_(True)
+        self.scales = sc.scales.to(dev).requires_grad_(True)
+        self.opac = sc.opacities.to(dev).requires_grad_(True)
+        self.colors = sc.colors.to(dev).requires_grad_(True)
+        vm = sc.viewmats.clone()
+        if args.mode == "ddp" and rank > 0:  # a different view of the same scene per rank
+            th = 0.02 * rank
+            vm[0, :3, :3] = torch.tensor([[np.cos(th), 0, np.sin(th)], [0, 1, 0], [-np.sin(th), 0, np.cos(th)]],
+                                         dtype=torch.float32)
+        self.viewmats = vm.to(dev)
+        self.Ks = sc.Ks.to(dev)
+        self.bg = torch.zeros(1, 3, device=dev)
+        g = torch.Generator().manual_seed(1000 + rank)
+        self.target = torch.rand(3, args.height, args.width, generator=g).to(dev)
+        self.params = [self.means, self.quats, self.scales, self.opac, self.colors]
+
+    def step(self):
+        for p in self.params:
+            p.grad = None
+        W, H = self.args.width, self.args.height
+        if self.args.gs == "3d":
+            out, alpha, meta = G.rasterization(self.means, self.quats, self.scales, self.opac, self.colors,
+                                               self.viewmats, self.Ks, W, H, packed=False,
+                                               backgrounds=self.bg, render_mode="RGB+ED")
+            meta["means2d"].retain_grad()
+        else:
+            (out, alpha, normals, nfd, distort, median), meta = G.rasterization_2dgs(
+                self.means, self.quats, self.scales, self.opac, self.colors, self.viewmats, self.Ks, W, H,
+                packed=False, backgrounds=self.bg, render_mode="RGB+ED")
+        rgb = out[0, ..., :3].permute(2, 0, 1)
+        loss = (rgb - self.target).abs().mean() + 0.01 * alpha.mean()
+        if self.args.gs == "2d":
+            n = normals[0].permute(2, 0, 1)
+            nd = (nfd * alpha.detach())[0].permute(2, 0, 1)
+            loss = loss + 0.05 * (1 - (n * nd).sum(0)).mean()
+        loss.backward()
+        if self.args.mode == "ddp" and dist.is_initialized():
+            for p in self.params:
+                dist.all_reduce(p.grad, op=dist.ReduceOp.AVG)
+        self.meta = meta
+        return loss
+
+
+def raster_pairs(wl):
+    """Evaluated (pixel, Gaussian) pairs of the last step: per tile, every Gaussian up to
+    the tile's latest contributor, times the 256 pixels of the tile."""
+    meta = wl.meta
+    offs = meta["isect_offsets"].reshape(-1).to(torch.int64)
+    n_isects = meta["flatten_ids"].numel()
+    C, H, W = 1, wl.args.height, wl.args.width
+    dev = wl.dev
+    m2 = meta["means2d"].detach().contiguous()
+    fl = meta["flatten_ids"]
+    th, tw = meta["tile_height"], meta["tile_width"]
+    rc = torch.empty((C, H, W, 4), device=dev)
+    ra = torch.empty((C, H, W, 1), device=dev)
+    last = torch.empty((C, H, W), dtype=torch.int32, device=dev)
+    opac = meta["opacities"].detach().contiguous()
+    cols = torch.cat([wl.colors.detach()[None], meta["depths"].detach()[..., None]], -1).contiguous()
+    if wl.args.gs == "3d":
+        NAT.call("hgsr_raster3d_fwd", C, wl.args.n, 4, NAT.ptr(m2), NAT.ptr(meta["conics"].detach().contiguous()),
+                 NAT.ptr(cols), NAT.ptr(opac), None, W, H, 16, tw, th, NAT.ptr(meta["isect_offsets"]), n_isects,
+                 NAT.ptr(fl), NAT.ptr(rc), NAT.ptr(ra), NAT.ptr(last), NAT.stream(dev))
+    else:
+        rn = torch.empty((C, H, W, 3), device=dev)
+        r1 = torch.empty((C, H, W, 1), device=dev)
+        r2 = torch.empty((C, H, W, 1), device=dev)
+        med = torch.empty((C, H, W), dtype=torch.int32, device=dev)
+        NAT.call("hgsr_raster2d_fwd", C, wl.args.n, 4, NAT.ptr(m2),
+                 NAT.ptr(meta["ray_transforms"].detach().reshape(C, -1, 9).contiguous()), NAT.ptr(cols),
+                 NAT.ptr(opac), NAT.ptr(meta["normals"].detach().contiguous()), None, W, H, 16, tw, th,
+                 NAT.ptr(meta["isect_offsets"]), n_isects, NAT.ptr(fl), NAT.ptr(rc), NAT.ptr(ra), NAT.ptr(rn),
+                 NAT.ptr(r1), NAT.ptr(r2), NAT.ptr(last), NAT.ptr(med), NAT.stream(dev))
+    # per-tile max last id (tile-major reduction on the host side of torch ops)
+    hp, wp = th * 16, tw * 16
+    lp = torch.full((C, hp, wp), -1, dtype=torch.int64, device=dev)
+    lp[:, :H, :W] = last.to(torch.int64)
+    contributed = (ra[..., 0] > 0)
+    lp[:, :H, :W] = torch.where(contributed, lp[:, :H, :W], torch.full_like(lp[:, :H, :W], -1))
+    tile_last = lp.reshape(C, th, 16, tw, 16).amax(dim=(2, 4)).reshape(-1)
+    visited = torch.clamp(tile_last - offs + 1, min=0)
+    return int(visited.sum().item()) * 256, n_isects
+
+
+def cpu_baseline(args, wl):
+    """The C oracle (scalar, 1 thread) on a bounded sample of the same workload."""
+    from oracle import oracle as O
+    sc = wl.sc
+    W, H = args.width, args.height
+    band = 160  # rasterise 160 of 1080 rows (10 of 68 tile rows), scale raster time by H / band
+    t = {}
+    t0 = time.perf_counter()
+    r, m2, d, con = O.proj3d_fwd(sc.means.numpy(), sc.quats.numpy(), sc.scales.numpy(), sc.viewmats.numpy(),
+                                 sc.Ks.numpy(), W, H)
+    t["proj_fwd"] = time.perf_counter() - t0
+    tw, th = O.tile_grid(W, H)
+    t0 = time.perf_counter()
+    tpg, ids, fl = O.isect_tiles(m2, r, d, 16, tw, th)
+    offs = O.isect_offsets(ids, 1, tw, th)
+    t["isect_sort"] = time.perf_counter() - t0
+    cols = np.concatenate([sc.colors.numpy()[None], d[..., None]], -1).astype(np.float32)
+    op = sc.opacities.numpy()[None].astype(np.float32)
+    t0 = time.perf_counter()
+    rc, ra, last = O.raster3d_fwd(m2, con, cols, op, None, W, band, 16, offs, fl)
+    t["raster_fwd_band"] = time.perf_counter() - t0
+    g = np.random.default_rng(0)
+    vrc = (g.standard_normal(rc.shape) * 1e-6).astype(np.float32)
+    vra = np.full(ra.shape, 1e-8, np.float32)
+    t0 = time.perf_counter()
+    vm2, vcon, vcol, vop = O.raster3d_bwd(m2, con, cols, op, None, W, band, 16, offs, fl, ra, last, vrc, vra)
+    t["raster_bwd_band"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    O.proj3d_bwd(sc.means.numpy(), sc.quats.numpy(), sc.scales.numpy(), sc.viewmats.numpy(), sc.Ks.numpy(), W, H,
+                 r, con, vm2, vcol[..., -1].copy(), vcon)
+    t["proj_bwd"] = time.perf_counter() - t0
+    scale = H / band
+    per_view = (t["proj_fwd"] + t["isect_sort"] + t["proj_bwd"]
+                + scale * (t["raster_fwd_band"] + t["raster_bwd_band"]))
+    return {
+        "value": 1.0 / per_view, "unit": "views/s", "cores": 1, "kind": "port",
+        "sample": (f"C oracle (oracle/hgsr_oracle.c, 1 thread): projection fwd/bwd and tile intersection+sort on "
+                   f"all {args.n} Gaussians; raster fwd+bwd on a {band}x{W} band (rows 0-{band - 1}), raster time "
+                   f"scaled by {H}/{band}; measured {sum(t.values()):.1f}s"),
+        "breakdown_s": {k: round(v, 3) for k, v in t.items()},
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    wl = Workload(args, rank, dev)
+    for _ in range(args.warmup):
+        wl.step()
+    torch.cuda.synchronize(dev)
+    timing = not args.no_timing
+    if timing:
+        NAT.call("hgsr_timing_reset")
+        NAT.call("hgsr_timing_enable", 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if timing:
+        NAT.call("hgsr_timing_enable", 0)
+    if world > 1:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    kernels = {}
+    if timing:
+        for k in KERNELS:
+            tot, cnt = NAT.kernel_time(k)
+            if cnt:
+                kernels[k] = {"avg_ms": round(tot / cnt, 4), "launches": cnt}
+    roof = None
+    if kernels and rank == 0:
+        dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
+        pairs, n_isects = raster_pairs(wl)
+        avg_s = kernels[dom]["avg_ms"] * 1e-3
+        if dom in FLOP_PER_PAIR:
+            flops = pairs * FLOP_PER_PAIR[dom]
+            ach = flops / avg_s / 1e12
+            roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": None, "kernel": dom,
+                    "note": (f"fp32 VALU-bound compositing: peak = fp32 vector rate (= f32 MFMA rate); "
+                             f"{pairs} (pixel,Gaussian) pairs visited x {FLOP_PER_PAIR[dom]:.0f} FLOP/pair "
+                             f"(SURVEY 8(d)); {n_isects} intersections")}
+        else:
+            roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                    "traffic": None, "kernel": dom}
+        # aggregate compulsory-bytes figure of SURVEY 8(d): B_step = 384 N + 132 I + 52 P
+        b_step = 384 * args.n + 132 * n_isects + 52 * args.width * args.height
+        roof["aggregate_hbm_frac"] = round(b_step / (dt / args.steps) / (HBM_PEAK_GBS * 1e9), 4)
+        roof["n_isects"] = n_isects
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.gs == "3d":
+        cpu = cpu_baseline(args, wl)
+    if rank == 0:
+        ms = dt / args.steps * 1e3
+        line = {
+            "metric": METRIC, "value": round(world * args.steps / dt, 3), "unit": "views/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded c2 scene, SURVEY 8(d); no dataset in the environment)",
+            "config": {"workload": f"c2 {'3DGS' if args.gs == '3d' else '2DGS'} train step: rasterization fwd + "
+                                   f"L1/alpha loss + bwd, RGB+ED",
+                       "gaussians": args.n, "width": args.width, "height": args.height,
+                       "parallelism": ("per-chunk, one scene per GPU, no collectives" if args.mode == "chunk"
+                                       else "DDP over views, RCCL all-reduce of Gaussian grads")},
+            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

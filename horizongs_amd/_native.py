@@ -48,6 +48,9 @@ _SIGS = {
     "hgsr_raster2d_bwd_ws_bytes": (SZ, [I, I, I]),
     "hgsr_raster2d_bwd": (I, [I, I, I, P, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, P,
                               P, P, P, SZ, P]),
+    "hgsr_timing_enable": (I, [I]),
+    "hgsr_timing_reset": (I, []),
+    "hgsr_timing_query": (I, [ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(I64)]),
 }
 
 EXPORTED = tuple(n for n in _SIGS)
@@ -78,6 +81,14 @@ def call(name, *args):
     if st != 0:
         msg = lib().hgsr_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed ({st}): {msg}")
+
+
+def kernel_time(kernel: str):
+    """(total_ms, launches) recorded for `kernel` since the last hgsr_timing_reset()."""
+    tot = ct.c_double(0.0)
+    cnt = ct.c_int64(0)
+    call("hgsr_timing_query", kernel.encode(), ct.byref(tot), ct.byref(cnt))
+    return tot.value, cnt.value
 
 
 def size_query(name, *args) -> int:

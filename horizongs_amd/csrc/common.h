@@ -10,6 +10,17 @@ namespace hgsr {
 
 void set_error(const char* fmt, ...);
 
+// Optional HIP-event timing of the main kernel of an entry point (timing.hip).
+bool timing_on();
+int timing_begin(const char* name, hipStream_t s);
+void timing_end(int id, hipStream_t s);
+struct KernelTimer {
+    int id;
+    hipStream_t s;
+    KernelTimer(const char* name, hipStream_t st) : id(timing_on() ? timing_begin(name, st) : -1), s(st) {}
+    ~KernelTimer() { timing_end(id, s); }
+};
+
 // Returns HGSR_ELAUNCH (and records the HIP error) if the last launch failed.
 int check_launch(const char* what);
 

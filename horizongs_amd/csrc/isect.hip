@@ -425,6 +425,7 @@ extern "C" int hgsr_isect_count(int C, int N, const float* means2d, const int32_
     hipStream_t s = as_stream(stream);
     if (g.lds) {
         if (g.CN > 0) {
+            KernelTimer kt("isect_count", s);
             hipLaunchKernelGGL(isect_count_lds_kernel, dim3(g.n_blocks), dim3(256), g.n_bins * 4, s, g.CN, N,
                                g.per_block, reinterpret_cast<const float2*>(means2d), radii, tile_size, tile_w,
                                tile_h, g.n_tiles, g.n_bins, tiles_per_gauss, w.blockhist);
@@ -463,6 +464,7 @@ extern "C" int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const 
     uint64_t* tmp = max_bin > kSortCap ? (uint64_t*)((char*)ws2 + align256((size_t)n_isects * 8)) : nullptr;
     hipStream_t s = as_stream(stream);
     if (g.lds) {
+        KernelTimer kt("isect_emit", s);
         hipLaunchKernelGGL(isect_emit_lds_kernel, dim3(g.n_blocks), dim3(256), g.n_bins * 4, s, g.CN, N,
                            g.per_block, reinterpret_cast<const float2*>(means2d), radii, depths, tile_size,
                            tile_w, tile_h, g.n_tiles, g.n_bins, isect_offsets, w.blockhist, keys);
@@ -474,6 +476,7 @@ extern "C" int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const 
                            g.n_tiles, w.cursor, keys);
     }
     if (int st = check_launch("isect_emit")) return st;
+    KernelTimer kt("tile_sort", s);
     hipLaunchKernelGGL(tile_sort_kernel, dim3(g.n_bins), dim3(256), 0, s, g.n_bins, g.n_tiles,
                        nbits64(g.n_tiles), isect_offsets, n_isects, keys, tmp, isect_ids, flatten_ids);
     return check_launch("tile_sort");

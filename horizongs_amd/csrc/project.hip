@@ -521,6 +521,7 @@ extern "C" int hgsr_project3d_fwd(int C, int N, const float* means, const float*
     HGSR_REQUIRE(N == 0 || (radii && means2d && depths && conics), "null output pointer");
     if (N == 0) return HGSR_OK;
     dim3 grid((N + 255) / 256, C);
+    KernelTimer kt("project3d_fwd", as_stream(stream));
     hipLaunchKernelGGL(project3d_fwd_kernel, grid, dim3(256), 0, as_stream(stream), N, means,
                        reinterpret_cast<const float4*>(quats), scales, viewmats, Ks, width, height,
                        eps2d, near_plane, far_plane, radius_clip, radii,
@@ -540,6 +541,7 @@ extern "C" int hgsr_project3d_bwd(int C, int N, const float* means, const float*
     HGSR_REQUIRE(N == 0 || (radii && conics && v_means2d && v_depths && v_conics && v_means && v_quats && v_scales),
                  "null pointer");
     if (N == 0) return HGSR_OK;
+    KernelTimer kt("project3d_bwd", as_stream(stream));
     hipLaunchKernelGGL(project3d_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, as_stream(stream), C, N,
                        means, reinterpret_cast<const float4*>(quats), scales, viewmats, Ks, width,
                        height, radii, conics, reinterpret_cast<const float2*>(v_means2d), v_depths,
@@ -557,6 +559,7 @@ extern "C" int hgsr_project2d_fwd(int C, int N, const float* means, const float*
     HGSR_REQUIRE(N == 0 || (radii && means2d && depths && ray_transforms && normals), "null output pointer");
     if (N == 0) return HGSR_OK;
     dim3 grid((N + 255) / 256, C);
+    KernelTimer kt("project2d_fwd", as_stream(stream));
     hipLaunchKernelGGL(project2d_fwd_kernel, grid, dim3(256), 0, as_stream(stream), N, means,
                        reinterpret_cast<const float4*>(quats), scales, viewmats, Ks, width, height,
                        near_plane, far_plane, radius_clip, radii, reinterpret_cast<float2*>(means2d),
@@ -577,6 +580,7 @@ extern "C" int hgsr_project2d_bwd(int C, int N, const float* means, const float*
                             v_means && v_quats && v_scales),
                  "null pointer");
     if (N == 0) return HGSR_OK;
+    KernelTimer kt("project2d_bwd", as_stream(stream));
     hipLaunchKernelGGL(project2d_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, as_stream(stream), C, N,
                        means, reinterpret_cast<const float4*>(quats), scales, viewmats, Ks, radii,
                        ray_transforms, reinterpret_cast<const float2*>(v_means2d), v_depths,

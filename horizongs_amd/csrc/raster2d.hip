@@ -360,6 +360,7 @@ extern "C" int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, cons
     const dim3 grid(C * tile_w * tile_h);
     hipStream_t s = as_stream(stream);
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
+    KernelTimer kt("raster2d_fwd", s);
 #define LAUNCH_F2(DD)                                                                                           \
     hipLaunchKernelGGL(raster2d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, m2,     \
                        ray_transforms, colors, opacities, normals, backgrounds, isect_offsets, n_isects,         \
@@ -402,10 +403,13 @@ extern "C" int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, cons
     const dim3 grid(C * tile_w * tile_h);
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
 #define LAUNCH_B2(DD)                                                                                            \
-    hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, \
+    {                                                                                                            \
+        KernelTimer kt("raster2d_bwd", s);                                                                       \
+        hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, \
                        m2, ray_transforms, colors, opacities, normals, backgrounds, isect_offsets, n_isects,       \
                        flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, v_render_normals,  \
                        rows);                                                                                    \
+    }                                                                                                            \
     hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)C * N + 255) / 256)), dim3(256), 0, \
                        s, (int64_t)C * N, rows, reinterpret_cast<float2*>(v_means2d), v_ray_transforms, v_colors, \
                        v_opacities, v_normals, reinterpret_cast<float2*>(v_densify), nullptr)

@@ -284,6 +284,7 @@ extern "C" int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, cons
     const dim3 grid(C * tile_w * tile_h);
     hipStream_t s = as_stream(stream);
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
+    KernelTimer kt("raster3d_fwd", s);
 #define LAUNCH_F(DD)                                                                                      \
     hipLaunchKernelGGL(raster3d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, m2, \
                        conics, colors, opacities, backgrounds, isect_offsets, n_isects, flatten_ids,        \
@@ -325,9 +326,12 @@ extern "C" int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, cons
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
     const bool abs = v_means2d_abs != nullptr;
 #define LAUNCH_B(DD, AA)                                                                                     \
-    hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, \
+    {                                                                                                        \
+        KernelTimer kt("raster3d_bwd", s);                                                                   \
+        hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, \
                        m2, conics, colors, opacities, backgrounds, isect_offsets, n_isects, flatten_ids,       \
                        render_alphas, last_ids, v_render_colors, v_render_alphas, rows);                       \
+    }                                                                                                        \
     hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)C * N + 255) / 256)), dim3(256), 0, s, \
                        (int64_t)C * N, rows, reinterpret_cast<float2*>(v_means2d), v_conics, v_colors,         \
                        v_opacities, reinterpret_cast<float2*>(v_means2d_abs))

@@ -148,6 +148,7 @@ extern "C" int hgsr_sh_fwd(int degree, int K, int64_t n, const float* dirs, cons
     HGSR_REQUIRE(dirs && coeffs && colors, "null pointer");
     dim3 grid((unsigned)((n + 255) / 256));
     hipStream_t s = as_stream(stream);
+    KernelTimer kt("sh_fwd", s);
     switch (degree) {
         case 0: hipLaunchKernelGGL(sh_fwd_kernel<0>, grid, dim3(256), 0, s, K, n, dirs, coeffs, masks, colors); break;
         case 1: hipLaunchKernelGGL(sh_fwd_kernel<1>, grid, dim3(256), 0, s, K, n, dirs, coeffs, masks, colors); break;
@@ -166,6 +167,7 @@ extern "C" int hgsr_sh_bwd(int degree, int K, int64_t n, const float* dirs, cons
     HGSR_REQUIRE(dirs && coeffs && v_colors && v_coeffs, "null pointer");
     dim3 grid((unsigned)((n + 255) / 256));
     hipStream_t s = as_stream(stream);
+    KernelTimer kt("sh_bwd", s);
     switch (degree) {
         case 0: hipLaunchKernelGGL(sh_bwd_kernel<0>, grid, dim3(256), 0, s, K, n, dirs, coeffs, masks, v_colors, v_coeffs, v_dirs); break;
         case 1: hipLaunchKernelGGL(sh_bwd_kernel<1>, grid, dim3(256), 0, s, K, n, dirs, coeffs, masks, v_colors, v_coeffs, v_dirs); break;

@@ -1,0 +1,86 @@
+// Optional per-kernel HIP-event timing (bench.py uses it for the live roofline
+// numbers; rocprofv3 gives the same durations from outside the process).
+#include <mutex>
+#include <string.h>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace hgsr {
+
+namespace {
+struct Rec {
+    const char* name;
+    hipEvent_t a, b;
+};
+std::mutex g_mu;
+bool g_on = false;
+std::vector<hipEvent_t> g_pool;
+std::vector<Rec> g_recs;
+size_t g_next = 0;
+constexpr size_t kMaxRecs = 1 << 16;
+}  // namespace
+
+bool timing_on() { return g_on; }
+
+int timing_begin(const char* name, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_on || g_recs.size() >= kMaxRecs) return -1;
+    while (g_pool.size() < g_next + 2) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return -1;
+        g_pool.push_back(e);
+    }
+    Rec r{name, g_pool[g_next], g_pool[g_next + 1]};
+    g_next += 2;
+    if (hipEventRecord(r.a, s) != hipSuccess) return -1;
+    g_recs.push_back(r);
+    return (int)g_recs.size() - 1;
+}
+
+void timing_end(int id, hipStream_t s) {
+    if (id < 0) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    (void)hipEventRecord(g_recs[id].b, s);
+}
+
+}  // namespace hgsr
+
+using namespace hgsr;
+
+extern "C" int hgsr_timing_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_on = on != 0;
+    return HGSR_OK;
+}
+
+extern "C" int hgsr_timing_reset(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_recs.clear();
+    g_next = 0;
+    return HGSR_OK;
+}
+
+extern "C" int hgsr_timing_query(const char* kernel, double* total_ms, int64_t* count) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    double tot = 0.0;
+    int64_t n = 0;
+    for (const Rec& r : g_recs) {
+        if (strcmp(r.name, kernel) != 0) continue;
+        if (hipEventSynchronize(r.b) != hipSuccess) {
+            set_error("timing: event sync failed");
+            return HGSR_ELAUNCH;
+        }
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) {
+            set_error("timing: elapsed time failed");
+            return HGSR_ELAUNCH;
+        }
+        tot += ms;
+        ++n;
+    }
+    if (total_ms) *total_ms = tot;
+    if (count) *count = n;
+    return HGSR_OK;
+}

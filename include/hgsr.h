@@ -177,6 +177,19 @@ int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, const float* ra
                       float* v_opacities, float* v_normals, float* v_densify, void* ws,
                       size_t ws_bytes, hgsr_stream_t stream);
 
+/* ---- measurement ----------------------------------------------------------
+ * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):
+ * when enabled, the main kernel of every entry point is bracketed by
+ * hipEventRecord on the stream it is launched on.  Not for production use
+ * (events are pooled; at most 1<<16 records between resets). */
+int hgsr_timing_enable(int on);
+int hgsr_timing_reset(void);
+/* total milliseconds and launch count recorded for `kernel` (synchronises the
+ * recorded events); kernel names: project3d_fwd, project3d_bwd, project2d_fwd,
+ * project2d_bwd, sh_fwd, sh_bwd, isect_count, isect_emit, tile_sort,
+ * raster3d_fwd, raster3d_bwd, raster2d_fwd, raster2d_bwd. */
+int hgsr_timing_query(const char* kernel, double* total_ms, int64_t* count);
+
 #ifdef __cplusplus
 }
 #endif
