@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 from horizongs_amd import _native as NAT  # noqa: E402
 from horizongs_amd import gsplat_api as G  # noqa: E402
+from horizongs_amd.multigpu import GradientAllReduce  # noqa: E402
 from horizongs_amd.synthetic import make_scene  # noqa: E402
 
 METRIC = "train-step views/sec (fwd+bwd raster) @2M Gaussians/1080p; PSNR delta vs ref"
@@ -82,6 +83,7 @@ class Workload:
         g = torch.Generator().manual_seed(1000 + rank)
         self.target = torch.rand(3, args.height, args.width, generator=g).to(dev)
         self.params = [self.means, self.quats, self.scales, self.opac, self.colors]
+        self.allreduce = GradientAllReduce(self.params, bucket_mb=64.0)
 
     def step(self):
         for p in self.params:
@@ -103,9 +105,8 @@ class Workload:
             nd = (nfd * alpha.detach())[0].permute(2, 0, 1)
             loss = loss + 0.05 * (1 - (n * nd).sum(0)).mean()
         loss.backward()
-        if self.args.mode == "ddp" and dist.is_initialized():
-            for p in self.params:
-                dist.all_reduce(p.grad, op=dist.ReduceOp.AVG)
+        if self.args.mode == "ddp":
+            self.allreduce()
         self.meta = meta
         return loss
 
