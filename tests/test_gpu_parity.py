@@ -12,51 +12,11 @@ from horizongs_amd import gsplat_api as G
 from horizongs_amd.synthetic import make_scene
 from oracle import oracle as O
 from oracle import pipeline as OP
+from oracle.checks import close, cond_close, grad_close
 
 pytestmark = pytest.mark.gpu
 
-ATOL, RTOL = 1e-5, 1e-4
 DEV = "cuda:0"
-
-
-def close(a, b, atol=ATOL, rtol=RTOL, frac_ok=0.0, name=""):
-    a = np.asarray(a, np.float64)
-    b = np.asarray(b, np.float64)
-    assert a.shape == b.shape, (name, a.shape, b.shape)
-    bad = np.abs(a - b) > atol + rtol * np.abs(b)
-    frac = bad.mean() if bad.size else 0.0
-    worst = np.abs(a - b).max() if bad.size else 0.0
-    assert frac <= frac_ok, f"{name}: {bad.sum()}/{bad.size} outside tol, max abs err {worst:.3g}"
-
-
-def grad_close(a, b, name, rel_floor=1e-4):
-    """Gradient comparison: within 1e-5 abs / 1e-4 rel, with the relative part taken
-    against max(|b|, rel_floor * max|b|) — gradients sum thousands of per-pixel terms
-    whose summation order differs (atomics), so near-cancelled entries are judged
-    against the tensor's scale."""
-    a = np.asarray(a, np.float64)
-    b = np.asarray(b, np.float64)
-    scale = np.maximum(np.abs(b), rel_floor * (np.abs(b).max() if b.size else 0.0))
-    bad = np.abs(a - b) > ATOL + RTOL * scale
-    assert not bad.any(), f"{name}: {bad.sum()}/{bad.size} bad, max err {np.abs(a - b).max():.3g}"
-
-
-def cond_close(a, b32, b64, name, rel_floor=1e-4):
-    """fp32-conditioning-aware check, used where the expected-depth normalisation
-    (depth / clamp_min(alpha, 1e-10)) amplifies fp32 rounding at low-alpha pixels:
-    the GPU result must be within 1e-5 abs / 1e-4 rel of the f32 oracle PLUS twice the
-    f32 oracle's own distance to the f64 oracle on that tensor (measured, not assumed),
-    and no further from the f64 answer than 3x the f32 oracle is (the kernels use the
-    hardware exp / reciprocal and FMA contraction, the oracle correctly rounded ops)."""
-    a = np.asarray(a, np.float64)
-    b = np.asarray(b32, np.float64)
-    c = np.asarray(b64, np.float64)
-    e32 = np.abs(b - c).max() if b.size else 0.0
-    scale = np.maximum(np.abs(b), rel_floor * (np.abs(b).max() if b.size else 0.0))
-    bad = np.abs(a - b) > ATOL + RTOL * scale + 2.0 * e32
-    assert not bad.any(), f"{name}: {bad.sum()}/{bad.size} bad, max err {np.abs(a - b).max():.3g} (e32 {e32:.3g})"
-    assert np.abs(a - c).max() <= 3.0 * e32 + ATOL, (
-        f"{name}: GPU err {np.abs(a - c).max():.3g} vs f32 oracle err {e32:.3g} (max|g| {np.abs(c).max():.3g})")
 
 
 def scene(n=400, W=96, H=80, seed=0, scale_range=(0.01, 0.06), depth_range=(2.0, 6.0), sh=None, C=1):
