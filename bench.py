@@ -128,9 +128,11 @@ def raster_pairs(wl):
     opac = meta["opacities"].detach().contiguous()
     cols = torch.cat([wl.colors.detach()[None], meta["depths"].detach()[..., None]], -1).contiguous()
     if wl.args.gs == "3d":
+        ws_b = NAT.size_query("hgsr_raster3d_fwd_ws_bytes", C, wl.args.n, 4)
+        ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
         NAT.call("hgsr_raster3d_fwd", C, wl.args.n, 4, NAT.ptr(m2), NAT.ptr(meta["conics"].detach().contiguous()),
                  NAT.ptr(cols), NAT.ptr(opac), None, W, H, 16, tw, th, NAT.ptr(meta["isect_offsets"]), n_isects,
-                 NAT.ptr(fl), NAT.ptr(rc), NAT.ptr(ra), NAT.ptr(last), NAT.stream(dev))
+                 NAT.ptr(fl), NAT.ptr(rc), NAT.ptr(ra), NAT.ptr(last), NAT.ptr(ws), ws_b, NAT.stream(dev))
     else:
         rn = torch.empty((C, H, W, 3), device=dev)
         r1 = torch.empty((C, H, W, 1), device=dev)

@@ -40,7 +40,8 @@ _SIGS = {
     "hgsr_isect_emit_sorted": (I, [I, I, P, P, P, I, I, I, P, I64, I64, P, P, P, SZ, P, SZ, P]),
     "hgsr_isect_emit_unsorted": (I, [I, I, P, P, P, I, I, I, P, P, P, P]),
     "hgsr_isect_offset_encode": (I, [I64, P, I, I, I, P, P]),
-    "hgsr_raster3d_fwd": (I, [I, I, I, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P]),
+    "hgsr_raster3d_fwd_ws_bytes": (SZ, [I, I, I]),
+    "hgsr_raster3d_fwd": (I, [I, I, I, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, SZ, P]),
     "hgsr_raster3d_bwd_ws_bytes": (SZ, [I, I, I]),
     "hgsr_raster3d_bwd": (I, [I, I, I, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, P, P,
                               SZ, P]),

@@ -2,17 +2,22 @@
 // rasterize_to_pixels semantics, as reached from reference
 // gaussian_renderer/render.py:40-54).
 //
-// CDNA4 mapping: one 256-lane workgroup per 16x16 tile = four wave64s, each
-// wave owning an 8x8 quadrant (compact footprint -> more wave-uniform skips in
-// the backward).  Gaussian records of the tile's depth-sorted list are staged in
-// LDS in batches and read back as broadcasts; the forward early-outs per tile
-// with a workgroup vote.  The backward replays back-to-front from each pixel's
-// last contributor, skips Gaussians no lane of the wave sees (wave ballot),
-// reduces each Gaussian's gradient across the wave with DPP row ops, combines
-// the four waves through LDS and issues ONE packed record of atomics per
-// (Gaussian, tile) into a 64-byte-aligned accumulator row (one memory request).
-// Work is bounded by the latest last_id in the tile (block-level skip of the
-// never-reached tail).
+// CDNA4 mapping
+//  * one 256-lane workgroup per 16x16 tile = four wave64s, each owning an 8x8
+//    quadrant (compact footprint -> more wave-uniform skips in the backward);
+//  * the Gaussians' raster attributes are first packed into 48-B records
+//    {x, y, a, b | c, opacity | colour[4]} (one coalesced pass over N), so a batch
+//    load is 3 x 16-B loads per Gaussian instead of 5 scattered gathers;
+//  * batches of the tile's depth-sorted list are register-prefetched one batch
+//    ahead (global latency hidden under the current batch) and staged in LDS,
+//    read back as wave-wide broadcasts;
+//  * inner loops are branch-free (predicated per lane) with a wave-uniform
+//    early exit, so the scalar unit is not saturated by exec-mask bookkeeping;
+//  * backward: replay back-to-front bounded by the tile's latest contributor,
+//    wave-ballot skip of Gaussians no lane sees, all gradient components
+//    reduced across the wave together (step-major DPP, no hazard stalls), the
+//    four wave partials combined in LDS and ONE packed record of float atomics
+//    per (Gaussian, tile) into a 64-byte accumulator row (one memory request).
 #include "common.h"
 
 namespace hgsr {
@@ -50,56 +55,115 @@ __device__ __forceinline__ TileCtx tile_ctx(int C, int W, int H, int tw, int th,
     return t;
 }
 
+// 48-B raster record of one (camera, Gaussian)
+struct Rec3 {
+    float4 g0;  // x, y, conic a, conic b
+    float4 g1;  // conic c, opacity, 0, 0
+    float4 col; // colour (D <= 4, zero padded)
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void pack3_kernel(int64_t n, const float2* __restrict__ means2d,
+                                                    const float* __restrict__ conics,
+                                                    const float* __restrict__ colors,
+                                                    const float* __restrict__ opacities, Rec3* __restrict__ rec) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    const float2 m = means2d[g];
+    Rec3 r;
+    r.g0 = make_float4(m.x, m.y, conics[g * 3], conics[g * 3 + 1]);
+    r.g1 = make_float4(conics[g * 3 + 2], opacities[g], 0.f, 0.f);
+    float c[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < D; ++k) c[k] = colors[g * D + k];
+    r.col = make_float4(c[0], c[1], c[2], c[3]);
+    rec[g] = r;
+}
+
+// one front-to-back compositing step, branch-free (predicated per lane)
+template <int D>
+__device__ __forceinline__ void fwd_step(const float4 g0, const float2 g1, const float4 c, int32_t idx, float px,
+                                         float py, float& T, float (&acc)[4], int32_t& cur, bool& done) {
+    const float dx = g0.x - px, dy = g0.y - py;
+    const float sigma = 0.5f * (g0.z * dx * dx + g1.x * dy * dy) + g0.w * dx * dy;
+    const float alpha = fminf(0.999f, g1.y * __expf(-sigma));
+    const float nT = T * (1.0f - alpha);
+    const bool valid = (sigma >= 0.f) & (alpha >= 1.0f / 255.0f) & !done;
+    const bool keep = nT > 1e-4f;
+    const bool ok = valid & keep;
+    done = done | (valid & !keep);  // this Gaussian would push T <= 1e-4: stop, exclusive
+    const float vis = ok ? alpha * T : 0.f;
+    acc[0] += c.x * vis;
+    if (D > 1) acc[1] += c.y * vis;
+    if (D > 2) acc[2] += c.z * vis;
+    if (D > 3) acc[3] += c.w * vis;
+    T = ok ? nT : T;
+    cur = ok ? idx : cur;
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
-    int C, int W, int H, int tw, int th, const float2* __restrict__ means2d,
-    const float* __restrict__ conics, const float* __restrict__ colors,
-    const float* __restrict__ opacities, const float* __restrict__ backgrounds,
+    int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
     const int32_t* __restrict__ offsets, int64_t n_isects, const int32_t* __restrict__ flatten_ids,
     float* __restrict__ render_colors, float* __restrict__ render_alphas, int32_t* __restrict__ last_ids) {
-    __shared__ float2 s_xy[kFwdBatch];
-    __shared__ float4 s_co[kFwdBatch];  // conic a, b, c, opacity
-    __shared__ float s_col[kFwdBatch * D];
+    __shared__ float4 s_g0[kFwdBatch];
+    __shared__ float2 s_g1[kFwdBatch];
+    __shared__ float4 s_col[kFwdBatch];
+    __shared__ int s_vote[2][4];
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     float T = 1.0f;
-    float acc[D];
-#pragma unroll
-    for (int k = 0; k < D; ++k) acc[k] = 0.f;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
     int32_t cur = 0;
     bool done = !tc.inside;
     const int nb = (tc.end - tc.start + kFwdBatch - 1) / kFwdBatch;
+    // two-deep software pipeline of the batch loads: ids two batches ahead,
+    // records one batch ahead; indices are clamped so every load is unconditional
+    // (no phi copies forcing an early vmcnt wait)
+    const int32_t last = tc.end - 1;
+    float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
+    int32_t nid = 0;
+    if (nb > 0) {
+        const int32_t id0 = flatten_ids[min(tc.start + tid, last)];
+        const float4* r = reinterpret_cast<const float4*>(rec + id0);
+        n0 = r[0]; n1 = r[1]; n2 = r[2];
+        nid = flatten_ids[min(tc.start + kFwdBatch + tid, last)];
+    }
     for (int b = 0; b < nb; ++b) {
-        if (__syncthreads_count(done) == 256) break;
+        // workgroup early-out vote (double-buffered slots; LDS-only barriers so the
+        // prefetch loads stay in flight)
+        const bool wave_done = __all(done);
+        if (lane == 0) s_vote[b & 1][wave] = wave_done;
+        lds_barrier();
+        if (s_vote[b & 1][0] & s_vote[b & 1][1] & s_vote[b & 1][2] & s_vote[b & 1][3]) break;
         const int32_t bs = tc.start + b * kFwdBatch;
-        const int32_t idx = bs + tid;
-        if (idx < tc.end) {
-            const int32_t g = flatten_ids[idx];
-            s_xy[tid] = means2d[g];
-            s_co[tid] = make_float4(conics[(int64_t)g * 3], conics[(int64_t)g * 3 + 1], conics[(int64_t)g * 3 + 2],
-                                    opacities[g]);
-#pragma unroll
-            for (int k = 0; k < D; ++k) s_col[tid * D + k] = colors[(int64_t)g * D + k];
-        }
-        __syncthreads();
         const int cnt = min(kFwdBatch, tc.end - bs);
-        for (int t = 0; t < cnt && !done; ++t) {
-            const float2 xy = s_xy[t];
-            const float4 co = s_co[t];
-            const float dx = xy.x - tc.px, dy = xy.y - tc.py;
-            const float sigma = 0.5f * (co.x * dx * dx + co.z * dy * dy) + co.y * dx * dy;
-            const float alpha = fminf(0.999f, co.w * __expf(-sigma));
-            if (sigma < 0.f || alpha < 1.0f / 255.0f) continue;
-            const float nT = T * (1.0f - alpha);
-            if (nT <= 1e-4f) {
-                done = true;
-                break;
-            }
-            const float vis = alpha * T;
-#pragma unroll
-            for (int k = 0; k < D; ++k) acc[k] += s_col[t * D + k] * vis;
-            cur = bs + t;
-            T = nT;
+        if (tid < cnt) {
+            s_g0[tid] = n0;
+            s_g1[tid] = make_float2(n1.x, n1.y);
+            s_col[tid] = n2;
+        } else if (tid < ((cnt + 3) & ~3)) {  // pad to a multiple of 4 with zero-opacity dummies
+            s_g0[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_g1[tid] = make_float2(0.f, 0.f);
+            s_col[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        lds_barrier();
+        // prefetch: records of batch b+1 (ids already here), ids of batch b+2
+        {
+            const float4* r = reinterpret_cast<const float4*>(rec + nid);
+            n0 = r[0]; n1 = r[1]; n2 = r[2];
+            nid = flatten_ids[min(bs + 2 * kFwdBatch + tid, last)];
+        }
+        if (wave_done) continue;
+        for (int t = 0; t < cnt; t += 4) {
+            const float4 a0 = s_g0[t], a1 = s_g0[t + 1], a2 = s_g0[t + 2], a3 = s_g0[t + 3];
+            const float2 b0 = s_g1[t], b1 = s_g1[t + 1], b2 = s_g1[t + 2], b3 = s_g1[t + 3];
+            const float4 c0 = s_col[t], c1 = s_col[t + 1], c2 = s_col[t + 2], c3 = s_col[t + 3];
+            fwd_step<D>(a0, b0, c0, bs + t, tc.px, tc.py, T, acc, cur, done);
+            fwd_step<D>(a1, b1, c1, bs + t + 1, tc.px, tc.py, T, acc, cur, done);
+            fwd_step<D>(a2, b2, c2, bs + t + 2, tc.px, tc.py, T, acc, cur, done);
+            fwd_step<D>(a3, b3, c3, bs + t + 3, tc.px, tc.py, T, acc, cur, done);
+            if (__all(done)) break;
         }
     }
     if (tc.inside) {
@@ -119,17 +183,15 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
 
 template <int D, bool ABS>
 __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
-    int C, int W, int H, int tw, int th, const float2* __restrict__ means2d,
-    const float* __restrict__ conics, const float* __restrict__ colors,
-    const float* __restrict__ opacities, const float* __restrict__ backgrounds,
+    int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
     const int32_t* __restrict__ offsets, int64_t n_isects, const int32_t* __restrict__ flatten_ids,
     const float* __restrict__ render_alphas, const int32_t* __restrict__ last_ids,
     const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
     float* __restrict__ acc_rows) {
     constexpr int KV = 6 + D + (ABS ? 2 : 0);
-    __shared__ float2 s_xy[kBwdBatch];
-    __shared__ float4 s_co[kBwdBatch];
-    __shared__ float s_col[kBwdBatch * D];
+    __shared__ float4 s_g0[kBwdBatch];
+    __shared__ float2 s_g1[kBwdBatch];
+    __shared__ float4 s_col[kBwdBatch];
     __shared__ int32_t s_id[kBwdBatch];
     __shared__ float s_part[kBwdBatch * 4 * KV];
     __shared__ int32_t s_last[4];
@@ -137,88 +199,112 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float T_final = tc.inside ? 1.0f - render_alphas[tc.pix] : 1.0f;
     float T = T_final;
-    float buf[D], vo[D];
+    float buf[4] = {0.f, 0.f, 0.f, 0.f}, vo[4] = {0.f, 0.f, 0.f, 0.f};
     float bg_dot = 0.f;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-        buf[k] = 0.f;
         vo[k] = tc.inside ? v_render_colors[tc.pix * D + k] : 0.f;
         if (backgrounds) bg_dot += backgrounds[tc.cam * D + k] * vo[k];
     }
     const float va = tc.inside ? v_render_alphas[tc.pix] : 0.f;
-    const int32_t bin_final = tc.inside ? last_ids[tc.pix] : 0;
-    const int32_t wave_final = wave_max_i32(tc.inside ? bin_final : -1);
+    const float va_term = T_final * (va - bg_dot);  // multiplied by ra per Gaussian
+    const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
+    const int32_t wave_final = wave_max_i32(bin_final);
     if (lane == 0) s_last[wave] = wave_final;
-    __syncthreads();
+    lds_barrier();
     const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
     // Gaussians after the block's last contributor are never reached
     const int32_t end = min(tc.end, blk_final + 1);
     const int nb = end > tc.start ? (end - tc.start + kBwdBatch - 1) / kBwdBatch : 0;
+    // two-deep software pipeline (ids two batches ahead, records one), clamped
+    // unconditional loads; only lanes < kBwdBatch load
+    float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
+    int32_t cid = 0, nid = 0;
+    const bool loader = tid < kBwdBatch;
+    if (nb > 0 && loader) {
+        cid = flatten_ids[max(end - 1 - tid, tc.start)];
+        const float4* r = reinterpret_cast<const float4*>(rec + cid);
+        n0 = r[0]; n1 = r[1]; n2 = r[2];
+        nid = flatten_ids[max(end - 1 - kBwdBatch - tid, tc.start)];
+    }
     for (int b = 0; b < nb; ++b) {
         const int32_t batch_end = end - 1 - b * kBwdBatch;
         const int bsz = min(kBwdBatch, batch_end + 1 - tc.start);
-        __syncthreads();
+        lds_barrier();  // previous batch's partials consumed (its atomics stay in flight)
         if (tid < bsz) {
-            const int32_t g = flatten_ids[batch_end - tid];
-            s_id[tid] = g;
-            s_xy[tid] = means2d[g];
-            s_co[tid] = make_float4(conics[(int64_t)g * 3], conics[(int64_t)g * 3 + 1], conics[(int64_t)g * 3 + 2],
-                                    opacities[g]);
-#pragma unroll
-            for (int k = 0; k < D; ++k) s_col[tid * D + k] = colors[(int64_t)g * D + k];
+            s_id[tid] = cid;
+            s_g0[tid] = n0;
+            s_g1[tid] = make_float2(n1.x, n1.y);
+            s_col[tid] = n2;
         }
         for (int e = tid; e < kBwdBatch * 4 * KV; e += 256) s_part[e] = 0.f;
-        __syncthreads();
+        lds_barrier();
+        if (loader) {
+            cid = nid;
+            const float4* r = reinterpret_cast<const float4*>(rec + cid);
+            n0 = r[0]; n1 = r[1]; n2 = r[2];
+            nid = flatten_ids[max(batch_end - 2 * kBwdBatch - tid, tc.start)];
+        }
         const int t0 = max(0, batch_end - wave_final);
+        using TR = TransposeReduce<KV>;
+        const int row = lane >> 4;
+        // LDS software pipeline: the next Gaussian's broadcast reads are issued
+        // before the current one is processed
+        float4 g0n = s_g0[min(t0, kBwdBatch - 1)];
+        float2 g1n = s_g1[min(t0, kBwdBatch - 1)];
+        float4 cn = s_col[min(t0, kBwdBatch - 1)];
         for (int t = t0; t < bsz; ++t) {
-            bool valid = tc.inside && (batch_end - t <= bin_final);
-            const float2 xy = s_xy[t];
-            const float4 co = s_co[t];
-            const float dx = xy.x - tc.px, dy = xy.y - tc.py;
-            const float sigma = 0.5f * (co.x * dx * dx + co.z * dy * dy) + co.y * dx * dy;
+            const float4 g0 = g0n;
+            const float2 g1 = g1n;
+            const float4 c = cn;
+            const int tn = min(t + 1, kBwdBatch - 1);
+            g0n = s_g0[tn];
+            g1n = s_g1[tn];
+            cn = s_col[tn];
+            const float dx = g0.x - tc.px, dy = g0.y - tc.py;
+            const float sigma = 0.5f * (g0.z * dx * dx + g1.x * dy * dy) + g0.w * dx * dy;
             const float vis = __expf(-sigma);
-            const float alpha = fminf(0.999f, co.w * vis);
-            valid = valid && !(sigma < 0.f || alpha < 1.0f / 255.0f);
+            const float alpha = fminf(0.999f, g1.y * vis);
+            const bool valid = (batch_end - t <= bin_final) & (sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
             if (!__any(valid)) continue;
+            const float ck[4] = {c.x, c.y, c.z, c.w};
+            const float ra = __builtin_amdgcn_rcpf(1.0f - alpha);
+            const float Tn = valid ? T * ra : T;
+            const float fac = valid ? alpha * Tn : 0.f;
             float gv[KV];
+            float v_alpha = va_term * ra;
 #pragma unroll
-            for (int k = 0; k < KV; ++k) gv[k] = 0.f;
-            if (valid) {
-                const float ra = __builtin_amdgcn_rcpf(1.0f - alpha);
-                T = T * ra;
-                const float fac = alpha * T;
-                float v_alpha = 0.f;
-#pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    const float ck = s_col[t * D + k];
-                    gv[6 + k] = fac * vo[k];
-                    v_alpha += (ck * T - buf[k] * ra) * vo[k];
-                    buf[k] += ck * fac;
-                }
-                v_alpha += T_final * ra * va;
-                v_alpha += -T_final * ra * bg_dot;
-                if (co.w * vis <= 0.999f) {
-                    const float v_sigma = -co.w * vis * v_alpha;
-                    gv[0] = v_sigma * (co.x * dx + co.y * dy);
-                    gv[1] = v_sigma * (co.y * dx + co.z * dy);
-                    gv[2] = 0.5f * v_sigma * dx * dx;
-                    gv[3] = v_sigma * dx * dy;
-                    gv[4] = 0.5f * v_sigma * dy * dy;
-                    gv[5] = vis * v_alpha;
-                    if (ABS) {
-                        gv[6 + D] = fabsf(gv[0]);
-                        gv[7 + D] = fabsf(gv[1]);
-                    }
-                }
+            for (int k = 0; k < D; ++k) {
+                gv[6 + k] = fac * vo[k];
+                v_alpha += (ck[k] * Tn - buf[k] * ra) * vo[k];
+                buf[k] += ck[k] * fac;
             }
-            float* dst = s_part + (t * 4 + wave) * KV;
+            const bool ok2 = valid & (g1.y * vis <= 0.999f);
+            const float v_sigma = ok2 ? -g1.y * vis * v_alpha : 0.f;
+            gv[0] = v_sigma * (g0.z * dx + g0.w * dy);
+            gv[1] = v_sigma * (g0.w * dx + g1.x * dy);
+            gv[2] = 0.5f * v_sigma * dx * dx;
+            gv[3] = v_sigma * dx * dy;
+            gv[4] = 0.5f * v_sigma * dy * dy;
+            gv[5] = ok2 ? vis * v_alpha : 0.f;
+            if (ABS) {
+                gv[6 + D] = fabsf(gv[0]);
+                gv[7 + D] = fabsf(gv[1]);
+            }
+            T = Tn;
+            float u[TR::G];
+            TR::run(gv, u);
+            if ((lane & 15) == 0) {
+                float* dst = s_part + (t * 4 + wave) * KV;
 #pragma unroll
-            for (int k = 0; k < KV; ++k) {
-                const float s = wave_sum_to_lane63(gv[k]);
-                if (lane == 63) dst[k] = s;
+                for (int j = 0; j < TR::G; ++j) {
+                    const int i0 = TR::index(j, 0), i1 = TR::index(j, 1), i2 = TR::index(j, 2), i3 = TR::index(j, 3);
+                    const int idx = row == 0 ? i0 : row == 1 ? i1 : row == 2 ? i2 : i3;
+                    if (idx >= 0) dst[idx] = u[j];
+                }
             }
         }
-        __syncthreads();
+        lds_barrier();
         for (int e = tid; e < bsz * KV; e += 256) {
             const int t = e / KV, k = e - t * KV;
             const float* p = s_part + t * 4 * KV + k;
@@ -272,23 +358,47 @@ static int check_raster(int C, int N, int D, int W, int H, int tile_size, int tw
     return HGSR_OK;
 }
 
+static size_t rec_bytes(int C, int N) { return ((size_t)C * N * sizeof(Rec3) + 255) & ~(size_t)255; }
+
+static int pack3(int C, int N, int D, const float* means2d, const float* conics, const float* colors,
+                 const float* opacities, Rec3* rec, hipStream_t s) {
+    const int64_t n = (int64_t)C * N;
+    if (n == 0) return HGSR_OK;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    const float2* m2 = reinterpret_cast<const float2*>(means2d);
+    switch (D) {
+        case 1: hipLaunchKernelGGL(pack3_kernel<1>, grid, dim3(256), 0, s, n, m2, conics, colors, opacities, rec); break;
+        case 2: hipLaunchKernelGGL(pack3_kernel<2>, grid, dim3(256), 0, s, n, m2, conics, colors, opacities, rec); break;
+        case 3: hipLaunchKernelGGL(pack3_kernel<3>, grid, dim3(256), 0, s, n, m2, conics, colors, opacities, rec); break;
+        default: hipLaunchKernelGGL(pack3_kernel<4>, grid, dim3(256), 0, s, n, m2, conics, colors, opacities, rec); break;
+    }
+    return check_launch("raster3d_pack");
+}
+
+extern "C" size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D) {
+    (void)D;
+    return rec_bytes(C, N);
+}
+
 extern "C" int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, const float* conics,
                                  const float* colors, const float* opacities, const float* backgrounds,
                                  int width, int height, int tile_size, int tile_w, int tile_h,
                                  const int32_t* isect_offsets, int64_t n_isects, const int32_t* flatten_ids,
-                                 float* render_colors, float* render_alphas, int32_t* last_ids,
-                                 hgsr_stream_t stream) {
+                                 float* render_colors, float* render_alphas, int32_t* last_ids, void* ws,
+                                 size_t ws_bytes, hgsr_stream_t stream) {
     if (int st = check_raster(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
+    HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_fwd_ws_bytes(C, N, D), "raster3d_fwd workspace too small");
     HGSR_REQUIRE(isect_offsets && render_colors && render_alphas && last_ids, "null pointer");
-    HGSR_REQUIRE(n_isects == 0 || (means2d && conics && colors && opacities && flatten_ids), "null pointer");
-    const dim3 grid(C * tile_w * tile_h);
+    HGSR_REQUIRE(n_isects == 0 || (means2d && conics && colors && opacities && flatten_ids && ws), "null pointer");
     hipStream_t s = as_stream(stream);
-    const float2* m2 = reinterpret_cast<const float2*>(means2d);
+    Rec3* rec = (Rec3*)ws;
+    if (n_isects > 0)
+        if (int st = pack3(C, N, D, means2d, conics, colors, opacities, rec, s)) return st;
+    const dim3 grid(C * tile_w * tile_h);
     KernelTimer kt("raster3d_fwd", s);
-#define LAUNCH_F(DD)                                                                                      \
-    hipLaunchKernelGGL(raster3d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, m2, \
-                       conics, colors, opacities, backgrounds, isect_offsets, n_isects, flatten_ids,        \
-                       render_colors, render_alphas, last_ids)
+#define LAUNCH_F(DD)                                                                                           \
+    hipLaunchKernelGGL(raster3d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,    \
+                       backgrounds, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas, last_ids)
     switch (D) {
         case 1: LAUNCH_F(1); break;
         case 2: LAUNCH_F(2); break;
@@ -301,7 +411,7 @@ extern "C" int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, cons
 
 extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D) {
     (void)D;
-    return (size_t)C * N * kRec3 * sizeof(float);
+    return (size_t)C * N * kRec3 * sizeof(float) + rec_bytes(C, N);
 }
 
 extern "C" int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, const float* conics,
@@ -320,18 +430,20 @@ extern "C" int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, cons
                      v_opacities && ws,
                  "null pointer");
     hipStream_t s = as_stream(stream);
+    const size_t rows_b = (size_t)C * N * kRec3 * sizeof(float);
     float* rows = (float*)ws;
-    if (int st = memset_async(rows, hgsr_raster3d_bwd_ws_bytes(C, N, D), s, "raster3d_bwd")) return st;
+    Rec3* rec = (Rec3*)((char*)ws + rows_b);
+    if (int st = memset_async(rows, rows_b, s, "raster3d_bwd")) return st;
+    if (int st = pack3(C, N, D, means2d, conics, colors, opacities, rec, s)) return st;
     const dim3 grid(C * tile_w * tile_h);
-    const float2* m2 = reinterpret_cast<const float2*>(means2d);
     const bool abs = v_means2d_abs != nullptr;
-#define LAUNCH_B(DD, AA)                                                                                     \
-    {                                                                                                        \
-        KernelTimer kt("raster3d_bwd", s);                                                                   \
-        hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, \
-                       m2, conics, colors, opacities, backgrounds, isect_offsets, n_isects, flatten_ids,       \
-                       render_alphas, last_ids, v_render_colors, v_render_alphas, rows);                       \
-    }                                                                                                        \
+#define LAUNCH_B(DD, AA)                                                                                       \
+    {                                                                                                          \
+        KernelTimer kt("raster3d_bwd", s);                                                                     \
+        hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
+                           tile_h, rec, backgrounds, isect_offsets, n_isects, flatten_ids, render_alphas,        \
+                           last_ids, v_render_colors, v_render_alphas, rows);                                    \
+    }                                                                                                          \
     hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)C * N + 255) / 256)), dim3(256), 0, s, \
                        (int64_t)C * N, rows, reinterpret_cast<float2*>(v_means2d), v_conics, v_colors,         \
                        v_opacities, reinterpret_cast<float2*>(v_means2d_abs))

@@ -275,9 +275,12 @@ class _Raster3D(torch.autograd.Function):
         rc = torch.empty((C, height, width, D), dtype=torch.float32, device=dev)
         ra = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
         last = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        ws_b = N.size_query("hgsr_raster3d_fwd_ws_bytes", C, Ng, D)
+        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
         N.call("hgsr_raster3d_fwd", C, Ng, D, ptr(means2d), ptr(conics), ptr(colors), ptr(opacities),
                ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
-               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), N.stream(dev))
+               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(ws), ws_b,
+               N.stream(dev))
         ctx.save_for_backward(means2d, conics, colors, opacities, backgrounds, isect_offsets, flatten_ids, ra, last)
         ctx.cfg = (width, height, tile_size, absgrad)
         return rc, ra

@@ -129,13 +129,15 @@ int hgsr_isect_offset_encode(int64_t n_isects, const int64_t* isect_ids, int C, 
  * replaces gsplat rasterize_to_pixels (packed=False, tile_size=16, D <= 4 per
  * call; callers chunk wider channel counts).  colors [C*N, D], opacities [C*N],
  * backgrounds [C, D] nullable.  Outputs render_colors [C,H,W,D],
- * render_alphas [C,H,W,1], last_ids [C,H,W]. */
+ * render_alphas [C,H,W,1], last_ids [C,H,W].  ws: caller scratch of
+ * hgsr_raster3d_fwd_ws_bytes() (packed 48-B per-Gaussian raster records). */
+size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D);
 int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, const float* conics,
                       const float* colors, const float* opacities, const float* backgrounds,
                       int width, int height, int tile_size, int tile_w, int tile_h,
                       const int32_t* isect_offsets, int64_t n_isects,
                       const int32_t* flatten_ids, float* render_colors, float* render_alphas,
-                      int32_t* last_ids, hgsr_stream_t stream);
+                      int32_t* last_ids, void* ws, size_t ws_bytes, hgsr_stream_t stream);
 /* accumulates v_means2d [C*N,2], v_conics [C*N,3], v_colors [C*N,D],
  * v_opacities [C*N]; v_means2d_abs nullable (gsplat absgrad).  ws: caller
  * scratch of hgsr_raster3d_bwd_ws_bytes(). */
