@@ -58,9 +58,23 @@ __device__ __forceinline__ TileCtx tile_ctx(int C, int W, int H, int tw, int th,
 // 48-B raster record of one (camera, Gaussian)
 struct Rec3 {
     float4 g0;  // x, y, conic a, conic b
-    float4 g1;  // conic c, opacity, 0, 0
+    float4 g1;  // conic c, opacity, footprint half-extent x, half-extent y
     float4 col; // colour (D <= 4, zero padded)
 };
+
+// Exact screen-space half-extents of the region where alpha = o*exp(-sigma) can
+// reach 1/255: 0.5 d^T Conic d <= L, L = ln(255 o); the ellipse's bounding box
+// is |dx| <= sqrt(2L * Cov_xx), |dy| <= sqrt(2L * Cov_yy) with Cov = Conic^-1.
+// Padded by 1 % + 0.01 px (the kernels use the hardware exp).  Purely a skip
+// test: a Gaussian outside a wave's quadrant by this box has alpha < 1/255 at
+// every pixel of it, so skipping it changes no result.
+__device__ __forceinline__ float2 footprint(float a, float b, float c, float opac) {
+    const float L = __logf(255.0f * opac);
+    const float det = a * c - b * b;
+    if (!(L > 0.f) || !(det > 0.f)) return make_float2(-1e30f, -1e30f);
+    const float k = 2.0f * L / det;
+    return make_float2(sqrtf(k * c) * 1.01f + 0.01f, sqrtf(k * a) * 1.01f + 0.01f);
+}
 
 template <int D>
 __global__ __launch_bounds__(256) void pack3_kernel(int64_t n, const float2* __restrict__ means2d,
@@ -70,19 +84,30 @@ __global__ __launch_bounds__(256) void pack3_kernel(int64_t n, const float2* __r
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
     const float2 m = means2d[g];
+    const float a = conics[g * 3], b = conics[g * 3 + 1], c = conics[g * 3 + 2], o = opacities[g];
+    const float2 ext = footprint(a, b, c, o);
     Rec3 r;
-    r.g0 = make_float4(m.x, m.y, conics[g * 3], conics[g * 3 + 1]);
-    r.g1 = make_float4(conics[g * 3 + 2], opacities[g], 0.f, 0.f);
-    float c[4] = {0.f, 0.f, 0.f, 0.f};
+    r.g0 = make_float4(m.x, m.y, a, b);
+    r.g1 = make_float4(c, o, ext.x, ext.y);
+    float col[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < D; ++k) c[k] = colors[g * D + k];
-    r.col = make_float4(c[0], c[1], c[2], c[3]);
+    for (int k = 0; k < D; ++k) col[k] = colors[g * D + k];
+    r.col = make_float4(col[0], col[1], col[2], col[3]);
     rec[g] = r;
+}
+
+// does the footprint box of (g0, g1) reach the 8x8 quadrant centred at (qx, qy)?
+__device__ __forceinline__ bool reaches(const float4 g0, const float4 g1, float qx, float qy) {
+    return fabsf(g0.x - qx) <= g1.z + 3.5f && fabsf(g0.y - qy) <= g1.w + 3.5f;
+}
+
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
 // one front-to-back compositing step, branch-free (predicated per lane)
 template <int D>
-__device__ __forceinline__ void fwd_step(const float4 g0, const float2 g1, const float4 c, int32_t idx, float px,
+__device__ __forceinline__ void fwd_step(const float4 g0, const float4 g1, const float4 c, int32_t idx, float px,
                                          float py, float& T, float (&acc)[4], int32_t& cur, bool& done) {
     const float dx = g0.x - px, dy = g0.y - py;
     const float sigma = 0.5f * (g0.z * dx * dx + g1.x * dy * dy) + g0.w * dx * dy;
@@ -106,12 +131,21 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
     const int32_t* __restrict__ offsets, int64_t n_isects, const int32_t* __restrict__ flatten_ids,
     float* __restrict__ render_colors, float* __restrict__ render_alphas, int32_t* __restrict__ last_ids) {
-    __shared__ float4 s_g0[kFwdBatch];
-    __shared__ float2 s_g1[kFwdBatch];
-    __shared__ float4 s_col[kFwdBatch];
+    // slot kFwdBatch is a zero-opacity dummy used to pad the per-wave lists
+    __shared__ float4 s_g0[kFwdBatch + 1];
+    __shared__ float4 s_g1[kFwdBatch + 1];
+    __shared__ float4 s_col[kFwdBatch + 1];
+    __shared__ uint16_t s_list[4][kFwdBatch + 4];
     __shared__ int s_vote[2][4];
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const float qx = (float)(tc.j - (lane & 7)) + 4.0f;   // centre of this wave's quadrant
+    const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
+    if (tid == 0) {
+        s_g0[kFwdBatch] = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_g1[kFwdBatch] = make_float4(0.f, 0.f, -1e30f, -1e30f);
+        s_col[kFwdBatch] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     float T = 1.0f;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     int32_t cur = 0;
@@ -129,6 +163,7 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
         n0 = r[0]; n1 = r[1]; n2 = r[2];
         nid = flatten_ids[min(tc.start + kFwdBatch + tid, last)];
     }
+    uint16_t* my_list = s_list[wave];
     for (int b = 0; b < nb; ++b) {
         // workgroup early-out vote (double-buffered slots; LDS-only barriers so the
         // prefetch loads stay in flight)
@@ -140,12 +175,8 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
         const int cnt = min(kFwdBatch, tc.end - bs);
         if (tid < cnt) {
             s_g0[tid] = n0;
-            s_g1[tid] = make_float2(n1.x, n1.y);
+            s_g1[tid] = n1;
             s_col[tid] = n2;
-        } else if (tid < ((cnt + 3) & ~3)) {  // pad to a multiple of 4 with zero-opacity dummies
-            s_g0[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
-            s_g1[tid] = make_float2(0.f, 0.f);
-            s_col[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         lds_barrier();
         // prefetch: records of batch b+1 (ids already here), ids of batch b+2
@@ -155,14 +186,27 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
             nid = flatten_ids[min(bs + 2 * kFwdBatch + tid, last)];
         }
         if (wave_done) continue;
-        for (int t = 0; t < cnt; t += 4) {
-            const float4 a0 = s_g0[t], a1 = s_g0[t + 1], a2 = s_g0[t + 2], a3 = s_g0[t + 3];
-            const float2 b0 = s_g1[t], b1 = s_g1[t + 1], b2 = s_g1[t + 2], b3 = s_g1[t + 3];
-            const float4 c0 = s_col[t], c1 = s_col[t + 1], c2 = s_col[t + 2], c3 = s_col[t + 3];
-            fwd_step<D>(a0, b0, c0, bs + t, tc.px, tc.py, T, acc, cur, done);
-            fwd_step<D>(a1, b1, c1, bs + t + 1, tc.px, tc.py, T, acc, cur, done);
-            fwd_step<D>(a2, b2, c2, bs + t + 2, tc.px, tc.py, T, acc, cur, done);
-            fwd_step<D>(a3, b3, c3, bs + t + 3, tc.px, tc.py, T, acc, cur, done);
+        // order-preserving compaction of the batch to the Gaussians that can reach
+        // this wave's quadrant (each lane tests 4 of them)
+        int n_mine = 0;
+#pragma unroll
+        for (int k = 0; k < kFwdBatch / 64; ++k) {
+            const int t = k * 64 + lane;
+            const bool rel = t < cnt && reaches(s_g0[t], s_g1[t], qx, qy);
+            const uint64_t m = __ballot(rel);
+            if (rel) my_list[n_mine + lanes_below(m)] = (uint16_t)t;
+            n_mine += __popcll(m);
+        }
+        if (lane < 4) my_list[n_mine + lane] = (uint16_t)kFwdBatch;  // pad to a multiple of 4
+        for (int i = 0; i < n_mine; i += 4) {
+            const int t0 = my_list[i], t1 = my_list[i + 1], t2 = my_list[i + 2], t3 = my_list[i + 3];
+            const float4 a0 = s_g0[t0], a1 = s_g0[t1], a2 = s_g0[t2], a3 = s_g0[t3];
+            const float4 b0 = s_g1[t0], b1 = s_g1[t1], b2 = s_g1[t2], b3 = s_g1[t3];
+            const float4 c0 = s_col[t0], c1 = s_col[t1], c2 = s_col[t2], c3 = s_col[t3];
+            fwd_step<D>(a0, b0, c0, bs + t0, tc.px, tc.py, T, acc, cur, done);
+            fwd_step<D>(a1, b1, c1, bs + t1, tc.px, tc.py, T, acc, cur, done);
+            fwd_step<D>(a2, b2, c2, bs + t2, tc.px, tc.py, T, acc, cur, done);
+            fwd_step<D>(a3, b3, c3, bs + t3, tc.px, tc.py, T, acc, cur, done);
             if (__all(done)) break;
         }
     }
@@ -190,13 +234,16 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     float* __restrict__ acc_rows) {
     constexpr int KV = 6 + D + (ABS ? 2 : 0);
     __shared__ float4 s_g0[kBwdBatch];
-    __shared__ float2 s_g1[kBwdBatch];
+    __shared__ float4 s_g1[kBwdBatch];
     __shared__ float4 s_col[kBwdBatch];
     __shared__ int32_t s_id[kBwdBatch];
     __shared__ float s_part[kBwdBatch * 4 * KV];
+    __shared__ uint8_t s_list[4][kBwdBatch];
     __shared__ int32_t s_last[4];
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
+    const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
     const float T_final = tc.inside ? 1.0f - render_alphas[tc.pix] : 1.0f;
     float T = T_final;
     float buf[4] = {0.f, 0.f, 0.f, 0.f}, vo[4] = {0.f, 0.f, 0.f, 0.f};
@@ -227,6 +274,9 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
         n0 = r[0]; n1 = r[1]; n2 = r[2];
         nid = flatten_ids[max(end - 1 - kBwdBatch - tid, tc.start)];
     }
+    using TR = TransposeReduce<KV>;
+    const int row = lane >> 4;
+    uint8_t* my_list = s_list[wave];
     for (int b = 0; b < nb; ++b) {
         const int32_t batch_end = end - 1 - b * kBwdBatch;
         const int bsz = min(kBwdBatch, batch_end + 1 - tc.start);
@@ -234,7 +284,7 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
         if (tid < bsz) {
             s_id[tid] = cid;
             s_g0[tid] = n0;
-            s_g1[tid] = make_float2(n1.x, n1.y);
+            s_g1[tid] = n1;
             s_col[tid] = n2;
         }
         for (int e = tid; e < kBwdBatch * 4 * KV; e += 256) s_part[e] = 0.f;
@@ -245,65 +295,71 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
             n0 = r[0]; n1 = r[1]; n2 = r[2];
             nid = flatten_ids[max(batch_end - 2 * kBwdBatch - tid, tc.start)];
         }
+        // order-preserving compaction to the Gaussians that reach this quadrant and
+        // are not behind every pixel's last contributor
         const int t0 = max(0, batch_end - wave_final);
-        using TR = TransposeReduce<KV>;
-        const int row = lane >> 4;
-        // LDS software pipeline: the next Gaussian's broadcast reads are issued
-        // before the current one is processed
-        float4 g0n = s_g0[min(t0, kBwdBatch - 1)];
-        float2 g1n = s_g1[min(t0, kBwdBatch - 1)];
-        float4 cn = s_col[min(t0, kBwdBatch - 1)];
-        for (int t = t0; t < bsz; ++t) {
-            const float4 g0 = g0n;
-            const float2 g1 = g1n;
-            const float4 c = cn;
-            const int tn = min(t + 1, kBwdBatch - 1);
-            g0n = s_g0[tn];
-            g1n = s_g1[tn];
-            cn = s_col[tn];
-            const float dx = g0.x - tc.px, dy = g0.y - tc.py;
-            const float sigma = 0.5f * (g0.z * dx * dx + g1.x * dy * dy) + g0.w * dx * dy;
-            const float vis = __expf(-sigma);
-            const float alpha = fminf(0.999f, g1.y * vis);
-            const bool valid = (batch_end - t <= bin_final) & (sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
-            if (!__any(valid)) continue;
-            const float ck[4] = {c.x, c.y, c.z, c.w};
-            const float ra = __builtin_amdgcn_rcpf(1.0f - alpha);
-            const float Tn = valid ? T * ra : T;
-            const float fac = valid ? alpha * Tn : 0.f;
-            float gv[KV];
-            float v_alpha = va_term * ra;
+        const bool rel = lane < bsz && lane >= t0 && reaches(s_g0[lane], s_g1[lane], qx, qy);
+        const uint64_t m = __ballot(rel);
+        if (rel) my_list[lanes_below(m)] = (uint8_t)lane;
+        const int n_mine = __popcll(m);
+        if (n_mine == 0) goto combine;
+        {
+            // LDS software pipeline: next Gaussian's broadcast reads issued early
+            int tn = my_list[0];
+            float4 g0n = s_g0[tn], g1n = s_g1[tn], cn = s_col[tn];
+            for (int i = 0; i < n_mine; ++i) {
+                const int t = tn;
+                const float4 g0 = g0n, g1 = g1n, c = cn;
+                tn = my_list[min(i + 1, n_mine - 1)];
+                g0n = s_g0[tn];
+                g1n = s_g1[tn];
+                cn = s_col[tn];
+                const float dx = g0.x - tc.px, dy = g0.y - tc.py;
+                const float sigma = 0.5f * (g0.z * dx * dx + g1.x * dy * dy) + g0.w * dx * dy;
+                const float vis = __expf(-sigma);
+                const float alpha = fminf(0.999f, g1.y * vis);
+                const bool valid = (batch_end - t <= bin_final) & (sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
+                if (!__any(valid)) continue;
+                const float ck[4] = {c.x, c.y, c.z, c.w};
+                const float ra = __builtin_amdgcn_rcpf(1.0f - alpha);
+                const float Tn = valid ? T * ra : T;
+                const float fac = valid ? alpha * Tn : 0.f;
+                float gv[KV];
+                float v_alpha = va_term * ra;
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                gv[6 + k] = fac * vo[k];
-                v_alpha += (ck[k] * Tn - buf[k] * ra) * vo[k];
-                buf[k] += ck[k] * fac;
-            }
-            const bool ok2 = valid & (g1.y * vis <= 0.999f);
-            const float v_sigma = ok2 ? -g1.y * vis * v_alpha : 0.f;
-            gv[0] = v_sigma * (g0.z * dx + g0.w * dy);
-            gv[1] = v_sigma * (g0.w * dx + g1.x * dy);
-            gv[2] = 0.5f * v_sigma * dx * dx;
-            gv[3] = v_sigma * dx * dy;
-            gv[4] = 0.5f * v_sigma * dy * dy;
-            gv[5] = ok2 ? vis * v_alpha : 0.f;
-            if (ABS) {
-                gv[6 + D] = fabsf(gv[0]);
-                gv[7 + D] = fabsf(gv[1]);
-            }
-            T = Tn;
-            float u[TR::G];
-            TR::run(gv, u);
-            if ((lane & 15) == 0) {
-                float* dst = s_part + (t * 4 + wave) * KV;
+                for (int k = 0; k < D; ++k) {
+                    gv[6 + k] = fac * vo[k];
+                    v_alpha += (ck[k] * Tn - buf[k] * ra) * vo[k];
+                    buf[k] += ck[k] * fac;
+                }
+                const bool ok2 = valid & (g1.y * vis <= 0.999f);
+                const float v_sigma = ok2 ? -g1.y * vis * v_alpha : 0.f;
+                gv[0] = v_sigma * (g0.z * dx + g0.w * dy);
+                gv[1] = v_sigma * (g0.w * dx + g1.x * dy);
+                gv[2] = 0.5f * v_sigma * dx * dx;
+                gv[3] = v_sigma * dx * dy;
+                gv[4] = 0.5f * v_sigma * dy * dy;
+                gv[5] = ok2 ? vis * v_alpha : 0.f;
+                if (ABS) {
+                    gv[6 + D] = fabsf(gv[0]);
+                    gv[7 + D] = fabsf(gv[1]);
+                }
+                T = Tn;
+                float u[TR::G];
+                TR::run(gv, u);
+                if ((lane & 15) == 0) {
+                    float* dst = s_part + (t * 4 + wave) * KV;
 #pragma unroll
-                for (int j = 0; j < TR::G; ++j) {
-                    const int i0 = TR::index(j, 0), i1 = TR::index(j, 1), i2 = TR::index(j, 2), i3 = TR::index(j, 3);
-                    const int idx = row == 0 ? i0 : row == 1 ? i1 : row == 2 ? i2 : i3;
-                    if (idx >= 0) dst[idx] = u[j];
+                    for (int j = 0; j < TR::G; ++j) {
+                        const int i0 = TR::index(j, 0), i1 = TR::index(j, 1), i2 = TR::index(j, 2),
+                                  i3 = TR::index(j, 3);
+                        const int idx = row == 0 ? i0 : row == 1 ? i1 : row == 2 ? i2 : i3;
+                        if (idx >= 0) dst[idx] = u[j];
+                    }
                 }
             }
         }
+    combine:
         lds_barrier();
         for (int e = tid; e < bsz * KV; e += 256) {
             const int t = e / KV, k = e - t * KV;
