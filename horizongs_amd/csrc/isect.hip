@@ -230,21 +230,132 @@ __global__ __launch_bounds__(256) void isect_emit_global_kernel(
 }
 
 // ---------------------------------------------------------------- stage 5
-__device__ __forceinline__ void bitonic_lds(uint64_t* s, int n) {
-    // n: power of two <= kSortCap; 256 lanes
-    for (int k = 2; k <= n; k <<= 1) {
+// Bitonic sort of 256*E keys held E per thread (thread t owns elements t*E..t*E+E-1).
+// Stages with j < E are register compare-exchanges.  The others pair thread t with
+// t ^ (j/E): inside a wave the partner's keys arrive by DPP (distance 1, 2, 8),
+// ds_swizzle (4, 16) or v_permlane32_swap (32) with no LDS memory traffic; only the
+// cross-wave stages (j/E >= 64; three of them at E = 8) go through LDS, whose
+// lane-contiguous layout s[r*256 + t] is free of bank conflicts.
+
+template <int PT>
+__device__ __forceinline__ uint32_t lane_xor32(uint32_t x) {
+    if constexpr (PT == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    else if constexpr (PT == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    else if constexpr (PT == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (4 << 10));  // xor 4
+    else if constexpr (PT == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
+    else if constexpr (PT == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (16 << 10));  // xor 16
+    else {
+        static_assert(PT == 32, "in-wave partner distance");
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (threadIdx.x & 32) ? r[0] : r[1];
+    }
+}
+
+// one in-wave exchange stage: every element meets its copy in lane t ^ PT
+template <int PT, int E>
+__device__ __forceinline__ void xchg_stage(uint64_t (&v)[E], bool keep_min) {
+    uint64_t p[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const uint32_t lo = lane_xor32<PT>((uint32_t)v[r]), hi = lane_xor32<PT>((uint32_t)(v[r] >> 32));
+        p[r] = ((uint64_t)hi << 32) | lo;
+    }
+#pragma unroll
+    for (int r = 0; r < E; ++r) v[r] = ((v[r] < p[r]) == keep_min) ? v[r] : p[r];  // keys are unique
+}
+
+template <int E>
+__device__ __forceinline__ void bitonic_regs(uint64_t (&v)[E], uint64_t* __restrict__ s) {
+    constexpr int N = 256 * E;
+    const int t = threadIdx.x;
+#pragma unroll 1
+    for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll 1
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < (n >> 1); i += 256) {
-                const int lo = 2 * j * (i / j) + (i % j);
-                const int hi = lo + j;
-                const uint64_t a = s[lo], b = s[hi];
-                const bool asc = (lo & k) == 0;
-                if ((a > b) == asc) {
-                    s[lo] = b;
-                    s[hi] = a;
+            if (j >= E) {
+                const int pt = j / E;
+                // the lower element of a pair keeps the min on ascending runs
+                const bool keep_min = (((t * E) & k) == 0) == ((t & pt) == 0);
+                if (pt >= 64) {
+                    lds_barrier();  // earlier reads of s are done
+#pragma unroll
+                    for (int r = 0; r < E; ++r) s[r * 256 + t] = v[r];
+                    lds_barrier();
+                    const int q = t ^ pt;
+#pragma unroll
+                    for (int r = 0; r < E; ++r) {
+                        const uint64_t p = s[r * 256 + q];
+                        v[r] = ((v[r] < p) == keep_min) ? v[r] : p;
+                    }
+                } else {
+                    switch (pt) {
+                    case 1: xchg_stage<1, E>(v, keep_min); break;
+                    case 2: xchg_stage<2, E>(v, keep_min); break;
+                    case 4: xchg_stage<4, E>(v, keep_min); break;
+                    case 8: xchg_stage<8, E>(v, keep_min); break;
+                    case 16: xchg_stage<16, E>(v, keep_min); break;
+                    default: xchg_stage<32, E>(v, keep_min); break;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < E; ++r) {
+                    if (r & j) continue;
+                    const bool asc = (((t * E + r) & k) == 0);
+                    const uint64_t a = v[r], b = v[r + j];
+                    const bool keep = (a < b) == asc;
+                    v[r] = keep ? a : b;
+                    v[r + j] = keep ? b : a;
                 }
             }
-            __syncthreads();
+        }
+    }
+    lds_barrier();
+}
+
+// load n <= 256*E keys (any order: the input is unsorted) lane-contiguously,
+// padding with ~0, and sort them; thread t ends holding sorted elements t*E..t*E+E-1
+template <int E>
+__device__ __forceinline__ void sort_chunk(const uint64_t* src, int n, uint64_t* s, uint64_t (&v)[E]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = r * 256 + t;
+        v[r] = i < n ? src[i] : ~0ull;
+    }
+    bitonic_regs<E>(v, s);
+}
+
+// back to lane-contiguous order through LDS so the global stores coalesce; the
+// row pitch of 260 keys keeps the transposed reads within two-way bank sharing
+constexpr int kSortPitch = 260;
+template <int E>
+__device__ __forceinline__ void untranspose(uint64_t (&v)[E], uint64_t* s) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < E; ++r) s[r * kSortPitch + t] = v[r];
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = r * 256 + t;
+        v[r] = s[(i % E) * kSortPitch + i / E];
+    }
+    lds_barrier();
+}
+
+template <int E>
+__device__ __forceinline__ void sort_and_emit(const uint64_t* keys, int n, uint64_t* s, int64_t hi,
+                                              int64_t* __restrict__ isect_ids, int32_t* __restrict__ flatten_ids) {
+    uint64_t v[E];
+    sort_chunk<E>(keys, n, s, v);
+    untranspose<E>(v, s);
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = r * 256 + t;
+        if (i < n) {
+            isect_ids[i] = hi | (int64_t)(v[r] >> 32);
+            flatten_ids[i] = (int32_t)(uint32_t)v[r];
         }
     }
 }
@@ -277,7 +388,7 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(int n_bins, int n_tiles,
                                                         uint64_t* __restrict__ tmp,
                                                         int64_t* __restrict__ isect_ids,
                                                         int32_t* __restrict__ flatten_ids) {
-    __shared__ uint64_t s_keys[kSortCap];
+    __shared__ uint64_t s_keys[8 * kSortPitch];
     const int bin = blockIdx.x;
     const int64_t start = offsets[bin];
     const int64_t end = bin + 1 < n_bins ? (int64_t)offsets[bin + 1] : n_isects;
@@ -286,16 +397,10 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(int n_bins, int n_tiles,
     const int cam = bin / n_tiles, tile = bin - cam * n_tiles;
     const int64_t hi = ((int64_t)cam << (32 + tile_bits)) | ((int64_t)tile << 32);
     if (n <= kSortCap) {
-        int npow = 1;
-        while (npow < n) npow <<= 1;
-        for (int i = threadIdx.x; i < npow; i += 256) s_keys[i] = i < n ? keys[start + i] : ~0ull;
-        __syncthreads();
-        bitonic_lds(s_keys, npow);
-        for (int i = threadIdx.x; i < n; i += 256) {
-            const uint64_t k = s_keys[i];
-            isect_ids[start + i] = hi | (int64_t)(k >> 32);
-            flatten_ids[start + i] = (int32_t)(uint32_t)k;
-        }
+        if (n <= 256) sort_and_emit<1>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
+        else if (n <= 512) sort_and_emit<2>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
+        else if (n <= 1024) sort_and_emit<4>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
+        else sort_and_emit<8>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         return;
     }
     // large bin: LDS-sorted chunks, then merge passes ping-ponging keys <-> tmp
@@ -303,12 +408,16 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(int n_bins, int n_tiles,
     uint64_t* b = tmp + start;
     for (int c0 = 0; c0 < n; c0 += kSortCap) {
         const int cn = min(kSortCap, n - c0);
-        for (int i = threadIdx.x; i < kSortCap; i += 256) s_keys[i] = i < cn ? a[c0 + i] : ~0ull;
-        __syncthreads();
-        bitonic_lds(s_keys, kSortCap);
-        for (int i = threadIdx.x; i < cn; i += 256) a[c0 + i] = s_keys[i];
-        __syncthreads();
+        uint64_t v[8];
+        sort_chunk<8>(a + c0, cn, s_keys, v);
+        untranspose<8>(v, s_keys);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int i = r * 256 + threadIdx.x;
+            if (i < cn) a[c0 + i] = v[r];
+        }
     }
+    __syncthreads();
     for (int L = kSortCap; L < n; L <<= 1) {
         for (int p = 0; p < n; p += 2 * L) {
             const int la = min(L, n - p);

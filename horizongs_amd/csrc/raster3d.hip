@@ -23,7 +23,7 @@
 namespace hgsr {
 
 constexpr int kFwdBatch = 256;
-constexpr int kBwdBatch = 64;
+constexpr int kBwdBatch = 128;
 constexpr int kRec3 = 16;  // floats per accumulator row: xy(2) conic(3) opac(1) color(D<=4) absxy(2)
 
 struct TileCtx {
@@ -225,7 +225,7 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
     return v;
 }
 
-template <int D, bool ABS>
+template <int D, bool ABS, bool DIAG_NOATOM = false>
 __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
     const int32_t* __restrict__ offsets, int64_t n_isects, const int32_t* __restrict__ flatten_ids,
@@ -233,12 +233,15 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
     float* __restrict__ acc_rows) {
     constexpr int KV = 6 + D + (ABS ? 2 : 0);
-    __shared__ float4 s_g0[kBwdBatch];
-    __shared__ float4 s_g1[kBwdBatch];
-    __shared__ float4 s_col[kBwdBatch];
-    __shared__ int32_t s_id[kBwdBatch];
-    __shared__ float s_part[kBwdBatch * 4 * KV];
-    __shared__ uint8_t s_list[4][kBwdBatch];
+    constexpr int NB = kBwdBatch;
+    // double-buffered staging: batch b+1 is staged while batch b's partials are
+    // combined, so each batch costs two barriers
+    __shared__ float4 s_g0[2][NB];
+    __shared__ float4 s_g1[2][NB];
+    __shared__ float4 s_col[2][NB];
+    __shared__ int32_t s_id[2][NB];
+    __shared__ float s_part[NB * KV];  // the four waves' partials merged with LDS float atomics
+    __shared__ uint8_t s_list[4][NB];
     __shared__ int32_t s_last[4];
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -246,7 +249,9 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
     const float T_final = tc.inside ? 1.0f - render_alphas[tc.pix] : 1.0f;
     float T = T_final;
-    float buf[4] = {0.f, 0.f, 0.f, 0.f}, vo[4] = {0.f, 0.f, 0.f, 0.f};
+    // B = sum_k buf_k * vo_k, the upstream-weighted colour composited behind the
+    // current Gaussian: v_alpha only ever needs this dot product, never buf_k itself
+    float B = 0.f, vo[4] = {0.f, 0.f, 0.f, 0.f};
     float bg_dot = 0.f;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
@@ -258,62 +263,87 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
     const int32_t wave_final = wave_max_i32(bin_final);
     if (lane == 0) s_last[wave] = wave_final;
+    for (int e = tid; e < NB * KV; e += 256) s_part[e] = 0.f;
     lds_barrier();
     const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
     // Gaussians after the block's last contributor are never reached
     const int32_t end = min(tc.end, blk_final + 1);
-    const int nb = end > tc.start ? (end - tc.start + kBwdBatch - 1) / kBwdBatch : 0;
+    const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
     // two-deep software pipeline (ids two batches ahead, records one), clamped
-    // unconditional loads; only lanes < kBwdBatch load
+    // unconditional loads; lanes < NB load one Gaussian each
     float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
     int32_t cid = 0, nid = 0;
-    const bool loader = tid < kBwdBatch;
+    const bool loader = tid < NB;
     if (nb > 0 && loader) {
         cid = flatten_ids[max(end - 1 - tid, tc.start)];
         const float4* r = reinterpret_cast<const float4*>(rec + cid);
         n0 = r[0]; n1 = r[1]; n2 = r[2];
-        nid = flatten_ids[max(end - 1 - kBwdBatch - tid, tc.start)];
+        nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
     }
     using TR = TransposeReduce<KV>;
     const int row = lane >> 4;
     uint8_t* my_list = s_list[wave];
-    for (int b = 0; b < nb; ++b) {
-        const int32_t batch_end = end - 1 - b * kBwdBatch;
-        const int bsz = min(kBwdBatch, batch_end + 1 - tc.start);
-        lds_barrier();  // previous batch's partials consumed (its atomics stay in flight)
+    int prev_bsz = 0;
+    for (int b = 0; b <= nb; ++b) {
+        const int cur = b & 1, prv = cur ^ 1;
+        const int32_t batch_end = end - 1 - b * NB;
+        const int bsz = b < nb ? min(NB, batch_end + 1 - tc.start) : 0;
+        // phase 1 (after the previous barrier): stage batch b, issue the loads of
+        // batch b+1, then combine batch b-1.  The atomics go last so that the next
+        // wait on prefetched loads (they share the vector-memory counter) finds
+        // them a whole batch old.
         if (tid < bsz) {
-            s_id[tid] = cid;
-            s_g0[tid] = n0;
-            s_g1[tid] = n1;
-            s_col[tid] = n2;
+            s_id[cur][tid] = cid;
+            s_g0[cur][tid] = n0;
+            s_g1[cur][tid] = n1;
+            s_col[cur][tid] = n2;
         }
-        for (int e = tid; e < kBwdBatch * 4 * KV; e += 256) s_part[e] = 0.f;
-        lds_barrier();
-        if (loader) {
+        if (b < nb && loader) {
             cid = nid;
             const float4* r = reinterpret_cast<const float4*>(rec + cid);
             n0 = r[0]; n1 = r[1]; n2 = r[2];
-            nid = flatten_ids[max(batch_end - 2 * kBwdBatch - tid, tc.start)];
+            nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
+        if (b > 0) {
+            for (int e = tid; e < prev_bsz * KV; e += 256) {
+                const int t = e / KV, k = e - t * KV;
+                const float sv = s_part[e];
+                s_part[e] = 0.f;
+                if (sv != 0.f) {
+                    if (DIAG_NOATOM) acc_rows[(int64_t)s_id[prv][t] * kRec3 + k] = sv;  // measurement build only
+                    else atomicAdd(acc_rows + (int64_t)s_id[prv][t] * kRec3 + k, sv);
+                }
+            }
+        }
+        if (b == nb) break;
+        lds_barrier();
+        // phase 2: composite batch b
         // order-preserving compaction to the Gaussians that reach this quadrant and
         // are not behind every pixel's last contributor
         const int t0 = max(0, batch_end - wave_final);
-        const bool rel = lane < bsz && lane >= t0 && reaches(s_g0[lane], s_g1[lane], qx, qy);
-        const uint64_t m = __ballot(rel);
-        if (rel) my_list[lanes_below(m)] = (uint8_t)lane;
-        const int n_mine = __popcll(m);
-        if (n_mine == 0) goto combine;
-        {
-            // LDS software pipeline: next Gaussian's broadcast reads issued early
-            int tn = my_list[0];
-            float4 g0n = s_g0[tn], g1n = s_g1[tn], cn = s_col[tn];
+        int n_mine = 0;
+#pragma unroll
+        for (int k = 0; k < NB / 64; ++k) {
+            const int t = k * 64 + lane;
+            const bool rel = t < bsz && t >= t0 && reaches(s_g0[cur][t], s_g1[cur][t], qx, qy);
+            const uint64_t m = __ballot(rel);
+            if (rel) my_list[n_mine + lanes_below(m)] = (uint8_t)t;
+            n_mine += __popcll(m);
+        }
+        if (n_mine > 0) {
+            // the list comes back into registers once per batch; the loop reads
+            // entries with readlane so no LDS index read sits on the critical path
+            const int lst0 = my_list[lane], lst1 = my_list[64 + lane];
+            int tn = __builtin_amdgcn_readfirstlane(lst0);
+            float4 g0n = s_g0[cur][tn], g1n = s_g1[cur][tn], cn = s_col[cur][tn];
             for (int i = 0; i < n_mine; ++i) {
                 const int t = tn;
                 const float4 g0 = g0n, g1 = g1n, c = cn;
-                tn = my_list[min(i + 1, n_mine - 1)];
-                g0n = s_g0[tn];
-                g1n = s_g1[tn];
-                cn = s_col[tn];
+                const int inext = min(i + 1, n_mine - 1);
+                tn = __builtin_amdgcn_readlane(inext < 64 ? lst0 : lst1, inext & 63);
+                g0n = s_g0[cur][tn];
+                g1n = s_g1[cur][tn];
+                cn = s_col[cur][tn];
                 const float dx = g0.x - tc.px, dy = g0.y - tc.py;
                 const float sigma = 0.5f * (g0.z * dx * dx + g1.x * dy * dy) + g0.w * dx * dy;
                 const float vis = __expf(-sigma);
@@ -325,13 +355,13 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
                 const float Tn = valid ? T * ra : T;
                 const float fac = valid ? alpha * Tn : 0.f;
                 float gv[KV];
-                float v_alpha = va_term * ra;
+                float cv = ck[0] * vo[0];
 #pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    gv[6 + k] = fac * vo[k];
-                    v_alpha += (ck[k] * Tn - buf[k] * ra) * vo[k];
-                    buf[k] += ck[k] * fac;
-                }
+                for (int k = 1; k < D; ++k) cv += ck[k] * vo[k];
+#pragma unroll
+                for (int k = 0; k < D; ++k) gv[6 + k] = fac * vo[k];
+                const float v_alpha = Tn * cv + ra * (va_term - B);
+                B += fac * cv;
                 const bool ok2 = valid & (g1.y * vis <= 0.999f);
                 const float v_sigma = ok2 ? -g1.y * vis * v_alpha : 0.f;
                 gv[0] = v_sigma * (g0.z * dx + g0.w * dy);
@@ -348,25 +378,19 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
                 float u[TR::G];
                 TR::run(gv, u);
                 if ((lane & 15) == 0) {
-                    float* dst = s_part + (t * 4 + wave) * KV;
+                    float* dst = s_part + t * KV;
 #pragma unroll
                     for (int j = 0; j < TR::G; ++j) {
                         const int i0 = TR::index(j, 0), i1 = TR::index(j, 1), i2 = TR::index(j, 2),
                                   i3 = TR::index(j, 3);
                         const int idx = row == 0 ? i0 : row == 1 ? i1 : row == 2 ? i2 : i3;
-                        if (idx >= 0) dst[idx] = u[j];
+                        if (idx >= 0) atomicAdd(dst + idx, u[j]);  // ds_add_f32
                     }
                 }
             }
         }
-    combine:
+        prev_bsz = bsz;
         lds_barrier();
-        for (int e = tid; e < bsz * KV; e += 256) {
-            const int t = e / KV, k = e - t * KV;
-            const float* p = s_part + t * 4 * KV + k;
-            const float s = p[0] + p[KV] + p[2 * KV] + p[3 * KV];
-            if (s != 0.f) atomicAdd(acc_rows + (int64_t)s_id[t] * kRec3 + k, s);
-        }
     }
 }
 
@@ -463,6 +487,38 @@ extern "C" int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, cons
     }
 #undef LAUNCH_F
     return check_launch("raster3d_fwd");
+}
+
+// Measurement-only: time the backward kernel with its float atomics replaced by
+// plain stores (wrong gradients), to price the atomic traffic.  bench.py --diag.
+extern "C" double hgsr_diag_raster3d_bwd_noatomic_ms(int C, int N, const float* rows_ws, const void* rec_ws,
+                                                      int width, int height, int tile_w, int tile_h,
+                                                      const int32_t* isect_offsets, int64_t n_isects,
+                                                      const int32_t* flatten_ids, const float* render_alphas,
+                                                      const int32_t* last_ids, const float* v_render_colors,
+                                                      const float* v_render_alphas, int noatom,
+                                                      hgsr_stream_t stream) {
+    hipStream_t s = as_stream(stream);
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    const dim3 grid(C * tile_w * tile_h);
+    (void)hipEventRecord(a, s);
+    if (noatom)
+        hipLaunchKernelGGL((raster3d_bwd_kernel<4, false, true>), grid, dim3(256), 0, s, C, width, height, tile_w,
+                           tile_h, (const Rec3*)rec_ws, nullptr, isect_offsets, n_isects, flatten_ids, render_alphas,
+                           last_ids, v_render_colors, v_render_alphas, (float*)rows_ws);
+    else
+        hipLaunchKernelGGL((raster3d_bwd_kernel<4, false, false>), grid, dim3(256), 0, s, C, width, height, tile_w,
+                           tile_h, (const Rec3*)rec_ws, nullptr, isect_offsets, n_isects, flatten_ids, render_alphas,
+                           last_ids, v_render_colors, v_render_alphas, (float*)rows_ws);
+    (void)hipEventRecord(b, s);
+    (void)hipEventSynchronize(b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return ms;
 }
 
 extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D) {
