@@ -230,100 +230,105 @@ __global__ __launch_bounds__(256) void isect_emit_global_kernel(
 }
 
 // ---------------------------------------------------------------- stage 5
-// Bitonic sort of 256*E keys held E per thread (thread t owns elements t*E..t*E+E-1).
-// Stages with j < E are register compare-exchanges.  The others pair thread t with
-// t ^ (j/E): inside a wave the partner's keys arrive by DPP (distance 1, 2, 8),
-// ds_swizzle (4, 16) or v_permlane32_swap (32) with no LDS memory traffic; only the
-// cross-wave stages (j/E >= 64; three of them at E = 8) go through LDS, whose
-// lane-contiguous layout s[r*256 + t] is free of bank conflicts.
-
-template <int PT>
+// Bitonic sort of 256*E keys held E per thread (thread t owns elements t*E..t*E+E-1),
+// in the "flip" form where every comparator is ascending: merge level K opens with
+// the mirror stage (i <-> i ^ (K-1)) and continues with i <-> i ^ J for J = K/4..1.
+// Padding keys (~0) start in the suffix and a comparator never moves one down, so
+// a wave whose elements are all padding skips every stage except the cross-wave
+// LDS exchanges it must still feed.  Partners inside a thread are registers; inside
+// a wave they arrive by DPP / ds_swizzle / v_permlane32_swap (no LDS memory); only
+// partners in another wave go through LDS (lane-contiguous, conflict-free layout).
+// The network is unrolled at compile time.
+template <int M>
 __device__ __forceinline__ uint32_t lane_xor32(uint32_t x) {
-    if constexpr (PT == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    else if constexpr (PT == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-    else if constexpr (PT == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (4 << 10));  // xor 4
-    else if constexpr (PT == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
-    else if constexpr (PT == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (16 << 10));  // xor 16
-    else {
-        static_assert(PT == 32, "in-wave partner distance");
+    if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    else if constexpr (M == 3) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x1B, 0xF, 0xF, false);  // quad_perm [3,2,1,0]
+    else if constexpr (M == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (4 << 10));
+    else if constexpr (M == 7) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
+    else if constexpr (M == 15) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);  // row_mirror
+    else if constexpr (M == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (16 << 10));
+    else if constexpr (M == 31) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (31 << 10));
+    else if constexpr (M == 32) {
         const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
         return (threadIdx.x & 32) ? r[0] : r[1];
+    } else {
+        static_assert(M == 63, "in-wave partner mask");
+        return lane_xor32<31>(lane_xor32<32>(x));
     }
 }
 
-// one in-wave exchange stage: every element meets its copy in lane t ^ PT
-template <int PT, int E>
-__device__ __forceinline__ void xchg_stage(uint64_t (&v)[E], bool keep_min) {
+template <int M>
+__device__ __forceinline__ uint64_t lane_xor64(uint64_t x) {
+    const uint32_t lo = lane_xor32<M>((uint32_t)x), hi = lane_xor32<M>((uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// cross-thread stage: partner thread t ^ M, partner slot r (FLIP: E-1-r); the lower
+// thread of the pair (t & LOWBIT == 0) keeps the minimum.  Keys are unique.
+template <int E, int M, int LOWBIT, bool FLIP>
+__device__ __forceinline__ void thread_stage(uint64_t (&v)[E], uint64_t* __restrict__ s, bool active) {
+    const int t = threadIdx.x;
+    const bool keep_min = (t & LOWBIT) == 0;
     uint64_t p[E];
+    if constexpr (M >= 64) {
+        lds_barrier();  // earlier reads of s are done
 #pragma unroll
-    for (int r = 0; r < E; ++r) {
-        const uint32_t lo = lane_xor32<PT>((uint32_t)v[r]), hi = lane_xor32<PT>((uint32_t)(v[r] >> 32));
-        p[r] = ((uint64_t)hi << 32) | lo;
+        for (int r = 0; r < E; ++r) s[r * 256 + t] = v[r];
+        lds_barrier();
+        if (!active) return;
+#pragma unroll
+        for (int r = 0; r < E; ++r) p[r] = s[(FLIP ? E - 1 - r : r) * 256 + (t ^ M)];
+    } else {
+        if (!active) return;
+#pragma unroll
+        for (int r = 0; r < E; ++r) p[r] = lane_xor64<M>(v[FLIP ? E - 1 - r : r]);
     }
 #pragma unroll
-    for (int r = 0; r < E; ++r) v[r] = ((v[r] < p[r]) == keep_min) ? v[r] : p[r];  // keys are unique
+    for (int r = 0; r < E; ++r) v[r] = ((v[r] < p[r]) == keep_min) ? v[r] : p[r];
+}
+
+// in-thread stage over aligned groups of G slots: FLIP pairs r <-> r ^ (G-1), else r <-> r + G/2
+template <int E, int G, bool FLIP>
+__device__ __forceinline__ void reg_stage(uint64_t (&v)[E], bool active) {
+    if (!active) return;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        if (r & (G / 2)) continue;
+        const int q = FLIP ? (r ^ (G - 1)) : (r + G / 2);
+        const uint64_t a = v[r], b = v[q];
+        const bool keep = a < b;
+        v[r] = keep ? a : b;
+        v[q] = keep ? b : a;
+    }
+}
+
+template <int E, int K, int J>
+__device__ __forceinline__ void half_stages(uint64_t (&v)[E], uint64_t* s, bool active) {
+    if constexpr (J >= 1) {
+        if constexpr (J >= E) thread_stage<E, J / E, J / E, false>(v, s, active);
+        else reg_stage<E, 2 * J, false>(v, active);
+        half_stages<E, K, J / 2>(v, s, active);
+    }
+}
+
+template <int E, int K>
+__device__ __forceinline__ void merge_levels(uint64_t (&v)[E], uint64_t* s, bool active) {
+    if constexpr (K <= 256 * E) {
+        if constexpr (K <= E) reg_stage<E, K, true>(v, active);
+        else thread_stage<E, K / E - 1, K / (2 * E), true>(v, s, active);
+        half_stages<E, K, K / 4>(v, s, active);
+        merge_levels<E, 2 * K>(v, s, active);
+    }
 }
 
 template <int E>
-__device__ __forceinline__ void bitonic_regs(uint64_t (&v)[E], uint64_t* __restrict__ s) {
-    constexpr int N = 256 * E;
-    const int t = threadIdx.x;
-#pragma unroll 1
-    for (int k = 2; k <= N; k <<= 1) {
-#pragma unroll 1
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j >= E) {
-                const int pt = j / E;
-                // the lower element of a pair keeps the min on ascending runs
-                const bool keep_min = (((t * E) & k) == 0) == ((t & pt) == 0);
-                if (pt >= 64) {
-                    lds_barrier();  // earlier reads of s are done
-#pragma unroll
-                    for (int r = 0; r < E; ++r) s[r * 256 + t] = v[r];
-                    lds_barrier();
-                    const int q = t ^ pt;
-#pragma unroll
-                    for (int r = 0; r < E; ++r) {
-                        const uint64_t p = s[r * 256 + q];
-                        v[r] = ((v[r] < p) == keep_min) ? v[r] : p;
-                    }
-                } else {
-                    switch (pt) {
-                    case 1: xchg_stage<1, E>(v, keep_min); break;
-                    case 2: xchg_stage<2, E>(v, keep_min); break;
-                    case 4: xchg_stage<4, E>(v, keep_min); break;
-                    case 8: xchg_stage<8, E>(v, keep_min); break;
-                    case 16: xchg_stage<16, E>(v, keep_min); break;
-                    default: xchg_stage<32, E>(v, keep_min); break;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < E; ++r) {
-                    if (r & j) continue;
-                    const bool asc = (((t * E + r) & k) == 0);
-                    const uint64_t a = v[r], b = v[r + j];
-                    const bool keep = (a < b) == asc;
-                    v[r] = keep ? a : b;
-                    v[r + j] = keep ? b : a;
-                }
-            }
-        }
-    }
+__device__ __forceinline__ void bitonic_regs(uint64_t (&v)[E], uint64_t* __restrict__ s, int n) {
+    // a wave holds elements [wave*64*E, (wave+1)*64*E)
+    const bool active = (int)(threadIdx.x >> 6) * 64 * E < n;
+    merge_levels<E, 2>(v, s, active);
     lds_barrier();
-}
-
-// load n <= 256*E keys (any order: the input is unsorted) lane-contiguously,
-// padding with ~0, and sort them; thread t ends holding sorted elements t*E..t*E+E-1
-template <int E>
-__device__ __forceinline__ void sort_chunk(const uint64_t* src, int n, uint64_t* s, uint64_t (&v)[E]) {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int r = 0; r < E; ++r) {
-        const int i = r * 256 + t;
-        v[r] = i < n ? src[i] : ~0ull;
-    }
-    bitonic_regs<E>(v, s);
 }
 
 // back to lane-contiguous order through LDS so the global stores coalesce; the
@@ -341,6 +346,36 @@ __device__ __forceinline__ void untranspose(uint64_t (&v)[E], uint64_t* s) {
         v[r] = s[(i % E) * kSortPitch + i / E];
     }
     lds_barrier();
+}
+
+// inverse of untranspose: lane-contiguous element i = r*256 + t -> thread i/E, slot i%E
+template <int E>
+__device__ __forceinline__ void to_blocked(uint64_t (&v)[E], uint64_t* s) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = r * 256 + t;
+        s[(i % E) * kSortPitch + i / E] = v[r];
+    }
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < E; ++r) v[r] = s[r * kSortPitch + t];
+    lds_barrier();
+}
+
+// load n <= 256*E keys (any order: the input is unsorted) lane-contiguously,
+// padding with ~0, and sort them; thread t ends holding sorted elements t*E..t*E+E-1
+template <int E>
+__device__ __forceinline__ void sort_chunk(const uint64_t* src, int n, uint64_t* s, uint64_t (&v)[E]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = r * 256 + t;
+        v[r] = i < n ? src[i] : ~0ull;
+    }
+    // the network wants the padding in the suffix of the blocked order t*E + r
+    to_blocked<E>(v, s);
+    bitonic_regs<E>(v, s, n);
 }
 
 template <int E>
