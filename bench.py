@@ -138,11 +138,13 @@ def raster_pairs(wl):
         r1 = torch.empty((C, H, W, 1), device=dev)
         r2 = torch.empty((C, H, W, 1), device=dev)
         med = torch.empty((C, H, W), dtype=torch.int32, device=dev)
+        ws_b = NAT.size_query("hgsr_raster2d_fwd_ws_bytes", C, wl.args.n, 4)
+        ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
         NAT.call("hgsr_raster2d_fwd", C, wl.args.n, 4, NAT.ptr(m2),
                  NAT.ptr(meta["ray_transforms"].detach().reshape(C, -1, 9).contiguous()), NAT.ptr(cols),
                  NAT.ptr(opac), NAT.ptr(meta["normals"].detach().contiguous()), None, W, H, 16, tw, th,
                  NAT.ptr(meta["isect_offsets"]), n_isects, NAT.ptr(fl), NAT.ptr(rc), NAT.ptr(ra), NAT.ptr(rn),
-                 NAT.ptr(r1), NAT.ptr(r2), NAT.ptr(last), NAT.ptr(med), NAT.stream(dev))
+                 NAT.ptr(r1), NAT.ptr(r2), NAT.ptr(last), NAT.ptr(med), NAT.ptr(ws), ws_b, NAT.stream(dev))
     # per-tile max last id (tile-major reduction on the host side of torch ops)
     hp, wp = th * 16, tw * 16
     lp = torch.full((C, hp, wp), -1, dtype=torch.int64, device=dev)

@@ -13,8 +13,8 @@
 namespace hgsr {
 
 constexpr int kFwd2Batch = 128;
-constexpr int kBwd2Batch = 32;
-constexpr int kRec2 = 32;  // xy(2) rt(9) opac(1) normal(3) densify(2) color(D<=4) absxy(2)
+constexpr int kBwd2Batch = 64;
+constexpr int kRec2 = 32;  // floats per accumulator row: xy(2) rt(9) opac(1) normal(3) densify(2) color(D<=4) absxy(2)
 
 struct Tile2 {
     int cam, tile, i, j;
@@ -45,89 +45,208 @@ __device__ __forceinline__ Tile2 tile2_ctx(int C, int W, int H, int tw, int th,
     return t;
 }
 
-struct SurfelRec {
-    float u[3], v[3], w[3];
-    float mx, my, opac;
+// 96-B raster record of one (camera, surfel); rows u, v, w of the ray transform
+struct Rec2 {
+    float4 r0;  // u0 u1 u2 w0
+    float4 r1;  // v0 v1 v2 w1
+    float4 r2;  // w2 mean_x mean_y opacity
+    float4 col; // colour (D <= 4, zero padded; the last channel is the depth in RGB+ED)
+    float4 r4;  // normal xyz, low-pass disk radius
+    float4 box; // centre xy and half-extents of the surfel ellipse's screen bounding box
 };
 
-__device__ __forceinline__ void stage_surfel(float* s, int64_t g, const float2* __restrict__ means2d,
-                                             const float* __restrict__ rt, const float* __restrict__ opac) {
-    const float* M = rt + g * 9;
+// Skip-test geometry.  alpha >= 1/255 needs sigma = min(|s|^2, 2|m-p|^2)/2 <= L =
+// ln(255 o), i.e. either the ray-plane hit s lies in the UV disk of radius
+// sqrt(2L) or p lies within sqrt(L) of the projected centre.  The disk projects to
+// the conic with dual Q* = M diag(R^2, R^2, -1) M^T (M = [u; v; w]); while Q*_22 < 0
+// it is an ellipse whose bounding box is centre Q*_i2/Q*_22, half-extent
+// sqrt(c_i^2 - Q*_ii/Q*_22).  Near-degenerate views (plane through the camera)
+// get an unbounded box.  Evaluated in f64 and padded (1 % + 0.01 px) because the
+// kernels use the hardware exp/rcp; it only ever skips pairs with alpha < 1/255.
+__device__ __forceinline__ void surfel_footprint(const float* u, const float* v, const float* w, float opac,
+                                                 float4& box, float& disk) {
+    const float L = __logf(255.0f * opac);
+    if (!(L > 0.f)) {
+        box = make_float4(0.f, 0.f, -1e30f, -1e30f);
+        disk = -1e30f;
+        return;
+    }
+    disk = sqrtf(L) * 1.01f + 0.01f;
+    const double R2 = 2.0 * (double)L;
+    const double f[3] = {R2, R2, -1.0};
+    double q00 = 0, q02 = 0, q11 = 0, q12 = 0, q22 = 0;
+    for (int k = 0; k < 3; ++k) {
+        q00 += (double)u[k] * u[k] * f[k];
+        q02 += (double)u[k] * w[k] * f[k];
+        q11 += (double)v[k] * v[k] * f[k];
+        q12 += (double)v[k] * w[k] * f[k];
+        q22 += (double)w[k] * w[k] * f[k];
+    }
+    const double w2 = (double)w[2] * w[2];
+    if (!(q22 < -1e-3 * w2)) {
+        box = make_float4(0.f, 0.f, 1e30f, 1e30f);
+        return;
+    }
+    const double cx = q02 / q22, cy = q12 / q22;
+    const double ex2 = cx * cx - q00 / q22, ey2 = cy * cy - q11 / q22;
+    const double ex = sqrt(fmax(ex2, 0.0)), ey = sqrt(fmax(ey2, 0.0));
+    box = make_float4((float)cx, (float)cy, (float)(ex * 1.01 + 0.01 + 1e-6 * fabs(cx)),
+                      (float)(ey * 1.01 + 0.01 + 1e-6 * fabs(cy)));
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void pack2_kernel(int64_t n, const float2* __restrict__ means2d,
+                                                    const float* __restrict__ rt, const float* __restrict__ colors,
+                                                    const float* __restrict__ opacities,
+                                                    const float* __restrict__ normals, Rec2* __restrict__ rec) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    float M[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) s[k] = M[k];
+    for (int k = 0; k < 9; ++k) M[k] = rt[g * 9 + k];
     const float2 m = means2d[g];
-    s[9] = m.x;
-    s[10] = m.y;
-    s[11] = opac[g];
+    const float o = opacities[g];
+    float4 box;
+    float disk;
+    surfel_footprint(M, M + 3, M + 6, o, box, disk);
+    Rec2 r;
+    r.r0 = make_float4(M[0], M[1], M[2], M[6]);
+    r.r1 = make_float4(M[3], M[4], M[5], M[7]);
+    r.r2 = make_float4(M[8], m.x, m.y, o);
+    float col[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < D; ++k) col[k] = colors[g * D + k];
+    r.col = make_float4(col[0], col[1], col[2], col[3]);
+    r.r4 = make_float4(normals[g * 3], normals[g * 3 + 1], normals[g * 3 + 2], disk);
+    r.box = box;
+    rec[g] = r;
+}
+
+// does the surfel's skip geometry reach the 8x8 quadrant centred at (qx, qy)?
+__device__ __forceinline__ bool reaches2(const float4 r2, const float4 r4, const float4 box, float qx, float qy) {
+    const bool in_box = fabsf(box.x - qx) <= box.z + 3.5f && fabsf(box.y - qy) <= box.w + 3.5f;
+    const bool in_disk = fabsf(r2.y - qx) <= r4.w + 3.5f && fabsf(r2.z - qy) <= r4.w + 3.5f;
+    return in_box | in_disk;
+}
+
+__device__ __forceinline__ int lanes_below2(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+// per-pair surfel geometry shared by forward and backward
+struct Hit2 {
+    float hu0, hu1, hu2, hv0, hv1, hv2, iz, sx, sy, g3, dx, dy, g2, sigma;
+    bool ok;  // the ray is not parallel to the surfel plane
+};
+
+__device__ __forceinline__ Hit2 hit2(const float4 r0, const float4 r1, const float4 r2, float px, float py) {
+    Hit2 h;
+    h.hu0 = px * r0.w - r0.x;
+    h.hu1 = px * r1.w - r0.y;
+    h.hu2 = px * r2.x - r0.z;
+    h.hv0 = py * r0.w - r1.x;
+    h.hv1 = py * r1.w - r1.y;
+    h.hv2 = py * r2.x - r1.z;
+    const float cx = h.hu1 * h.hv2 - h.hu2 * h.hv1;
+    const float cy = h.hu2 * h.hv0 - h.hu0 * h.hv2;
+    const float cz = h.hu0 * h.hv1 - h.hu1 * h.hv0;
+    h.ok = cz != 0.f;
+    h.iz = h.ok ? __builtin_amdgcn_rcpf(cz) : 0.f;
+    h.sx = cx * h.iz;
+    h.sy = cy * h.iz;
+    h.g3 = h.sx * h.sx + h.sy * h.sy;
+    h.dx = r2.y - px;
+    h.dy = r2.z - py;
+    h.g2 = 2.0f * (h.dx * h.dx + h.dy * h.dy);
+    h.sigma = 0.5f * fminf(h.g3, h.g2);
+    return h;
 }
 
 template <int D>
 __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
-    int C, int W, int H, int tw, int th, const float2* __restrict__ means2d, const float* __restrict__ rt,
-    const float* __restrict__ colors, const float* __restrict__ opacities, const float* __restrict__ normals,
-    const float* __restrict__ backgrounds, const int32_t* __restrict__ offsets, int64_t n_isects,
-    const int32_t* __restrict__ flatten_ids, float* __restrict__ render_colors, float* __restrict__ render_alphas,
-    float* __restrict__ render_normals, float* __restrict__ render_distort, float* __restrict__ render_median,
-    int32_t* __restrict__ last_ids, int32_t* __restrict__ median_ids) {
-    constexpr int S = 12 + D + 3;  // floats staged per surfel
-    __shared__ float s_rec[kFwd2Batch * S];
+    int C, int W, int H, int tw, int th, const Rec2* __restrict__ rec, const float* __restrict__ backgrounds,
+    const int32_t* __restrict__ offsets, int64_t n_isects, const int32_t* __restrict__ flatten_ids,
+    float* __restrict__ render_colors, float* __restrict__ render_alphas, float* __restrict__ render_normals,
+    float* __restrict__ render_distort, float* __restrict__ render_median, int32_t* __restrict__ last_ids,
+    int32_t* __restrict__ median_ids) {
+    constexpr int NB = kFwd2Batch;
+    __shared__ float4 s_r0[NB], s_r1[NB], s_r2[NB], s_col[NB], s_r4[NB], s_box[NB];
+    __shared__ uint8_t s_list[4][NB];
+    __shared__ int s_vote[2][4];
     const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects);
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
+    const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
     float T = 1.0f, distort = 0.f, acc_vd = 0.f, median = 0.f;
-    float acc[D], nacc[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < D; ++k) acc[k] = 0.f;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f}, nacc[3] = {0.f, 0.f, 0.f};
     int32_t cur = 0, med_idx = 0;
     bool done = !tc.inside;
-    const int nb = (tc.end - tc.start + kFwd2Batch - 1) / kFwd2Batch;
+    const int nb = (tc.end - tc.start + NB - 1) / NB;
+    const int32_t last = tc.end - 1;
+    const bool loader = tid < NB;
+    float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0, n3 = n0, n4 = n0, n5 = n0;
+    int32_t nid = 0;
+    if (nb > 0 && loader) {
+        const int32_t id0 = flatten_ids[min(tc.start + tid, last)];
+        const float4* r = reinterpret_cast<const float4*>(rec + id0);
+        n0 = r[0]; n1 = r[1]; n2 = r[2]; n3 = r[3]; n4 = r[4]; n5 = r[5];
+        nid = flatten_ids[min(tc.start + NB + tid, last)];
+    }
+    uint8_t* my_list = s_list[wave];
     for (int b = 0; b < nb; ++b) {
-        if (__syncthreads_count(done) == 256) break;
-        const int32_t bs = tc.start + b * kFwd2Batch;
-        if (tid < kFwd2Batch && bs + tid < tc.end) {
-            const int32_t g = flatten_ids[bs + tid];
-            float* s = s_rec + tid * S;
-            stage_surfel(s, g, means2d, rt, opacities);
-#pragma unroll
-            for (int k = 0; k < D; ++k) s[12 + k] = colors[(int64_t)g * D + k];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) s[12 + D + k] = normals[(int64_t)g * 3 + k];
+        const bool wave_done = __all(done);
+        if (lane == 0) s_vote[b & 1][wave] = wave_done;
+        lds_barrier();
+        if (s_vote[b & 1][0] & s_vote[b & 1][1] & s_vote[b & 1][2] & s_vote[b & 1][3]) break;
+        const int32_t bs = tc.start + b * NB;
+        const int cnt = min(NB, tc.end - bs);
+        if (tid < cnt) {
+            s_r0[tid] = n0; s_r1[tid] = n1; s_r2[tid] = n2; s_col[tid] = n3; s_r4[tid] = n4; s_box[tid] = n5;
         }
-        __syncthreads();
-        const int cnt = min(kFwd2Batch, tc.end - bs);
-        for (int t = 0; t < cnt && !done; ++t) {
-            const float* s = s_rec + t * S;
-            const float hu0 = tc.px * s[6] - s[0], hu1 = tc.px * s[7] - s[1], hu2 = tc.px * s[8] - s[2];
-            const float hv0 = tc.py * s[6] - s[3], hv1 = tc.py * s[7] - s[4], hv2 = tc.py * s[8] - s[5];
-            const float cx = hu1 * hv2 - hu2 * hv1;
-            const float cy = hu2 * hv0 - hu0 * hv2;
-            const float cz = hu0 * hv1 - hu1 * hv0;
-            if (cz == 0.f) continue;
-            const float sx = cx / cz, sy = cy / cz;
-            const float g3 = sx * sx + sy * sy;
-            const float dx = s[9] - tc.px, dy = s[10] - tc.py;
-            const float g2 = 2.0f * (dx * dx + dy * dy);
-            const float sigma = 0.5f * fminf(g3, g2);
-            const float alpha = fminf(0.999f, s[11] * __expf(-sigma));
-            if (sigma < 0.f || alpha < 1.0f / 255.0f) continue;
+        lds_barrier();
+        if (loader) {
+            const float4* r = reinterpret_cast<const float4*>(rec + nid);
+            n0 = r[0]; n1 = r[1]; n2 = r[2]; n3 = r[3]; n4 = r[4]; n5 = r[5];
+            nid = flatten_ids[min(bs + 2 * NB + tid, last)];
+        }
+        if (wave_done) continue;
+        int n_mine = 0;
+#pragma unroll
+        for (int k = 0; k < NB / 64; ++k) {
+            const int t = k * 64 + lane;
+            const bool rel = t < cnt && reaches2(s_r2[t], s_r4[t], s_box[t], qx, qy);
+            const uint64_t m = __ballot(rel);
+            if (rel) my_list[n_mine + lanes_below2(m)] = (uint8_t)t;
+            n_mine += __popcll(m);
+        }
+        if (n_mine == 0) continue;
+        const int lst0 = my_list[lane], lst1 = my_list[64 + lane];
+        for (int i = 0; i < n_mine; ++i) {
+            const int t = __builtin_amdgcn_readlane(i < 64 ? lst0 : lst1, i & 63);
+            const float4 r0 = s_r0[t], r1 = s_r1[t], r2 = s_r2[t], c = s_col[t], r4 = s_r4[t];
+            const Hit2 h = hit2(r0, r1, r2, tc.px, tc.py);
+            const float alpha = fminf(0.999f, r2.w * __expf(-h.sigma));
+            const bool valid = h.ok & (h.sigma >= 0.f) & (alpha >= 1.0f / 255.0f) & !done;
             const float nT = T * (1.0f - alpha);
-            if (nT <= 1e-4f) {
-                done = true;
-                break;
-            }
-            const float vis = alpha * T;
+            const bool keep = nT > 1e-4f;
+            const bool ok = valid & keep;
+            done = done | (valid & !keep);  // exclusive stop at T <= 1e-4
+            const float vis = ok ? alpha * T : 0.f;
+            const float ck[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
-            for (int k = 0; k < D; ++k) acc[k] += s[12 + k] * vis;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) nacc[k] += s[12 + D + k] * vis;
-            const float depth = s[12 + D - 1];
+            for (int k = 0; k < D; ++k) acc[k] += ck[k] * vis;
+            nacc[0] += r4.x * vis;
+            nacc[1] += r4.y * vis;
+            nacc[2] += r4.z * vis;
+            const float depth = ck[D - 1];
             distort += 2.0f * (vis * depth * (1.0f - T) - vis * acc_vd);
             acc_vd += vis * depth;
-            if (T > 0.5f) {
-                median = depth;
-                med_idx = bs + t;
-            }
-            cur = bs + t;
-            T = nT;
+            const bool med = ok & (T > 0.5f);
+            median = med ? depth : median;
+            med_idx = med ? bs + t : med_idx;
+            cur = ok ? bs + t : cur;
+            T = ok ? nT : T;
+            if (__all(done)) break;
         }
     }
     if (tc.inside) {
@@ -152,152 +271,161 @@ __device__ __forceinline__ int32_t wave_max2(int32_t v) {
 
 template <int D, bool ABS>
 __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
-    int C, int W, int H, int tw, int th, const float2* __restrict__ means2d, const float* __restrict__ rt,
-    const float* __restrict__ colors, const float* __restrict__ opacities, const float* __restrict__ normals,
-    const float* __restrict__ backgrounds, const int32_t* __restrict__ offsets, int64_t n_isects,
-    const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
-    const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
-    const float* __restrict__ v_render_alphas, const float* __restrict__ v_render_normals,
-    float* __restrict__ acc_rows) {
-    constexpr int S = 12 + D + 3;
+    int C, int W, int H, int tw, int th, const Rec2* __restrict__ rec, const float* __restrict__ backgrounds,
+    const int32_t* __restrict__ offsets, int64_t n_isects, const int32_t* __restrict__ flatten_ids,
+    const float* __restrict__ render_alphas, const int32_t* __restrict__ last_ids,
+    const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
+    const float* __restrict__ v_render_normals, float* __restrict__ acc_rows) {
+    // row layout: 0-1 xy, 2-10 rt (u, v, w rows), 11 opac, 12-14 normal, 15-16 densify, 17.. colour, then abs
     constexpr int KV = 17 + D + (ABS ? 2 : 0);
-    // record layout: 0-1 xy, 2-10 rt, 11 opac, 12-14 normal, 15-16 densify, 17.. color, then abs
-    __shared__ float s_rec[kBwd2Batch * S];
-    __shared__ int32_t s_id[kBwd2Batch];
-    __shared__ float s_part[kBwd2Batch * 4 * KV];
+    constexpr int NB = kBwd2Batch;
+    __shared__ float4 s_r0[2][NB], s_r1[2][NB], s_r2[2][NB], s_col[2][NB], s_r4[2][NB], s_box[2][NB];
+    __shared__ int32_t s_id[2][NB];
+    __shared__ float s_part[NB * KV];  // the four waves' partials merged with LDS float atomics
+    __shared__ uint8_t s_list[4][NB];
     __shared__ int32_t s_last[4];
     const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
+    const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
     const float T_final = tc.inside ? 1.0f - render_alphas[tc.pix] : 1.0f;
     float T = T_final;
-    float buf[D], vo[D], nbuf[3] = {0.f, 0.f, 0.f}, vn[3];
+    // Bsum = sum_k buf_k vo_k + sum_k nbuf_k vn_k: the only form in which the
+    // colour/normal composited behind the current surfel enters v_alpha
+    float Bsum = 0.f, vo[4] = {0.f, 0.f, 0.f, 0.f}, vn[3];
     float bg_dot = 0.f;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-        buf[k] = 0.f;
         vo[k] = tc.inside ? v_render_colors[tc.pix * D + k] : 0.f;
         if (backgrounds) bg_dot += backgrounds[tc.cam * D + k] * vo[k];
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) vn[k] = tc.inside ? v_render_normals[tc.pix * 3 + k] : 0.f;
     const float va = tc.inside ? v_render_alphas[tc.pix] : 0.f;
-    const int32_t bin_final = tc.inside ? last_ids[tc.pix] : 0;
-    const int32_t wave_final = wave_max2(tc.inside ? bin_final : -1);
+    const float va_term = T_final * (va - bg_dot);
+    const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
+    const int32_t wave_final = wave_max2(bin_final);
     if (lane == 0) s_last[wave] = wave_final;
-    __syncthreads();
+    for (int e = tid; e < NB * KV; e += 256) s_part[e] = 0.f;
+    lds_barrier();
     const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
     const int32_t end = min(tc.end, blk_final + 1);
-    const int nb = end > tc.start ? (end - tc.start + kBwd2Batch - 1) / kBwd2Batch : 0;
-    for (int b = 0; b < nb; ++b) {
-        const int32_t batch_end = end - 1 - b * kBwd2Batch;
-        const int bsz = min(kBwd2Batch, batch_end + 1 - tc.start);
-        __syncthreads();
+    const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
+    float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0, n3 = n0, n4 = n0, n5 = n0;
+    int32_t cid = 0, nid = 0;
+    const bool loader = tid < NB;
+    if (nb > 0 && loader) {
+        cid = flatten_ids[max(end - 1 - tid, tc.start)];
+        const float4* r = reinterpret_cast<const float4*>(rec + cid);
+        n0 = r[0]; n1 = r[1]; n2 = r[2]; n3 = r[3]; n4 = r[4]; n5 = r[5];
+        nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
+    }
+    using TR = TransposeReduce<KV>;
+    const int row = lane >> 4;
+    uint8_t* my_list = s_list[wave];
+    int prev_bsz = 0;
+    for (int b = 0; b <= nb; ++b) {
+        const int cur = b & 1, prv = cur ^ 1;
+        const int32_t batch_end = end - 1 - b * NB;
+        const int bsz = b < nb ? min(NB, batch_end + 1 - tc.start) : 0;
+        // stage batch b, issue batch b+1's loads, then combine batch b-1 (atomics last)
         if (tid < bsz) {
-            const int32_t g = flatten_ids[batch_end - tid];
-            s_id[tid] = g;
-            float* s = s_rec + tid * S;
-            stage_surfel(s, g, means2d, rt, opacities);
-#pragma unroll
-            for (int k = 0; k < D; ++k) s[12 + k] = colors[(int64_t)g * D + k];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) s[12 + D + k] = normals[(int64_t)g * 3 + k];
+            s_id[cur][tid] = cid;
+            s_r0[cur][tid] = n0; s_r1[cur][tid] = n1; s_r2[cur][tid] = n2;
+            s_col[cur][tid] = n3; s_r4[cur][tid] = n4; s_box[cur][tid] = n5;
         }
-        for (int e = tid; e < kBwd2Batch * 4 * KV; e += 256) s_part[e] = 0.f;
-        __syncthreads();
+        if (b < nb && loader) {
+            cid = nid;
+            const float4* r = reinterpret_cast<const float4*>(rec + cid);
+            n0 = r[0]; n1 = r[1]; n2 = r[2]; n3 = r[3]; n4 = r[4]; n5 = r[5];
+            nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
+        }
+        if (b > 0) {
+            for (int e = tid; e < prev_bsz * KV; e += 256) {
+                const int t = e / KV, k = e - t * KV;
+                const float sv = s_part[e];
+                s_part[e] = 0.f;
+                if (sv != 0.f) atomicAdd(acc_rows + (int64_t)s_id[prv][t] * kRec2 + k, sv);
+            }
+        }
+        if (b == nb) break;
+        lds_barrier();
         const int t0 = max(0, batch_end - wave_final);
-        for (int t = t0; t < bsz; ++t) {
-            const float* s = s_rec + t * S;
-            bool valid = tc.inside && (batch_end - t <= bin_final);
-            const float hu0 = tc.px * s[6] - s[0], hu1 = tc.px * s[7] - s[1], hu2 = tc.px * s[8] - s[2];
-            const float hv0 = tc.py * s[6] - s[3], hv1 = tc.py * s[7] - s[4], hv2 = tc.py * s[8] - s[5];
-            const float cx = hu1 * hv2 - hu2 * hv1;
-            const float cy = hu2 * hv0 - hu0 * hv2;
-            const float cz = hu0 * hv1 - hu1 * hv0;
-            valid = valid && cz != 0.f;
-            const float iz = 1.0f / cz;
-            const float sx = cx * iz, sy = cy * iz;
-            const float g3 = sx * sx + sy * sy;
-            const float dx = s[9] - tc.px, dy = s[10] - tc.py;
-            const float g2 = 2.0f * (dx * dx + dy * dy);
-            const float sigma = 0.5f * fminf(g3, g2);
-            const float vis = __expf(-sigma);
-            const float alpha = fminf(0.999f, s[11] * vis);
-            valid = valid && !(sigma < 0.f || alpha < 1.0f / 255.0f);
-            if (!__any(valid)) continue;
-            float gv[KV];
-#pragma unroll
-            for (int k = 0; k < KV; ++k) gv[k] = 0.f;
-            if (valid) {
+        const int t = lane;
+        const bool rel = t < bsz && t >= t0 && reaches2(s_r2[cur][t], s_r4[cur][t], s_box[cur][t], qx, qy);
+        const uint64_t m = __ballot(rel);
+        if (rel) my_list[lanes_below2(m)] = (uint8_t)t;
+        const int n_mine = __popcll(m);
+        if (n_mine > 0) {
+            const int lst = my_list[lane];
+            for (int i = 0; i < n_mine; ++i) {
+                const int t = __builtin_amdgcn_readlane(lst, i);
+                const float4 r0 = s_r0[cur][t], r1 = s_r1[cur][t], r2 = s_r2[cur][t], c = s_col[cur][t],
+                             r4 = s_r4[cur][t];
+                const Hit2 h = hit2(r0, r1, r2, tc.px, tc.py);
+                const float vis = __expf(-h.sigma);
+                const float alpha = fminf(0.999f, r2.w * vis);
+                const bool valid = (batch_end - t <= bin_final) & h.ok & (h.sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
+                if (!__any(valid)) continue;
                 const float ra = __builtin_amdgcn_rcpf(1.0f - alpha);
-                T = T * ra;
-                const float fac = alpha * T;
-                float v_alpha = 0.f;
+                const float Tn = valid ? T * ra : T;
+                const float fac = valid ? alpha * Tn : 0.f;
+                const float ck[4] = {c.x, c.y, c.z, c.w};
+                float gv[KV];
+                float cv = r4.x * vn[0] + r4.y * vn[1] + r4.z * vn[2];
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
-                    const float ck = s[12 + k];
+                    cv += ck[k] * vo[k];
                     gv[17 + k] = fac * vo[k];
-                    v_alpha += (ck * T - buf[k] * ra) * vo[k];
-                    buf[k] += ck * fac;
                 }
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const float nk = s[12 + D + k];
-                    gv[12 + k] = fac * vn[k];
-                    v_alpha += (nk * T - nbuf[k] * ra) * vn[k];
-                    nbuf[k] += nk * fac;
+                for (int k = 0; k < 3; ++k) gv[12 + k] = fac * vn[k];
+                const float v_alpha = Tn * cv + ra * (va_term - Bsum);
+                Bsum += fac * cv;
+                const bool ok2 = valid & (r2.w * vis <= 0.999f);
+                const float v_sigma = ok2 ? -r2.w * vis * v_alpha : 0.f;
+                // sigma = |s|^2/2 (ray-plane hit) or |m - p|^2 (low-pass), whichever is smaller
+                const bool ell = h.g3 <= h.g2;
+                const float ve = ell ? v_sigma : 0.f, vp = ell ? 0.f : v_sigma;
+                const float vs0 = ve * h.sx, vs1 = ve * h.sy;
+                const float vc0 = vs0 * h.iz, vc1 = vs1 * h.iz, vc2 = -(vs0 * h.sx + vs1 * h.sy) * h.iz;
+                // d/d h_u = h_v x v_c, d/d h_v = v_c x h_u; h_u = p_x w - u, h_v = p_y w - v
+                const float vhu0 = h.hv1 * vc2 - h.hv2 * vc1, vhu1 = h.hv2 * vc0 - h.hv0 * vc2,
+                            vhu2 = h.hv0 * vc1 - h.hv1 * vc0;
+                const float vhv0 = vc1 * h.hu2 - vc2 * h.hu1, vhv1 = vc2 * h.hu0 - vc0 * h.hu2,
+                            vhv2 = vc0 * h.hu1 - vc1 * h.hu0;
+                const float vx = 2.0f * vp * h.dx, vy = 2.0f * vp * h.dy;
+                gv[0] = vx;
+                gv[1] = vy;
+                gv[2] = -vhu0; gv[3] = -vhu1; gv[4] = -vhu2;
+                gv[5] = -vhv0; gv[6] = -vhv1; gv[7] = -vhv2;
+                gv[8] = tc.px * vhu0 + tc.py * vhv0;
+                gv[9] = tc.px * vhu1 + tc.py * vhv1;
+                gv[10] = tc.px * vhu2 + tc.py * vhv2;
+                gv[11] = ok2 ? vis * v_alpha : 0.f;
+                gv[15] = vx - (vhu0 * r0.w + vhu1 * r1.w + vhu2 * r2.x);
+                gv[16] = vy - (vhv0 * r0.w + vhv1 * r1.w + vhv2 * r2.x);
+                if (ABS) {
+                    gv[17 + D] = fabsf(vx);
+                    gv[18 + D] = fabsf(vy);
                 }
-                v_alpha += T_final * ra * va;
-                v_alpha += -T_final * ra * bg_dot;
-                if (s[11] * vis <= 0.999f) {
-                    const float v_sigma = -s[11] * vis * v_alpha;
-                    float vu[3] = {0.f, 0.f, 0.f}, vv[3] = {0.f, 0.f, 0.f}, vw[3] = {0.f, 0.f, 0.f};
-                    float vx = 0.f, vy = 0.f;
-                    if (g3 <= g2) {
-                        const float vs0 = v_sigma * sx, vs1 = v_sigma * sy;
-                        const float vc0 = vs0 * iz, vc1 = vs1 * iz, vc2 = -(vs0 * sx + vs1 * sy) * iz;
-                        // v_hu = hv x vc ; v_hv = vc x hu
-                        const float vhu0 = hv1 * vc2 - hv2 * vc1, vhu1 = hv2 * vc0 - hv0 * vc2, vhu2 = hv0 * vc1 - hv1 * vc0;
-                        const float vhv0 = vc1 * hu2 - vc2 * hu1, vhv1 = vc2 * hu0 - vc0 * hu2, vhv2 = vc0 * hu1 - vc1 * hu0;
-                        vu[0] = -vhu0; vu[1] = -vhu1; vu[2] = -vhu2;
-                        vv[0] = -vhv0; vv[1] = -vhv1; vv[2] = -vhv2;
-                        vw[0] = tc.px * vhu0 + tc.py * vhv0;
-                        vw[1] = tc.px * vhu1 + tc.py * vhv1;
-                        vw[2] = tc.px * vhu2 + tc.py * vhv2;
-                    } else {
-                        vx = 2.0f * v_sigma * dx;
-                        vy = 2.0f * v_sigma * dy;
-                    }
-                    gv[0] = vx;
-                    gv[1] = vy;
+                T = Tn;
+                float u[TR::G];
+                TR::run(gv, u);
+                if ((lane & 15) == 0) {
+                    float* dst = s_part + t * KV;
 #pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        gv[2 + k] = vu[k];
-                        gv[5 + k] = vv[k];
-                        gv[8 + k] = vw[k];
-                    }
-                    gv[11] = vis * v_alpha;
-                    gv[15] = vu[0] * s[6] + vu[1] * s[7] + vu[2] * s[8] + vx;
-                    gv[16] = vv[0] * s[6] + vv[1] * s[7] + vv[2] * s[8] + vy;
-                    if (ABS) {
-                        gv[17 + D] = fabsf(vx);
-                        gv[18 + D] = fabsf(vy);
+                    for (int j = 0; j < TR::G; ++j) {
+                        const int i0 = TR::index(j, 0), i1 = TR::index(j, 1), i2 = TR::index(j, 2),
+                                  i3 = TR::index(j, 3);
+                        const int idx = row == 0 ? i0 : row == 1 ? i1 : row == 2 ? i2 : i3;
+                        if (idx >= 0) atomicAdd(dst + idx, u[j]);  // ds_add_f32
                     }
                 }
             }
-            float* dst = s_part + (t * 4 + wave) * KV;
-#pragma unroll
-            for (int k = 0; k < KV; ++k) {
-                const float sm = wave_sum_to_lane63(gv[k]);
-                if (lane == 63) dst[k] = sm;
-            }
         }
-        __syncthreads();
-        for (int e = tid; e < bsz * KV; e += 256) {
-            const int t = e / KV, k = e - t * KV;
-            const float* p = s_part + t * 4 * KV + k;
-            const float sm = p[0] + p[KV] + p[2 * KV] + p[3 * KV];
-            if (sm != 0.f) atomicAdd(acc_rows + (int64_t)s_id[t] * kRec2 + k, sm);
-        }
+        prev_bsz = bsz;
+        lds_barrier();
     }
 }
 
@@ -309,7 +437,13 @@ __global__ __launch_bounds__(256) void split2_kernel(int64_t n, const float* __r
                                                      float2* __restrict__ v_abs) {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
-    const float* r = rows + g * kRec2;
+    const float4* r4 = reinterpret_cast<const float4*>(rows + g * kRec2);
+    float r[kRec2];
+#pragma unroll
+    for (int q = 0; q < (17 + D + 2 + 3) / 4; ++q) {
+        const float4 v = r4[q];
+        r[q * 4] = v.x; r[q * 4 + 1] = v.y; r[q * 4 + 2] = v.z; r[q * 4 + 3] = v.w;
+    }
     float2 m = v_means2d[g];
     m.x += r[0]; m.y += r[1];
     v_means2d[g] = m;
@@ -344,28 +478,56 @@ static int check_raster2(int C, int N, int D, int W, int H, int tile_size, int t
     return HGSR_OK;
 }
 
+static size_t rec2_bytes(int C, int N) { return ((size_t)C * N * sizeof(Rec2) + 255) & ~(size_t)255; }
+
+static int pack2(int C, int N, int D, const float* means2d, const float* rt, const float* colors,
+                 const float* opacities, const float* normals, Rec2* rec, hipStream_t s) {
+    const int64_t n = (int64_t)C * N;
+    if (n == 0) return HGSR_OK;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    const float2* m2 = reinterpret_cast<const float2*>(means2d);
+#define LAUNCH_P2(DD) \
+    hipLaunchKernelGGL(pack2_kernel<DD>, grid, dim3(256), 0, s, n, m2, rt, colors, opacities, normals, rec)
+    switch (D) {
+        case 1: LAUNCH_P2(1); break;
+        case 2: LAUNCH_P2(2); break;
+        case 3: LAUNCH_P2(3); break;
+        default: LAUNCH_P2(4); break;
+    }
+#undef LAUNCH_P2
+    return check_launch("raster2d_pack");
+}
+
+extern "C" size_t hgsr_raster2d_fwd_ws_bytes(int C, int N, int D) {
+    (void)D;
+    return rec2_bytes(C, N);
+}
+
 extern "C" int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
                                  const float* colors, const float* opacities, const float* normals,
                                  const float* backgrounds, int width, int height, int tile_size, int tile_w,
                                  int tile_h, const int32_t* isect_offsets, int64_t n_isects,
                                  const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                                  float* render_normals, float* render_distort, float* render_median,
-                                 int32_t* last_ids, int32_t* median_ids, hgsr_stream_t stream) {
+                                 int32_t* last_ids, int32_t* median_ids, void* ws, size_t ws_bytes,
+                                 hgsr_stream_t stream) {
     if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
+    HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_fwd_ws_bytes(C, N, D), "raster2d_fwd workspace too small");
     HGSR_REQUIRE(isect_offsets && render_colors && render_alphas && render_normals && render_distort &&
                      render_median && last_ids && median_ids,
                  "null pointer");
-    HGSR_REQUIRE(n_isects == 0 || (means2d && ray_transforms && colors && opacities && normals && flatten_ids),
+    HGSR_REQUIRE(n_isects == 0 || (means2d && ray_transforms && colors && opacities && normals && flatten_ids && ws),
                  "null pointer");
-    const dim3 grid(C * tile_w * tile_h);
     hipStream_t s = as_stream(stream);
-    const float2* m2 = reinterpret_cast<const float2*>(means2d);
+    Rec2* rec = (Rec2*)ws;
+    if (n_isects > 0)
+        if (int st = pack2(C, N, D, means2d, ray_transforms, colors, opacities, normals, rec, s)) return st;
+    const dim3 grid(C * tile_w * tile_h);
     KernelTimer kt("raster2d_fwd", s);
-#define LAUNCH_F2(DD)                                                                                           \
-    hipLaunchKernelGGL(raster2d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, m2,     \
-                       ray_transforms, colors, opacities, normals, backgrounds, isect_offsets, n_isects,         \
-                       flatten_ids, render_colors, render_alphas, render_normals, render_distort, render_median, \
-                       last_ids, median_ids)
+#define LAUNCH_F2(DD)                                                                                            \
+    hipLaunchKernelGGL(raster2d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,     \
+                       backgrounds, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,          \
+                       render_normals, render_distort, render_median, last_ids, median_ids)
     switch (D) {
         case 1: LAUNCH_F2(1); break;
         case 2: LAUNCH_F2(2); break;
@@ -378,7 +540,7 @@ extern "C" int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, cons
 
 extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D) {
     (void)D;
-    return (size_t)C * N * kRec2 * sizeof(float);
+    return (size_t)C * N * kRec2 * sizeof(float) + rec2_bytes(C, N);
 }
 
 extern "C" int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
@@ -398,20 +560,21 @@ extern "C" int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, cons
                      v_means2d && v_ray_transforms && v_colors && v_opacities && v_normals && ws,
                  "null pointer");
     hipStream_t s = as_stream(stream);
+    const size_t rows_b = (size_t)C * N * kRec2 * sizeof(float);
     float* rows = (float*)ws;
-    if (int st = memset_async(rows, hgsr_raster2d_bwd_ws_bytes(C, N, D), s, "raster2d_bwd")) return st;
+    Rec2* rec = (Rec2*)((char*)ws + rows_b);
+    if (int st = memset_async(rows, rows_b, s, "raster2d_bwd")) return st;
+    if (int st = pack2(C, N, D, means2d, ray_transforms, colors, opacities, normals, rec, s)) return st;
     const dim3 grid(C * tile_w * tile_h);
-    const float2* m2 = reinterpret_cast<const float2*>(means2d);
-#define LAUNCH_B2(DD)                                                                                            \
-    {                                                                                                            \
-        KernelTimer kt("raster2d_bwd", s);                                                                       \
-        hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, \
-                       m2, ray_transforms, colors, opacities, normals, backgrounds, isect_offsets, n_isects,       \
-                       flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, v_render_normals,  \
-                       rows);                                                                                    \
-    }                                                                                                            \
-    hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)C * N + 255) / 256)), dim3(256), 0, \
-                       s, (int64_t)C * N, rows, reinterpret_cast<float2*>(v_means2d), v_ray_transforms, v_colors, \
+#define LAUNCH_B2(DD)                                                                                             \
+    {                                                                                                             \
+        KernelTimer kt("raster2d_bwd", s);                                                                        \
+        hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
+                           tile_h, rec, backgrounds, isect_offsets, n_isects, flatten_ids, render_alphas, last_ids, \
+                           v_render_colors, v_render_alphas, v_render_normals, rows);                             \
+    }                                                                                                             \
+    hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)C * N + 255) / 256)), dim3(256), 0,  \
+                       s, (int64_t)C * N, rows, reinterpret_cast<float2*>(v_means2d), v_ray_transforms, v_colors,  \
                        v_opacities, v_normals, reinterpret_cast<float2*>(v_densify), nullptr)
     switch (D) {
         case 1: LAUNCH_B2(1); break;

@@ -356,10 +356,12 @@ class _Raster2D(torch.autograd.Function):
         rm = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
         last = torch.empty((C, height, width), dtype=torch.int32, device=dev)
         med = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        ws_b = N.size_query("hgsr_raster2d_fwd_ws_bytes", C, Ng, D)
+        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
         N.call("hgsr_raster2d_fwd", C, Ng, D, ptr(means2d), ptr(rt), ptr(colors), ptr(opacities), ptr(normals),
                ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
                ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(rn), ptr(rd), ptr(rm),
-               ptr(last), ptr(med), N.stream(dev))
+               ptr(last), ptr(med), ptr(ws), ws_b, N.stream(dev))
         ctx.save_for_backward(means2d, rt, colors, opacities, normals, backgrounds, isect_offsets, flatten_ids,
                               ra, last)
         ctx.cfg = (width, height, tile_size)

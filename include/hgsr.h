@@ -156,14 +156,17 @@ int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, const float* co
  * replaces gsplat rasterize_to_pixels_2dgs.  The LAST colour channel is the
  * depth (render_mode RGB+ED / RGB+D) used for the median depth and distortion.
  * Outputs colors [C,H,W,D], alphas [C,H,W,1], normals [C,H,W,3],
- * distort [C,H,W,1], median [C,H,W,1], last_ids, median_ids [C,H,W]. */
+ * distort [C,H,W,1], median [C,H,W,1], last_ids, median_ids [C,H,W].
+ * ws (hgsr_raster2d_fwd_ws_bytes) receives the packed 96-B surfel records. */
+size_t hgsr_raster2d_fwd_ws_bytes(int C, int N, int D);
 int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
                       const float* colors, const float* opacities, const float* normals,
                       const float* backgrounds, int width, int height, int tile_size,
                       int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
                       const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                       float* render_normals, float* render_distort, float* render_median,
-                      int32_t* last_ids, int32_t* median_ids, hgsr_stream_t stream);
+                      int32_t* last_ids, int32_t* median_ids, void* ws, size_t ws_bytes,
+                      hgsr_stream_t stream);
 /* accumulates v_means2d [C*N,2], v_ray_transforms [C*N,9], v_colors [C*N,D],
  * v_opacities [C*N], v_normals [C*N,3], v_densify [C*N,2] (d loss / d screen
  * translation; nullable). */
