@@ -134,7 +134,7 @@ struct TransposeReduce {
             const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(hi), false, false);
             w[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
         }
-        if (H < 2 * G) w[H] = 0.f;
+        if constexpr (H < 2 * G) w[H] = 0.f;
 #pragma unroll
         for (int j = 0; j < G; ++j) {
             const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[2 * j]), __float_as_uint(w[2 * j + 1]),

@@ -45,11 +45,16 @@ __device__ __forceinline__ Tile2 tile2_ctx(int C, int W, int H, int tw, int th,
     return t;
 }
 
-// 96-B raster record of one (camera, surfel); rows u, v, w of the ray transform
+// 96-B raster record of one (camera, surfel).  With rows u, v, w of the ray
+// transform, h_u x h_v = (p_x w - u) x (p_y w - v) = p_x A + p_y B + C for
+// A = v x w, B = w x u, C = u x v.  Relative to the projected mean m this is
+// (p_x - m_x) A + (p_y - m_y) B + C' with C' = C + m_x A + m_y B (the hit at m), so
+// the kernels store A, B, C' (from f64) and evaluate the hit with six FMAs on
+// small offsets, keeping cancellation out of both passes.
 struct Rec2 {
-    float4 r0;  // u0 u1 u2 w0
-    float4 r1;  // v0 v1 v2 w1
-    float4 r2;  // w2 mean_x mean_y opacity
+    float4 r0;  // A.x A.y A.z B.x
+    float4 r1;  // B.y B.z C'.x C'.y
+    float4 r2;  // C'.z mean_x mean_y opacity
     float4 col; // colour (D <= 4, zero padded; the last channel is the depth in RGB+ED)
     float4 r4;  // normal xyz, low-pass disk radius
     float4 box; // centre xy and half-extents of the surfel ellipse's screen bounding box
@@ -94,6 +99,30 @@ __device__ __forceinline__ void surfel_footprint(const float* u, const float* v,
                       (float)(ey * 1.01 + 0.01 + 1e-6 * fabs(cy)));
 }
 
+__device__ __forceinline__ void cross3d(const double* a, const double* b, double* c) {
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// A = v x w, B = w x u, C' = (m_x w - u) x (m_y w - v), in f64, rounded once
+__device__ __forceinline__ void cross_abc(const float* M, float mx, float my, float* abc) {
+    const double u[3] = {M[0], M[1], M[2]}, v[3] = {M[3], M[4], M[5]}, w[3] = {M[6], M[7], M[8]};
+    double A[3], B[3], C[3], hu[3], hv[3];
+    for (int k = 0; k < 3; ++k) {
+        hu[k] = (double)mx * w[k] - u[k];
+        hv[k] = (double)my * w[k] - v[k];
+    }
+    cross3d(v, w, A);
+    cross3d(w, u, B);
+    cross3d(hu, hv, C);
+    for (int k = 0; k < 3; ++k) {
+        abc[k] = (float)A[k];
+        abc[3 + k] = (float)B[k];
+        abc[6 + k] = (float)C[k];
+    }
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void pack2_kernel(int64_t n, const float2* __restrict__ means2d,
                                                     const float* __restrict__ rt, const float* __restrict__ colors,
@@ -109,10 +138,12 @@ __global__ __launch_bounds__(256) void pack2_kernel(int64_t n, const float2* __r
     float4 box;
     float disk;
     surfel_footprint(M, M + 3, M + 6, o, box, disk);
+    float abc[9];
+    cross_abc(M, m.x, m.y, abc);
     Rec2 r;
-    r.r0 = make_float4(M[0], M[1], M[2], M[6]);
-    r.r1 = make_float4(M[3], M[4], M[5], M[7]);
-    r.r2 = make_float4(M[8], m.x, m.y, o);
+    r.r0 = make_float4(abc[0], abc[1], abc[2], abc[3]);
+    r.r1 = make_float4(abc[4], abc[5], abc[6], abc[7]);
+    r.r2 = make_float4(abc[8], m.x, m.y, o);
     float col[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < D; ++k) col[k] = colors[g * D + k];
@@ -135,28 +166,23 @@ __device__ __forceinline__ int lanes_below2(uint64_t m) {
 
 // per-pair surfel geometry shared by forward and backward
 struct Hit2 {
-    float hu0, hu1, hu2, hv0, hv1, hv2, iz, sx, sy, g3, dx, dy, g2, sigma;
+    float iz, sx, sy, g3, dx, dy, g2, sigma;
     bool ok;  // the ray is not parallel to the surfel plane
 };
 
 __device__ __forceinline__ Hit2 hit2(const float4 r0, const float4 r1, const float4 r2, float px, float py) {
     Hit2 h;
-    h.hu0 = px * r0.w - r0.x;
-    h.hu1 = px * r1.w - r0.y;
-    h.hu2 = px * r2.x - r0.z;
-    h.hv0 = py * r0.w - r1.x;
-    h.hv1 = py * r1.w - r1.y;
-    h.hv2 = py * r2.x - r1.z;
-    const float cx = h.hu1 * h.hv2 - h.hu2 * h.hv1;
-    const float cy = h.hu2 * h.hv0 - h.hu0 * h.hv2;
-    const float cz = h.hu0 * h.hv1 - h.hu1 * h.hv0;
+    h.dx = r2.y - px;
+    h.dy = r2.z - py;
+    // c = (p - m)_x A + (p - m)_y B + C'
+    const float cx = fmaf(-h.dx, r0.x, fmaf(-h.dy, r0.w, r1.z));
+    const float cy = fmaf(-h.dx, r0.y, fmaf(-h.dy, r1.x, r1.w));
+    const float cz = fmaf(-h.dx, r0.z, fmaf(-h.dy, r1.y, r2.x));
     h.ok = cz != 0.f;
     h.iz = h.ok ? __builtin_amdgcn_rcpf(cz) : 0.f;
     h.sx = cx * h.iz;
     h.sy = cy * h.iz;
     h.g3 = h.sx * h.sx + h.sy * h.sy;
-    h.dx = r2.y - px;
-    h.dy = r2.z - py;
     h.g2 = 2.0f * (h.dx * h.dx + h.dy * h.dy);
     h.sigma = 0.5f * fminf(h.g3, h.g2);
     return h;
@@ -276,8 +302,9 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     const float* __restrict__ render_alphas, const int32_t* __restrict__ last_ids,
     const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
     const float* __restrict__ v_render_normals, float* __restrict__ acc_rows) {
-    // row layout: 0-1 xy, 2-10 rt (u, v, w rows), 11 opac, 12-14 normal, 15-16 densify, 17.. colour, then abs
-    constexpr int KV = 17 + D + (ABS ? 2 : 0);
+    // row layout: 0-1 xy, 2-4 sum (p-m)_x v_c, 5-7 sum (p-m)_y v_c, 8-10 sum v_c (v_c = dL/d(h_u x h_v)),
+    // 11 opac, 12-14 normal, 15.. colour, then abs xy; split2 maps v_c sums to u, v, w and densify
+    constexpr int KV = 15 + D + (ABS ? 2 : 0);
     constexpr int NB = kBwd2Batch;
     __shared__ float4 s_r0[2][NB], s_r1[2][NB], s_r2[2][NB], s_col[2][NB], s_r4[2][NB], s_box[2][NB];
     __shared__ int32_t s_id[2][NB];
@@ -376,7 +403,7 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
                     cv += ck[k] * vo[k];
-                    gv[17 + k] = fac * vo[k];
+                    gv[15 + k] = fac * vo[k];
                 }
 #pragma unroll
                 for (int k = 0; k < 3; ++k) gv[12 + k] = fac * vn[k];
@@ -389,25 +416,16 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
                 const float ve = ell ? v_sigma : 0.f, vp = ell ? 0.f : v_sigma;
                 const float vs0 = ve * h.sx, vs1 = ve * h.sy;
                 const float vc0 = vs0 * h.iz, vc1 = vs1 * h.iz, vc2 = -(vs0 * h.sx + vs1 * h.sy) * h.iz;
-                // d/d h_u = h_v x v_c, d/d h_v = v_c x h_u; h_u = p_x w - u, h_v = p_y w - v
-                const float vhu0 = h.hv1 * vc2 - h.hv2 * vc1, vhu1 = h.hv2 * vc0 - h.hv0 * vc2,
-                            vhu2 = h.hv0 * vc1 - h.hv1 * vc0;
-                const float vhv0 = vc1 * h.hu2 - vc2 * h.hu1, vhv1 = vc2 * h.hu0 - vc0 * h.hu2,
-                            vhv2 = vc0 * h.hu1 - vc1 * h.hu0;
                 const float vx = 2.0f * vp * h.dx, vy = 2.0f * vp * h.dy;
                 gv[0] = vx;
                 gv[1] = vy;
-                gv[2] = -vhu0; gv[3] = -vhu1; gv[4] = -vhu2;
-                gv[5] = -vhv0; gv[6] = -vhv1; gv[7] = -vhv2;
-                gv[8] = tc.px * vhu0 + tc.py * vhv0;
-                gv[9] = tc.px * vhu1 + tc.py * vhv1;
-                gv[10] = tc.px * vhu2 + tc.py * vhv2;
+                gv[2] = -h.dx * vc0; gv[3] = -h.dx * vc1; gv[4] = -h.dx * vc2;
+                gv[5] = -h.dy * vc0; gv[6] = -h.dy * vc1; gv[7] = -h.dy * vc2;
+                gv[8] = vc0; gv[9] = vc1; gv[10] = vc2;
                 gv[11] = ok2 ? vis * v_alpha : 0.f;
-                gv[15] = vx - (vhu0 * r0.w + vhu1 * r1.w + vhu2 * r2.x);
-                gv[16] = vy - (vhv0 * r0.w + vhv1 * r1.w + vhv2 * r2.x);
-                if (ABS) {
-                    gv[17 + D] = fabsf(vx);
-                    gv[18 + D] = fabsf(vy);
+                if constexpr (ABS) {
+                    gv[15 + D] = fabsf(vx);
+                    gv[16 + D] = fabsf(vy);
                 }
                 T = Tn;
                 float u[TR::G];
@@ -429,8 +447,14 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     }
 }
 
+// Per surfel: fold the accumulated sums into gsplat's gradient tensors (+=), in f64.
+// gA = sum p_x v_c = gA' + m_x gC (gA' = sum (p-m)_x v_c), gB likewise, gC = sum v_c; with
+// d(a x b).g = da.(b x g) + db.(g x a):
+//   v_u = gB x w + v x gC,  v_v = w x gA + gC x u,  v_w = gA x v + u x gB;
+// the densification proxy (d loss / d screen translation) is v_xy - (A.gC, B.gC).
 template <int D, bool ABS>
 __global__ __launch_bounds__(256) void split2_kernel(int64_t n, const float* __restrict__ rows,
+                                                     const float* __restrict__ rt, const float2* __restrict__ means2d,
                                                      float2* __restrict__ v_means2d, float* __restrict__ v_rt,
                                                      float* __restrict__ v_colors, float* __restrict__ v_opacities,
                                                      float* __restrict__ v_normals, float2* __restrict__ v_densify,
@@ -440,28 +464,54 @@ __global__ __launch_bounds__(256) void split2_kernel(int64_t n, const float* __r
     const float4* r4 = reinterpret_cast<const float4*>(rows + g * kRec2);
     float r[kRec2];
 #pragma unroll
-    for (int q = 0; q < (17 + D + 2 + 3) / 4; ++q) {
+    for (int q = 0; q < (15 + D + 2 + 3) / 4; ++q) {
         const float4 v = r4[q];
         r[q * 4] = v.x; r[q * 4 + 1] = v.y; r[q * 4 + 2] = v.z; r[q * 4 + 3] = v.w;
     }
+    double u[3], v[3], w[3], gA[3], gB[3], gC[3];
+    const float2 mm = means2d[g];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        u[k] = rt[g * 9 + k];
+        v[k] = rt[g * 9 + 3 + k];
+        w[k] = rt[g * 9 + 6 + k];
+        gC[k] = r[8 + k];
+        gA[k] = (double)r[2 + k] + (double)mm.x * gC[k];
+        gB[k] = (double)r[5 + k] + (double)mm.y * gC[k];
+    }
+    double t0[3], t1[3];
+    cross3d(gB, w, t0);
+    cross3d(v, gC, t1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) v_rt[g * 9 + k] += (float)(t0[k] + t1[k]);
+    cross3d(w, gA, t0);
+    cross3d(gC, u, t1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) v_rt[g * 9 + 3 + k] += (float)(t0[k] + t1[k]);
+    cross3d(gA, v, t0);
+    cross3d(u, gB, t1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) v_rt[g * 9 + 6 + k] += (float)(t0[k] + t1[k]);
     float2 m = v_means2d[g];
     m.x += r[0]; m.y += r[1];
     v_means2d[g] = m;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) v_rt[g * 9 + k] += r[2 + k];
     v_opacities[g] += r[11];
 #pragma unroll
     for (int k = 0; k < 3; ++k) v_normals[g * 3 + k] += r[12 + k];
     if (v_densify) {
+        double A[3], B[3];
+        cross3d(v, w, A);
+        cross3d(w, u, B);
         float2 d = v_densify[g];
-        d.x += r[15]; d.y += r[16];
+        d.x += (float)((double)r[0] - (A[0] * gC[0] + A[1] * gC[1] + A[2] * gC[2]));
+        d.y += (float)((double)r[1] - (B[0] * gC[0] + B[1] * gC[1] + B[2] * gC[2]));
         v_densify[g] = d;
     }
 #pragma unroll
-    for (int k = 0; k < D; ++k) v_colors[g * D + k] += r[17 + k];
+    for (int k = 0; k < D; ++k) v_colors[g * D + k] += r[15 + k];
     if (ABS) {
         float2 a = v_abs[g];
-        a.x += r[17 + D]; a.y += r[18 + D];
+        a.x += r[15 + D]; a.y += r[16 + D];
         v_abs[g] = a;
     }
 }
@@ -563,6 +613,7 @@ extern "C" int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, cons
     const size_t rows_b = (size_t)C * N * kRec2 * sizeof(float);
     float* rows = (float*)ws;
     Rec2* rec = (Rec2*)((char*)ws + rows_b);
+    const float2* m2 = reinterpret_cast<const float2*>(means2d);
     if (int st = memset_async(rows, rows_b, s, "raster2d_bwd")) return st;
     if (int st = pack2(C, N, D, means2d, ray_transforms, colors, opacities, normals, rec, s)) return st;
     const dim3 grid(C * tile_w * tile_h);
@@ -574,7 +625,9 @@ extern "C" int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, cons
                            v_render_colors, v_render_alphas, v_render_normals, rows);                             \
     }                                                                                                             \
     hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)C * N + 255) / 256)), dim3(256), 0,  \
-                       s, (int64_t)C * N, rows, reinterpret_cast<float2*>(v_means2d), v_ray_transforms, v_colors,  \
+                       s, (int64_t)C * N, rows, ray_transforms, m2, reinterpret_cast<float2*>(v_means2d),          \
+                       v_ray_transforms,                                                                           \
+                       v_colors,                                                                                   \
                        v_opacities, v_normals, reinterpret_cast<float2*>(v_densify), nullptr)
     switch (D) {
         case 1: LAUNCH_B2(1); break;
