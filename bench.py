@@ -156,6 +156,25 @@ def raster_pairs(wl):
     return int(visited.sum().item()) * 256, n_isects
 
 
+def pmc_traffic(args):
+    """HBM bytes per launch of each kernel from the newest committed PMC summary
+    (profiles/rNN_pmc_traffic.json, written by scripts/profile_summary.py from separate
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench on the default config,
+    gfx950-corrected).  Counters cannot be read inside a timed run, so this is the
+    profiled figure for the same command, or {} when no summary matches the config."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_pmc_traffic.json")))
+    if not files or args.n != 2_000_000 or (args.width, args.height) != (1920, 1080):
+        return {}, None
+    d = json.load(open(files[-1]))
+    out = {}
+    for k, v in d["kernels"].get(f"{args.gs}gs", {}).items():
+        base = k.split("_kernel")[0]
+        if base not in out:
+            out[base] = v["hbm_bytes_corrected"]
+    return out, os.path.basename(files[-1]) + ": 2*FETCH_SIZE + WRITE_SIZE"
+
+
 def cpu_baseline(args, wl):
     """The C oracle (scalar, 1 thread) on a bounded sample of the same workload."""
     from oracle import oracle as O
@@ -239,6 +258,7 @@ def main():
             if cnt:
                 kernels[k] = {"avg_ms": round(tot / cnt, 4), "launches": cnt}
     roof = None
+    traffic, traffic_src = pmc_traffic(args)
     if kernels and rank == 0:
         dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
         pairs, n_isects = raster_pairs(wl)
@@ -247,7 +267,7 @@ def main():
             flops = pairs * FLOP_PER_PAIR[dom]
             ach = flops / avg_s / 1e12
             roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": None, "kernel": dom,
+                    "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": traffic.get(dom), "kernel": dom,
                     "note": (f"fp32 VALU-bound compositing: peak = fp32 vector rate (= f32 MFMA rate); "
                              f"{pairs} (pixel,Gaussian) pairs visited x {FLOP_PER_PAIR[dom]:.0f} FLOP/pair "
                              f"(SURVEY 8(d)); {n_isects} intersections")}
@@ -256,6 +276,9 @@ def main():
                     "traffic": None, "kernel": dom}
         # aggregate compulsory-bytes figure of SURVEY 8(d): B_step = 384 N + 132 I + 52 P
         b_step = 384 * args.n + 132 * n_isects + 52 * args.width * args.height
+        if roof.get("traffic") is not None:
+            roof["traffic_unit"] = "bytes/launch"
+            roof["traffic_source"] = traffic_src
         roof["aggregate_hbm_frac"] = round(b_step / (dt / args.steps) / (HBM_PEAK_GBS * 1e9), 4)
         roof["n_isects"] = n_isects
     cpu = None

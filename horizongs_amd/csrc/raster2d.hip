@@ -447,7 +447,7 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     }
 }
 
-// Per surfel: fold the accumulated sums into gsplat's gradient tensors (+=), in f64.
+// Per surfel: fold the accumulated sums into gsplat's gradient tensors (overwrite), in f64.
 // gA = sum p_x v_c = gA' + m_x gC (gA' = sum (p-m)_x v_c), gB likewise, gC = sum v_c; with
 // d(a x b).g = da.(b x g) + db.(g x a):
 //   v_u = gB x w + v x gC,  v_v = w x gA + gC x u,  v_w = gA x v + u x gB;
@@ -483,37 +483,29 @@ __global__ __launch_bounds__(256) void split2_kernel(int64_t n, const float* __r
     cross3d(gB, w, t0);
     cross3d(v, gC, t1);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) v_rt[g * 9 + k] += (float)(t0[k] + t1[k]);
+    for (int k = 0; k < 3; ++k) v_rt[g * 9 + k] = (float)(t0[k] + t1[k]);
     cross3d(w, gA, t0);
     cross3d(gC, u, t1);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) v_rt[g * 9 + 3 + k] += (float)(t0[k] + t1[k]);
+    for (int k = 0; k < 3; ++k) v_rt[g * 9 + 3 + k] = (float)(t0[k] + t1[k]);
     cross3d(gA, v, t0);
     cross3d(u, gB, t1);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) v_rt[g * 9 + 6 + k] += (float)(t0[k] + t1[k]);
-    float2 m = v_means2d[g];
-    m.x += r[0]; m.y += r[1];
-    v_means2d[g] = m;
-    v_opacities[g] += r[11];
+    for (int k = 0; k < 3; ++k) v_rt[g * 9 + 6 + k] = (float)(t0[k] + t1[k]);
+    v_means2d[g] = make_float2(r[0], r[1]);
+    v_opacities[g] = r[11];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) v_normals[g * 3 + k] += r[12 + k];
+    for (int k = 0; k < 3; ++k) v_normals[g * 3 + k] = r[12 + k];
     if (v_densify) {
         double A[3], B[3];
         cross3d(v, w, A);
         cross3d(w, u, B);
-        float2 d = v_densify[g];
-        d.x += (float)((double)r[0] - (A[0] * gC[0] + A[1] * gC[1] + A[2] * gC[2]));
-        d.y += (float)((double)r[1] - (B[0] * gC[0] + B[1] * gC[1] + B[2] * gC[2]));
-        v_densify[g] = d;
+        v_densify[g] = make_float2((float)((double)r[0] - (A[0] * gC[0] + A[1] * gC[1] + A[2] * gC[2])),
+                                   (float)((double)r[1] - (B[0] * gC[0] + B[1] * gC[1] + B[2] * gC[2])));
     }
 #pragma unroll
-    for (int k = 0; k < D; ++k) v_colors[g * D + k] += r[15 + k];
-    if (ABS) {
-        float2 a = v_abs[g];
-        a.x += r[15 + D]; a.y += r[16 + D];
-        v_abs[g] = a;
-    }
+    for (int k = 0; k < D; ++k) v_colors[g * D + k] = r[15 + k];
+    if (ABS) v_abs[g] = make_float2(r[15 + D], r[16 + D]);
 }
 
 }  // namespace hgsr
@@ -588,9 +580,10 @@ extern "C" int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, cons
     return check_launch("raster2d_fwd");
 }
 
-extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D) {
+extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
     (void)D;
-    return (size_t)C * N * kRec2 * sizeof(float) + rec2_bytes(C, N);
+    const size_t rows_b = ((size_t)C * N * kRec2 * sizeof(float) + 255) & ~(size_t)255;
+    return rows_b + (reuse_fwd ? 0 : rec2_bytes(C, N));
 }
 
 extern "C" int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
@@ -601,21 +594,38 @@ extern "C" int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, cons
                                  const float* v_render_colors, const float* v_render_alphas,
                                  const float* v_render_normals, float* v_means2d, float* v_ray_transforms,
                                  float* v_colors, float* v_opacities, float* v_normals, float* v_densify,
-                                 void* ws, size_t ws_bytes, hgsr_stream_t stream) {
+                                 const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
     if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
-    HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_bwd_ws_bytes(C, N, D), "raster2d_bwd workspace too small");
-    if (n_isects == 0 || N == 0) return HGSR_OK;
+    HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
+                 "raster2d_bwd workspace too small");
+    if (N == 0) return HGSR_OK;
+    hipStream_t s = as_stream(stream);
+    if (n_isects == 0) {  // nothing composited: every gradient is zero
+        HGSR_REQUIRE(v_means2d && v_ray_transforms && v_colors && v_opacities && v_normals, "null pointer");
+        const size_t n = (size_t)C * N;
+        if (int st = memset_async(v_means2d, n * 2 * sizeof(float), s, "raster2d_bwd")) return st;
+        if (int st = memset_async(v_ray_transforms, n * 9 * sizeof(float), s, "raster2d_bwd")) return st;
+        if (int st = memset_async(v_colors, n * D * sizeof(float), s, "raster2d_bwd")) return st;
+        if (int st = memset_async(v_opacities, n * sizeof(float), s, "raster2d_bwd")) return st;
+        if (int st = memset_async(v_normals, n * 3 * sizeof(float), s, "raster2d_bwd")) return st;
+        if (v_densify)
+            if (int st = memset_async(v_densify, n * 2 * sizeof(float), s, "raster2d_bwd")) return st;
+        return HGSR_OK;
+    }
     HGSR_REQUIRE(means2d && ray_transforms && colors && opacities && normals && isect_offsets && flatten_ids &&
                      render_alphas && last_ids && v_render_colors && v_render_alphas && v_render_normals &&
                      v_means2d && v_ray_transforms && v_colors && v_opacities && v_normals && ws,
                  "null pointer");
-    hipStream_t s = as_stream(stream);
-    const size_t rows_b = (size_t)C * N * kRec2 * sizeof(float);
+    const size_t rows_b = ((size_t)C * N * kRec2 * sizeof(float) + 255) & ~(size_t)255;
     float* rows = (float*)ws;
-    Rec2* rec = (Rec2*)((char*)ws + rows_b);
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
-    if (int st = memset_async(rows, rows_b, s, "raster2d_bwd")) return st;
-    if (int st = pack2(C, N, D, means2d, ray_transforms, colors, opacities, normals, rec, s)) return st;
+    if (int st = memset_async(rows, (size_t)C * N * kRec2 * sizeof(float), s, "raster2d_bwd")) return st;
+    const Rec2* rec = (const Rec2*)fwd_ws;
+    if (!rec) {
+        Rec2* own = (Rec2*)((char*)ws + rows_b);
+        if (int st = pack2(C, N, D, means2d, ray_transforms, colors, opacities, normals, own, s)) return st;
+        rec = own;
+    }
     const dim3 grid(C * tile_w * tile_h);
 #define LAUNCH_B2(DD)                                                                                             \
     {                                                                                                             \

@@ -394,7 +394,7 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     }
 }
 
-// scatter accumulator rows into gsplat's separate gradient tensors (+=)
+// scatter accumulator rows into gsplat's separate gradient tensors (overwrite)
 template <int D, bool ABS>
 __global__ __launch_bounds__(256) void split3_kernel(int64_t n, const float* __restrict__ rows,
                                                      float2* __restrict__ v_means2d, float* __restrict__ v_conics,
@@ -409,20 +409,14 @@ __global__ __launch_bounds__(256) void split3_kernel(int64_t n, const float* __r
         const float4 v = r4[q];
         r[q * 4] = v.x; r[q * 4 + 1] = v.y; r[q * 4 + 2] = v.z; r[q * 4 + 3] = v.w;
     }
-    float2 m = v_means2d[g];
-    m.x += r[0]; m.y += r[1];
-    v_means2d[g] = m;
-    v_conics[g * 3] += r[2];
-    v_conics[g * 3 + 1] += r[3];
-    v_conics[g * 3 + 2] += r[4];
-    v_opacities[g] += r[5];
+    v_means2d[g] = make_float2(r[0], r[1]);
+    v_conics[g * 3] = r[2];
+    v_conics[g * 3 + 1] = r[3];
+    v_conics[g * 3 + 2] = r[4];
+    v_opacities[g] = r[5];
 #pragma unroll
-    for (int k = 0; k < D; ++k) v_colors[g * D + k] += r[6 + k];
-    if (ABS) {
-        float2 a = v_abs[g];
-        a.x += r[6 + D]; a.y += r[7 + D];
-        v_abs[g] = a;
-    }
+    for (int k = 0; k < D; ++k) v_colors[g * D + k] = r[6 + k];
+    if (ABS) v_abs[g] = make_float2(r[6 + D], r[7 + D]);
 }
 
 }  // namespace hgsr
@@ -521,9 +515,10 @@ extern "C" double hgsr_diag_raster3d_bwd_noatomic_ms(int C, int N, const float* 
     return ms;
 }
 
-extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D) {
+extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
     (void)D;
-    return (size_t)C * N * kRec3 * sizeof(float) + rec_bytes(C, N);
+    const size_t rows_b = ((size_t)C * N * kRec3 * sizeof(float) + 255) & ~(size_t)255;
+    return rows_b + (reuse_fwd ? 0 : rec_bytes(C, N));
 }
 
 extern "C" int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, const float* conics,
@@ -533,20 +528,37 @@ extern "C" int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, cons
                                  const float* render_alphas, const int32_t* last_ids,
                                  const float* v_render_colors, const float* v_render_alphas, float* v_means2d,
                                  float* v_conics, float* v_colors, float* v_opacities, float* v_means2d_abs,
-                                 void* ws, size_t ws_bytes, hgsr_stream_t stream) {
+                                 const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
     if (int st = check_raster(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
-    HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_bwd_ws_bytes(C, N, D), "raster3d_bwd workspace too small");
-    if (n_isects == 0 || N == 0) return HGSR_OK;
+    HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
+                 "raster3d_bwd workspace too small");
+    if (N == 0) return HGSR_OK;
+    hipStream_t s = as_stream(stream);
+    if (n_isects == 0) {  // nothing composited: every gradient is zero
+        HGSR_REQUIRE(v_means2d && v_conics && v_colors && v_opacities, "null pointer");
+        const size_t n = (size_t)C * N;
+        if (int st = memset_async(v_means2d, n * 2 * sizeof(float), s, "raster3d_bwd")) return st;
+        if (int st = memset_async(v_conics, n * 3 * sizeof(float), s, "raster3d_bwd")) return st;
+        if (int st = memset_async(v_colors, n * D * sizeof(float), s, "raster3d_bwd")) return st;
+        if (int st = memset_async(v_opacities, n * sizeof(float), s, "raster3d_bwd")) return st;
+        if (v_means2d_abs)
+            if (int st = memset_async(v_means2d_abs, n * 2 * sizeof(float), s, "raster3d_bwd")) return st;
+        return HGSR_OK;
+    }
     HGSR_REQUIRE(means2d && conics && colors && opacities && isect_offsets && flatten_ids && render_alphas &&
                      last_ids && v_render_colors && v_render_alphas && v_means2d && v_conics && v_colors &&
                      v_opacities && ws,
                  "null pointer");
-    hipStream_t s = as_stream(stream);
-    const size_t rows_b = (size_t)C * N * kRec3 * sizeof(float);
+    const size_t rows_b = ((size_t)C * N * kRec3 * sizeof(float) + 255) & ~(size_t)255;
     float* rows = (float*)ws;
-    Rec3* rec = (Rec3*)((char*)ws + rows_b);
-    if (int st = memset_async(rows, rows_b, s, "raster3d_bwd")) return st;
-    if (int st = pack3(C, N, D, means2d, conics, colors, opacities, rec, s)) return st;
+    if (int st = memset_async(rows, (size_t)C * N * kRec3 * sizeof(float), s, "raster3d_bwd")) return st;
+    // the forward's packed records when the caller kept them, else pack again
+    const Rec3* rec = (const Rec3*)fwd_ws;
+    if (!rec) {
+        Rec3* own = (Rec3*)((char*)ws + rows_b);
+        if (int st = pack3(C, N, D, means2d, conics, colors, opacities, own, s)) return st;
+        rec = own;
+    }
     const dim3 grid(C * tile_w * tile_h);
     const bool abs = v_means2d_abs != nullptr;
 #define LAUNCH_B(DD, AA)                                                                                       \

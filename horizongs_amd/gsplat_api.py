@@ -283,6 +283,7 @@ class _Raster3D(torch.autograd.Function):
                N.stream(dev))
         ctx.save_for_backward(means2d, conics, colors, opacities, backgrounds, isect_offsets, flatten_ids, ra, last)
         ctx.cfg = (width, height, tile_size, absgrad)
+        ctx.fwd_ws = ws  # packed raster records, reused by the backward
         return rc, ra
 
     @staticmethod
@@ -292,19 +293,22 @@ class _Raster3D(torch.autograd.Function):
         C, Ng, D = means2d.shape[0], means2d.shape[1], colors.shape[-1]
         th, tw = offsets.shape[1:]
         dev = means2d.device
-        v_means2d = torch.zeros_like(means2d)
-        v_conics = torch.zeros_like(conics)
-        v_colors = torch.zeros_like(colors)
-        v_opac = torch.zeros_like(opacities)
-        v_abs = torch.zeros_like(means2d) if absgrad else None
-        ws_b = N.size_query("hgsr_raster3d_bwd_ws_bytes", C, Ng, D)
+        # the kernels overwrite every gradient element
+        v_means2d = torch.empty_like(means2d)
+        v_conics = torch.empty_like(conics)
+        v_colors = torch.empty_like(colors)
+        v_opac = torch.empty_like(opacities)
+        v_abs = torch.empty_like(means2d) if absgrad else None
+        fwd_ws = ctx.fwd_ws
+        ws_b = N.size_query("hgsr_raster3d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
         ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
         v_rc = _f32(v_rc)
         v_ra = _f32(v_ra)
         N.call("hgsr_raster3d_bwd", C, Ng, D, ptr(means2d), ptr(conics), ptr(colors), ptr(opacities),
                ptr(backgrounds), width, height, tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
                ptr(flatten_ids) if flatten_ids.numel() else None, ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
-               ptr(v_means2d), ptr(v_conics), ptr(v_colors), ptr(v_opac), ptr(v_abs), ptr(ws), ws_b, N.stream(dev))
+               ptr(v_means2d), ptr(v_conics), ptr(v_colors), ptr(v_opac), ptr(v_abs), ptr(fwd_ws), ptr(ws), ws_b,
+               N.stream(dev))
         if absgrad:
             means2d.absgrad = v_abs
         v_bg = None
@@ -365,6 +369,7 @@ class _Raster2D(torch.autograd.Function):
         ctx.save_for_backward(means2d, rt, colors, opacities, normals, backgrounds, isect_offsets, flatten_ids,
                               ra, last)
         ctx.cfg = (width, height, tile_size)
+        ctx.fwd_ws = ws  # packed surfel records, reused by the backward
         ctx.mark_non_differentiable(rd, rm)
         return rc, ra, rn, rd, rm
 
@@ -375,20 +380,22 @@ class _Raster2D(torch.autograd.Function):
         C, Ng, D = means2d.shape[0], means2d.shape[1], colors.shape[-1]
         th, tw = offsets.shape[1:]
         dev = means2d.device
-        v_means2d = torch.zeros_like(means2d)
-        v_rt = torch.zeros_like(rt)
-        v_colors = torch.zeros_like(colors)
-        v_opac = torch.zeros_like(opacities)
-        v_normals = torch.zeros_like(normals)
-        v_dens = torch.zeros_like(means2d)
-        ws_b = N.size_query("hgsr_raster2d_bwd_ws_bytes", C, Ng, D)
+        # the kernels overwrite every gradient element
+        v_means2d = torch.empty_like(means2d)
+        v_rt = torch.empty_like(rt)
+        v_colors = torch.empty_like(colors)
+        v_opac = torch.empty_like(opacities)
+        v_normals = torch.empty_like(normals)
+        v_dens = torch.empty_like(means2d)
+        fwd_ws = ctx.fwd_ws
+        ws_b = N.size_query("hgsr_raster2d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
         ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
         v_rc, v_ra, v_rn = _f32(v_rc), _f32(v_ra), _f32(v_rn)
         N.call("hgsr_raster2d_bwd", C, Ng, D, ptr(means2d), ptr(rt), ptr(colors), ptr(opacities), ptr(normals),
                ptr(backgrounds), width, height, tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
                ptr(flatten_ids) if flatten_ids.numel() else None, ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_rn), ptr(v_means2d), ptr(v_rt), ptr(v_colors), ptr(v_opac), ptr(v_normals), ptr(v_dens),
-               ptr(ws), ws_b, N.stream(dev))
+               ptr(fwd_ws), ptr(ws), ws_b, N.stream(dev))
         v_bg = None
         if backgrounds is not None and ctx.needs_input_grad[6]:
             v_bg = (v_rc * (1.0 - ra)).sum(dim=(1, 2))

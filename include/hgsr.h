@@ -138,10 +138,12 @@ int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, const float* co
                       const int32_t* isect_offsets, int64_t n_isects,
                       const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                       int32_t* last_ids, void* ws, size_t ws_bytes, hgsr_stream_t stream);
-/* accumulates v_means2d [C*N,2], v_conics [C*N,3], v_colors [C*N,D],
- * v_opacities [C*N]; v_means2d_abs nullable (gsplat absgrad).  ws: caller
- * scratch of hgsr_raster3d_bwd_ws_bytes(). */
-size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D);
+/* writes (overwrites) v_means2d [C*N,2], v_conics [C*N,3], v_colors [C*N,D],
+ * v_opacities [C*N]; v_means2d_abs nullable (gsplat absgrad).  fwd_ws: the
+ * workspace hgsr_raster3d_fwd filled for the same inputs (its packed records
+ * are reused), or NULL to pack again.  ws: caller scratch of
+ * hgsr_raster3d_bwd_ws_bytes(C, N, D, fwd_ws != NULL). */
+size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd);
 int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, const float* conics,
                       const float* colors, const float* opacities, const float* backgrounds,
                       int width, int height, int tile_size, int tile_w, int tile_h,
@@ -149,8 +151,8 @@ int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, const float* co
                       const int32_t* flatten_ids, const float* render_alphas,
                       const int32_t* last_ids, const float* v_render_colors,
                       const float* v_render_alphas, float* v_means2d, float* v_conics,
-                      float* v_colors, float* v_opacities, float* v_means2d_abs, void* ws,
-                      size_t ws_bytes, hgsr_stream_t stream);
+                      float* v_colors, float* v_opacities, float* v_means2d_abs,
+                      const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream);
 
 /* ---- K11/K12: 2DGS surfel rasterization -----------------------------------
  * replaces gsplat rasterize_to_pixels_2dgs.  The LAST colour channel is the
@@ -167,10 +169,10 @@ int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, const float* ra
                       float* render_normals, float* render_distort, float* render_median,
                       int32_t* last_ids, int32_t* median_ids, void* ws, size_t ws_bytes,
                       hgsr_stream_t stream);
-/* accumulates v_means2d [C*N,2], v_ray_transforms [C*N,9], v_colors [C*N,D],
+/* writes (overwrites) v_means2d [C*N,2], v_ray_transforms [C*N,9], v_colors [C*N,D],
  * v_opacities [C*N], v_normals [C*N,3], v_densify [C*N,2] (d loss / d screen
  * translation; nullable). */
-size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D);
+size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd);
 int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
                       const float* colors, const float* opacities, const float* normals,
                       const float* backgrounds, int width, int height, int tile_size,
@@ -179,8 +181,8 @@ int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, const float* ra
                       const int32_t* last_ids, const float* v_render_colors,
                       const float* v_render_alphas, const float* v_render_normals,
                       float* v_means2d, float* v_ray_transforms, float* v_colors,
-                      float* v_opacities, float* v_normals, float* v_densify, void* ws,
-                      size_t ws_bytes, hgsr_stream_t stream);
+                      float* v_opacities, float* v_normals, float* v_densify,
+                      const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream);
 
 /* ---- measurement ----------------------------------------------------------
  * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):
