@@ -76,24 +76,40 @@ __device__ __forceinline__ float2 footprint(float a, float b, float c, float opa
     return make_float2(sqrtf(k * c) * 1.01f + 0.01f, sqrtf(k * a) * 1.01f + 0.01f);
 }
 
+// Where a raster call's channels come from.  gsplat's rasterize_to_pixels takes
+// colors [C,N,D] and opacities [C,N]; rasterization() itself concatenates the depth
+// and repeats shared colours/opacities over cameras, which the fused entry points do
+// here instead: channel k < dc is colors[c*col_cstride + g*dc + k] (col_cstride 0 =
+// shared over cameras), channel dc is depths[c*N + g] when depths != nullptr.
+struct ChanSrc {
+    const float* colors;
+    int64_t col_cstride;
+    int dc;
+    const float* depths;
+    const float* opac;
+    int64_t op_cstride;
+};
+
 template <int D>
-__global__ __launch_bounds__(256) void pack3_kernel(int64_t n, const float2* __restrict__ means2d,
-                                                    const float* __restrict__ conics,
-                                                    const float* __restrict__ colors,
-                                                    const float* __restrict__ opacities, Rec3* __restrict__ rec) {
-    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (g >= n) return;
-    const float2 m = means2d[g];
-    const float a = conics[g * 3], b = conics[g * 3 + 1], c = conics[g * 3 + 2], o = opacities[g];
-    const float2 ext = footprint(a, b, c, o);
+__global__ __launch_bounds__(256) void pack3_kernel(int64_t n, int N, const float2* __restrict__ means2d,
+                                                    const float* __restrict__ conics, ChanSrc cs,
+                                                    Rec3* __restrict__ rec) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int64_t c = i / N, g = i - c * N;
+    const float2 m = means2d[i];
+    const float a = conics[i * 3], b = conics[i * 3 + 1], cc = conics[i * 3 + 2];
+    const float o = cs.opac[c * cs.op_cstride + g];
+    const float2 ext = footprint(a, b, cc, o);
     Rec3 r;
     r.g0 = make_float4(m.x, m.y, a, b);
-    r.g1 = make_float4(c, o, ext.x, ext.y);
+    r.g1 = make_float4(cc, o, ext.x, ext.y);
     float col[4] = {0.f, 0.f, 0.f, 0.f};
+    const float* src = cs.colors + c * cs.col_cstride + g * cs.dc;
 #pragma unroll
-    for (int k = 0; k < D; ++k) col[k] = colors[g * D + k];
+    for (int k = 0; k < D; ++k) col[k] = k < cs.dc ? src[k] : cs.depths[i];
     r.col = make_float4(col[0], col[1], col[2], col[3]);
-    rec[g] = r;
+    rec[i] = r;
 }
 
 // does the footprint box of (g0, g1) reach the 8x8 quadrant centred at (qx, qy)?
@@ -129,8 +145,9 @@ __device__ __forceinline__ void fwd_step(const float4 g0, const float4 g1, const
 template <int D>
 __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
-    const int32_t* __restrict__ offsets, int64_t n_isects, const int32_t* __restrict__ flatten_ids,
-    float* __restrict__ render_colors, float* __restrict__ render_alphas, int32_t* __restrict__ last_ids) {
+    int bg_ch, int ed_ch, const int32_t* __restrict__ offsets, int64_t n_isects,
+    const int32_t* __restrict__ flatten_ids, float* __restrict__ render_colors, float* __restrict__ render_alphas,
+    int32_t* __restrict__ last_ids) {
     // slot kFwdBatch is a zero-opacity dummy used to pad the per-wave lists
     __shared__ float4 s_g0[kFwdBatch + 1];
     __shared__ float4 s_g1[kFwdBatch + 1];
@@ -211,10 +228,14 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
         }
     }
     if (tc.inside) {
-        render_alphas[tc.pix] = 1.0f - T;
+        const float alpha = 1.0f - T;
+        render_alphas[tc.pix] = alpha;
 #pragma unroll
-        for (int k = 0; k < D; ++k)
-            render_colors[tc.pix * D + k] = backgrounds ? acc[k] + T * backgrounds[tc.cam * D + k] : acc[k];
+        for (int k = 0; k < D; ++k) {
+            float v = (backgrounds && k < bg_ch) ? acc[k] + T * backgrounds[tc.cam * bg_ch + k] : acc[k];
+            if (k == ed_ch) v = v / fmaxf(alpha, 1e-10f);  // expected depth (rasterization ED)
+            render_colors[tc.pix * D + k] = v;
+        }
         last_ids[tc.pix] = cur;
     }
 }
@@ -225,13 +246,13 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
     return v;
 }
 
-template <int D, bool ABS, bool DIAG_NOATOM = false>
+template <int D, bool ABS>
 __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
-    const int32_t* __restrict__ offsets, int64_t n_isects, const int32_t* __restrict__ flatten_ids,
-    const float* __restrict__ render_alphas, const int32_t* __restrict__ last_ids,
-    const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
-    float* __restrict__ acc_rows) {
+    int bg_ch, int ed_ch, const float* __restrict__ render_colors, const int32_t* __restrict__ offsets,
+    int64_t n_isects, const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
+    const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
+    const float* __restrict__ v_render_alphas, float* __restrict__ acc_rows) {
     constexpr int KV = 6 + D + (ABS ? 2 : 0);
     constexpr int NB = kBwdBatch;
     // double-buffered staging: batch b+1 is staged while batch b's partials are
@@ -252,13 +273,25 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     // B = sum_k buf_k * vo_k, the upstream-weighted colour composited behind the
     // current Gaussian: v_alpha only ever needs this dot product, never buf_k itself
     float B = 0.f, vo[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < D; ++k) vo[k] = tc.inside ? v_render_colors[tc.pix * D + k] : 0.f;
+    float va = tc.inside ? v_render_alphas[tc.pix] : 0.f;
+    if (ed_ch >= 0 && tc.inside) {
+        // ED = raw / max(alpha, 1e-10): d/d raw = 1/ac, d/d alpha = -ED/ac (alpha >= 1e-10)
+        const float alpha = 1.0f - T_final, ac = fmaxf(alpha, 1e-10f);
+        float v_ed = 0.f;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+            if (k == ed_ch) {
+                v_ed = vo[k];
+                vo[k] = v_ed / ac;
+            }
+        if (alpha >= 1e-10f) va -= v_ed * render_colors[tc.pix * D + ed_ch] / ac;
+    }
     float bg_dot = 0.f;
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-        vo[k] = tc.inside ? v_render_colors[tc.pix * D + k] : 0.f;
-        if (backgrounds) bg_dot += backgrounds[tc.cam * D + k] * vo[k];
-    }
-    const float va = tc.inside ? v_render_alphas[tc.pix] : 0.f;
+    for (int k = 0; k < D; ++k)
+        if (backgrounds && k < bg_ch) bg_dot += backgrounds[tc.cam * bg_ch + k] * vo[k];
     const float va_term = T_final * (va - bg_dot);  // multiplied by ra per Gaussian
     const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
     const int32_t wave_final = wave_max_i32(bin_final);
@@ -309,10 +342,7 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
                 const int t = e / KV, k = e - t * KV;
                 const float sv = s_part[e];
                 s_part[e] = 0.f;
-                if (sv != 0.f) {
-                    if (DIAG_NOATOM) acc_rows[(int64_t)s_id[prv][t] * kRec3 + k] = sv;  // measurement build only
-                    else atomicAdd(acc_rows + (int64_t)s_id[prv][t] * kRec3 + k, sv);
-                }
+                if (sv != 0.f) atomicAdd(acc_rows + (int64_t)s_id[prv][t] * kRec3 + k, sv);
             }
         }
         if (b == nb) break;
@@ -394,29 +424,58 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     }
 }
 
-// scatter accumulator rows into gsplat's separate gradient tensors (overwrite)
+// Where a backward's channel gradients go (mirror of ChanSrc): v_colors has the
+// layout of the colours (shared ones are summed over cameras), v_depths [C,N]
+// (nullable), v_opac has the layout of the opacities.
+struct ChanDst {
+    float* colors;
+    bool col_shared;
+    int dc;
+    float* depths;
+    float* opac;
+    bool op_shared;
+};
+
+// scatter accumulator rows into gsplat's separate gradient tensors (overwrite);
+// one lane per Gaussian, looping cameras in order (deterministic sums)
 template <int D, bool ABS>
-__global__ __launch_bounds__(256) void split3_kernel(int64_t n, const float* __restrict__ rows,
+__global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* __restrict__ rows,
                                                      float2* __restrict__ v_means2d, float* __restrict__ v_conics,
-                                                     float* __restrict__ v_colors, float* __restrict__ v_opacities,
-                                                     float2* __restrict__ v_abs) {
+                                                     ChanDst cd, float2* __restrict__ v_abs) {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (g >= n) return;
-    const float4* r4 = reinterpret_cast<const float4*>(rows + g * kRec3);
-    float r[kRec3];
+    if (g >= N) return;
+    float col_sum[4] = {0.f, 0.f, 0.f, 0.f}, op_sum = 0.f;
+    for (int c = 0; c < C; ++c) {
+        const int64_t i = (int64_t)c * N + g;
+        const float4* r4 = reinterpret_cast<const float4*>(rows + i * kRec3);
+        float r[kRec3];
 #pragma unroll
-    for (int q = 0; q < kRec3 / 4; ++q) {
-        const float4 v = r4[q];
-        r[q * 4] = v.x; r[q * 4 + 1] = v.y; r[q * 4 + 2] = v.z; r[q * 4 + 3] = v.w;
+        for (int q = 0; q < kRec3 / 4; ++q) {
+            const float4 v = r4[q];
+            r[q * 4] = v.x; r[q * 4 + 1] = v.y; r[q * 4 + 2] = v.z; r[q * 4 + 3] = v.w;
+        }
+        v_means2d[i] = make_float2(r[0], r[1]);
+        v_conics[i * 3] = r[2];
+        v_conics[i * 3 + 1] = r[3];
+        v_conics[i * 3 + 2] = r[4];
+        if (cd.op_shared) op_sum += r[5];
+        else cd.opac[i] = r[5];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            if (k < cd.dc) {
+                if (cd.col_shared) col_sum[k] += r[6 + k];
+                else cd.colors[i * cd.dc + k] = r[6 + k];
+            } else if (cd.depths) {
+                cd.depths[i] = r[6 + k];
+            }
+        }
+        if (ABS) v_abs[i] = make_float2(r[6 + D], r[7 + D]);
     }
-    v_means2d[g] = make_float2(r[0], r[1]);
-    v_conics[g * 3] = r[2];
-    v_conics[g * 3 + 1] = r[3];
-    v_conics[g * 3 + 2] = r[4];
-    v_opacities[g] = r[5];
+    if (cd.op_shared) cd.opac[g] = op_sum;
+    if (cd.col_shared)
 #pragma unroll
-    for (int k = 0; k < D; ++k) v_colors[g * D + k] = r[6 + k];
-    if (ABS) v_abs[g] = make_float2(r[6 + D], r[7 + D]);
+        for (int k = 0; k < D; ++k)
+            if (k < cd.dc) cd.colors[g * cd.dc + k] = col_sum[k];
 }
 
 }  // namespace hgsr
@@ -434,18 +493,20 @@ static int check_raster(int C, int N, int D, int W, int H, int tile_size, int tw
 
 static size_t rec_bytes(int C, int N) { return ((size_t)C * N * sizeof(Rec3) + 255) & ~(size_t)255; }
 
-static int pack3(int C, int N, int D, const float* means2d, const float* conics, const float* colors,
-                 const float* opacities, Rec3* rec, hipStream_t s) {
+static int pack3(int C, int N, int D, const float* means2d, const float* conics, const ChanSrc& cs, Rec3* rec,
+                 hipStream_t s) {
     const int64_t n = (int64_t)C * N;
     if (n == 0) return HGSR_OK;
     const dim3 grid((unsigned)((n + 255) / 256));
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
+#define LAUNCH_P(DD) hipLaunchKernelGGL(pack3_kernel<DD>, grid, dim3(256), 0, s, n, N, m2, conics, cs, rec)
     switch (D) {
-        case 1: hipLaunchKernelGGL(pack3_kernel<1>, grid, dim3(256), 0, s, n, m2, conics, colors, opacities, rec); break;
-        case 2: hipLaunchKernelGGL(pack3_kernel<2>, grid, dim3(256), 0, s, n, m2, conics, colors, opacities, rec); break;
-        case 3: hipLaunchKernelGGL(pack3_kernel<3>, grid, dim3(256), 0, s, n, m2, conics, colors, opacities, rec); break;
-        default: hipLaunchKernelGGL(pack3_kernel<4>, grid, dim3(256), 0, s, n, m2, conics, colors, opacities, rec); break;
+        case 1: LAUNCH_P(1); break;
+        case 2: LAUNCH_P(2); break;
+        case 3: LAUNCH_P(3); break;
+        default: LAUNCH_P(4); break;
     }
+#undef LAUNCH_P
     return check_launch("raster3d_pack");
 }
 
@@ -454,25 +515,26 @@ extern "C" size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D) {
     return rec_bytes(C, N);
 }
 
-extern "C" int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, const float* conics,
-                                 const float* colors, const float* opacities, const float* backgrounds,
-                                 int width, int height, int tile_size, int tile_w, int tile_h,
-                                 const int32_t* isect_offsets, int64_t n_isects, const int32_t* flatten_ids,
-                                 float* render_colors, float* render_alphas, int32_t* last_ids, void* ws,
-                                 size_t ws_bytes, hgsr_stream_t stream) {
+static int raster3d_fwd_impl(int C, int N, int D, const float* means2d, const float* conics, const ChanSrc& cs,
+                             const float* backgrounds, int bg_ch, int ed_ch, int width, int height, int tile_size,
+                             int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                             const int32_t* flatten_ids, float* render_colors, float* render_alphas,
+                             int32_t* last_ids, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
     if (int st = check_raster(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_fwd_ws_bytes(C, N, D), "raster3d_fwd workspace too small");
     HGSR_REQUIRE(isect_offsets && render_colors && render_alphas && last_ids, "null pointer");
-    HGSR_REQUIRE(n_isects == 0 || (means2d && conics && colors && opacities && flatten_ids && ws), "null pointer");
+    HGSR_REQUIRE(n_isects == 0 || (means2d && conics && (cs.colors || cs.dc == 0) && cs.opac && flatten_ids && ws),
+                 "null pointer");
     hipStream_t s = as_stream(stream);
     Rec3* rec = (Rec3*)ws;
     if (n_isects > 0)
-        if (int st = pack3(C, N, D, means2d, conics, colors, opacities, rec, s)) return st;
+        if (int st = pack3(C, N, D, means2d, conics, cs, rec, s)) return st;
     const dim3 grid(C * tile_w * tile_h);
     KernelTimer kt("raster3d_fwd", s);
 #define LAUNCH_F(DD)                                                                                           \
     hipLaunchKernelGGL(raster3d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,    \
-                       backgrounds, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas, last_ids)
+                       backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,          \
+                       render_alphas, last_ids)
     switch (D) {
         case 1: LAUNCH_F(1); break;
         case 2: LAUNCH_F(2); break;
@@ -483,36 +545,33 @@ extern "C" int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, cons
     return check_launch("raster3d_fwd");
 }
 
-// Measurement-only: time the backward kernel with its float atomics replaced by
-// plain stores (wrong gradients), to price the atomic traffic.  bench.py --diag.
-extern "C" double hgsr_diag_raster3d_bwd_noatomic_ms(int C, int N, const float* rows_ws, const void* rec_ws,
-                                                      int width, int height, int tile_w, int tile_h,
-                                                      const int32_t* isect_offsets, int64_t n_isects,
-                                                      const int32_t* flatten_ids, const float* render_alphas,
-                                                      const int32_t* last_ids, const float* v_render_colors,
-                                                      const float* v_render_alphas, int noatom,
-                                                      hgsr_stream_t stream) {
-    hipStream_t s = as_stream(stream);
-    hipEvent_t a, b;
-    (void)hipEventCreate(&a);
-    (void)hipEventCreate(&b);
-    const dim3 grid(C * tile_w * tile_h);
-    (void)hipEventRecord(a, s);
-    if (noatom)
-        hipLaunchKernelGGL((raster3d_bwd_kernel<4, false, true>), grid, dim3(256), 0, s, C, width, height, tile_w,
-                           tile_h, (const Rec3*)rec_ws, nullptr, isect_offsets, n_isects, flatten_ids, render_alphas,
-                           last_ids, v_render_colors, v_render_alphas, (float*)rows_ws);
-    else
-        hipLaunchKernelGGL((raster3d_bwd_kernel<4, false, false>), grid, dim3(256), 0, s, C, width, height, tile_w,
-                           tile_h, (const Rec3*)rec_ws, nullptr, isect_offsets, n_isects, flatten_ids, render_alphas,
-                           last_ids, v_render_colors, v_render_alphas, (float*)rows_ws);
-    (void)hipEventRecord(b, s);
-    (void)hipEventSynchronize(b);
-    float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, a, b);
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
-    return ms;
+extern "C" int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, const float* conics,
+                                 const float* colors, const float* opacities, const float* backgrounds,
+                                 int width, int height, int tile_size, int tile_w, int tile_h,
+                                 const int32_t* isect_offsets, int64_t n_isects, const int32_t* flatten_ids,
+                                 float* render_colors, float* render_alphas, int32_t* last_ids, void* ws,
+                                 size_t ws_bytes, hgsr_stream_t stream) {
+    const ChanSrc cs{colors, (int64_t)N * D, D, nullptr, opacities, (int64_t)N};
+    return raster3d_fwd_impl(C, N, D, means2d, conics, cs, backgrounds, D, -1, width, height, tile_size, tile_w,
+                             tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas, last_ids,
+                             ws, ws_bytes, stream);
+}
+
+extern "C" int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2d, const float* conics,
+                                       const float* colors, int colors_shared, const float* depths,
+                                       int expected_depth, const float* opacities, int opacities_shared,
+                                       const float* backgrounds, int width, int height, int tile_size,
+                                       int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                                       const int32_t* flatten_ids, float* render_colors, float* render_alphas,
+                                       int32_t* last_ids, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
+    HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
+    HGSR_REQUIRE(!(expected_depth && !depths), "expected_depth needs depths");
+    const int D = Dc + (depths ? 1 : 0);
+    const ChanSrc cs{colors, colors_shared ? 0 : (int64_t)N * Dc, Dc, depths, opacities,
+                     opacities_shared ? 0 : (int64_t)N};
+    return raster3d_fwd_impl(C, N, D, means2d, conics, cs, backgrounds, Dc, expected_depth ? Dc : -1, width,
+                             height, tile_size, tile_w, tile_h, isect_offsets, n_isects, flatten_ids,
+                             render_colors, render_alphas, last_ids, ws, ws_bytes, stream);
 }
 
 extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
@@ -521,33 +580,37 @@ extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd)
     return rows_b + (reuse_fwd ? 0 : rec_bytes(C, N));
 }
 
-extern "C" int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, const float* conics,
-                                 const float* colors, const float* opacities, const float* backgrounds,
-                                 int width, int height, int tile_size, int tile_w, int tile_h,
-                                 const int32_t* isect_offsets, int64_t n_isects, const int32_t* flatten_ids,
-                                 const float* render_alphas, const int32_t* last_ids,
-                                 const float* v_render_colors, const float* v_render_alphas, float* v_means2d,
-                                 float* v_conics, float* v_colors, float* v_opacities, float* v_means2d_abs,
-                                 const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
+static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const float* conics, const ChanSrc& cs,
+                             const float* backgrounds, int bg_ch, int ed_ch, const float* render_colors,
+                             int width, int height, int tile_size, int tile_w, int tile_h,
+                             const int32_t* isect_offsets, int64_t n_isects, const int32_t* flatten_ids,
+                             const float* render_alphas, const int32_t* last_ids, const float* v_render_colors,
+                             const float* v_render_alphas, float* v_means2d, float* v_conics, const ChanDst& cd,
+                             float* v_means2d_abs, const void* fwd_ws, void* ws, size_t ws_bytes,
+                             hgsr_stream_t stream) {
     if (int st = check_raster(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
                  "raster3d_bwd workspace too small");
+    HGSR_REQUIRE(ed_ch < 0 || render_colors, "expected-depth backward needs render_colors");
     if (N == 0) return HGSR_OK;
+    HGSR_REQUIRE(v_means2d && v_conics && (cd.colors || cd.dc == 0) && cd.opac, "null pointer");
     hipStream_t s = as_stream(stream);
+    const int64_t n = (int64_t)C * N;
     if (n_isects == 0) {  // nothing composited: every gradient is zero
-        HGSR_REQUIRE(v_means2d && v_conics && v_colors && v_opacities, "null pointer");
-        const size_t n = (size_t)C * N;
         if (int st = memset_async(v_means2d, n * 2 * sizeof(float), s, "raster3d_bwd")) return st;
         if (int st = memset_async(v_conics, n * 3 * sizeof(float), s, "raster3d_bwd")) return st;
-        if (int st = memset_async(v_colors, n * D * sizeof(float), s, "raster3d_bwd")) return st;
-        if (int st = memset_async(v_opacities, n * sizeof(float), s, "raster3d_bwd")) return st;
+        if (cd.dc)
+            if (int st = memset_async(cd.colors, (cd.col_shared ? N : n) * cd.dc * sizeof(float), s, "raster3d_bwd"))
+                return st;
+        if (cd.depths)
+            if (int st = memset_async(cd.depths, n * sizeof(float), s, "raster3d_bwd")) return st;
+        if (int st = memset_async(cd.opac, (cd.op_shared ? N : n) * sizeof(float), s, "raster3d_bwd")) return st;
         if (v_means2d_abs)
             if (int st = memset_async(v_means2d_abs, n * 2 * sizeof(float), s, "raster3d_bwd")) return st;
         return HGSR_OK;
     }
-    HGSR_REQUIRE(means2d && conics && colors && opacities && isect_offsets && flatten_ids && render_alphas &&
-                     last_ids && v_render_colors && v_render_alphas && v_means2d && v_conics && v_colors &&
-                     v_opacities && ws,
+    HGSR_REQUIRE(means2d && conics && isect_offsets && flatten_ids && render_alphas && last_ids && v_render_colors &&
+                     v_render_alphas && ws,
                  "null pointer");
     const size_t rows_b = ((size_t)C * N * kRec3 * sizeof(float) + 255) & ~(size_t)255;
     float* rows = (float*)ws;
@@ -556,7 +619,7 @@ extern "C" int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, cons
     const Rec3* rec = (const Rec3*)fwd_ws;
     if (!rec) {
         Rec3* own = (Rec3*)((char*)ws + rows_b);
-        if (int st = pack3(C, N, D, means2d, conics, colors, opacities, own, s)) return st;
+        if (int st = pack3(C, N, D, means2d, conics, cs, own, s)) return st;
         rec = own;
     }
     const dim3 grid(C * tile_w * tile_h);
@@ -565,12 +628,12 @@ extern "C" int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, cons
     {                                                                                                          \
         KernelTimer kt("raster3d_bwd", s);                                                                     \
         hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
-                           tile_h, rec, backgrounds, isect_offsets, n_isects, flatten_ids, render_alphas,        \
-                           last_ids, v_render_colors, v_render_alphas, rows);                                    \
+                           tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,       \
+                           flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows);        \
     }                                                                                                          \
-    hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)C * N + 255) / 256)), dim3(256), 0, s, \
-                       (int64_t)C * N, rows, reinterpret_cast<float2*>(v_means2d), v_conics, v_colors,         \
-                       v_opacities, reinterpret_cast<float2*>(v_means2d_abs))
+    hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, \
+                       N, rows, reinterpret_cast<float2*>(v_means2d), v_conics, cd,                             \
+                       reinterpret_cast<float2*>(v_means2d_abs))
     switch (D * 2 + (abs ? 1 : 0)) {
         case 2: LAUNCH_B(1, false); break;
         case 3: LAUNCH_B(1, true); break;
@@ -583,4 +646,45 @@ extern "C" int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, cons
     }
 #undef LAUNCH_B
     return check_launch("raster3d_bwd");
+}
+
+extern "C" int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, const float* conics,
+                                 const float* colors, const float* opacities, const float* backgrounds,
+                                 int width, int height, int tile_size, int tile_w, int tile_h,
+                                 const int32_t* isect_offsets, int64_t n_isects, const int32_t* flatten_ids,
+                                 const float* render_alphas, const int32_t* last_ids,
+                                 const float* v_render_colors, const float* v_render_alphas, float* v_means2d,
+                                 float* v_conics, float* v_colors, float* v_opacities, float* v_means2d_abs,
+                                 const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
+    const ChanSrc cs{colors, (int64_t)N * D, D, nullptr, opacities, (int64_t)N};
+    const ChanDst cd{v_colors, false, D, nullptr, v_opacities, false};
+    return raster3d_bwd_impl(C, N, D, means2d, conics, cs, backgrounds, D, -1, nullptr, width, height, tile_size,
+                             tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_alphas, last_ids,
+                             v_render_colors, v_render_alphas, v_means2d, v_conics, cd, v_means2d_abs, fwd_ws, ws,
+                             ws_bytes, stream);
+}
+
+extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* conics,
+                                       const float* colors, int colors_shared, const float* depths,
+                                       int expected_depth, const float* opacities, int opacities_shared,
+                                       const float* backgrounds, int width, int height, int tile_size,
+                                       int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                                       const int32_t* flatten_ids, const float* render_colors,
+                                       const float* render_alphas, const int32_t* last_ids,
+                                       const float* v_render_colors, const float* v_render_alphas,
+                                       float* v_means2d, float* v_conics, float* v_colors, float* v_depths,
+                                       float* v_opacities, float* v_means2d_abs, const void* fwd_ws, void* ws,
+                                       size_t ws_bytes, hgsr_stream_t stream) {
+    HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
+    HGSR_REQUIRE(!(expected_depth && !depths), "expected_depth needs depths");
+    HGSR_REQUIRE(!depths || v_depths, "null pointer");
+    const int D = Dc + (depths ? 1 : 0);
+    const ChanSrc cs{colors, colors_shared ? 0 : (int64_t)N * Dc, Dc, depths, opacities,
+                     opacities_shared ? 0 : (int64_t)N};
+    const ChanDst cd{v_colors, colors_shared != 0, Dc, depths ? v_depths : nullptr, v_opacities,
+                     opacities_shared != 0};
+    return raster3d_bwd_impl(C, N, D, means2d, conics, cs, backgrounds, Dc, expected_depth ? Dc : -1,
+                             render_colors, width, height, tile_size, tile_w, tile_h, isect_offsets, n_isects,
+                             flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, v_means2d,
+                             v_conics, cd, v_means2d_abs, fwd_ws, ws, ws_bytes, stream);
 }

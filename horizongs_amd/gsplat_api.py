@@ -317,6 +317,70 @@ class _Raster3D(torch.autograd.Function):
         return v_means2d, v_conics, v_colors, v_opac, v_bg, None, None, None, None, None, None
 
 
+class _Raster3DFused(torch.autograd.Function):
+    """rasterization()'s colour assembly + rasterize_to_pixels + ED normalisation as one
+    native call each way (hgsr_raster3d_{fwd,bwd}_fused): colours shared over cameras or
+    per camera, the depth channel, shared opacities and expected depth are handled in the
+    kernels instead of torch cat / repeat / divide (gsplat rendering.py does those in torch)."""
+
+    @staticmethod
+    def forward(ctx, means2d, conics, colors, depths, opacities, backgrounds, width, height, tile_size,
+                isect_offsets, flatten_ids, expected_depth, absgrad):
+        C, Ng = means2d.shape[:2]
+        Dc = 0 if colors is None else colors.shape[-1]
+        D = Dc + (0 if depths is None else 1)
+        col_shared = colors is not None and colors.dim() == 2
+        op_shared = opacities.dim() == 1
+        th, tw = isect_offsets.shape[1:]
+        dev = means2d.device
+        rc = torch.empty((C, height, width, D), dtype=torch.float32, device=dev)
+        ra = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
+        last = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        ws_b = N.size_query("hgsr_raster3d_fwd_ws_bytes", C, Ng, D)
+        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+        N.call("hgsr_raster3d_fwd_fused", C, Ng, Dc, ptr(means2d), ptr(conics), ptr(colors), int(col_shared),
+               ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(backgrounds), width, height,
+               tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
+               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(ws), ws_b,
+               N.stream(dev))
+        ctx.save_for_backward(means2d, conics, colors, depths, opacities, backgrounds, isect_offsets, flatten_ids,
+                              rc, ra, last)
+        ctx.cfg = (width, height, tile_size, expected_depth, absgrad, Dc, col_shared, op_shared)
+        ctx.fwd_ws = ws  # packed raster records, reused by the backward
+        return rc, ra
+
+    @staticmethod
+    def backward(ctx, v_rc, v_ra):
+        means2d, conics, colors, depths, opacities, backgrounds, offsets, flatten_ids, rc, ra, last = ctx.saved_tensors
+        width, height, tile_size, expected_depth, absgrad, Dc, col_shared, op_shared = ctx.cfg
+        C, Ng = means2d.shape[:2]
+        D = Dc + (0 if depths is None else 1)
+        th, tw = offsets.shape[1:]
+        dev = means2d.device
+        v_means2d = torch.empty_like(means2d)
+        v_conics = torch.empty_like(conics)
+        v_colors = None if colors is None else torch.empty_like(colors)
+        v_depths = None if depths is None else torch.empty_like(depths)
+        v_opac = torch.empty_like(opacities)
+        v_abs = torch.empty_like(means2d) if absgrad else None
+        fwd_ws = ctx.fwd_ws
+        ws_b = N.size_query("hgsr_raster3d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
+        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+        v_rc, v_ra = _f32(v_rc), _f32(v_ra)
+        N.call("hgsr_raster3d_bwd_fused", C, Ng, Dc, ptr(means2d), ptr(conics), ptr(colors), int(col_shared),
+               ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(backgrounds), width, height,
+               tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
+               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
+               ptr(v_means2d), ptr(v_conics), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_abs), ptr(fwd_ws),
+               ptr(ws), ws_b, N.stream(dev))
+        if absgrad:
+            means2d.absgrad = v_abs
+        v_bg = None
+        if backgrounds is not None and ctx.needs_input_grad[5]:
+            v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))
+        return (v_means2d, v_conics, v_colors, v_depths, v_opac, v_bg, None, None, None, None, None, None, None)
+
+
 def rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_height, tile_size, isect_offsets,
                         flatten_ids, backgrounds=None, masks=None, packed=False, absgrad=False):
     """gsplat rasterize_to_pixels (non-packed): colors [C,N,D] -> (render_colors [C,H,W,D], alphas [C,H,W,1])."""
@@ -438,9 +502,8 @@ def _camera_centers(viewmats):
 
 
 def _colors_for_raster(means, colors, viewmats, radii, sh_degree, C):
+    """Colours per raster call: [N,D] (shared over cameras) or [C,N,D]."""
     if sh_degree is None:
-        if colors.dim() == 2:
-            return colors.expand(C, -1, -1)
         return colors
     campos = _camera_centers(viewmats)
     dirs = means[None, :, :] - campos[:, None, :]
@@ -476,17 +539,31 @@ def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, 
         means, covars, quats, scales, viewmats, Ks, width, height, eps2d=eps2d, packed=False,
         near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip, sparse_grad=sparse_grad,
         calc_compensations=False, camera_model=camera_model)
-    opac = opacities.repeat(C, 1)
     cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
-    cols, bgs = _with_depth(cols, backgrounds, depths, render_mode, C)
     tw, th = _tile_grid(width, height, tile_size)
     tpg, isect_ids, flatten_ids, isect_offsets = _isect_binned(means2d, radii, int(tile_size), tw, th, depths)
-    render_colors, render_alphas = rasterize_to_pixels(
-        means2d, conics, cols, opac, width, height, tile_size, isect_offsets, flatten_ids, backgrounds=bgs,
-        absgrad=absgrad)
-    if render_mode in ("ED", "RGB+ED"):
-        render_colors = torch.cat([render_colors[..., :-1],
-                                   render_colors[..., -1:] / render_alphas.clamp(min=1e-10)], dim=-1)
+    with_depth = render_mode in ("RGB+D", "RGB+ED", "D", "ED")
+    rgb = render_mode in ("RGB", "RGB+D", "RGB+ED")
+    Dc = cols.shape[-1] if rgb else 0
+    if Dc + int(with_depth) <= _MAX_CH:
+        # one fused native call each way: no cat / repeat / ED divide in torch
+        bgs = None if (backgrounds is None or not rgb) else _f32(backgrounds)
+        render_colors, render_alphas = _Raster3DFused.apply(
+            _f32(means2d), _f32(conics), _f32(cols) if rgb else None, _f32(depths) if with_depth else None,
+            _f32(opacities), bgs, int(width), int(height), int(tile_size), isect_offsets.contiguous(),
+            flatten_ids.contiguous(), render_mode in ("ED", "RGB+ED"), absgrad)
+        opac = opacities.expand(C, -1)
+    else:
+        opac = opacities.repeat(C, 1)
+        if cols.dim() == 2:
+            cols = cols.expand(C, -1, -1)
+        cols, bgs = _with_depth(cols, backgrounds, depths, render_mode, C)
+        render_colors, render_alphas = rasterize_to_pixels(
+            means2d, conics, cols, opac, width, height, tile_size, isect_offsets, flatten_ids, backgrounds=bgs,
+            absgrad=absgrad)
+        if render_mode in ("ED", "RGB+ED"):
+            render_colors = torch.cat([render_colors[..., :-1],
+                                       render_colors[..., -1:] / render_alphas.clamp(min=1e-10)], dim=-1)
     meta = {
         "camera_ids": None, "gaussian_ids": None, "radii": radii, "means2d": means2d, "depths": depths,
         "conics": conics, "opacities": opac, "tile_width": tw, "tile_height": th,
@@ -551,6 +628,8 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
         near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip, sparse_grad=sparse_grad)
     opac = opacities.repeat(C, 1)
     cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
+    if cols.dim() == 2:
+        cols = cols.expand(C, -1, -1)
     cols, bgs = _with_depth(cols, backgrounds, depths, render_mode, C)
     tw, th = _tile_grid(width, height, tile_size)
     tpg, isect_ids, flatten_ids, isect_offsets = _isect_binned(means2d, radii, int(tile_size), tw, th, depths)

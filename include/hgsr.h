@@ -154,6 +154,37 @@ int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, const float* co
                       float* v_colors, float* v_opacities, float* v_means2d_abs,
                       const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream);
 
+/* Fused channel assembly for gsplat rasterization() (rendering.py: colour/depth
+ * concatenation, opacity repeat and the ED normalisation are done in Python there;
+ * reference gaussian_renderer/render.py:40-54 calls it with render_mode "RGB+ED").
+ * Channels: colors[..., :Dc] (colors [N,Dc] shared over cameras when colors_shared,
+ * else [C,N,Dc]) followed by depths [C,N] when depths != NULL; opacities [N] when
+ * opacities_shared else [C,N]; backgrounds [C,Dc] (the depth channel has none);
+ * expected_depth divides the depth channel by max(alpha, 1e-10).  Outputs
+ * render_colors [C,H,W,Dc+(depths?1:0)], render_alphas, last_ids; ws as
+ * hgsr_raster3d_fwd_ws_bytes(C, N, Dc + (depths ? 1 : 0)). */
+int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2d, const float* conics,
+                            const float* colors, int colors_shared, const float* depths,
+                            int expected_depth, const float* opacities, int opacities_shared,
+                            const float* backgrounds, int width, int height, int tile_size,
+                            int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                            const int32_t* flatten_ids, float* render_colors, float* render_alphas,
+                            int32_t* last_ids, void* ws, size_t ws_bytes, hgsr_stream_t stream);
+/* vjp of hgsr_raster3d_fwd_fused: v_colors in the colours' layout (shared colours
+ * summed over cameras in camera order), v_depths [C,N] (when depths), v_opacities
+ * in the opacities' layout; render_colors is the forward output (needed for ED). */
+int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* conics,
+                            const float* colors, int colors_shared, const float* depths,
+                            int expected_depth, const float* opacities, int opacities_shared,
+                            const float* backgrounds, int width, int height, int tile_size,
+                            int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                            const int32_t* flatten_ids, const float* render_colors,
+                            const float* render_alphas, const int32_t* last_ids,
+                            const float* v_render_colors, const float* v_render_alphas,
+                            float* v_means2d, float* v_conics, float* v_colors, float* v_depths,
+                            float* v_opacities, float* v_means2d_abs, const void* fwd_ws, void* ws,
+                            size_t ws_bytes, hgsr_stream_t stream);
+
 /* ---- K11/K12: 2DGS surfel rasterization -----------------------------------
  * replaces gsplat rasterize_to_pixels_2dgs.  The LAST colour channel is the
  * depth (render_mode RGB+ED / RGB+D) used for the median depth and distortion.

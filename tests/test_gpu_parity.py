@@ -263,7 +263,8 @@ def test_rasterization_3dgs_odd_size_two_cameras():
     r64.forward()
     means, quats, scales, opac, cols, vm, K = to_dev(sc.means, sc.quats, sc.scales, sc.opacities, sc.colors,
                                                      sc.viewmats, sc.Ks)
-    means.requires_grad_(True)
+    for t in (means, opac, cols):  # colours / opacities shared by both cameras: grads summed over them
+        t.requires_grad_(True)
     out, alpha, meta = G.rasterization(means, quats, scales, opac, cols, vm, K, sc.width, sc.height, packed=False,
                                        render_mode="RGB+D")
     close(out.detach().cpu().numpy(), rc, name="render_colors")
@@ -275,6 +276,8 @@ def test_rasterization_3dgs_odd_size_two_cameras():
     grads = ref.backward(vrc.numpy(), vra.numpy())
     g64 = r64.backward(vrc.numpy(), vra.numpy())
     cond_close(means.grad.cpu().numpy(), grads["means"], g64["means"], "means")
+    cond_close(opac.grad.cpu().numpy(), grads["opacities"], g64["opacities"], "opacities")
+    cond_close(cols.grad.cpu().numpy(), grads["colors"], g64["colors"], "colors")
 
 
 def test_rasterize_to_pixels_last_ids_and_absgrad():
