@@ -54,6 +54,10 @@ _SIGS = {
     "hgsr_raster2d_bwd_ws_bytes": (SZ, [I, I, I, I]),
     "hgsr_raster2d_bwd": (I, [I, I, I, P, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, P,
                               P, P, P, P, SZ, P]),
+    "hgsr_raster2d_fwd_fused": (I, [I, I, I, P, P, P, I, P, I, P, I, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P,
+                                    P, P, P, SZ, P]),
+    "hgsr_raster2d_bwd_fused": (I, [I, I, I, P, P, P, I, P, I, P, I, P, P, I, I, I, I, I, P, I64, P, P, P, P, P,
+                                    P, P, P, P, P, P, P, P, P, P, P, SZ, P]),
     "hgsr_timing_enable": (I, [I]),
     "hgsr_timing_reset": (I, []),
     "hgsr_timing_query": (I, [ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(I64)]),

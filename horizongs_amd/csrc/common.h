@@ -154,4 +154,30 @@ struct TransposeReduce {
     }
 };
 
+// Where a raster call's channels come from.  gsplat's rasterize_to_pixels takes
+// colors [C,N,D] and opacities [C,N]; rasterization() itself concatenates the depth
+// and repeats shared colours/opacities over cameras, which the fused entry points do
+// here instead: channel k < dc is colors[c*col_cstride + g*dc + k] (col_cstride 0 =
+// shared over cameras), channel dc is depths[c*N + g] when depths != nullptr.
+struct ChanSrc {
+    const float* colors;
+    int64_t col_cstride;
+    int dc;
+    const float* depths;
+    const float* opac;
+    int64_t op_cstride;
+};
+
+// Where a backward's channel gradients go (mirror of ChanSrc): v_colors has the
+// layout of the colours (shared ones are summed over cameras), v_depths [C,N]
+// (nullable), v_opac has the layout of the opacities.
+struct ChanDst {
+    float* colors;
+    bool col_shared;
+    int dc;
+    float* depths;
+    float* opac;
+    bool op_shared;
+};
+
 }  // namespace hgsr

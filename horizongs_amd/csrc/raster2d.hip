@@ -124,17 +124,17 @@ __device__ __forceinline__ void cross_abc(const float* M, float mx, float my, fl
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void pack2_kernel(int64_t n, const float2* __restrict__ means2d,
-                                                    const float* __restrict__ rt, const float* __restrict__ colors,
-                                                    const float* __restrict__ opacities,
+__global__ __launch_bounds__(256) void pack2_kernel(int64_t n, int N, const float2* __restrict__ means2d,
+                                                    const float* __restrict__ rt, ChanSrc cs,
                                                     const float* __restrict__ normals, Rec2* __restrict__ rec) {
-    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (g >= n) return;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int64_t c = i / N, g = i - c * N;
     float M[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) M[k] = rt[g * 9 + k];
-    const float2 m = means2d[g];
-    const float o = opacities[g];
+    for (int k = 0; k < 9; ++k) M[k] = rt[i * 9 + k];
+    const float2 m = means2d[i];
+    const float o = cs.opac[c * cs.op_cstride + g];
     float4 box;
     float disk;
     surfel_footprint(M, M + 3, M + 6, o, box, disk);
@@ -145,12 +145,13 @@ __global__ __launch_bounds__(256) void pack2_kernel(int64_t n, const float2* __r
     r.r1 = make_float4(abc[4], abc[5], abc[6], abc[7]);
     r.r2 = make_float4(abc[8], m.x, m.y, o);
     float col[4] = {0.f, 0.f, 0.f, 0.f};
+    const float* src = cs.colors + c * cs.col_cstride + g * cs.dc;
 #pragma unroll
-    for (int k = 0; k < D; ++k) col[k] = colors[g * D + k];
+    for (int k = 0; k < D; ++k) col[k] = k < cs.dc ? src[k] : cs.depths[i];
     r.col = make_float4(col[0], col[1], col[2], col[3]);
-    r.r4 = make_float4(normals[g * 3], normals[g * 3 + 1], normals[g * 3 + 2], disk);
+    r.r4 = make_float4(normals[i * 3], normals[i * 3 + 1], normals[i * 3 + 2], disk);
     r.box = box;
-    rec[g] = r;
+    rec[i] = r;
 }
 
 // does the surfel's skip geometry reach the 8x8 quadrant centred at (qx, qy)?
@@ -191,8 +192,9 @@ __device__ __forceinline__ Hit2 hit2(const float4 r0, const float4 r1, const flo
 template <int D>
 __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     int C, int W, int H, int tw, int th, const Rec2* __restrict__ rec, const float* __restrict__ backgrounds,
-    const int32_t* __restrict__ offsets, int64_t n_isects, const int32_t* __restrict__ flatten_ids,
-    float* __restrict__ render_colors, float* __restrict__ render_alphas, float* __restrict__ render_normals,
+    int bg_ch, int ed_ch, const int32_t* __restrict__ offsets, int64_t n_isects,
+    const int32_t* __restrict__ flatten_ids, float* __restrict__ render_colors, float* __restrict__ render_alphas,
+    float* __restrict__ render_normals,
     float* __restrict__ render_distort, float* __restrict__ render_median, int32_t* __restrict__ last_ids,
     int32_t* __restrict__ median_ids) {
     constexpr int NB = kFwd2Batch;
@@ -276,10 +278,14 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
         }
     }
     if (tc.inside) {
-        render_alphas[tc.pix] = 1.0f - T;
+        const float alpha = 1.0f - T;
+        render_alphas[tc.pix] = alpha;
 #pragma unroll
-        for (int k = 0; k < D; ++k)
-            render_colors[tc.pix * D + k] = backgrounds ? acc[k] + T * backgrounds[tc.cam * D + k] : acc[k];
+        for (int k = 0; k < D; ++k) {
+            float v = (backgrounds && k < bg_ch) ? acc[k] + T * backgrounds[tc.cam * bg_ch + k] : acc[k];
+            if (k == ed_ch) v = v / fmaxf(alpha, 1e-10f);  // expected depth (rasterization ED)
+            render_colors[tc.pix * D + k] = v;
+        }
 #pragma unroll
         for (int k = 0; k < 3; ++k) render_normals[tc.pix * 3 + k] = nacc[k];
         render_distort[tc.pix] = distort;
@@ -298,10 +304,11 @@ __device__ __forceinline__ int32_t wave_max2(int32_t v) {
 template <int D, bool ABS>
 __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     int C, int W, int H, int tw, int th, const Rec2* __restrict__ rec, const float* __restrict__ backgrounds,
-    const int32_t* __restrict__ offsets, int64_t n_isects, const int32_t* __restrict__ flatten_ids,
-    const float* __restrict__ render_alphas, const int32_t* __restrict__ last_ids,
-    const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
-    const float* __restrict__ v_render_normals, float* __restrict__ acc_rows) {
+    int bg_ch, int ed_ch, const float* __restrict__ render_colors, const int32_t* __restrict__ offsets,
+    int64_t n_isects, const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
+    const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
+    const float* __restrict__ v_render_alphas, const float* __restrict__ v_render_normals,
+    float* __restrict__ acc_rows) {
     // row layout: 0-1 xy, 2-4 sum (p-m)_x v_c, 5-7 sum (p-m)_y v_c, 8-10 sum v_c (v_c = dL/d(h_u x h_v)),
     // 11 opac, 12-14 normal, 15.. colour, then abs xy; split2 maps v_c sums to u, v, w and densify
     constexpr int KV = 15 + D + (ABS ? 2 : 0);
@@ -320,15 +327,27 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     // Bsum = sum_k buf_k vo_k + sum_k nbuf_k vn_k: the only form in which the
     // colour/normal composited behind the current surfel enters v_alpha
     float Bsum = 0.f, vo[4] = {0.f, 0.f, 0.f, 0.f}, vn[3];
-    float bg_dot = 0.f;
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-        vo[k] = tc.inside ? v_render_colors[tc.pix * D + k] : 0.f;
-        if (backgrounds) bg_dot += backgrounds[tc.cam * D + k] * vo[k];
-    }
+    for (int k = 0; k < D; ++k) vo[k] = tc.inside ? v_render_colors[tc.pix * D + k] : 0.f;
 #pragma unroll
     for (int k = 0; k < 3; ++k) vn[k] = tc.inside ? v_render_normals[tc.pix * 3 + k] : 0.f;
-    const float va = tc.inside ? v_render_alphas[tc.pix] : 0.f;
+    float va = tc.inside ? v_render_alphas[tc.pix] : 0.f;
+    if (ed_ch >= 0 && tc.inside) {
+        // ED = raw / max(alpha, 1e-10): d/d raw = 1/ac, d/d alpha = -ED/ac (alpha >= 1e-10)
+        const float alpha = 1.0f - T_final, ac = fmaxf(alpha, 1e-10f);
+        float v_ed = 0.f;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+            if (k == ed_ch) {
+                v_ed = vo[k];
+                vo[k] = v_ed / ac;
+            }
+        if (alpha >= 1e-10f) va -= v_ed * render_colors[tc.pix * D + ed_ch] / ac;
+    }
+    float bg_dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+        if (backgrounds && k < bg_ch) bg_dot += backgrounds[tc.cam * bg_ch + k] * vo[k];
     const float va_term = T_final * (va - bg_dot);
     const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
     const int32_t wave_final = wave_max2(bin_final);
@@ -453,59 +472,75 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
 //   v_u = gB x w + v x gC,  v_v = w x gA + gC x u,  v_w = gA x v + u x gB;
 // the densification proxy (d loss / d screen translation) is v_xy - (A.gC, B.gC).
 template <int D, bool ABS>
-__global__ __launch_bounds__(256) void split2_kernel(int64_t n, const float* __restrict__ rows,
+__global__ __launch_bounds__(256) void split2_kernel(int C, int N, const float* __restrict__ rows,
                                                      const float* __restrict__ rt, const float2* __restrict__ means2d,
                                                      float2* __restrict__ v_means2d, float* __restrict__ v_rt,
-                                                     float* __restrict__ v_colors, float* __restrict__ v_opacities,
-                                                     float* __restrict__ v_normals, float2* __restrict__ v_densify,
-                                                     float2* __restrict__ v_abs) {
+                                                     ChanDst cd, float* __restrict__ v_normals,
+                                                     float2* __restrict__ v_densify, float2* __restrict__ v_abs) {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (g >= n) return;
-    const float4* r4 = reinterpret_cast<const float4*>(rows + g * kRec2);
-    float r[kRec2];
+    if (g >= N) return;
+    float col_sum[4] = {0.f, 0.f, 0.f, 0.f}, op_sum = 0.f;
+    for (int c = 0; c < C; ++c) {
+        const int64_t i = (int64_t)c * N + g;
+        const float4* r4 = reinterpret_cast<const float4*>(rows + i * kRec2);
+        float r[kRec2];
 #pragma unroll
-    for (int q = 0; q < (15 + D + 2 + 3) / 4; ++q) {
-        const float4 v = r4[q];
-        r[q * 4] = v.x; r[q * 4 + 1] = v.y; r[q * 4 + 2] = v.z; r[q * 4 + 3] = v.w;
+        for (int q = 0; q < (15 + D + 2 + 3) / 4; ++q) {
+            const float4 v = r4[q];
+            r[q * 4] = v.x; r[q * 4 + 1] = v.y; r[q * 4 + 2] = v.z; r[q * 4 + 3] = v.w;
+        }
+        double u[3], v[3], w[3], gA[3], gB[3], gC[3];
+        const float2 mm = means2d[i];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            u[k] = rt[i * 9 + k];
+            v[k] = rt[i * 9 + 3 + k];
+            w[k] = rt[i * 9 + 6 + k];
+            gC[k] = r[8 + k];
+            gA[k] = (double)r[2 + k] + (double)mm.x * gC[k];
+            gB[k] = (double)r[5 + k] + (double)mm.y * gC[k];
+        }
+        double t0[3], t1[3];
+        cross3d(gB, w, t0);
+        cross3d(v, gC, t1);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) v_rt[i * 9 + k] = (float)(t0[k] + t1[k]);
+        cross3d(w, gA, t0);
+        cross3d(gC, u, t1);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) v_rt[i * 9 + 3 + k] = (float)(t0[k] + t1[k]);
+        cross3d(gA, v, t0);
+        cross3d(u, gB, t1);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) v_rt[i * 9 + 6 + k] = (float)(t0[k] + t1[k]);
+        v_means2d[i] = make_float2(r[0], r[1]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) v_normals[i * 3 + k] = r[12 + k];
+        if (v_densify) {
+            double A[3], B[3];
+            cross3d(v, w, A);
+            cross3d(w, u, B);
+            v_densify[i] = make_float2((float)((double)r[0] - (A[0] * gC[0] + A[1] * gC[1] + A[2] * gC[2])),
+                                       (float)((double)r[1] - (B[0] * gC[0] + B[1] * gC[1] + B[2] * gC[2])));
+        }
+        if (cd.op_shared) op_sum += r[11];
+        else cd.opac[i] = r[11];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            if (k < cd.dc) {
+                if (cd.col_shared) col_sum[k] += r[15 + k];
+                else cd.colors[i * cd.dc + k] = r[15 + k];
+            } else if (cd.depths) {
+                cd.depths[i] = r[15 + k];
+            }
+        }
+        if (ABS) v_abs[i] = make_float2(r[15 + D], r[16 + D]);
     }
-    double u[3], v[3], w[3], gA[3], gB[3], gC[3];
-    const float2 mm = means2d[g];
+    if (cd.op_shared) cd.opac[g] = op_sum;
+    if (cd.col_shared)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        u[k] = rt[g * 9 + k];
-        v[k] = rt[g * 9 + 3 + k];
-        w[k] = rt[g * 9 + 6 + k];
-        gC[k] = r[8 + k];
-        gA[k] = (double)r[2 + k] + (double)mm.x * gC[k];
-        gB[k] = (double)r[5 + k] + (double)mm.y * gC[k];
-    }
-    double t0[3], t1[3];
-    cross3d(gB, w, t0);
-    cross3d(v, gC, t1);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) v_rt[g * 9 + k] = (float)(t0[k] + t1[k]);
-    cross3d(w, gA, t0);
-    cross3d(gC, u, t1);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) v_rt[g * 9 + 3 + k] = (float)(t0[k] + t1[k]);
-    cross3d(gA, v, t0);
-    cross3d(u, gB, t1);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) v_rt[g * 9 + 6 + k] = (float)(t0[k] + t1[k]);
-    v_means2d[g] = make_float2(r[0], r[1]);
-    v_opacities[g] = r[11];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) v_normals[g * 3 + k] = r[12 + k];
-    if (v_densify) {
-        double A[3], B[3];
-        cross3d(v, w, A);
-        cross3d(w, u, B);
-        v_densify[g] = make_float2((float)((double)r[0] - (A[0] * gC[0] + A[1] * gC[1] + A[2] * gC[2])),
-                                   (float)((double)r[1] - (B[0] * gC[0] + B[1] * gC[1] + B[2] * gC[2])));
-    }
-#pragma unroll
-    for (int k = 0; k < D; ++k) v_colors[g * D + k] = r[15 + k];
-    if (ABS) v_abs[g] = make_float2(r[15 + D], r[16 + D]);
+        for (int k = 0; k < D; ++k)
+            if (k < cd.dc) cd.colors[g * cd.dc + k] = col_sum[k];
 }
 
 }  // namespace hgsr
@@ -522,14 +557,13 @@ static int check_raster2(int C, int N, int D, int W, int H, int tile_size, int t
 
 static size_t rec2_bytes(int C, int N) { return ((size_t)C * N * sizeof(Rec2) + 255) & ~(size_t)255; }
 
-static int pack2(int C, int N, int D, const float* means2d, const float* rt, const float* colors,
-                 const float* opacities, const float* normals, Rec2* rec, hipStream_t s) {
+static int pack2(int C, int N, int D, const float* means2d, const float* rt, const ChanSrc& cs,
+                 const float* normals, Rec2* rec, hipStream_t s) {
     const int64_t n = (int64_t)C * N;
     if (n == 0) return HGSR_OK;
     const dim3 grid((unsigned)((n + 255) / 256));
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
-#define LAUNCH_P2(DD) \
-    hipLaunchKernelGGL(pack2_kernel<DD>, grid, dim3(256), 0, s, n, m2, rt, colors, opacities, normals, rec)
+#define LAUNCH_P2(DD) hipLaunchKernelGGL(pack2_kernel<DD>, grid, dim3(256), 0, s, n, N, m2, rt, cs, normals, rec)
     switch (D) {
         case 1: LAUNCH_P2(1); break;
         case 2: LAUNCH_P2(2); break;
@@ -545,31 +579,31 @@ extern "C" size_t hgsr_raster2d_fwd_ws_bytes(int C, int N, int D) {
     return rec2_bytes(C, N);
 }
 
-extern "C" int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
-                                 const float* colors, const float* opacities, const float* normals,
-                                 const float* backgrounds, int width, int height, int tile_size, int tile_w,
-                                 int tile_h, const int32_t* isect_offsets, int64_t n_isects,
-                                 const int32_t* flatten_ids, float* render_colors, float* render_alphas,
-                                 float* render_normals, float* render_distort, float* render_median,
-                                 int32_t* last_ids, int32_t* median_ids, void* ws, size_t ws_bytes,
-                                 hgsr_stream_t stream) {
+static int raster2d_fwd_impl(int C, int N, int D, const float* means2d, const float* rt, const ChanSrc& cs,
+                             const float* normals, const float* backgrounds, int bg_ch, int ed_ch, int width,
+                             int height, int tile_size, int tile_w, int tile_h, const int32_t* isect_offsets,
+                             int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
+                             float* render_alphas, float* render_normals, float* render_distort,
+                             float* render_median, int32_t* last_ids, int32_t* median_ids, void* ws,
+                             size_t ws_bytes, hgsr_stream_t stream) {
     if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_fwd_ws_bytes(C, N, D), "raster2d_fwd workspace too small");
     HGSR_REQUIRE(isect_offsets && render_colors && render_alphas && render_normals && render_distort &&
                      render_median && last_ids && median_ids,
                  "null pointer");
-    HGSR_REQUIRE(n_isects == 0 || (means2d && ray_transforms && colors && opacities && normals && flatten_ids && ws),
+    HGSR_REQUIRE(n_isects == 0 || (means2d && rt && (cs.colors || cs.dc == 0) && cs.opac && normals &&
+                                   flatten_ids && ws),
                  "null pointer");
     hipStream_t s = as_stream(stream);
     Rec2* rec = (Rec2*)ws;
     if (n_isects > 0)
-        if (int st = pack2(C, N, D, means2d, ray_transforms, colors, opacities, normals, rec, s)) return st;
+        if (int st = pack2(C, N, D, means2d, rt, cs, normals, rec, s)) return st;
     const dim3 grid(C * tile_w * tile_h);
     KernelTimer kt("raster2d_fwd", s);
 #define LAUNCH_F2(DD)                                                                                            \
     hipLaunchKernelGGL(raster2d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,     \
-                       backgrounds, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,          \
-                       render_normals, render_distort, render_median, last_ids, median_ids)
+                       backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,           \
+                       render_alphas, render_normals, render_distort, render_median, last_ids, median_ids)
     switch (D) {
         case 1: LAUNCH_F2(1); break;
         case 2: LAUNCH_F2(2); break;
@@ -580,10 +614,110 @@ extern "C" int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, cons
     return check_launch("raster2d_fwd");
 }
 
+extern "C" int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
+                                 const float* colors, const float* opacities, const float* normals,
+                                 const float* backgrounds, int width, int height, int tile_size, int tile_w,
+                                 int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                                 const int32_t* flatten_ids, float* render_colors, float* render_alphas,
+                                 float* render_normals, float* render_distort, float* render_median,
+                                 int32_t* last_ids, int32_t* median_ids, void* ws, size_t ws_bytes,
+                                 hgsr_stream_t stream) {
+    const ChanSrc cs{colors, (int64_t)N * D, D, nullptr, opacities, (int64_t)N};
+    return raster2d_fwd_impl(C, N, D, means2d, ray_transforms, cs, normals, backgrounds, D, -1, width, height,
+                             tile_size, tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors,
+                             render_alphas, render_normals, render_distort, render_median, last_ids, median_ids, ws,
+                             ws_bytes, stream);
+}
+
+extern "C" int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
+                                       const float* colors, int colors_shared, const float* depths,
+                                       int expected_depth, const float* opacities, int opacities_shared,
+                                       const float* normals, const float* backgrounds, int width, int height,
+                                       int tile_size, int tile_w, int tile_h, const int32_t* isect_offsets,
+                                       int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
+                                       float* render_alphas, float* render_normals, float* render_distort,
+                                       float* render_median, int32_t* last_ids, int32_t* median_ids, void* ws,
+                                       size_t ws_bytes, hgsr_stream_t stream) {
+    HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
+    HGSR_REQUIRE(!(expected_depth && !depths), "expected_depth needs depths");
+    const int D = Dc + (depths ? 1 : 0);
+    const ChanSrc cs{colors, colors_shared ? 0 : (int64_t)N * Dc, Dc, depths, opacities,
+                     opacities_shared ? 0 : (int64_t)N};
+    return raster2d_fwd_impl(C, N, D, means2d, ray_transforms, cs, normals, backgrounds, Dc,
+                             expected_depth ? Dc : -1, width, height, tile_size, tile_w, tile_h, isect_offsets,
+                             n_isects, flatten_ids, render_colors, render_alphas, render_normals, render_distort,
+                             render_median, last_ids, median_ids, ws, ws_bytes, stream);
+}
+
 extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
     (void)D;
     const size_t rows_b = ((size_t)C * N * kRec2 * sizeof(float) + 255) & ~(size_t)255;
     return rows_b + (reuse_fwd ? 0 : rec2_bytes(C, N));
+}
+
+static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const float* rt, const ChanSrc& cs,
+                             const float* normals, const float* backgrounds, int bg_ch, int ed_ch,
+                             const float* render_colors, int width, int height, int tile_size, int tile_w,
+                             int tile_h, const int32_t* isect_offsets, int64_t n_isects, const int32_t* flatten_ids,
+                             const float* render_alphas, const int32_t* last_ids, const float* v_render_colors,
+                             const float* v_render_alphas, const float* v_render_normals, float* v_means2d,
+                             float* v_rt, const ChanDst& cd, float* v_normals, float* v_densify,
+                             const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
+    if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
+    HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
+                 "raster2d_bwd workspace too small");
+    HGSR_REQUIRE(ed_ch < 0 || render_colors, "expected-depth backward needs render_colors");
+    if (N == 0) return HGSR_OK;
+    HGSR_REQUIRE(v_means2d && v_rt && (cd.colors || cd.dc == 0) && cd.opac && v_normals, "null pointer");
+    hipStream_t s = as_stream(stream);
+    const int64_t n = (int64_t)C * N;
+    if (n_isects == 0) {  // nothing composited: every gradient is zero
+        if (int st = memset_async(v_means2d, n * 2 * sizeof(float), s, "raster2d_bwd")) return st;
+        if (int st = memset_async(v_rt, n * 9 * sizeof(float), s, "raster2d_bwd")) return st;
+        if (cd.dc)
+            if (int st = memset_async(cd.colors, (cd.col_shared ? N : n) * cd.dc * sizeof(float), s, "raster2d_bwd"))
+                return st;
+        if (cd.depths)
+            if (int st = memset_async(cd.depths, n * sizeof(float), s, "raster2d_bwd")) return st;
+        if (int st = memset_async(cd.opac, (cd.op_shared ? N : n) * sizeof(float), s, "raster2d_bwd")) return st;
+        if (int st = memset_async(v_normals, n * 3 * sizeof(float), s, "raster2d_bwd")) return st;
+        if (v_densify)
+            if (int st = memset_async(v_densify, n * 2 * sizeof(float), s, "raster2d_bwd")) return st;
+        return HGSR_OK;
+    }
+    HGSR_REQUIRE(means2d && rt && normals && isect_offsets && flatten_ids && render_alphas && last_ids &&
+                     v_render_colors && v_render_alphas && v_render_normals && ws,
+                 "null pointer");
+    const size_t rows_b = ((size_t)C * N * kRec2 * sizeof(float) + 255) & ~(size_t)255;
+    float* rows = (float*)ws;
+    const float2* m2 = reinterpret_cast<const float2*>(means2d);
+    if (int st = memset_async(rows, (size_t)C * N * kRec2 * sizeof(float), s, "raster2d_bwd")) return st;
+    const Rec2* rec = (const Rec2*)fwd_ws;
+    if (!rec) {
+        Rec2* own = (Rec2*)((char*)ws + rows_b);
+        if (int st = pack2(C, N, D, means2d, rt, cs, normals, own, s)) return st;
+        rec = own;
+    }
+    const dim3 grid(C * tile_w * tile_h);
+#define LAUNCH_B2(DD)                                                                                             \
+    {                                                                                                             \
+        KernelTimer kt("raster2d_bwd", s);                                                                        \
+        hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
+                           tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,        \
+                           flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,                \
+                           v_render_normals, rows);                                                               \
+    }                                                                                                             \
+    hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s,   \
+                       C, N, rows, rt, m2, reinterpret_cast<float2*>(v_means2d), v_rt, cd, v_normals,             \
+                       reinterpret_cast<float2*>(v_densify), nullptr)
+    switch (D) {
+        case 1: LAUNCH_B2(1); break;
+        case 2: LAUNCH_B2(2); break;
+        case 3: LAUNCH_B2(3); break;
+        default: LAUNCH_B2(4); break;
+    }
+#undef LAUNCH_B2
+    return check_launch("raster2d_bwd");
 }
 
 extern "C" int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
@@ -595,56 +729,37 @@ extern "C" int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, cons
                                  const float* v_render_normals, float* v_means2d, float* v_ray_transforms,
                                  float* v_colors, float* v_opacities, float* v_normals, float* v_densify,
                                  const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
-    if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
-    HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
-                 "raster2d_bwd workspace too small");
-    if (N == 0) return HGSR_OK;
-    hipStream_t s = as_stream(stream);
-    if (n_isects == 0) {  // nothing composited: every gradient is zero
-        HGSR_REQUIRE(v_means2d && v_ray_transforms && v_colors && v_opacities && v_normals, "null pointer");
-        const size_t n = (size_t)C * N;
-        if (int st = memset_async(v_means2d, n * 2 * sizeof(float), s, "raster2d_bwd")) return st;
-        if (int st = memset_async(v_ray_transforms, n * 9 * sizeof(float), s, "raster2d_bwd")) return st;
-        if (int st = memset_async(v_colors, n * D * sizeof(float), s, "raster2d_bwd")) return st;
-        if (int st = memset_async(v_opacities, n * sizeof(float), s, "raster2d_bwd")) return st;
-        if (int st = memset_async(v_normals, n * 3 * sizeof(float), s, "raster2d_bwd")) return st;
-        if (v_densify)
-            if (int st = memset_async(v_densify, n * 2 * sizeof(float), s, "raster2d_bwd")) return st;
-        return HGSR_OK;
-    }
-    HGSR_REQUIRE(means2d && ray_transforms && colors && opacities && normals && isect_offsets && flatten_ids &&
-                     render_alphas && last_ids && v_render_colors && v_render_alphas && v_render_normals &&
-                     v_means2d && v_ray_transforms && v_colors && v_opacities && v_normals && ws,
-                 "null pointer");
-    const size_t rows_b = ((size_t)C * N * kRec2 * sizeof(float) + 255) & ~(size_t)255;
-    float* rows = (float*)ws;
-    const float2* m2 = reinterpret_cast<const float2*>(means2d);
-    if (int st = memset_async(rows, (size_t)C * N * kRec2 * sizeof(float), s, "raster2d_bwd")) return st;
-    const Rec2* rec = (const Rec2*)fwd_ws;
-    if (!rec) {
-        Rec2* own = (Rec2*)((char*)ws + rows_b);
-        if (int st = pack2(C, N, D, means2d, ray_transforms, colors, opacities, normals, own, s)) return st;
-        rec = own;
-    }
-    const dim3 grid(C * tile_w * tile_h);
-#define LAUNCH_B2(DD)                                                                                             \
-    {                                                                                                             \
-        KernelTimer kt("raster2d_bwd", s);                                                                        \
-        hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
-                           tile_h, rec, backgrounds, isect_offsets, n_isects, flatten_ids, render_alphas, last_ids, \
-                           v_render_colors, v_render_alphas, v_render_normals, rows);                             \
-    }                                                                                                             \
-    hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)C * N + 255) / 256)), dim3(256), 0,  \
-                       s, (int64_t)C * N, rows, ray_transforms, m2, reinterpret_cast<float2*>(v_means2d),          \
-                       v_ray_transforms,                                                                           \
-                       v_colors,                                                                                   \
-                       v_opacities, v_normals, reinterpret_cast<float2*>(v_densify), nullptr)
-    switch (D) {
-        case 1: LAUNCH_B2(1); break;
-        case 2: LAUNCH_B2(2); break;
-        case 3: LAUNCH_B2(3); break;
-        default: LAUNCH_B2(4); break;
-    }
-#undef LAUNCH_B2
-    return check_launch("raster2d_bwd");
+    const ChanSrc cs{colors, (int64_t)N * D, D, nullptr, opacities, (int64_t)N};
+    const ChanDst cd{v_colors, false, D, nullptr, v_opacities, false};
+    return raster2d_bwd_impl(C, N, D, means2d, ray_transforms, cs, normals, backgrounds, D, -1, nullptr, width,
+                             height, tile_size, tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_alphas,
+                             last_ids, v_render_colors, v_render_alphas, v_render_normals, v_means2d,
+                             v_ray_transforms, cd, v_normals, v_densify, fwd_ws, ws, ws_bytes, stream);
+}
+
+extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
+                                       const float* colors, int colors_shared, const float* depths,
+                                       int expected_depth, const float* opacities, int opacities_shared,
+                                       const float* normals, const float* backgrounds, int width, int height,
+                                       int tile_size, int tile_w, int tile_h, const int32_t* isect_offsets,
+                                       int64_t n_isects, const int32_t* flatten_ids, const float* render_colors,
+                                       const float* render_alphas, const int32_t* last_ids,
+                                       const float* v_render_colors, const float* v_render_alphas,
+                                       const float* v_render_normals, float* v_means2d, float* v_ray_transforms,
+                                       float* v_colors, float* v_depths, float* v_opacities, float* v_normals,
+                                       float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
+                                       hgsr_stream_t stream) {
+    HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
+    HGSR_REQUIRE(!(expected_depth && !depths), "expected_depth needs depths");
+    HGSR_REQUIRE(!depths || v_depths, "null pointer");
+    const int D = Dc + (depths ? 1 : 0);
+    const ChanSrc cs{colors, colors_shared ? 0 : (int64_t)N * Dc, Dc, depths, opacities,
+                     opacities_shared ? 0 : (int64_t)N};
+    const ChanDst cd{v_colors, colors_shared != 0, Dc, depths ? v_depths : nullptr, v_opacities,
+                     opacities_shared != 0};
+    return raster2d_bwd_impl(C, N, D, means2d, ray_transforms, cs, normals, backgrounds, Dc,
+                             expected_depth ? Dc : -1, render_colors, width, height, tile_size, tile_w, tile_h,
+                             isect_offsets, n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
+                             v_render_alphas, v_render_normals, v_means2d, v_ray_transforms, cd, v_normals,
+                             v_densify, fwd_ws, ws, ws_bytes, stream);
 }

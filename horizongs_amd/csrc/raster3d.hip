@@ -76,20 +76,6 @@ __device__ __forceinline__ float2 footprint(float a, float b, float c, float opa
     return make_float2(sqrtf(k * c) * 1.01f + 0.01f, sqrtf(k * a) * 1.01f + 0.01f);
 }
 
-// Where a raster call's channels come from.  gsplat's rasterize_to_pixels takes
-// colors [C,N,D] and opacities [C,N]; rasterization() itself concatenates the depth
-// and repeats shared colours/opacities over cameras, which the fused entry points do
-// here instead: channel k < dc is colors[c*col_cstride + g*dc + k] (col_cstride 0 =
-// shared over cameras), channel dc is depths[c*N + g] when depths != nullptr.
-struct ChanSrc {
-    const float* colors;
-    int64_t col_cstride;
-    int dc;
-    const float* depths;
-    const float* opac;
-    int64_t op_cstride;
-};
-
 template <int D>
 __global__ __launch_bounds__(256) void pack3_kernel(int64_t n, int N, const float2* __restrict__ means2d,
                                                     const float* __restrict__ conics, ChanSrc cs,
@@ -423,18 +409,6 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
         lds_barrier();
     }
 }
-
-// Where a backward's channel gradients go (mirror of ChanSrc): v_colors has the
-// layout of the colours (shared ones are summed over cameras), v_depths [C,N]
-// (nullable), v_opac has the layout of the opacities.
-struct ChanDst {
-    float* colors;
-    bool col_shared;
-    int dc;
-    float* depths;
-    float* opac;
-    bool op_shared;
-};
 
 // scatter accumulator rows into gsplat's separate gradient tensors (overwrite);
 // one lane per Gaussian, looping cameras in order (deterministic sums)

@@ -466,6 +466,74 @@ class _Raster2D(torch.autograd.Function):
         return v_means2d, v_rt, v_colors, v_opac, v_normals, v_dens, v_bg, None, None, None, None, None
 
 
+class _Raster2DFused(torch.autograd.Function):
+    """rasterization_2dgs()'s colour assembly + rasterize_to_pixels_2dgs + ED as one
+    native call each way (hgsr_raster2d_{fwd,bwd}_fused); see _Raster3DFused."""
+
+    @staticmethod
+    def forward(ctx, means2d, rt, colors, depths, opacities, normals, densify, backgrounds, width, height,
+                tile_size, isect_offsets, flatten_ids, expected_depth):
+        C, Ng = means2d.shape[:2]
+        Dc = 0 if colors is None else colors.shape[-1]
+        D = Dc + (0 if depths is None else 1)
+        col_shared = colors is not None and colors.dim() == 2
+        op_shared = opacities.dim() == 1
+        th, tw = isect_offsets.shape[1:]
+        dev = means2d.device
+        rc = torch.empty((C, height, width, D), dtype=torch.float32, device=dev)
+        ra = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
+        rn = torch.empty((C, height, width, 3), dtype=torch.float32, device=dev)
+        rd = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
+        rm = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
+        last = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        med = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        ws_b = N.size_query("hgsr_raster2d_fwd_ws_bytes", C, Ng, D)
+        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+        N.call("hgsr_raster2d_fwd_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors), int(col_shared),
+               ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(normals), ptr(backgrounds),
+               width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
+               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(rn), ptr(rd), ptr(rm),
+               ptr(last), ptr(med), ptr(ws), ws_b, N.stream(dev))
+        ctx.save_for_backward(means2d, rt, colors, depths, opacities, normals, backgrounds, isect_offsets,
+                              flatten_ids, rc, ra, last)
+        ctx.cfg = (width, height, tile_size, expected_depth, Dc, col_shared, op_shared)
+        ctx.fwd_ws = ws  # packed surfel records, reused by the backward
+        ctx.mark_non_differentiable(rd, rm)
+        return rc, ra, rn, rd, rm
+
+    @staticmethod
+    def backward(ctx, v_rc, v_ra, v_rn, v_rd, v_rm):
+        (means2d, rt, colors, depths, opacities, normals, backgrounds, offsets, flatten_ids, rc, ra,
+         last) = ctx.saved_tensors
+        width, height, tile_size, expected_depth, Dc, col_shared, op_shared = ctx.cfg
+        C, Ng = means2d.shape[:2]
+        D = Dc + (0 if depths is None else 1)
+        th, tw = offsets.shape[1:]
+        dev = means2d.device
+        v_means2d = torch.empty_like(means2d)
+        v_rt = torch.empty_like(rt)
+        v_colors = None if colors is None else torch.empty_like(colors)
+        v_depths = None if depths is None else torch.empty_like(depths)
+        v_opac = torch.empty_like(opacities)
+        v_normals = torch.empty_like(normals)
+        v_dens = torch.empty_like(means2d)
+        fwd_ws = ctx.fwd_ws
+        ws_b = N.size_query("hgsr_raster2d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
+        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+        v_rc, v_ra, v_rn = _f32(v_rc), _f32(v_ra), _f32(v_rn)
+        N.call("hgsr_raster2d_bwd_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors), int(col_shared),
+               ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(normals), ptr(backgrounds),
+               width, height, tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
+               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
+               ptr(v_rn), ptr(v_means2d), ptr(v_rt), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_normals),
+               ptr(v_dens), ptr(fwd_ws), ptr(ws), ws_b, N.stream(dev))
+        v_bg = None
+        if backgrounds is not None and ctx.needs_input_grad[7]:
+            v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))
+        return (v_means2d, v_rt, v_colors, v_depths, v_opac, v_normals, v_dens, v_bg, None, None, None, None, None,
+                None)
+
+
 def rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals, densify, image_width,
                              image_height, tile_size, isect_offsets, flatten_ids, backgrounds=None, masks=None,
                              packed=False, absgrad=False, distloss=False):
@@ -621,24 +689,38 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
     chain-rule gradient and the densification proxy goes to meta["gradient_2dgs"].grad."""
     assert render_mode in ("RGB", "D", "ED", "RGB+D", "RGB+ED"), render_mode
     _unsupported(packed, "packed=True")
+    _unsupported(distloss, "distloss backward")
     C, Ng = viewmats.shape[0], means.shape[0]
     densifications = torch.zeros((C, Ng, 2), dtype=means.dtype, device=means.device, requires_grad=True)
     radii, means2d, depths, ray_transforms, normals = fully_fused_projection_2dgs(
         means, quats, scales, viewmats, densifications, Ks, width, height, eps2d=eps2d, packed=False,
         near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip, sparse_grad=sparse_grad)
-    opac = opacities.repeat(C, 1)
     cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
-    if cols.dim() == 2:
-        cols = cols.expand(C, -1, -1)
-    cols, bgs = _with_depth(cols, backgrounds, depths, render_mode, C)
     tw, th = _tile_grid(width, height, tile_size)
     tpg, isect_ids, flatten_ids, isect_offsets = _isect_binned(means2d, radii, int(tile_size), tw, th, depths)
-    render_colors, render_alphas, render_normals, render_distort, render_median = rasterize_to_pixels_2dgs(
-        means2d, ray_transforms, cols, opac, normals, densifications, width, height, tile_size, isect_offsets,
-        flatten_ids, backgrounds=bgs, absgrad=absgrad, distloss=distloss)
-    if render_mode in ("ED", "RGB+ED"):
-        render_colors = torch.cat([render_colors[..., :-1],
-                                   render_colors[..., -1:] / render_alphas.clamp(min=1e-10)], dim=-1)
+    with_depth = render_mode in ("RGB+D", "RGB+ED", "D", "ED")
+    rgb = render_mode in ("RGB", "RGB+D", "RGB+ED")
+    Dc = cols.shape[-1] if rgb else 0
+    if Dc + int(with_depth) <= _MAX_CH and not absgrad:
+        # one fused native call each way: no cat / repeat / ED divide in torch
+        bgs = None if (backgrounds is None or not rgb) else _f32(backgrounds)
+        opac = opacities.expand(C, -1)
+        render_colors, render_alphas, render_normals, render_distort, render_median = _Raster2DFused.apply(
+            _f32(means2d), _f32(ray_transforms.reshape(C, Ng, 9)), _f32(cols) if rgb else None,
+            _f32(depths) if with_depth else None, _f32(opacities), _f32(normals), densifications, bgs, int(width),
+            int(height), int(tile_size), isect_offsets.contiguous(), flatten_ids.contiguous(),
+            render_mode in ("ED", "RGB+ED"))
+    else:
+        opac = opacities.repeat(C, 1)
+        if cols.dim() == 2:
+            cols = cols.expand(C, -1, -1)
+        cols, bgs = _with_depth(cols, backgrounds, depths, render_mode, C)
+        render_colors, render_alphas, render_normals, render_distort, render_median = rasterize_to_pixels_2dgs(
+            means2d, ray_transforms, cols, opac, normals, densifications, width, height, tile_size, isect_offsets,
+            flatten_ids, backgrounds=bgs, absgrad=absgrad, distloss=distloss)
+        if render_mode in ("ED", "RGB+ED"):
+            render_colors = torch.cat([render_colors[..., :-1],
+                                       render_colors[..., -1:] / render_alphas.clamp(min=1e-10)], dim=-1)
     c2w = _camtoworlds(viewmats)
     render_normals_from_depth = None
     if render_mode in ("RGB+ED", "RGB+D"):

@@ -215,6 +215,31 @@ int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, const float* ra
                       float* v_opacities, float* v_normals, float* v_densify,
                       const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream);
 
+/* Fused channel assembly for rasterization_2dgs (same conventions as
+ * hgsr_raster3d_fwd_fused; the depth channel, when present, also drives the
+ * median depth and the distortion map). */
+int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
+                            const float* colors, int colors_shared, const float* depths,
+                            int expected_depth, const float* opacities, int opacities_shared,
+                            const float* normals, const float* backgrounds, int width, int height,
+                            int tile_size, int tile_w, int tile_h, const int32_t* isect_offsets,
+                            int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
+                            float* render_alphas, float* render_normals, float* render_distort,
+                            float* render_median, int32_t* last_ids, int32_t* median_ids, void* ws,
+                            size_t ws_bytes, hgsr_stream_t stream);
+int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
+                            const float* colors, int colors_shared, const float* depths,
+                            int expected_depth, const float* opacities, int opacities_shared,
+                            const float* normals, const float* backgrounds, int width, int height,
+                            int tile_size, int tile_w, int tile_h, const int32_t* isect_offsets,
+                            int64_t n_isects, const int32_t* flatten_ids, const float* render_colors,
+                            const float* render_alphas, const int32_t* last_ids,
+                            const float* v_render_colors, const float* v_render_alphas,
+                            const float* v_render_normals, float* v_means2d, float* v_ray_transforms,
+                            float* v_colors, float* v_depths, float* v_opacities, float* v_normals,
+                            float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
+                            hgsr_stream_t stream);
+
 /* ---- measurement ----------------------------------------------------------
  * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):
  * when enabled, the main kernel of every entry point is bracketed by
