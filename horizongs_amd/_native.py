@@ -58,6 +58,12 @@ _SIGS = {
                                     P, P, P, SZ, P]),
     "hgsr_raster2d_bwd_fused": (I, [I, I, I, P, P, P, I, P, I, P, I, P, P, I, I, I, I, I, P, I64, P, P, P, P, P,
                                     P, P, P, P, P, P, P, P, P, P, P, SZ, P]),
+    "hgsr_lod_mask": (I, [I, P, P, P, P, F, F, F, I, P, P]),
+    "hgsr_decode_ws_bytes": (SZ, [I]),
+    "hgsr_decode_count": (I, [I, I, I, I, I, P, P, P, P, P, P, SZ, P, P]),
+    "hgsr_decode_fwd": (I, [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P]),
+    "hgsr_decode_bwd_ws_bytes": (SZ, [I]),
+    "hgsr_decode_bwd": (I, [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P]),
     "hgsr_timing_enable": (I, [I]),
     "hgsr_timing_reset": (I, []),
     "hgsr_timing_query": (I, [ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(I64)]),

@@ -1,0 +1,841 @@
+// K14: anchor -> neural-Gaussian decode, forward.
+//
+// Reference semantics: scene/lod_model.py:286-290 (LoD mask), scene/basic_model.py:297-371
+// (generate_neural_gaussians) with the MLPs of scene/lod_model.py:67-84
+// (Linear(F+vd -> F) -> ReLU -> Linear(F -> O) [-> Tanh for the opacity head]),
+// appearance_dim = 0 and dist2level != 'progressive' (smooth_complement = 1).
+//
+// CDNA4 mapping
+//  * one 256-lane workgroup per 64 visible anchors (grid-stride), each wave64 owning
+//    16 anchors; the three MLPs' weights staged once per workgroup in LDS;
+//  * both layers on exact-f32 MFMA (v_mfma_f32_16x16x4_f32), computed TRANSPOSED
+//    (anchors are the N = 16 columns): the first layer's accumulator registers hold
+//    H^T[hidden = 4g + r][anchor] (g = lane >> 4), which is directly the B operand of
+//    the second layer's k-step r when the k order inside each 16-hidden group is
+//    permuted to 4g + r -- absorbed by staging W2 with permuted columns, so no lane
+//    movement between the layers;
+//  * LDS strides chosen bank-conflict-free for the 16x4 fragment reads (kDecS, kDecYS);
+//  * opacity > 0 compaction is order-preserving (anchor-major, then offset) with
+//    wave ballots + a per-tile offset table from a count pass and a scan;
+//  * the colour head (pure linear) is stored straight from the accumulators.
+#include "common.h"
+
+namespace hgsr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kDecTile = 64;      // visible anchors per workgroup iteration (4 waves x 16)
+constexpr int kDecF = 32;         // feat_dim (every reference config)
+constexpr int kDecS = 38;         // LDS row stride (floats) of W1 / W2 / X: conflict-free 16x4 fragment reads
+constexpr int kDecYS = 20;        // LDS row stride of the Y^T tiles: conflict-free accumulator stores
+constexpr int kDecMaxRows = 368;  // W2 rows (opacity + cov + colour heads, padded to 16): SH2 x 10 offsets
+
+struct MlpPtrs {
+    const float* w1[3];  // [F, F+vd] (nn.Linear layout), heads: 0 opacity, 1 cov, 2 colour
+    const float* b1[3];
+    const float* w2[3];  // [O_h, F]
+    const float* b2[3];
+};
+
+struct DecodeDims {
+    int Av, vd, noff, cd;
+    int O[3];     // outputs per head: noff, 7 noff, cd noff
+    int T[3];     // 16-row tiles per head
+    int row0[3];  // first W2 row of each head in LDS
+    int rows;     // total padded W2 rows
+};
+
+static DecodeDims decode_dims(int Av, int vd, int noff, int cd) {
+    DecodeDims d;
+    d.Av = Av;
+    d.vd = vd;
+    d.noff = noff;
+    d.cd = cd;
+    d.O[0] = noff;
+    d.O[1] = 7 * noff;
+    d.O[2] = cd * noff;
+    int r = 0;
+    for (int h = 0; h < 3; ++h) {
+        d.T[h] = (d.O[h] + 15) / 16;
+        d.row0[h] = r;
+        r += 16 * d.T[h];
+    }
+    d.rows = r;
+    return d;
+}
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// LDS column of hidden unit h inside its 16-group, so that the second layer's
+// k-step r reads 4 consecutive columns across the lane groups g: 4 (h % 4) + (h % 16) / 4
+__device__ __forceinline__ int w2_col(int h) { return (h & ~15) | ((h & 3) << 2) | ((h & 15) >> 2); }
+
+// LoD mask: dist = |anchor - cam| * res_scale; pred = log2(sd / dist) / log2(fork) + extra;
+// mask = level <= clamp(floor(pred), 0, max_level).  Operation order as the reference.
+__global__ __launch_bounds__(256) void lod_mask_kernel(int A, const float* __restrict__ anchor,
+                                                       const int32_t* __restrict__ level,
+                                                       const float* __restrict__ extra_level,
+                                                       const float* __restrict__ cam, float res_scale,
+                                                       float standard_dist, float log2_fork, int max_level,
+                                                       uint8_t* __restrict__ mask) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= A) return;
+    const float dx = anchor[i * 3] - cam[0], dy = anchor[i * 3 + 1] - cam[1], dz = anchor[i * 3 + 2] - cam[2];
+    const float dist = sqrtf(dx * dx + dy * dy + dz * dz) * res_scale;
+    const float pred = log2f(standard_dist / dist) / log2_fork + extra_level[i];
+    const float fl = floorf(pred);
+    int il = fl <= 0.f ? 0 : (fl >= (float)max_level ? max_level : (int)fl);
+    mask[i] = level[i] <= il ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- shared pieces
+struct DecodeSmem {
+    float w1[96 * kDecS];
+    float b1[96];
+    float w2[kDecMaxRows * kDecS];
+    float b2[kDecMaxRows];
+    float x[4][16 * kDecS];    // per wave: X rows (feat | ob_view | 0)
+    float y[4][80 * kDecYS];   // per wave: opacity / cov pre-activations Y^T[o][anchor]
+    int pos[4][16 * 16];       // per wave: output row of (anchor, offset), -1 if dropped
+    int wave_cnt[4];
+};
+
+__device__ void stage_weights(DecodeSmem& sm, const MlpPtrs& mp, const DecodeDims& d) {
+    const int K1 = kDecF + d.vd;
+    for (int e = threadIdx.x; e < 96 * kDecS; e += 256) {
+        const int h = e / kDecS, k = e - h * kDecS;
+        const int head = h >> 5, hh = h & 31;
+        sm.w1[e] = k < K1 ? mp.w1[head][hh * K1 + k] : 0.f;
+    }
+    for (int h = threadIdx.x; h < 96; h += 256) sm.b1[h] = mp.b1[h >> 5][h & 31];
+    for (int e = threadIdx.x; e < d.rows * kDecF; e += 256) {
+        const int row = e / kDecF, h = e - row * kDecF;
+        int head = 0;
+        while (head < 2 && row >= d.row0[head + 1]) ++head;
+        const int o = row - d.row0[head];
+        sm.w2[row * kDecS + w2_col(h)] = o < d.O[head] ? mp.w2[head][o * kDecF + h] : 0.f;
+    }
+    for (int row = threadIdx.x; row < d.rows; row += 256) {
+        int head = 0;
+        while (head < 2 && row >= d.row0[head + 1]) ++head;
+        const int o = row - d.row0[head];
+        sm.b2[row] = o < d.O[head] ? mp.b2[head][o] : 0.f;
+    }
+}
+
+// X rows of this wave's 16 anchors: feat (F) | ob_view (vd) | zero padding
+__device__ void stage_x(float* sx, const int32_t* __restrict__ vis_idx, int a0, int Av, int vd,
+                        const float* __restrict__ anchor, const float* __restrict__ feat,
+                        const float* __restrict__ cam) {
+    const int lane = threadIdx.x & 63;
+    for (int e = lane; e < 16 * kDecF; e += 64) {
+        const int a = e >> 5, k = e & 31;
+        const int v = a0 + a;
+        float val = 0.f;
+        if (v < Av) {
+            const int id = vis_idx ? vis_idx[v] : v;
+            val = feat[(int64_t)id * kDecF + k];
+        }
+        sx[a * kDecS + k] = val;
+    }
+    if (lane < 16) {
+        const int v = a0 + lane;
+        float ov[3] = {0.f, 0.f, 0.f};
+        if (v < Av && vd > 0) {
+            const int id = vis_idx ? vis_idx[v] : v;
+            const float dx = anchor[id * 3] - cam[0], dy = anchor[id * 3 + 1] - cam[1], dz = anchor[id * 3 + 2] - cam[2];
+            const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
+            ov[0] = dx / dist;
+            ov[1] = dy / dist;
+            ov[2] = dz / dist;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sx[lane * kDecS + kDecF + k] = (k < 3 && vd > 0) ? ov[k] : 0.f;
+    }
+}
+
+// first layer of head `head` (or all three): H^T tiles [16 hidden x 16 anchors], bias + ReLU
+template <int KSTEPS>
+__device__ __forceinline__ f32x4 layer1_tile(const DecodeSmem& sm, const float* sx, int mt) {
+    const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KSTEPS; ++kk)
+        acc = mfma4(sm.w1[(mt * 16 + i) * kDecS + 4 * kk + g], sx[i * kDecS + 4 * kk + g], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = fmaxf(acc[r] + sm.b1[mt * 16 + 4 * g + r], 0.f);
+    return acc;
+}
+
+// second layer: Y^T tile [16 outputs x 16 anchors] of W2 rows [row, row + 16) from the
+// head's two H^T tiles (k = 32 hidden in 8 k-steps, no lane movement)
+__device__ __forceinline__ f32x4 layer2_tile(const DecodeSmem& sm, int row, f32x4 h0, f32x4 h1) {
+    const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* w = sm.w2 + (row + i) * kDecS + g;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc = mfma4(w[4 * r], h0[r], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc = mfma4(w[16 + 4 * r], h1[r], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] += sm.b2[row + 4 * g + r];
+    return acc;
+}
+
+__device__ __forceinline__ int lanes_below_d(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+// opacity head of this wave's 16 anchors -> tanh values in sm.y rows [0, 16); returns
+// the wave's kept count (and the ballot-ordered local position of every kept slot)
+template <int KSTEPS>
+__device__ int opacity_head(DecodeSmem& sm, int wave, int a0, int Av, const DecodeDims& d, bool want_pos) {
+    const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    const float* sx = sm.x[wave];
+    const f32x4 h0 = layer1_tile<KSTEPS>(sm, sx, 0), h1 = layer1_tile<KSTEPS>(sm, sx, 1);
+    const f32x4 y = layer2_tile(sm, d.row0[0], h0, h1);
+    float* sy = sm.y[wave];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sy[(4 * g + r) * kDecYS + i] = tanhf(y[r]);
+    // order-preserving keep positions over slots s = a * noff + k
+    const int nslots = 16 * d.noff;
+    int cnt = 0;
+    for (int s0 = 0; s0 < nslots; s0 += 64) {
+        const int s = s0 + lane;
+        const int a = s / d.noff, k = s - a * d.noff;
+        const bool keep = s < nslots && a0 + a < Av && sy[k * kDecYS + a] > 0.f;
+        const uint64_t m = __ballot(keep);
+        if (want_pos && s < nslots) sm.pos[wave][s] = keep ? cnt + lanes_below_d(m) : -1;
+        cnt += __popcll(m);
+    }
+    return cnt;
+}
+
+// ---------------------------------------------------------------- count pass
+template <int KSTEPS>
+__global__ __launch_bounds__(256) void decode_count_kernel(DecodeDims d, MlpPtrs mp,
+                                                           const int32_t* __restrict__ vis_idx,
+                                                           const float* __restrict__ anchor,
+                                                           const float* __restrict__ feat,
+                                                           const float* __restrict__ cam,
+                                                           int32_t* __restrict__ tile_cnt) {
+    __shared__ DecodeSmem sm;
+    stage_weights(sm, mp, d);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        __syncthreads();
+        const int a0 = t * kDecTile + wave * 16;
+        stage_x(sm.x[wave], vis_idx, a0, d.Av, d.vd, anchor, feat, cam);
+        __syncthreads();
+        const int c = opacity_head<KSTEPS>(sm, wave, a0, d.Av, d, false);
+        if (lane == 0) sm.wave_cnt[wave] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) tile_cnt[t] = sm.wave_cnt[0] + sm.wave_cnt[1] + sm.wave_cnt[2] + sm.wave_cnt[3];
+    }
+}
+
+// exclusive scan of the tile counts -> tile offsets; total = number of kept Gaussians
+__global__ __launch_bounds__(1024) void decode_scan_kernel(int n, const int32_t* __restrict__ cnt,
+                                                           int32_t* __restrict__ off, int64_t* __restrict__ total) {
+    __shared__ int64_t s_sum[1024];
+    const int tid = threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int b0 = min(tid * per, n), b1 = min(b0 + per, n);
+    int64_t local = 0;
+    for (int i = b0; i < b1; ++i) local += cnt[i];
+    s_sum[tid] = local;
+    __syncthreads();
+    for (int dd = 1; dd < 1024; dd <<= 1) {
+        const int64_t v = tid >= dd ? s_sum[tid - dd] : 0;
+        __syncthreads();
+        s_sum[tid] += v;
+        __syncthreads();
+    }
+    int64_t run = s_sum[tid] - local;
+    for (int i = b0; i < b1; ++i) {
+        off[i] = (int32_t)run;
+        run += cnt[i];
+    }
+    if (tid == 1023) total[0] = s_sum[1023];
+}
+
+// ---------------------------------------------------------------- forward
+struct DecodeOut {
+    float* xyz;      // [M,3]
+    float* offsets;  // [M,3]
+    float* color;    // [M,cd]
+    float* opacity;  // [M]
+    float* scaling;  // [M,3]
+    float* rot;      // [M,4]
+    uint8_t* mask;   // [Av*noff]
+    int32_t* slot_row;  // [Av*noff] output row or -1 (kept for the backward)
+};
+
+template <int KSTEPS>
+__global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs mp,
+                                                         const int32_t* __restrict__ vis_idx,
+                                                         const float* __restrict__ anchor,
+                                                         const float* __restrict__ feat,
+                                                         const float* __restrict__ offset,
+                                                         const float* __restrict__ scaling_raw,
+                                                         const float* __restrict__ cam,
+                                                         const int32_t* __restrict__ tile_off, DecodeOut out) {
+    __shared__ DecodeSmem sm;
+    stage_weights(sm, mp, d);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
+    const int noff = d.noff, cd = d.cd;
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        __syncthreads();
+        const int a0 = t * kDecTile + wave * 16;
+        stage_x(sm.x[wave], vis_idx, a0, d.Av, d.vd, anchor, feat, cam);
+        __syncthreads();
+        const int c = opacity_head<KSTEPS>(sm, wave, a0, d.Av, d, true);
+        if (lane == 0) sm.wave_cnt[wave] = c;
+        __syncthreads();
+        int base = tile_off[t];
+        for (int w = 0; w < wave; ++w) base += sm.wave_cnt[w];
+        int* pos = sm.pos[wave];
+        const float* sy = sm.y[wave];
+        // opacity + mask + slot rows
+        for (int s = lane; s < 16 * noff; s += 64) {
+            const int a = s / noff, k = s - a * noff;
+            if (a0 + a >= d.Av) continue;
+            const int p = pos[s] >= 0 ? base + pos[s] : -1;
+            pos[s] = p;
+            const int64_t slot = (int64_t)(a0 + a) * noff + k;
+            out.mask[slot] = p >= 0;
+            out.slot_row[slot] = p;
+            if (p >= 0) out.opacity[p] = sy[k * kDecYS + a];
+        }
+        // hidden layer of the cov and colour heads
+        const float* sx = sm.x[wave];
+        const f32x4 hc0 = layer1_tile<KSTEPS>(sm, sx, 2), hc1 = layer1_tile<KSTEPS>(sm, sx, 3);
+        const f32x4 hl0 = layer1_tile<KSTEPS>(sm, sx, 4), hl1 = layer1_tile<KSTEPS>(sm, sx, 5);
+        // cov head -> LDS, then scaling / rotation / position per kept slot
+        float* syw = sm.y[wave];
+        for (int ot = 0; ot < d.T[1]; ++ot) {
+            const f32x4 y = layer2_tile(sm, d.row0[1] + ot * 16, hc0, hc1);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) syw[(ot * 16 + 4 * g + r) * kDecYS + i] = y[r];
+        }
+        for (int s = lane; s < 16 * noff; s += 64) {
+            const int a = s / noff, k = s - a * noff;
+            if (a0 + a >= d.Av) continue;
+            const int p = pos[s];
+            if (p < 0) continue;
+            const int id = vis_idx ? vis_idx[a0 + a] : a0 + a;
+            float cv[7];
+#pragma unroll
+            for (int q = 0; q < 7; ++q) cv[q] = syw[(7 * k + q) * kDecYS + a];
+            const float* sr = scaling_raw + (int64_t)id * 6;
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                out.scaling[(int64_t)p * 3 + q] = expf(sr[3 + q]) * (1.0f / (1.0f + expf(-cv[q])));
+            const float nrm = fmaxf(sqrtf(cv[3] * cv[3] + cv[4] * cv[4] + cv[5] * cv[5] + cv[6] * cv[6]), 1e-12f);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) out.rot[(int64_t)p * 4 + q] = cv[3 + q] / nrm;
+            const float* of = offset + ((int64_t)id * noff + k) * 3;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const float o = of[q] * expf(sr[q]);
+                out.offsets[(int64_t)p * 3 + q] = o;
+                out.xyz[(int64_t)p * 3 + q] = anchor[(int64_t)id * 3 + q] + o;
+            }
+        }
+        // colour head straight from the accumulators (linear output)
+        for (int ot = 0; ot < d.T[2]; ++ot) {
+            const f32x4 y = layer2_tile(sm, d.row0[2] + ot * 16, hl0, hl1);
+            if (a0 + i >= d.Av) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int o = ot * 16 + 4 * g + r;
+                if (o >= cd * noff) continue;
+                const int k = o / cd;
+                const int p = pos[i * noff + k];
+                if (p >= 0) out.color[(int64_t)p * cd + (o - k * cd)] = y[r];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- backward
+// One launch per (head, chunk of <= 5 output tiles): the colour head of an SH model
+// has 17 tiles, whose dW2 accumulators would not fit registers in one pass.  Every
+// launch recomputes its head's hidden layer, forms dY from the output gradients,
+// and adds its share of dH = W2^T dY (ReLU-masked), dX = W1^T dH (-> d feat, d anchor
+// through ob_view), dW2 = dY H^T and dW1 = dH X^T.  Weight gradients accumulate in
+// registers over the launch's grid-stride tiles and are flushed as per-wave partials
+// that decode_wgrad_reduce_kernel sums in a fixed order (deterministic).
+constexpr int kBwdChunk = 5;  // output tiles per launch
+
+struct DecodeGrads {
+    const float* g_xyz;      // [M,3]
+    const float* g_offsets;  // [M,3] nullable
+    const float* g_color;    // [M,cd] nullable
+    const float* g_opacity;  // [M] nullable
+    const float* g_scaling;  // [M,3] nullable
+    const float* g_rot;      // [M,4] nullable
+    float* d_anchor;         // [A,3] accumulated (+=), nullable
+    float* d_feat;           // [A,F] accumulated (+=)
+    float* d_offset;         // [A,noff,3] written by the cov launch
+    float* d_scaling;        // [A,6] accumulated (+=)
+};
+
+struct DecodeBwdSmem {
+    float w1[32 * kDecS];
+    float b1[32];
+    float w2[kBwdChunk * 16 * kDecS];
+    float b2[kBwdChunk * 16];
+    float x[4][16 * kDecS];
+    float y[4][kBwdChunk * 16 * kDecYS];   // recomputed pre-activations (opacity / cov)
+    float dy[4][kBwdChunk * 16 * kDecYS];  // dY^T[o][anchor]
+    float h[4][32 * kDecYS];               // H^T, then dH^T [hidden][anchor]
+    float acc[4][16 * 9];                  // per-anchor d scaling_raw (6) + d anchor (3)
+};
+
+// partial layout per wave: dW2 chunk [nt*16][32] | db2 chunk [nt*16] | dW1 [32][48] | db1 [32]
+__host__ __device__ inline int bwd_partial_floats(int nt) { return nt * 16 * 32 + nt * 16 + 32 * 48 + 32; }
+
+template <int KSTEPS>
+__global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs mp, int head, int t0, int nt,
+                                                         const int32_t* __restrict__ vis_idx,
+                                                         const float* __restrict__ anchor,
+                                                         const float* __restrict__ feat,
+                                                         const float* __restrict__ offset,
+                                                         const float* __restrict__ scaling_raw,
+                                                         const float* __restrict__ cam,
+                                                         const int32_t* __restrict__ slot_row, DecodeGrads gr,
+                                                         float* __restrict__ partials) {
+    __shared__ DecodeBwdSmem sm;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    const int K1 = kDecF + d.vd;
+    const int noff = d.noff, cd = d.cd;
+    const int o0 = t0 * 16, O = d.O[head], rows = nt * 16;
+    // stage this head's layer-1 weights and the chunk of layer-2 rows (permuted columns)
+    for (int e = threadIdx.x; e < 32 * kDecS; e += 256) {
+        const int h = e / kDecS, k = e - h * kDecS;
+        sm.w1[e] = k < K1 ? mp.w1[head][h * K1 + k] : 0.f;
+    }
+    if (threadIdx.x < 32) sm.b1[threadIdx.x] = mp.b1[head][threadIdx.x];
+    for (int e = threadIdx.x; e < rows * kDecF; e += 256) {
+        const int row = e / kDecF, h = e - row * kDecF;
+        const int o = o0 + row;
+        sm.w2[row * kDecS + w2_col(h)] = o < O ? mp.w2[head][o * kDecF + h] : 0.f;
+    }
+    for (int row = threadIdx.x; row < rows; row += 256) sm.b2[row] = o0 + row < O ? mp.b2[head][o0 + row] : 0.f;
+    f32x4 aw2[kBwdChunk][2], aw1[2][3];
+#pragma unroll
+    for (int a = 0; a < kBwdChunk; ++a) aw2[a][0] = aw2[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < 2; ++a) aw1[a][0] = aw1[a][1] = aw1[a][2] = f32x4{0.f, 0.f, 0.f, 0.f};
+    double ab2[2] = {0.0, 0.0}, ab1 = 0.0;  // bias sums over many anchors: f64
+    float* sx = sm.x[wave];
+    float* sy = sm.y[wave];
+    float* sdy = sm.dy[wave];
+    float* sh = sm.h[wave];
+    float* sacc = sm.acc[wave];
+    const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        __syncthreads();  // weights staged / previous tile's LDS reads done
+        const int a0 = t * kDecTile + wave * 16;
+        stage_x(sx, vis_idx, a0, d.Av, d.vd, anchor, feat, cam);
+        for (int e = lane; e < 16 * 9; e += 64) sacc[e] = 0.f;
+        __syncthreads();
+        // hidden layer of this head (rows 0..31 of sm.w1)
+        f32x4 h0 = {0.f, 0.f, 0.f, 0.f}, h1 = h0;
+#pragma unroll
+        for (int kk = 0; kk < KSTEPS; ++kk) {
+            h0 = mfma4(sm.w1[i * kDecS + 4 * kk + g], sx[i * kDecS + 4 * kk + g], h0);
+            h1 = mfma4(sm.w1[(16 + i) * kDecS + 4 * kk + g], sx[i * kDecS + 4 * kk + g], h1);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            h0[r] = fmaxf(h0[r] + sm.b1[4 * g + r], 0.f);
+            h1[r] = fmaxf(h1[r] + sm.b1[16 + 4 * g + r], 0.f);
+            sh[(4 * g + r) * kDecYS + i] = h0[r];
+            sh[(16 + 4 * g + r) * kDecYS + i] = h1[r];
+        }
+        // recompute the pre-activations the derivative needs
+        if (head < 2) {
+            for (int ot = 0; ot < nt; ++ot) {
+                f32x4 y = {0.f, 0.f, 0.f, 0.f};
+                const float* w = sm.w2 + (ot * 16 + i) * kDecS + g;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) y = mfma4(w[4 * r], h0[r], y);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) y = mfma4(w[16 + 4 * r], h1[r], y);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sy[(ot * 16 + 4 * g + r) * kDecYS + i] = y[r] + sm.b2[ot * 16 + 4 * g + r];
+            }
+        }
+        // dY^T for the chunk (zero for dropped slots, padding rows and absent anchors)
+        for (int e = lane; e < rows * 16; e += 64) sdy[(e >> 4) * kDecYS + (e & 15)] = 0.f;
+        if (head == 0) {
+            for (int s = lane; s < 16 * noff; s += 64) {
+                const int a = s / noff, k = s - a * noff;
+                if (a0 + a >= d.Av) continue;
+                const int p = slot_row[(int64_t)(a0 + a) * noff + k];
+                if (p < 0 || !gr.g_opacity) continue;
+                const float th = tanhf(sy[k * kDecYS + a]);
+                sdy[k * kDecYS + a] = gr.g_opacity[p] * (1.0f - th * th);
+            }
+        } else if (head == 1) {
+            for (int s = lane; s < 16 * noff; s += 64) {
+                const int a = s / noff, k = s - a * noff;
+                if (a0 + a >= d.Av) continue;
+                const int id = vis_idx ? vis_idx[a0 + a] : a0 + a;
+                const int p = slot_row[(int64_t)(a0 + a) * noff + k];
+                float* dof = gr.d_offset + ((int64_t)id * noff + k) * 3;
+                if (p < 0) {
+                    dof[0] = dof[1] = dof[2] = 0.f;
+                    continue;
+                }
+                const float* sr = scaling_raw + (int64_t)id * 6;
+                float cv[7];
+#pragma unroll
+                for (int q = 0; q < 7; ++q) cv[q] = sy[(7 * k + q) * kDecYS + a];
+                // scaling = exp(sr[3:6]) * sigmoid(cv[0:3])
+                if (gr.g_scaling) {
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        const float es = expf(sr[3 + q]), sg = 1.0f / (1.0f + expf(-cv[q]));
+                        const float gs = gr.g_scaling[(int64_t)p * 3 + q];
+                        sdy[(7 * k + q) * kDecYS + a] = gs * es * sg * (1.0f - sg);
+                        atomicAdd(&sacc[a * 9 + 3 + q], gs * es * sg);
+                    }
+                }
+                // rot = v / max(|v|, 1e-12)
+                if (gr.g_rot) {
+                    const float nr = sqrtf(cv[3] * cv[3] + cv[4] * cv[4] + cv[5] * cv[5] + cv[6] * cv[6]);
+                    const float* gq = gr.g_rot + (int64_t)p * 4;
+                    if (nr > 1e-12f) {
+                        const float inv = 1.0f / nr;
+                        float dot = 0.f;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) dot += cv[3 + q] * inv * gq[q];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) sdy[(7 * k + 3 + q) * kDecYS + a] = (gq[q] - cv[3 + q] * inv * dot) * inv;
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) sdy[(7 * k + 3 + q) * kDecYS + a] = gq[q] * 1e12f;
+                    }
+                }
+                // xyz = anchor + offset * exp(sr[0:3]); offsets_out = offset * exp(sr[0:3])
+                const float* of = offset + ((int64_t)id * noff + k) * 3;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const float gx = gr.g_xyz ? gr.g_xyz[(int64_t)p * 3 + q] : 0.f;
+                    const float gt = gx + (gr.g_offsets ? gr.g_offsets[(int64_t)p * 3 + q] : 0.f);
+                    const float es = expf(sr[q]);
+                    dof[q] = gt * es;
+                    atomicAdd(&sacc[a * 9 + q], gt * of[q] * es);
+                    atomicAdd(&sacc[a * 9 + 6 + q], gx);
+                }
+            }
+        } else if (gr.g_color) {
+            for (int e = lane; e < rows * 16; e += 64) {
+                const int ol = e >> 4, a = e & 15;
+                const int o = o0 + ol;
+                if (o >= O || a0 + a >= d.Av) continue;
+                const int k = o / cd, c = o - k * cd;
+                const int p = slot_row[(int64_t)(a0 + a) * noff + k];
+                if (p >= 0) sdy[ol * kDecYS + a] = gr.g_color[(int64_t)p * cd + c];
+            }
+        }
+        // per-anchor d scaling_raw / d anchor of the cov head (xyz and scaling outputs)
+        if (head == 1 && lane < 16 && a0 + lane < d.Av) {
+            const int id = vis_idx ? vis_idx[a0 + lane] : a0 + lane;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) gr.d_scaling[(int64_t)id * 6 + q] += sacc[lane * 9 + q];
+            if (gr.d_anchor)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) gr.d_anchor[(int64_t)id * 3 + q] += sacc[lane * 9 + 6 + q];
+        }
+        // dW2 += dY H^T (k = anchors), db2 += row sums of dY
+        for (int ot = 0; ot < kBwdChunk; ++ot) {
+            if (ot >= nt) break;
+#pragma unroll
+            for (int ht = 0; ht < 2; ++ht) {
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                    aw2[ot][ht] = mfma4(sdy[(ot * 16 + i) * kDecYS + 4 * kk + g], sh[(ht * 16 + i) * kDecYS + 4 * kk + g],
+                                        aw2[ot][ht]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int ol = lane + 64 * q;
+            if (ol < rows) {
+                float sum = 0.f;
+#pragma unroll
+                for (int a = 0; a < 16; ++a) sum += sdy[ol * kDecYS + a];
+                ab2[q] += sum;
+            }
+        }
+        // dH = W2^T dY, masked by ReLU; then stored transposed for dW1
+        f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
+        for (int kk = 0; kk < rows / 4; ++kk) {
+            const int o = 4 * kk + g;
+            const float b = sdy[o * kDecYS + i];
+            d0 = mfma4(sm.w2[o * kDecS + w2_col(i)], b, d0);
+            d1 = mfma4(sm.w2[o * kDecS + w2_col(16 + i)], b, d1);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            d0[r] = h0[r] > 0.f ? d0[r] : 0.f;
+            d1[r] = h1[r] > 0.f ? d1[r] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            sh[(4 * g + r) * kDecYS + i] = d0[r];
+            sh[(16 + 4 * g + r) * kDecYS + i] = d1[r];
+        }
+        // dW1 += dH X^T (k = anchors), db1 += row sums of dH
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+            for (int kt = 0; kt < 3; ++kt) {
+                if (kt * 16 >= K1) break;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                    aw1[ht][kt] = mfma4(sh[(ht * 16 + i) * kDecYS + 4 * kk + g], sx[(4 * kk + g) * kDecS + kt * 16 + i],
+                                        aw1[ht][kt]);
+            }
+        if (lane < 32) {
+            float sum = 0.f;
+#pragma unroll
+            for (int a = 0; a < 16; ++a) sum += sh[lane * kDecYS + a];
+            ab1 += sum;
+        }
+        // dX = W1^T dH -> d feat (k < 32), d ob_view (k = 32..34) -> d anchor.  The MFMAs run
+        // with the whole wave (an MFMA consumes every lane's operands whatever EXEC says);
+        // only the stores are predicated on the anchor being present.
+        const bool present = a0 + i < d.Av;
+        const int id = present ? (vis_idx ? vis_idx[a0 + i] : a0 + i) : 0;
+        for (int kt = 0; kt < 3; ++kt) {
+            if (kt * 16 >= K1) break;
+            f32x4 dx = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dx = mfma4(sm.w1[(4 * g + r) * kDecS + kt * 16 + i], d0[r], dx);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dx = mfma4(sm.w1[(16 + 4 * g + r) * kDecS + kt * 16 + i], d1[r], dx);
+            if (!present) continue;
+            if (kt < 2) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) gr.d_feat[(int64_t)id * kDecF + kt * 16 + 4 * g + r] += dx[r];
+            } else if (g == 0 && gr.d_anchor) {
+                const float ex = anchor[id * 3] - cam[0], ey = anchor[id * 3 + 1] - cam[1], ez = anchor[id * 3 + 2] - cam[2];
+                const float dist = sqrtf(ex * ex + ey * ey + ez * ez);
+                const float ov[3] = {ex / dist, ey / dist, ez / dist};
+                const float dot = ov[0] * dx[0] + ov[1] * dx[1] + ov[2] * dx[2];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) gr.d_anchor[(int64_t)id * 3 + q] += (dx[q] - ov[q] * dot) / dist;
+            }
+        }
+    }
+    // flush this wave's weight-gradient partials
+    float* out = partials + (int64_t)(blockIdx.x * 4 + wave) * bwd_partial_floats(nt);
+    for (int ot = 0; ot < kBwdChunk; ++ot) {
+        if (ot >= nt) break;
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[(ot * 16 + 4 * g + r) * 32 + ht * 16 + i] = aw2[ot][ht][r];
+    }
+    float* ob2 = out + rows * 32;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+        if (lane + 64 * q < rows) ob2[lane + 64 * q] = (float)ab2[q];
+    float* ow1 = ob2 + rows;
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+        for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ow1[(ht * 16 + 4 * g + r) * 48 + kt * 16 + i] = aw1[ht][kt][r];
+    if (lane < 32) ow1[32 * 48 + lane] = (float)ab1;
+}
+
+// sum the per-wave partials of one launch into the weight gradients (+=; fixed order)
+__global__ __launch_bounds__(256) void decode_wgrad_reduce_kernel(int n_parts, int nt, int o0, int O, int K1,
+                                                                  const float* __restrict__ partials,
+                                                                  float* __restrict__ dw2, float* __restrict__ db2,
+                                                                  float* __restrict__ dw1, float* __restrict__ db1) {
+    const int pf = bwd_partial_floats(nt);
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= pf) return;
+    double acc = 0.0;
+    for (int q = 0; q < n_parts; ++q) acc += partials[(int64_t)q * pf + e];
+    const float sum = (float)acc;
+    const int rows = nt * 16;
+    if (e < rows * 32) {
+        const int o = o0 + e / 32, h = e % 32;
+        if (o < O) dw2[o * 32 + h] += sum;
+    } else if (e < rows * 33) {
+        const int o = o0 + e - rows * 32;
+        if (o < O) db2[o] += sum;
+    } else if (e < rows * 33 + 32 * 48) {
+        const int q = e - rows * 33, h = q / 48, k = q % 48;
+        if (k < K1) dw1[h * K1 + k] += sum;
+    } else {
+        db1[e - rows * 33 - 32 * 48] += sum;
+    }
+}
+
+}  // namespace hgsr
+
+using namespace hgsr;
+
+extern "C" int hgsr_lod_mask(int A, const float* anchor, const int32_t* level, const float* extra_level,
+                             const float* cam_center, float res_scale, float standard_dist, float log2_fork,
+                             int max_level, uint8_t* mask, hgsr_stream_t stream) {
+    HGSR_REQUIRE(A >= 0 && max_level >= 0, "bad dims");
+    if (A == 0) return HGSR_OK;
+    HGSR_REQUIRE(anchor && level && extra_level && cam_center && mask, "null pointer");
+    hipLaunchKernelGGL(lod_mask_kernel, dim3((A + 255) / 256), dim3(256), 0, as_stream(stream), A, anchor, level,
+                       extra_level, cam_center, res_scale, standard_dist, log2_fork, max_level, mask);
+    return check_launch("lod_mask");
+}
+
+static int check_decode(int Av, int F, int vd, int noff, int cd, const DecodeDims& d) {
+    HGSR_REQUIRE(Av >= 0, "bad dims");
+    HGSR_REQUIRE(F == kDecF, "decode: feat_dim must be %d (got %d)", kDecF, F);
+    HGSR_REQUIRE(vd == 0 || vd == 3, "decode: view_dim must be 0 or 3 (got %d)", vd);
+    HGSR_REQUIRE(noff >= 1 && noff <= 16, "decode: n_offsets must be 1..16 (got %d)", noff);
+    HGSR_REQUIRE(cd >= 1 && cd % 3 == 0, "decode: color_dim must be a positive multiple of 3 (got %d)", cd);
+    HGSR_REQUIRE(d.rows <= kDecMaxRows, "decode: %d second-layer rows exceed the LDS plan (%d)", d.rows, kDecMaxRows);
+    HGSR_REQUIRE(d.T[1] <= 5, "decode: n_offsets too large for the cov head plan");
+    return HGSR_OK;
+}
+
+static int decode_grid(int Av) {
+    const int n_tiles = (Av + kDecTile - 1) / kDecTile;
+    return n_tiles < 1024 ? (n_tiles > 0 ? n_tiles : 1) : 1024;
+}
+
+static MlpPtrs mlp_ptrs(const float* const* w) {
+    MlpPtrs mp;
+    for (int h = 0; h < 3; ++h) {
+        mp.w1[h] = w[4 * h];
+        mp.b1[h] = w[4 * h + 1];
+        mp.w2[h] = w[4 * h + 2];
+        mp.b2[h] = w[4 * h + 3];
+    }
+    return mp;
+}
+
+extern "C" size_t hgsr_decode_ws_bytes(int Av) {
+    const size_t n_tiles = ((size_t)Av + kDecTile - 1) / kDecTile + 1;
+    return ((n_tiles * 4 + 255) & ~(size_t)255) * 2 + 256;
+}
+
+extern "C" int hgsr_decode_count(int Av, int F, int view_dim, int n_offsets, int color_dim,
+                                 const int32_t* vis_idx, const float* anchor, const float* feat,
+                                 const float* cam_center, const float* const* mlp, void* ws, size_t ws_bytes,
+                                 int64_t* total, hgsr_stream_t stream) {
+    const DecodeDims d = decode_dims(Av, view_dim, n_offsets, color_dim);
+    if (int st = check_decode(Av, F, view_dim, n_offsets, color_dim, d)) return st;
+    HGSR_REQUIRE(ws_bytes >= hgsr_decode_ws_bytes(Av), "decode workspace too small");
+    HGSR_REQUIRE(mlp && ws && total, "null pointer");
+    hipStream_t s = as_stream(stream);
+    if (Av == 0) return memset_async(total, sizeof(int64_t), s, "decode_count");
+    HGSR_REQUIRE(anchor && feat && cam_center, "null pointer");
+    for (int q = 0; q < 12; ++q) HGSR_REQUIRE(mlp[q], "null MLP pointer %d", q);
+    const MlpPtrs mp = mlp_ptrs(mlp);
+    const int n_tiles = (Av + kDecTile - 1) / kDecTile;
+    int32_t* cnt = (int32_t*)ws;
+    int32_t* off = (int32_t*)((char*)ws + (((size_t)(n_tiles + 1) * 4 + 255) & ~(size_t)255));
+    KernelTimer kt("decode_count", s);
+    if (view_dim == 3)
+        hipLaunchKernelGGL(decode_count_kernel<9>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
+                           feat, cam_center, cnt);
+    else
+        hipLaunchKernelGGL(decode_count_kernel<8>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
+                           feat, cam_center, cnt);
+    if (int st = check_launch("decode_count")) return st;
+    hipLaunchKernelGGL(decode_scan_kernel, dim3(1), dim3(1024), 0, s, n_tiles, cnt, off, total);
+    return check_launch("decode_scan");
+}
+
+extern "C" int hgsr_decode_fwd(int Av, int F, int view_dim, int n_offsets, int color_dim, const int32_t* vis_idx,
+                               const float* anchor, const float* feat, const float* offset, const float* scaling_raw,
+                               const float* cam_center, const float* const* mlp, float* xyz, float* offsets_out,
+                               float* color, float* opacity, float* scaling, float* rot, uint8_t* mask,
+                               int32_t* slot_row, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
+    const DecodeDims d = decode_dims(Av, view_dim, n_offsets, color_dim);
+    if (int st = check_decode(Av, F, view_dim, n_offsets, color_dim, d)) return st;
+    HGSR_REQUIRE(ws_bytes >= hgsr_decode_ws_bytes(Av), "decode workspace too small");
+    if (Av == 0) return HGSR_OK;
+    HGSR_REQUIRE(mlp && ws && anchor && feat && offset && scaling_raw && cam_center && mask && slot_row,
+                 "null pointer");
+    for (int q = 0; q < 12; ++q) HGSR_REQUIRE(mlp[q], "null MLP pointer %d", q);
+    const MlpPtrs mp = mlp_ptrs(mlp);
+    const int n_tiles = (Av + kDecTile - 1) / kDecTile;
+    const int32_t* off = (const int32_t*)((char*)ws + (((size_t)(n_tiles + 1) * 4 + 255) & ~(size_t)255));
+    DecodeOut out{xyz, offsets_out, color, opacity, scaling, rot, mask, slot_row};
+    hipStream_t s = as_stream(stream);
+    KernelTimer kt("decode_fwd", s);
+    if (view_dim == 3)
+        hipLaunchKernelGGL(decode_fwd_kernel<9>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
+                           feat, offset, scaling_raw, cam_center, off, out);
+    else
+        hipLaunchKernelGGL(decode_fwd_kernel<8>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
+                           feat, offset, scaling_raw, cam_center, off, out);
+    return check_launch("decode_fwd");
+}
+
+static int bwd_grid(int Av) {
+    const int n_tiles = (Av + kDecTile - 1) / kDecTile;
+    return n_tiles < 256 ? (n_tiles > 0 ? n_tiles : 1) : 256;
+}
+
+extern "C" size_t hgsr_decode_bwd_ws_bytes(int Av) {
+    return (size_t)bwd_grid(Av) * 4 * bwd_partial_floats(kBwdChunk) * sizeof(float);
+}
+
+extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim, const int32_t* vis_idx,
+                               const float* anchor, const float* feat, const float* offset, const float* scaling_raw,
+                               const float* cam_center, const float* const* mlp, const int32_t* slot_row,
+                               const float* g_xyz, const float* g_offsets, const float* g_color,
+                               const float* g_opacity, const float* g_scaling, const float* g_rot, float* d_anchor,
+                               float* d_feat, float* d_offset, float* d_scaling, float* const* d_mlp, void* ws,
+                               size_t ws_bytes, hgsr_stream_t stream) {
+    const DecodeDims d = decode_dims(Av, view_dim, n_offsets, color_dim);
+    if (int st = check_decode(Av, F, view_dim, n_offsets, color_dim, d)) return st;
+    HGSR_REQUIRE(ws_bytes >= hgsr_decode_bwd_ws_bytes(Av), "decode_bwd workspace too small");
+    if (Av == 0) return HGSR_OK;
+    HGSR_REQUIRE(mlp && d_mlp && ws && anchor && feat && offset && scaling_raw && cam_center && slot_row && d_feat &&
+                     d_offset && d_scaling,
+                 "null pointer");
+    for (int q = 0; q < 12; ++q) HGSR_REQUIRE(mlp[q] && d_mlp[q], "null MLP pointer %d", q);
+    const MlpPtrs mp = mlp_ptrs(mlp);
+    const DecodeGrads gr{g_xyz, g_offsets, g_color, g_opacity, g_scaling, g_rot, d_anchor, d_feat, d_offset, d_scaling};
+    hipStream_t s = as_stream(stream);
+    const int grid = bwd_grid(Av);
+    float* partials = (float*)ws;
+    const int K1 = kDecF + view_dim;
+    KernelTimer kt("decode_bwd", s);
+    for (int head = 0; head < 3; ++head) {
+        for (int t0 = 0; t0 < d.T[head]; t0 += kBwdChunk) {
+            const int nt = d.T[head] - t0 < kBwdChunk ? d.T[head] - t0 : kBwdChunk;
+            if (view_dim == 3)
+                hipLaunchKernelGGL(decode_bwd_kernel<9>, dim3(grid), dim3(256), 0, s, d, mp, head, t0, nt, vis_idx,
+                                   anchor, feat, offset, scaling_raw, cam_center, slot_row, gr, partials);
+            else
+                hipLaunchKernelGGL(decode_bwd_kernel<8>, dim3(grid), dim3(256), 0, s, d, mp, head, t0, nt, vis_idx,
+                                   anchor, feat, offset, scaling_raw, cam_center, slot_row, gr, partials);
+            if (int st = check_launch("decode_bwd")) return st;
+            const int pf = bwd_partial_floats(nt);
+            hipLaunchKernelGGL(decode_wgrad_reduce_kernel, dim3((pf + 255) / 256), dim3(256), 0, s, grid * 4, nt,
+                               t0 * 16, d.O[head], K1, partials, d_mlp[4 * head + 2], d_mlp[4 * head + 3],
+                               d_mlp[4 * head], d_mlp[4 * head + 1]);
+            if (int st = check_launch("decode_wgrad_reduce")) return st;
+        }
+    }
+    return HGSR_OK;
+}

@@ -1,0 +1,158 @@
+"""Anchor -> neural-Gaussian decode on the MI355X, host side.
+
+Mirrors the reference's per-view decode so that a Horizon-GS model can hand its
+anchors to the fused HIP kernels instead of the ~10 torch launches of
+`generate_neural_gaussians`:
+
+* `lod_mask`       <- scene/lod_model.py:286-290 set_anchor_mask (dist2level 'floor')
+* `decode`         <- scene/basic_model.py:297-371 generate_neural_gaussians on the
+                      visible anchors, MLPs of scene/lod_model.py:67-84
+* `generate_neural_gaussians(model, camera, visible_mask)` takes the reference model
+  object itself and returns the same 8-tuple, so a maintainer can bind it in place of
+  `BasicModel.generate_neural_gaussians`.
+
+Supported: feat_dim 32, view_dim 0 or 3, appearance_dim 0, dist2level != 'progressive'
+(smooth_complement = 1), RGB or SH colours; anything else raises NotImplementedError.
+There is no CPU path: inputs must be HIP device tensors.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import math
+
+import torch
+
+from . import _native as N
+from ._native import ptr
+
+_HEADS = ("opacity", "cov", "color")
+
+
+def _check_dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("hgsr: inputs must be HIP device tensors (no CPU fallback)")
+
+
+def _f32(t):
+    return t.contiguous() if t.dtype == torch.float32 else t.float().contiguous()
+
+
+def _ptr_array(ts):
+    arr = (ct.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+    return arr, ct.cast(arr, ct.c_void_p)
+
+
+@torch.no_grad()
+def lod_mask(anchor, level, extra_level, cam_center, res_scale, standard_dist, fork, street_levels):
+    """Boolean [A]: level <= clamp(floor(log2(sd/dist)/log2(fork) + extra_level), 0, street_levels-1)."""
+    _check_dev(anchor, level, extra_level, cam_center)
+    A = anchor.shape[0]
+    mask = torch.empty(A, dtype=torch.uint8, device=anchor.device)
+    N.call("hgsr_lod_mask", A, ptr(_f32(anchor)), ptr(level.reshape(-1).to(torch.int32).contiguous()),
+           ptr(_f32(extra_level.reshape(-1))), ptr(_f32(cam_center.reshape(3))), float(res_scale),
+           float(standard_dist), float(math.log2(fork)), int(street_levels) - 1, ptr(mask),
+           N.stream(anchor.device))
+    return mask.bool()
+
+
+class _Decode(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, feat, offset, scaling_raw, cam_center, vis_idx, cfg, *weights):
+        view_dim, n_off, color_dim = cfg
+        dev = anchor.device
+        Av = vis_idx.numel()
+        F = feat.shape[1]
+        w = [_f32(t) for t in weights]
+        arr, mlp = _ptr_array(w)
+        ws_b = N.size_query("hgsr_decode_ws_bytes", Av)
+        ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
+        total = torch.empty(1, dtype=torch.int64, device=dev)
+        s = N.stream(dev)
+        N.call("hgsr_decode_count", Av, F, view_dim, n_off, color_dim, ptr(vis_idx), ptr(anchor), ptr(feat),
+               ptr(cam_center), mlp, ptr(ws), ws_b, ptr(total), s)
+        M = int(total.item())  # the one host sync (the reference's boolean masking has it too)
+        out = dict(xyz=(M, 3), offsets=(M, 3), color=(M, color_dim), opacity=(M, 1), scaling=(M, 3), rot=(M, 4))
+        t = {k: torch.empty(v, dtype=torch.float32, device=dev) for k, v in out.items()}
+        mask = torch.empty(Av * n_off, dtype=torch.uint8, device=dev)
+        slot_row = torch.empty(Av * n_off, dtype=torch.int32, device=dev)
+        N.call("hgsr_decode_fwd", Av, F, view_dim, n_off, color_dim, ptr(vis_idx), ptr(anchor), ptr(feat),
+               ptr(offset), ptr(scaling_raw), ptr(cam_center), mlp, ptr(t["xyz"]), ptr(t["offsets"]),
+               ptr(t["color"]), ptr(t["opacity"]), ptr(t["scaling"]), ptr(t["rot"]), ptr(mask), ptr(slot_row),
+               ptr(ws), ws_b, s)
+        del arr
+        ctx.save_for_backward(anchor, feat, offset, scaling_raw, cam_center, vis_idx, slot_row, *w)
+        ctx.cfg = cfg
+        ctx.mark_non_differentiable(mask)
+        return t["xyz"], t["offsets"], t["color"], t["opacity"], t["scaling"], t["rot"], mask.bool()
+
+    @staticmethod
+    def backward(ctx, g_xyz, g_offs, g_color, g_opac, g_scaling, g_rot, g_mask):
+        anchor, feat, offset, scaling_raw, cam_center, vis_idx, slot_row, *w = ctx.saved_tensors
+        view_dim, n_off, color_dim = ctx.cfg
+        dev = anchor.device
+        Av = vis_idx.numel()
+        F = feat.shape[1]
+        d_anchor = torch.zeros_like(anchor) if ctx.needs_input_grad[0] else None
+        d_feat = torch.zeros_like(feat)
+        d_offset = torch.zeros_like(offset)
+        d_scaling = torch.zeros_like(scaling_raw)
+        d_w = [torch.zeros_like(t) for t in w]
+        arr, mlp = _ptr_array(w)
+        darr, dmlp = _ptr_array(d_w)
+        ws_b = N.size_query("hgsr_decode_bwd_ws_bytes", Av)
+        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+        g = [None if x is None else _f32(x) for x in (g_xyz, g_offs, g_color, g_opac, g_scaling, g_rot)]
+        N.call("hgsr_decode_bwd", Av, F, view_dim, n_off, color_dim, ptr(vis_idx), ptr(anchor), ptr(feat),
+               ptr(offset), ptr(scaling_raw), ptr(cam_center), mlp, ptr(slot_row), *[ptr(x) for x in g],
+               ptr(d_anchor), ptr(d_feat), ptr(d_offset), ptr(d_scaling), dmlp, ptr(ws), ws_b, N.stream(dev))
+        del arr, darr
+        return (d_anchor, d_feat, d_offset, d_scaling, None, None, None, *d_w)
+
+
+def decode(anchor, feat, offset, scaling_raw, cam_center, mlps, visible=None, view_dim=3, n_offsets=10,
+           color_dim=3):
+    """Fused generate_neural_gaussians on the visible anchors.
+
+    mlps: (mlp_opacity, mlp_cov, mlp_color) nn.Sequentials, or a dict with
+    '{opacity,cov,color}_{w1,b1,w2,b2}' tensors.  visible: bool mask [A] or int index
+    tensor (None = all).  Returns (xyz, offsets, color, opacity, scaling, rot, mask)
+    like the reference (colour [M, color_dim//3, 3] for SH)."""
+    _check_dev(anchor, feat, offset, scaling_raw, cam_center)
+    if isinstance(mlps, dict):
+        weights = [mlps[f"{h}_{n}"] for h in _HEADS for n in ("w1", "b1", "w2", "b2")]
+    else:
+        weights = []
+        for m in mlps:
+            if len(m) < 3 or not isinstance(m[1], torch.nn.ReLU):
+                raise NotImplementedError("hgsr decode: MLPs must be Linear -> ReLU -> Linear [-> Tanh]")
+            weights += [m[0].weight, m[0].bias, m[2].weight, m[2].bias]
+    A = anchor.shape[0]
+    if visible is None:
+        vis_idx = torch.arange(A, dtype=torch.int32, device=anchor.device)
+    elif visible.dtype == torch.bool:
+        vis_idx = torch.nonzero(visible, as_tuple=False).reshape(-1).to(torch.int32)
+    else:
+        vis_idx = visible.to(torch.int32).contiguous()
+    xyz, offs, color, opac, scaling, rot, mask = _Decode.apply(
+        _f32(anchor), _f32(feat), _f32(offset), _f32(scaling_raw), _f32(cam_center.reshape(3)), vis_idx,
+        (int(view_dim), int(n_offsets), int(color_dim)), *weights)
+    if color_dim != 3:
+        color = color.reshape(color.shape[0], color_dim // 3, 3)
+    return xyz, offs, color, opac, scaling, rot, mask
+
+
+def generate_neural_gaussians(model, viewpoint_camera, visible_mask=None):
+    """Drop-in for reference BasicModel.generate_neural_gaussians (scene/basic_model.py:297):
+    returns (xyz, offsets, color, opacity, scaling, rot, active_sh_degree, mask)."""
+    if getattr(model, "appearance_dim", 0) > 0:
+        raise NotImplementedError("hgsr decode: appearance embeddings are not supported")
+    if getattr(model, "dist2level", "floor") == "progressive":
+        raise NotImplementedError("hgsr decode: dist2level='progressive' is not supported")
+    if visible_mask is None:
+        visible_mask = torch.ones(model.get_anchor.shape[0], dtype=torch.bool, device=model.get_anchor.device)
+    xyz, offs, color, opac, scaling, rot, mask = decode(
+        model.get_anchor, model.get_anchor_feat, model.get_offset, model._scaling,
+        viewpoint_camera.camera_center, (model.get_opacity_mlp, model.get_cov_mlp, model.get_color_mlp),
+        visible_mask, model.view_dim, model.n_offsets, model.color_dim)
+    return xyz, offs, color, opac, scaling, rot, model.active_sh_degree, mask

@@ -240,6 +240,56 @@ int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
                             hgsr_stream_t stream);
 
+/* ---- K14: anchor -> neural-Gaussian decode --------------
+ * replaces scene/lod_model.py:286-290 set_anchor_mask (LoD mask, dist2level
+ * 'floor') and scene/basic_model.py:297-371 generate_neural_gaussians with the MLPs
+ * of scene/lod_model.py:67-84 (appearance_dim = 0, smooth_complement = 1).
+ * mask[A] = level <= clamp(floor(log2(sd / (|anchor - cam| * res_scale)) / log2_fork
+ * + extra_level), 0, max_level); cam_center is a device pointer to 3 floats. */
+int hgsr_lod_mask(int A, const float* anchor, const int32_t* level, const float* extra_level,
+                  const float* cam_center, float res_scale, float standard_dist, float log2_fork,
+                  int max_level, uint8_t* mask, hgsr_stream_t stream);
+/* Decode of Av visible anchors (vis_idx [Av] int32 anchor ids, NULL = 0..Av-1):
+ * feat_dim F = 32, view_dim 0 or 3, n_offsets <= 16, color_dim = 3 (RGB) or
+ * 3 (deg+1)^2 (SH); mlp is a HOST array of 12 device pointers: for the opacity,
+ * cov and colour heads in that order {w1 [F, F+vd], b1 [F], w2 [O, F], b2 [O]}
+ * (nn.Linear layout).  Two passes: hgsr_decode_count writes the number of kept
+ * Gaussians (tanh opacity > 0) to *total (device int64), the caller sizes the
+ * outputs, hgsr_decode_fwd writes them in the reference order (anchor-major, then
+ * offset): xyz, offsets (scaled), color [M, cd], opacity [M], scaling [M,3],
+ * rot [M,4]; mask [Av*n_offsets] (uint8) and slot_row [Av*n_offsets] (output row
+ * or -1, consumed by the backward).  ws: hgsr_decode_ws_bytes(Av), kept between
+ * the two calls. */
+size_t hgsr_decode_ws_bytes(int Av);
+int hgsr_decode_count(int Av, int F, int view_dim, int n_offsets, int color_dim,
+                      const int32_t* vis_idx, const float* anchor, const float* feat,
+                      const float* cam_center, const float* const* mlp, void* ws, size_t ws_bytes,
+                      int64_t* total, hgsr_stream_t stream);
+int hgsr_decode_fwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
+                    const int32_t* vis_idx, const float* anchor, const float* feat,
+                    const float* offset, const float* scaling_raw, const float* cam_center,
+                    const float* const* mlp, float* xyz, float* offsets_out, float* color,
+                    float* opacity, float* scaling, float* rot, uint8_t* mask, int32_t* slot_row,
+                    void* ws, size_t ws_bytes, hgsr_stream_t stream);
+
+/* vjp of the decode.  Gradients of the outputs (rows as written by
+ * hgsr_decode_fwd; any of them may be NULL = zero): g_xyz, g_offsets, g_color,
+ * g_opacity, g_scaling, g_rot.  Results are ACCUMULATED (+=) into caller-zeroed
+ * d_anchor [A,3] (nullable), d_feat [A,F], d_scaling [A,6] (d w.r.t. the raw
+ * _scaling parameter) and the 12 weight gradients d_mlp (same order as mlp);
+ * d_offset [A, n_offsets, 3] rows of visible anchors are written.  Weight
+ * gradients are reduced in a fixed order (deterministic).  ws:
+ * hgsr_decode_bwd_ws_bytes(Av). */
+size_t hgsr_decode_bwd_ws_bytes(int Av);
+int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
+                    const int32_t* vis_idx, const float* anchor, const float* feat,
+                    const float* offset, const float* scaling_raw, const float* cam_center,
+                    const float* const* mlp, const int32_t* slot_row, const float* g_xyz,
+                    const float* g_offsets, const float* g_color, const float* g_opacity,
+                    const float* g_scaling, const float* g_rot, float* d_anchor, float* d_feat,
+                    float* d_offset, float* d_scaling, float* const* d_mlp, void* ws,
+                    size_t ws_bytes, hgsr_stream_t stream);
+
 /* ---- measurement ----------------------------------------------------------
  * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):
  * when enabled, the main kernel of every entry point is bracketed by

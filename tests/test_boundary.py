@@ -40,6 +40,17 @@ def test_ctypes_binding_covers_header():
     assert set(header_symbols()) == set(_native.EXPORTED)
 
 
+def test_ctypes_arity_matches_header():
+    """Every binding declares exactly as many arguments as its prototype in hgsr.h."""
+    from horizongs_amd import _native
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    for name, (_, args) in _native._SIGS.items():
+        m = re.search(r"\b" + name + r"\((.*?)\);", txt, flags=re.S)
+        assert m, name
+        params = [a for a in m.group(1).split(",") if a.strip() and a.strip() != "void"]
+        assert len(params) == len(args), f"{name}: header {len(params)} args, binding {len(args)}"
+
+
 def test_pure_host_entry_points(lib):
     from horizongs_amd import _native
     assert lib.hgsr_version() == 1

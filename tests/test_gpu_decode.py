@@ -1,0 +1,117 @@
+"""GPU parity of the fused anchor decode (horizongs_amd.decode) -- SURVEY 8(f) rank 1.
+
+Forward and LoD mask against tests/golden/decode_{rgb,sh2}.npz (outputs of the
+reference module itself, scripts/make_golden.py); backward against torch autograd of
+the oracle restatement oracle/decode_ref.py in fp64 (and fp32 for the conditioning-aware
+check).  Tolerance: fp32, 1e-5 abs / 1e-4 rel (exact-f32 MFMA with a different
+summation order than the reference GEMM)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import decode_ref as D
+from oracle.checks import close, cond_close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _gold(tag):
+    return np.load(os.path.join(GOLD, f"decode_{tag}.npz"))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+@pytest.mark.parametrize("tag", ["rgb", "sh2"])
+def test_lod_mask_matches_reference(tag):
+    from horizongs_amd import decode as HD
+    g = _gold(tag)
+    t = lambda a: torch.from_numpy(np.asarray(a)).to(DEV)
+    m = HD.lod_mask(t(g["anchor"]), t(g["level"]), t(g["extra_level"]), t(g["cam_center"]), float(g["res_scale"]),
+                    float(g["standard_dist"]), int(g["fork"]), int(g["street_levels"]))
+    np.testing.assert_array_equal(m.cpu().numpy(), g["anchor_mask"])
+
+
+@pytest.mark.parametrize("tag", ["rgb", "sh2"])
+def test_decode_forward_matches_reference(tag):
+    from horizongs_amd import decode as HD
+    g = _gold(tag)
+    a = D.golden_inputs(g, torch.float32)
+    t = lambda x: x.to(DEV)
+    mlps = {k: t(v) for k, v in a["mlps"].items()}
+    vis = torch.from_numpy(g["anchor_mask"]).to(DEV)
+    xyz, offs, col, op, sc, rot, mask = HD.decode(t(torch.from_numpy(g["anchor"])),
+                                                  t(torch.from_numpy(g["anchor_feat"])),
+                                                  t(torch.from_numpy(g["offset"])),
+                                                  t(torch.from_numpy(g["scaling"])), t(a["cam_center"]), mlps, vis,
+                                                  a["view_dim"], a["n_offsets"], a["color_dim"])
+    np.testing.assert_array_equal(mask.cpu().numpy(), g["out_mask"])
+    close(xyz.cpu().numpy(), g["out_xyz"], name="xyz")
+    close(col.cpu().numpy(), g["out_color"], name="color")
+    close(op.cpu().numpy(), g["out_opacity"], name="opacity")
+    close(sc.cpu().numpy(), g["out_scaling"], name="scaling")
+    close(rot.cpu().numpy(), g["out_rot"], name="rot")
+
+
+def _random_model(n_anchor, view_dim, color_dim, seed, n_off=10):
+    gen = torch.Generator().manual_seed(seed)
+    F = 32
+    r = lambda *s, sd=1.0: torch.randn(*s, generator=gen) * sd
+    anchor = r(n_anchor, 3, sd=2.0)
+    inputs = dict(anchor=anchor, feat=r(n_anchor, F, sd=0.3), offset=r(n_anchor, n_off, 3, sd=0.1),
+                  scaling_raw=np.log(0.01) + r(n_anchor, 6, sd=0.1), cam_center=torch.tensor([0.3, -0.5, 6.0]))
+    K1 = F + view_dim
+    mlps = {}
+    for h, O in (("opacity", n_off), ("cov", 7 * n_off), ("color", color_dim * n_off)):
+        mlps[f"{h}_w1"] = r(F, K1, sd=1 / np.sqrt(K1))
+        mlps[f"{h}_b1"] = r(F, sd=0.1)
+        mlps[f"{h}_w2"] = r(O, F, sd=1 / np.sqrt(F))
+        mlps[f"{h}_b2"] = r(O, sd=0.1)
+    return inputs, mlps
+
+
+@pytest.mark.parametrize("view_dim,color_dim,n_anchor", [(3, 3, 1000), (0, 27, 700), (3, 3, 20011)])
+def test_decode_backward(view_dim, color_dim, n_anchor):
+    """All input and weight gradients vs fp64 / fp32 autograd of the oracle restatement."""
+    from horizongs_amd import decode as HD
+    inputs, mlps = _random_model(n_anchor, view_dim, color_dim, seed=5 + n_anchor)
+    gen = torch.Generator().manual_seed(77)
+    vis = torch.rand(n_anchor, generator=gen) < 0.8
+
+    def run_ref(dtype):
+        ins = {k: v.to(dtype).clone().requires_grad_(k != "cam_center") for k, v in inputs.items()}
+        ws = {k: v.to(dtype).clone().requires_grad_(True) for k, v in mlps.items()}
+        sub = {k: (v[vis] if k != "cam_center" else v) for k, v in ins.items()}
+        outs = D.decode_torch(sub["anchor"], sub["feat"], sub["offset"], sub["scaling_raw"], sub["cam_center"], ws,
+                              view_dim, 10, color_dim)
+        return ins, ws, outs
+
+    ins32, ws32, outs32 = run_ref(torch.float32)
+    mask_ref = outs32[6]
+    gg = torch.Generator().manual_seed(78)
+    ups = [torch.randn(o.shape, generator=gg) for o in outs32[:6]]
+    sum(((o * u.to(o.dtype)).sum() for o, u in zip(outs32[:6], ups))).backward()
+    ins64, ws64, outs64 = run_ref(torch.float64)
+    assert torch.equal(outs64[6], mask_ref)
+    sum(((o * u.to(o.dtype)).sum() for o, u in zip(outs64[:6], ups))).backward()
+
+    dev_in = {k: v.to(DEV).clone().requires_grad_(k != "cam_center") for k, v in inputs.items()}
+    dev_w = {k: v.to(DEV).clone().requires_grad_(True) for k, v in mlps.items()}
+    outs = HD.decode(dev_in["anchor"], dev_in["feat"], dev_in["offset"], dev_in["scaling_raw"], dev_in["cam_center"],
+                     dev_w, vis.to(DEV), view_dim, 10, color_dim)
+    np.testing.assert_array_equal(outs[6].cpu().numpy(), mask_ref.numpy())
+    for o, r32, r64, name in zip(outs[:6], outs32[:6], outs64[:6], ("xyz", "offsets", "color", "opacity", "scaling",
+                                                                   "rot")):
+        cond_close(o.detach().cpu().numpy(), r32.detach().numpy(), r64.detach().numpy(), name)
+    sum(((o * u.to(DEV)).sum() for o, u in zip(outs[:6], ups))).backward()
+    for k in ("anchor", "feat", "offset", "scaling_raw"):
+        cond_close(dev_in[k].grad.cpu().numpy(), ins32[k].grad.numpy(), ins64[k].grad.numpy(), "d_" + k)
+    for k in mlps:
+        cond_close(dev_w[k].grad.cpu().numpy(), ws32[k].grad.numpy(), ws64[k].grad.numpy(), "d_" + k)
