@@ -33,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from horizongs_amd import _native as NAT  # noqa: E402
+from horizongs_amd import decode as HD  # noqa: E402
 from horizongs_amd import gsplat_api as G  # noqa: E402
 from horizongs_amd.multigpu import GradientAllReduce  # noqa: E402
 from horizongs_amd.synthetic import make_scene  # noqa: E402
@@ -42,7 +43,8 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 vector (= f32 MFMA) peak, MI355X_MICROA
 HBM_PEAK_GBS = 8000.0      # HBM3E spec
 FLOP_PER_PAIR = {"raster3d_fwd": 20.0, "raster3d_bwd": 60.0, "raster2d_fwd": 40.0, "raster2d_bwd": 120.0}
 KERNELS = ["project3d_fwd", "isect_count", "isect_emit", "tile_sort", "raster3d_fwd", "raster3d_bwd",
-           "project3d_bwd", "project2d_fwd", "raster2d_fwd", "raster2d_bwd", "project2d_bwd", "sh_fwd", "sh_bwd"]
+           "project3d_bwd", "project2d_fwd", "raster2d_fwd", "raster2d_bwd", "project2d_bwd", "sh_fwd", "sh_bwd",
+           "decode_count", "decode_fwd", "decode_bwd"]
 
 
 def parse():
@@ -57,6 +59,8 @@ def parse():
     ap.add_argument("--mode", choices=["chunk", "ddp"], default="chunk")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events (rocprof runs)")
+    ap.add_argument("--anchors", type=int, default=0,
+                    help="decode-inclusive variant (SURVEY 8(d) c2): A anchors -> fused decode -> raster")
     return ap.parse_args()
 
 
@@ -83,20 +87,46 @@ class Workload:
         g = torch.Generator().manual_seed(1000 + rank)
         self.target = torch.rand(3, args.height, args.width, generator=g).to(dev)
         self.params = [self.means, self.quats, self.scales, self.opac, self.colors]
+        if args.anchors:
+            self._init_anchors(args, seed, dev)
         self.allreduce = GradientAllReduce(self.params, bucket_mb=64.0)
+
+    def _init_anchors(self, args, seed, dev):
+        """SURVEY 8(d) decode-inclusive c2: anchors placed like the c2 Gaussians, feat ~ N(0, 0.1),
+        offsets ~ N(0, 0.1), _scaling = ln 0.01 + N(0, 0.1), default-initialised MLPs (seed 2),
+        feat_dim 32, view_dim 3, 10 offsets, RGB (scene/lod_model.py:67-84)."""
+        A = args.anchors
+        sc = make_scene(A, args.width, args.height, seed=seed)
+        g = torch.Generator().manual_seed(2)
+        self.anchor = sc.means.to(dev).requires_grad_(True)
+        self.feat = (torch.randn(A, 32, generator=g) * 0.1).to(dev).requires_grad_(True)
+        self.offset = (torch.randn(A, 10, 3, generator=g) * 0.1).to(dev).requires_grad_(True)
+        self.scaling_raw = (np.log(0.01) + torch.randn(A, 6, generator=g) * 0.1).float().to(dev).requires_grad_(True)
+        torch.manual_seed(2)
+        nn = torch.nn
+        self.mlps = [nn.Sequential(nn.Linear(35, 32), nn.ReLU(True), nn.Linear(32, o)).to(dev) for o in (10, 70, 30)]
+        self.cam_center = torch.zeros(3, device=dev)
+        self.params = [self.anchor, self.feat, self.offset, self.scaling_raw] + [
+            p for m in self.mlps for p in m.parameters()]
 
     def step(self):
         for p in self.params:
             p.grad = None
         W, H = self.args.width, self.args.height
+        if self.args.anchors:
+            xyz, _, cols, opac, scales, quats, _ = HD.decode(self.anchor, self.feat, self.offset, self.scaling_raw,
+                                                             self.cam_center, self.mlps, None, 3, 10, 3)
+            opac = opac.reshape(-1)
+        else:
+            xyz, quats, scales, opac, cols = self.means, self.quats, self.scales, self.opac, self.colors
+        self.last_colors = cols
         if self.args.gs == "3d":
-            out, alpha, meta = G.rasterization(self.means, self.quats, self.scales, self.opac, self.colors,
-                                               self.viewmats, self.Ks, W, H, packed=False,
-                                               backgrounds=self.bg, render_mode="RGB+ED")
+            out, alpha, meta = G.rasterization(xyz, quats, scales, opac, cols, self.viewmats, self.Ks, W, H,
+                                               packed=False, backgrounds=self.bg, render_mode="RGB+ED")
             meta["means2d"].retain_grad()
         else:
             (out, alpha, normals, nfd, distort, median), meta = G.rasterization_2dgs(
-                self.means, self.quats, self.scales, self.opac, self.colors, self.viewmats, self.Ks, W, H,
+                xyz, quats, scales, opac, cols, self.viewmats, self.Ks, W, H,
                 packed=False, backgrounds=self.bg, render_mode="RGB+ED")
         rgb = out[0, ..., :3].permute(2, 0, 1)
         loss = (rgb - self.target).abs().mean() + 0.01 * alpha.mean()
@@ -126,11 +156,12 @@ def raster_pairs(wl):
     ra = torch.empty((C, H, W, 1), device=dev)
     last = torch.empty((C, H, W), dtype=torch.int32, device=dev)
     opac = meta["opacities"].detach().contiguous()
-    cols = torch.cat([wl.colors.detach()[None], meta["depths"].detach()[..., None]], -1).contiguous()
+    cols = torch.cat([wl.last_colors.detach()[None], meta["depths"].detach()[..., None]], -1).contiguous()
+    n_g = cols.shape[1]
     if wl.args.gs == "3d":
-        ws_b = NAT.size_query("hgsr_raster3d_fwd_ws_bytes", C, wl.args.n, 4)
+        ws_b = NAT.size_query("hgsr_raster3d_fwd_ws_bytes", C, n_g, 4)
         ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
-        NAT.call("hgsr_raster3d_fwd", C, wl.args.n, 4, NAT.ptr(m2), NAT.ptr(meta["conics"].detach().contiguous()),
+        NAT.call("hgsr_raster3d_fwd", C, n_g, 4, NAT.ptr(m2), NAT.ptr(meta["conics"].detach().contiguous()),
                  NAT.ptr(cols), NAT.ptr(opac), None, W, H, 16, tw, th, NAT.ptr(meta["isect_offsets"]), n_isects,
                  NAT.ptr(fl), NAT.ptr(rc), NAT.ptr(ra), NAT.ptr(last), NAT.ptr(ws), ws_b, NAT.stream(dev))
     else:
@@ -138,9 +169,9 @@ def raster_pairs(wl):
         r1 = torch.empty((C, H, W, 1), device=dev)
         r2 = torch.empty((C, H, W, 1), device=dev)
         med = torch.empty((C, H, W), dtype=torch.int32, device=dev)
-        ws_b = NAT.size_query("hgsr_raster2d_fwd_ws_bytes", C, wl.args.n, 4)
+        ws_b = NAT.size_query("hgsr_raster2d_fwd_ws_bytes", C, n_g, 4)
         ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
-        NAT.call("hgsr_raster2d_fwd", C, wl.args.n, 4, NAT.ptr(m2),
+        NAT.call("hgsr_raster2d_fwd", C, n_g, 4, NAT.ptr(m2),
                  NAT.ptr(meta["ray_transforms"].detach().reshape(C, -1, 9).contiguous()), NAT.ptr(cols),
                  NAT.ptr(opac), NAT.ptr(meta["normals"].detach().contiguous()), None, W, H, 16, tw, th,
                  NAT.ptr(meta["isect_offsets"]), n_isects, NAT.ptr(fl), NAT.ptr(rc), NAT.ptr(ra), NAT.ptr(rn),
@@ -164,7 +195,7 @@ def pmc_traffic(args):
     profiled figure for the same command, or {} when no summary matches the config."""
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_pmc_traffic.json")))
-    if not files or args.n != 2_000_000 or (args.width, args.height) != (1920, 1080):
+    if not files or args.anchors or args.n != 2_000_000 or (args.width, args.height) != (1920, 1080):
         return {}, None
     d = json.load(open(files[-1]))
     out = {}
@@ -275,14 +306,14 @@ def main():
             roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                     "traffic": None, "kernel": dom}
         # aggregate compulsory-bytes figure of SURVEY 8(d): B_step = 384 N + 132 I + 52 P
-        b_step = 384 * args.n + 132 * n_isects + 52 * args.width * args.height
+        b_step = 384 * wl.last_colors.shape[0] + 132 * n_isects + 52 * args.width * args.height
         if roof.get("traffic") is not None:
             roof["traffic_unit"] = "bytes/launch"
             roof["traffic_source"] = traffic_src
         roof["aggregate_hbm_frac"] = round(b_step / (dt / args.steps) / (HBM_PEAK_GBS * 1e9), 4)
         roof["n_isects"] = n_isects
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.gs == "3d":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.gs == "3d" and not args.anchors:
         cpu = cpu_baseline(args, wl)
     if rank == 0:
         ms = dt / args.steps * 1e3
@@ -291,9 +322,10 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (seeded c2 scene, SURVEY 8(d); no dataset in the environment)",
-            "config": {"workload": f"c2 {'3DGS' if args.gs == '3d' else '2DGS'} train step: rasterization fwd + "
-                                   f"L1/alpha loss + bwd, RGB+ED",
-                       "gaussians": args.n, "width": args.width, "height": args.height,
+            "config": {"workload": (f"c2 {'3DGS' if args.gs == '3d' else '2DGS'} train step: "
+                                    + (f"fused anchor decode ({args.anchors} anchors) + " if args.anchors else "")
+                                    + "rasterization fwd + L1/alpha loss + bwd, RGB+ED"),
+                       "gaussians": int(wl.last_colors.shape[0]), "width": args.width, "height": args.height,
                        "parallelism": ("per-chunk, one scene per GPU, no collectives" if args.mode == "chunk"
                                        else "DDP over views, RCCL all-reduce of Gaussian grads")},
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,

@@ -92,33 +92,38 @@ __global__ __launch_bounds__(256) void lod_mask_kernel(int A, const float* __res
 }
 
 // ---------------------------------------------------------------- shared pieces
+// LDS of the forward / count passes, sized per pass: W1R first-layer rows (96 = all
+// three heads, 32 = opacity head only), W2R second-layer rows, YR pre-activation rows
+template <int W1R, int W2R, int YR>
 struct DecodeSmem {
-    float w1[96 * kDecS];
-    float b1[96];
-    float w2[kDecMaxRows * kDecS];
-    float b2[kDecMaxRows];
+    float w1[W1R * kDecS];
+    float b1[W1R];
+    float w2[W2R * kDecS];
+    float b2[W2R];
     float x[4][16 * kDecS];    // per wave: X rows (feat | ob_view | 0)
-    float y[4][80 * kDecYS];   // per wave: opacity / cov pre-activations Y^T[o][anchor]
+    float y[4][YR * kDecYS];   // per wave: opacity / cov pre-activations Y^T[o][anchor]
     int pos[4][16 * 16];       // per wave: output row of (anchor, offset), -1 if dropped
     int wave_cnt[4];
 };
+using CountSmem = DecodeSmem<32, 16, 16>;
 
-__device__ void stage_weights(DecodeSmem& sm, const MlpPtrs& mp, const DecodeDims& d) {
+template <class S>
+__device__ void stage_weights(S& sm, const MlpPtrs& mp, const DecodeDims& d, int w1_rows, int w2_rows) {
     const int K1 = kDecF + d.vd;
-    for (int e = threadIdx.x; e < 96 * kDecS; e += 256) {
+    for (int e = threadIdx.x; e < w1_rows * kDecS; e += 256) {
         const int h = e / kDecS, k = e - h * kDecS;
         const int head = h >> 5, hh = h & 31;
         sm.w1[e] = k < K1 ? mp.w1[head][hh * K1 + k] : 0.f;
     }
-    for (int h = threadIdx.x; h < 96; h += 256) sm.b1[h] = mp.b1[h >> 5][h & 31];
-    for (int e = threadIdx.x; e < d.rows * kDecF; e += 256) {
+    for (int h = threadIdx.x; h < w1_rows; h += 256) sm.b1[h] = mp.b1[h >> 5][h & 31];
+    for (int e = threadIdx.x; e < w2_rows * kDecF; e += 256) {
         const int row = e / kDecF, h = e - row * kDecF;
         int head = 0;
         while (head < 2 && row >= d.row0[head + 1]) ++head;
         const int o = row - d.row0[head];
         sm.w2[row * kDecS + w2_col(h)] = o < d.O[head] ? mp.w2[head][o * kDecF + h] : 0.f;
     }
-    for (int row = threadIdx.x; row < d.rows; row += 256) {
+    for (int row = threadIdx.x; row < w2_rows; row += 256) {
         int head = 0;
         while (head < 2 && row >= d.row0[head + 1]) ++head;
         const int o = row - d.row0[head];
@@ -158,8 +163,8 @@ __device__ void stage_x(float* sx, const int32_t* __restrict__ vis_idx, int a0, 
 }
 
 // first layer of head `head` (or all three): H^T tiles [16 hidden x 16 anchors], bias + ReLU
-template <int KSTEPS>
-__device__ __forceinline__ f32x4 layer1_tile(const DecodeSmem& sm, const float* sx, int mt) {
+template <int KSTEPS, class S>
+__device__ __forceinline__ f32x4 layer1_tile(const S& sm, const float* sx, int mt) {
     const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -172,7 +177,8 @@ __device__ __forceinline__ f32x4 layer1_tile(const DecodeSmem& sm, const float* 
 
 // second layer: Y^T tile [16 outputs x 16 anchors] of W2 rows [row, row + 16) from the
 // head's two H^T tiles (k = 32 hidden in 8 k-steps, no lane movement)
-__device__ __forceinline__ f32x4 layer2_tile(const DecodeSmem& sm, int row, f32x4 h0, f32x4 h1) {
+template <class S>
+__device__ __forceinline__ f32x4 layer2_tile(const S& sm, int row, f32x4 h0, f32x4 h1) {
     const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const float* w = sm.w2 + (row + i) * kDecS + g;
@@ -191,8 +197,8 @@ __device__ __forceinline__ int lanes_below_d(uint64_t m) {
 
 // opacity head of this wave's 16 anchors -> tanh values in sm.y rows [0, 16); returns
 // the wave's kept count (and the ballot-ordered local position of every kept slot)
-template <int KSTEPS>
-__device__ int opacity_head(DecodeSmem& sm, int wave, int a0, int Av, const DecodeDims& d, bool want_pos) {
+template <int KSTEPS, class S>
+__device__ int opacity_head(S& sm, int wave, int a0, int Av, const DecodeDims& d, bool want_pos) {
     const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
     const float* sx = sm.x[wave];
     const f32x4 h0 = layer1_tile<KSTEPS>(sm, sx, 0), h1 = layer1_tile<KSTEPS>(sm, sx, 1);
@@ -222,8 +228,8 @@ __global__ __launch_bounds__(256) void decode_count_kernel(DecodeDims d, MlpPtrs
                                                            const float* __restrict__ feat,
                                                            const float* __restrict__ cam,
                                                            int32_t* __restrict__ tile_cnt) {
-    __shared__ DecodeSmem sm;
-    stage_weights(sm, mp, d);
+    __shared__ CountSmem sm;
+    stage_weights(sm, mp, d, 32, 16);  // opacity head only
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
     for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
@@ -275,7 +281,7 @@ struct DecodeOut {
     int32_t* slot_row;  // [Av*noff] output row or -1 (kept for the backward)
 };
 
-template <int KSTEPS>
+template <int KSTEPS, int W2R>
 __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs mp,
                                                          const int32_t* __restrict__ vis_idx,
                                                          const float* __restrict__ anchor,
@@ -284,8 +290,8 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
                                                          const float* __restrict__ scaling_raw,
                                                          const float* __restrict__ cam,
                                                          const int32_t* __restrict__ tile_off, DecodeOut out) {
-    __shared__ DecodeSmem sm;
-    stage_weights(sm, mp, d);
+    __shared__ DecodeSmem<96, W2R, 80> sm;
+    stage_weights(sm, mp, d, 96, d.rows);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
     const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
     const int noff = d.noff, cd = d.cd;
@@ -386,23 +392,26 @@ struct DecodeGrads {
     float* d_scaling;        // [A,6] accumulated (+=)
 };
 
+// LDS of a backward launch, sized per head: R = second-layer rows of a chunk,
+// YR = recomputed pre-activation rows (0 for the linear colour head)
+template <int R, int YR>
 struct DecodeBwdSmem {
     float w1[32 * kDecS];
     float b1[32];
-    float w2[kBwdChunk * 16 * kDecS];
-    float b2[kBwdChunk * 16];
+    float w2[R * kDecS];
+    float b2[R];
     float x[4][16 * kDecS];
-    float y[4][kBwdChunk * 16 * kDecYS];   // recomputed pre-activations (opacity / cov)
-    float dy[4][kBwdChunk * 16 * kDecYS];  // dY^T[o][anchor]
-    float h[4][32 * kDecYS];               // H^T, then dH^T [hidden][anchor]
-    float acc[4][16 * 9];                  // per-anchor d scaling_raw (6) + d anchor (3)
+    float y[4][(YR > 0 ? YR : 1) * kDecYS];  // recomputed pre-activations (opacity / cov)
+    float dy[4][R * kDecYS];                 // dY^T[o][anchor]
+    float h[4][32 * kDecYS];                 // H^T, then dH^T [hidden][anchor]
+    float acc[4][16 * 9];                    // per-anchor d scaling_raw (6) + d anchor (3)
 };
 
 // partial layout per wave: dW2 chunk [nt*16][32] | db2 chunk [nt*16] | dW1 [32][48] | db1 [32]
 __host__ __device__ inline int bwd_partial_floats(int nt) { return nt * 16 * 32 + nt * 16 + 32 * 48 + 32; }
 
-template <int KSTEPS>
-__global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs mp, int head, int t0, int nt,
+template <int KSTEPS, int HEAD>
+__global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs mp, int t0, int nt,
                                                          const int32_t* __restrict__ vis_idx,
                                                          const float* __restrict__ anchor,
                                                          const float* __restrict__ feat,
@@ -411,7 +420,9 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
                                                          const float* __restrict__ cam,
                                                          const int32_t* __restrict__ slot_row, DecodeGrads gr,
                                                          float* __restrict__ partials) {
-    __shared__ DecodeBwdSmem sm;
+    constexpr int R = HEAD == 0 ? 16 : kBwdChunk * 16;
+    __shared__ DecodeBwdSmem<R, HEAD == 2 ? 0 : R> sm;
+    constexpr int head = HEAD;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
     const int K1 = kDecF + d.vd;
     const int noff = d.noff, cd = d.cd;
@@ -557,14 +568,16 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
                 for (int q = 0; q < 3; ++q) gr.d_anchor[(int64_t)id * 3 + q] += sacc[lane * 9 + 6 + q];
         }
         // dW2 += dY H^T (k = anchors), db2 += row sums of dY
+#pragma unroll
         for (int ot = 0; ot < kBwdChunk; ++ot) {
-            if (ot >= nt) break;
+            if (ot < nt) {  // static indices: the accumulators stay in registers
 #pragma unroll
-            for (int ht = 0; ht < 2; ++ht) {
+                for (int ht = 0; ht < 2; ++ht) {
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk)
-                    aw2[ot][ht] = mfma4(sdy[(ot * 16 + i) * kDecYS + 4 * kk + g], sh[(ht * 16 + i) * kDecYS + 4 * kk + g],
-                                        aw2[ot][ht]);
+                    for (int kk = 0; kk < 4; ++kk)
+                        aw2[ot][ht] = mfma4(sdy[(ot * 16 + i) * kDecYS + 4 * kk + g],
+                                            sh[(ht * 16 + i) * kDecYS + 4 * kk + g], aw2[ot][ht]);
+                }
             }
         }
 #pragma unroll
@@ -640,12 +653,14 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
     }
     // flush this wave's weight-gradient partials
     float* out = partials + (int64_t)(blockIdx.x * 4 + wave) * bwd_partial_floats(nt);
+#pragma unroll
     for (int ot = 0; ot < kBwdChunk; ++ot) {
-        if (ot >= nt) break;
+        if (ot < nt) {
 #pragma unroll
-        for (int ht = 0; ht < 2; ++ht)
+            for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) out[(ot * 16 + 4 * g + r) * 32 + ht * 16 + i] = aw2[ot][ht][r];
+                for (int r = 0; r < 4; ++r) out[(ot * 16 + 4 * g + r) * 32 + ht * 16 + i] = aw2[ot][ht][r];
+        }
     }
     float* ob2 = out + rows * 32;
 #pragma unroll
@@ -661,16 +676,31 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
     if (lane < 32) ow1[32 * 48 + lane] = (float)ab1;
 }
 
-// sum the per-wave partials of one launch into the weight gradients (+=; fixed order)
-__global__ __launch_bounds__(256) void decode_wgrad_reduce_kernel(int n_parts, int nt, int o0, int O, int K1,
-                                                                  const float* __restrict__ partials,
+// sum the per-wave partials of one launch into the weight gradients (+=), in two
+// fixed-order levels: decode_wgrad_sum_kernel folds groups of partials (f64 sums),
+// decode_wgrad_reduce_kernel folds the groups and scatters into the gradient tensors
+constexpr int kRedGroups = 32;
+
+__global__ __launch_bounds__(256) void decode_wgrad_sum_kernel(int n_parts, int pf, const float* __restrict__ partials,
+                                                               double* __restrict__ level2) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= pf) return;
+    const int per = (n_parts + kRedGroups - 1) / kRedGroups;
+    const int q0 = blockIdx.y * per, q1 = min(q0 + per, n_parts);
+    double acc = 0.0;
+    for (int q = q0; q < q1; ++q) acc += partials[(int64_t)q * pf + e];
+    level2[(int64_t)blockIdx.y * pf + e] = acc;
+}
+
+__global__ __launch_bounds__(256) void decode_wgrad_reduce_kernel(int nt, int o0, int O, int K1,
+                                                                  const double* __restrict__ level2,
                                                                   float* __restrict__ dw2, float* __restrict__ db2,
                                                                   float* __restrict__ dw1, float* __restrict__ db1) {
     const int pf = bwd_partial_floats(nt);
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (e >= pf) return;
     double acc = 0.0;
-    for (int q = 0; q < n_parts; ++q) acc += partials[(int64_t)q * pf + e];
+    for (int q = 0; q < kRedGroups; ++q) acc += level2[(int64_t)q * pf + e];
     const float sum = (float)acc;
     const int rows = nt * 16;
     if (e < rows * 32) {
@@ -780,22 +810,29 @@ extern "C" int hgsr_decode_fwd(int Av, int F, int view_dim, int n_offsets, int c
     DecodeOut out{xyz, offsets_out, color, opacity, scaling, rot, mask, slot_row};
     hipStream_t s = as_stream(stream);
     KernelTimer kt("decode_fwd", s);
-    if (view_dim == 3)
-        hipLaunchKernelGGL(decode_fwd_kernel<9>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
-                           feat, offset, scaling_raw, cam_center, off, out);
-    else
-        hipLaunchKernelGGL(decode_fwd_kernel<8>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
-                           feat, offset, scaling_raw, cam_center, off, out);
+#define LAUNCH_DF(KS, R)                                                                                      \
+    hipLaunchKernelGGL((decode_fwd_kernel<KS, R>), dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor, \
+                       feat, offset, scaling_raw, cam_center, off, out)
+    // LDS sized to the model: RGB heads fit 128 second-layer rows (2 workgroups per CU)
+    if (d.rows <= 128) {
+        if (view_dim == 3) LAUNCH_DF(9, 128);
+        else LAUNCH_DF(8, 128);
+    } else {
+        if (view_dim == 3) LAUNCH_DF(9, kDecMaxRows);
+        else LAUNCH_DF(8, kDecMaxRows);
+    }
+#undef LAUNCH_DF
     return check_launch("decode_fwd");
 }
 
 static int bwd_grid(int Av) {
     const int n_tiles = (Av + kDecTile - 1) / kDecTile;
-    return n_tiles < 256 ? (n_tiles > 0 ? n_tiles : 1) : 256;
+    return n_tiles < 1024 ? (n_tiles > 0 ? n_tiles : 1) : 1024;
 }
 
 extern "C" size_t hgsr_decode_bwd_ws_bytes(int Av) {
-    return (size_t)bwd_grid(Av) * 4 * bwd_partial_floats(kBwdChunk) * sizeof(float);
+    const size_t parts = ((size_t)bwd_grid(Av) * 4 * bwd_partial_floats(kBwdChunk) * sizeof(float) + 255) & ~(size_t)255;
+    return parts + (size_t)kRedGroups * bwd_partial_floats(kBwdChunk) * sizeof(double);
 }
 
 extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim, const int32_t* vis_idx,
@@ -818,22 +855,34 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
     hipStream_t s = as_stream(stream);
     const int grid = bwd_grid(Av);
     float* partials = (float*)ws;
+    double* level2 = (double*)((char*)ws + (((size_t)grid * 4 * bwd_partial_floats(kBwdChunk) * sizeof(float) + 255) &
+                                            ~(size_t)255));
     const int K1 = kDecF + view_dim;
     KernelTimer kt("decode_bwd", s);
     for (int head = 0; head < 3; ++head) {
         for (int t0 = 0; t0 < d.T[head]; t0 += kBwdChunk) {
             const int nt = d.T[head] - t0 < kBwdChunk ? d.T[head] - t0 : kBwdChunk;
-            if (view_dim == 3)
-                hipLaunchKernelGGL(decode_bwd_kernel<9>, dim3(grid), dim3(256), 0, s, d, mp, head, t0, nt, vis_idx,
-                                   anchor, feat, offset, scaling_raw, cam_center, slot_row, gr, partials);
-            else
-                hipLaunchKernelGGL(decode_bwd_kernel<8>, dim3(grid), dim3(256), 0, s, d, mp, head, t0, nt, vis_idx,
-                                   anchor, feat, offset, scaling_raw, cam_center, slot_row, gr, partials);
+#define LAUNCH_DB(KS, HD)                                                                                      \
+    hipLaunchKernelGGL((decode_bwd_kernel<KS, HD>), dim3(grid), dim3(256), 0, s, d, mp, t0, nt, vis_idx, anchor,    \
+                       feat, offset, scaling_raw, cam_center, slot_row, gr, partials)
+            if (view_dim == 3) {
+                if (head == 0) LAUNCH_DB(9, 0);
+                else if (head == 1) LAUNCH_DB(9, 1);
+                else LAUNCH_DB(9, 2);
+            } else {
+                if (head == 0) LAUNCH_DB(8, 0);
+                else if (head == 1) LAUNCH_DB(8, 1);
+                else LAUNCH_DB(8, 2);
+            }
+#undef LAUNCH_DB
             if (int st = check_launch("decode_bwd")) return st;
             const int pf = bwd_partial_floats(nt);
-            hipLaunchKernelGGL(decode_wgrad_reduce_kernel, dim3((pf + 255) / 256), dim3(256), 0, s, grid * 4, nt,
-                               t0 * 16, d.O[head], K1, partials, d_mlp[4 * head + 2], d_mlp[4 * head + 3],
-                               d_mlp[4 * head], d_mlp[4 * head + 1]);
+            hipLaunchKernelGGL(decode_wgrad_sum_kernel, dim3((pf + 255) / 256, kRedGroups), dim3(256), 0, s, grid * 4,
+                               pf, partials, level2);
+            if (int st = check_launch("decode_wgrad_sum")) return st;
+            hipLaunchKernelGGL(decode_wgrad_reduce_kernel, dim3((pf + 255) / 256), dim3(256), 0, s, nt, t0 * 16,
+                               d.O[head], K1, level2, d_mlp[4 * head + 2], d_mlp[4 * head + 3], d_mlp[4 * head],
+                               d_mlp[4 * head + 1]);
             if (int st = check_launch("decode_wgrad_reduce")) return st;
         }
     }
