@@ -398,11 +398,10 @@ template <int R, int YR>
 struct DecodeBwdSmem {
     float w1[32 * kDecS];
     float b1[32];
-    float w2[R * kDecS];
-    float b2[R];
+    float w2[YR * kDecS];  // YR >= R rows: the cov head stages (and recomputes) all of its rows
+    float b2[YR];
     float x[4][16 * kDecS];
-    float y[4][(YR > 0 ? YR : 1) * kDecYS];  // recomputed pre-activations (opacity / cov)
-    float dy[4][R * kDecYS];                 // dY^T[o][anchor]
+    float dy[4][YR * kDecYS];  // recomputed pre-activations Y^T, overwritten in place by dY^T[o][anchor]
     float h[4][32 * kDecYS];                 // H^T, then dH^T [hidden][anchor]
     float acc[4][16 * 9];                    // per-anchor d scaling_raw (6) + d anchor (3)
 };
@@ -410,8 +409,8 @@ struct DecodeBwdSmem {
 // partial layout per wave: dW2 chunk [nt*16][32] | db2 chunk [nt*16] | dW1 [32][48] | db1 [32]
 __host__ __device__ inline int bwd_partial_floats(int nt) { return nt * 16 * 32 + nt * 16 + 32 * 48 + 32; }
 
-template <int KSTEPS, int HEAD>
-__global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs mp, int t0, int nt,
+template <int KSTEPS, int HEAD, int NT>
+__global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtrs mp, int t0, int nt,
                                                          const int32_t* __restrict__ vis_idx,
                                                          const float* __restrict__ anchor,
                                                          const float* __restrict__ feat,
@@ -420,34 +419,38 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
                                                          const float* __restrict__ cam,
                                                          const int32_t* __restrict__ slot_row, DecodeGrads gr,
                                                          float* __restrict__ partials) {
-    constexpr int R = HEAD == 0 ? 16 : kBwdChunk * 16;
-    __shared__ DecodeBwdSmem<R, HEAD == 2 ? 0 : R> sm;
+    constexpr int R = NT * 16;                     // NT >= nt: accumulators sized to the chunk
+    constexpr int RY = HEAD == 1 ? 5 * 16 : R;     // cov: all rows (a slot's 7 outputs straddle tiles)
+    __shared__ DecodeBwdSmem<R, RY> sm;
     constexpr int head = HEAD;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
     const int K1 = kDecF + d.vd;
     const int noff = d.noff, cd = d.cd;
     const int o0 = t0 * 16, O = d.O[head], rows = nt * 16;
+    // rows of W2 / Y staged in LDS: the whole head for cov (chunk rows start at co), else the chunk
+    const int srow0 = head == 1 ? 0 : o0, srows = head == 1 ? d.T[1] * 16 : rows, co = head == 1 ? o0 : 0;
     // stage this head's layer-1 weights and the chunk of layer-2 rows (permuted columns)
     for (int e = threadIdx.x; e < 32 * kDecS; e += 256) {
         const int h = e / kDecS, k = e - h * kDecS;
         sm.w1[e] = k < K1 ? mp.w1[head][h * K1 + k] : 0.f;
     }
     if (threadIdx.x < 32) sm.b1[threadIdx.x] = mp.b1[head][threadIdx.x];
-    for (int e = threadIdx.x; e < rows * kDecF; e += 256) {
+    for (int e = threadIdx.x; e < srows * kDecF; e += 256) {
         const int row = e / kDecF, h = e - row * kDecF;
-        const int o = o0 + row;
+        const int o = srow0 + row;
         sm.w2[row * kDecS + w2_col(h)] = o < O ? mp.w2[head][o * kDecF + h] : 0.f;
     }
-    for (int row = threadIdx.x; row < rows; row += 256) sm.b2[row] = o0 + row < O ? mp.b2[head][o0 + row] : 0.f;
-    f32x4 aw2[kBwdChunk][2], aw1[2][3];
+    for (int row = threadIdx.x; row < srows; row += 256)
+        sm.b2[row] = srow0 + row < O ? mp.b2[head][srow0 + row] : 0.f;
+    f32x4 aw2[NT][2], aw1[2][3];
 #pragma unroll
-    for (int a = 0; a < kBwdChunk; ++a) aw2[a][0] = aw2[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < NT; ++a) aw2[a][0] = aw2[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int a = 0; a < 2; ++a) aw1[a][0] = aw1[a][1] = aw1[a][2] = f32x4{0.f, 0.f, 0.f, 0.f};
     double ab2[2] = {0.0, 0.0}, ab1 = 0.0;  // bias sums over many anchors: f64
     float* sx = sm.x[wave];
-    float* sy = sm.y[wave];
     float* sdy = sm.dy[wave];
+    float* sy = sdy;  // every slot reads its own Y entries before writing its dY there
     float* sh = sm.h[wave];
     float* sacc = sm.acc[wave];
     const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
@@ -473,7 +476,7 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
         }
         // recompute the pre-activations the derivative needs
         if (head < 2) {
-            for (int ot = 0; ot < nt; ++ot) {
+            for (int ot = 0; ot < srows / 16; ++ot) {
                 f32x4 y = {0.f, 0.f, 0.f, 0.f};
                 const float* w = sm.w2 + (ot * 16 + i) * kDecS + g;
 #pragma unroll
@@ -484,40 +487,56 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
                 for (int r = 0; r < 4; ++r) sy[(ot * 16 + 4 * g + r) * kDecYS + i] = y[r] + sm.b2[ot * 16 + 4 * g + r];
             }
         }
-        // dY^T for the chunk (zero for dropped slots, padding rows and absent anchors)
-        for (int e = lane; e < rows * 16; e += 64) sdy[(e >> 4) * kDecYS + (e & 15)] = 0.f;
+        // dY^T for the chunk, in place over Y^T for the opacity / cov heads: every slot writes
+        // all of its rows (zeros when dropped or absent), padding rows are zeroed separately
+        if (head == 2) {
+            for (int e = lane; e < rows * 16; e += 64) sdy[(e >> 4) * kDecYS + (e & 15)] = 0.f;
+        } else {
+            const int used = head == 0 ? noff : 7 * noff;
+            for (int e = lane; e < (srows - used) * 16; e += 64) sdy[(used + (e >> 4)) * kDecYS + (e & 15)] = 0.f;
+        }
         if (head == 0) {
             for (int s = lane; s < 16 * noff; s += 64) {
                 const int a = s / noff, k = s - a * noff;
-                if (a0 + a >= d.Av) continue;
-                const int p = slot_row[(int64_t)(a0 + a) * noff + k];
-                if (p < 0 || !gr.g_opacity) continue;
-                const float th = tanhf(sy[k * kDecYS + a]);
-                sdy[k * kDecYS + a] = gr.g_opacity[p] * (1.0f - th * th);
+                const int p = a0 + a < d.Av ? slot_row[(int64_t)(a0 + a) * noff + k] : -1;
+                float v = 0.f;
+                if (p >= 0 && gr.g_opacity) {
+                    const float th = tanhf(sy[k * kDecYS + a]);
+                    v = gr.g_opacity[p] * (1.0f - th * th);
+                }
+                sdy[k * kDecYS + a] = v;
             }
         } else if (head == 1) {
             for (int s = lane; s < 16 * noff; s += 64) {
                 const int a = s / noff, k = s - a * noff;
-                if (a0 + a >= d.Av) continue;
-                const int id = vis_idx ? vis_idx[a0 + a] : a0 + a;
-                const int p = slot_row[(int64_t)(a0 + a) * noff + k];
-                float* dof = gr.d_offset + ((int64_t)id * noff + k) * 3;
+                const bool present = a0 + a < d.Av;
+                const int id = present ? (vis_idx ? vis_idx[a0 + a] : a0 + a) : 0;
+                const int p = present ? slot_row[(int64_t)(a0 + a) * noff + k] : -1;
+                float cv[7], dv[7];
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    cv[q] = sy[(7 * k + q) * kDecYS + a];
+                    dv[q] = 0.f;
+                }
                 if (p < 0) {
-                    dof[0] = dof[1] = dof[2] = 0.f;
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) sdy[(7 * k + q) * kDecYS + a] = 0.f;
+                    if (present && t0 == 0) {
+                        float* dof = gr.d_offset + ((int64_t)id * noff + k) * 3;
+                        dof[0] = dof[1] = dof[2] = 0.f;
+                    }
                     continue;
                 }
+                float* dof = gr.d_offset + ((int64_t)id * noff + k) * 3;
                 const float* sr = scaling_raw + (int64_t)id * 6;
-                float cv[7];
-#pragma unroll
-                for (int q = 0; q < 7; ++q) cv[q] = sy[(7 * k + q) * kDecYS + a];
                 // scaling = exp(sr[3:6]) * sigmoid(cv[0:3])
                 if (gr.g_scaling) {
 #pragma unroll
                     for (int q = 0; q < 3; ++q) {
                         const float es = expf(sr[3 + q]), sg = 1.0f / (1.0f + expf(-cv[q]));
                         const float gs = gr.g_scaling[(int64_t)p * 3 + q];
-                        sdy[(7 * k + q) * kDecYS + a] = gs * es * sg * (1.0f - sg);
-                        atomicAdd(&sacc[a * 9 + 3 + q], gs * es * sg);
+                        dv[q] = gs * es * sg * (1.0f - sg);
+                        if (t0 == 0) atomicAdd(&sacc[a * 9 + 3 + q], gs * es * sg);
                     }
                 }
                 // rot = v / max(|v|, 1e-12)
@@ -530,12 +549,15 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
 #pragma unroll
                         for (int q = 0; q < 4; ++q) dot += cv[3 + q] * inv * gq[q];
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) sdy[(7 * k + 3 + q) * kDecYS + a] = (gq[q] - cv[3 + q] * inv * dot) * inv;
+                        for (int q = 0; q < 4; ++q) dv[3 + q] = (gq[q] - cv[3 + q] * inv * dot) * inv;
                     } else {
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) sdy[(7 * k + 3 + q) * kDecYS + a] = gq[q] * 1e12f;
+                        for (int q = 0; q < 4; ++q) dv[3 + q] = gq[q] * 1e12f;
                     }
                 }
+#pragma unroll
+                for (int q = 0; q < 7; ++q) sdy[(7 * k + q) * kDecYS + a] = dv[q];
+                if (t0 != 0) continue;  // the position / offset chain belongs to the first cov chunk
                 // xyz = anchor + offset * exp(sr[0:3]); offsets_out = offset * exp(sr[0:3])
                 const float* of = offset + ((int64_t)id * noff + k) * 3;
 #pragma unroll
@@ -559,7 +581,7 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
             }
         }
         // per-anchor d scaling_raw / d anchor of the cov head (xyz and scaling outputs)
-        if (head == 1 && lane < 16 && a0 + lane < d.Av) {
+        if (head == 1 && t0 == 0 && lane < 16 && a0 + lane < d.Av) {
             const int id = vis_idx ? vis_idx[a0 + lane] : a0 + lane;
 #pragma unroll
             for (int q = 0; q < 6; ++q) gr.d_scaling[(int64_t)id * 6 + q] += sacc[lane * 9 + q];
@@ -569,13 +591,13 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
         }
         // dW2 += dY H^T (k = anchors), db2 += row sums of dY
 #pragma unroll
-        for (int ot = 0; ot < kBwdChunk; ++ot) {
+        for (int ot = 0; ot < NT; ++ot) {
             if (ot < nt) {  // static indices: the accumulators stay in registers
 #pragma unroll
                 for (int ht = 0; ht < 2; ++ht) {
 #pragma unroll
                     for (int kk = 0; kk < 4; ++kk)
-                        aw2[ot][ht] = mfma4(sdy[(ot * 16 + i) * kDecYS + 4 * kk + g],
+                        aw2[ot][ht] = mfma4(sdy[(co + ot * 16 + i) * kDecYS + 4 * kk + g],
                                             sh[(ht * 16 + i) * kDecYS + 4 * kk + g], aw2[ot][ht]);
                 }
             }
@@ -586,14 +608,14 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
             if (ol < rows) {
                 float sum = 0.f;
 #pragma unroll
-                for (int a = 0; a < 16; ++a) sum += sdy[ol * kDecYS + a];
+                for (int a = 0; a < 16; ++a) sum += sdy[(co + ol) * kDecYS + a];
                 ab2[q] += sum;
             }
         }
         // dH = W2^T dY, masked by ReLU; then stored transposed for dW1
         f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
         for (int kk = 0; kk < rows / 4; ++kk) {
-            const int o = 4 * kk + g;
+            const int o = co + 4 * kk + g;
             const float b = sdy[o * kDecYS + i];
             d0 = mfma4(sm.w2[o * kDecS + w2_col(i)], b, d0);
             d1 = mfma4(sm.w2[o * kDecS + w2_col(16 + i)], b, d1);
@@ -654,7 +676,7 @@ __global__ __launch_bounds__(256) void decode_bwd_kernel(DecodeDims d, MlpPtrs m
     // flush this wave's weight-gradient partials
     float* out = partials + (int64_t)(blockIdx.x * 4 + wave) * bwd_partial_floats(nt);
 #pragma unroll
-    for (int ot = 0; ot < kBwdChunk; ++ot) {
+    for (int ot = 0; ot < NT; ++ot) {
         if (ot < nt) {
 #pragma unroll
             for (int ht = 0; ht < 2; ++ht)
@@ -860,20 +882,31 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
     const int K1 = kDecF + view_dim;
     KernelTimer kt("decode_bwd", s);
     for (int head = 0; head < 3; ++head) {
-        for (int t0 = 0; t0 < d.T[head]; t0 += kBwdChunk) {
-            const int nt = d.T[head] - t0 < kBwdChunk ? d.T[head] - t0 : kBwdChunk;
-#define LAUNCH_DB(KS, HD)                                                                                      \
-    hipLaunchKernelGGL((decode_bwd_kernel<KS, HD>), dim3(grid), dim3(256), 0, s, d, mp, t0, nt, vis_idx, anchor,    \
-                       feat, offset, scaling_raw, cam_center, slot_row, gr, partials)
+        // up to 5 output tiles per launch (the cov head in one launch; measured: splitting it
+        // into 3 + 2 tiles gains nothing, its time is the per-tile work, not the accumulators)
+        const int chunk = kBwdChunk;
+        for (int t0 = 0; t0 < d.T[head]; t0 += chunk) {
+            const int nt = d.T[head] - t0 < chunk ? d.T[head] - t0 : chunk;
+#define LAUNCH_DB(KS, HD, NTT)                                                                                 \
+    hipLaunchKernelGGL((decode_bwd_kernel<KS, HD, NTT>), dim3(grid), dim3(256), 0, s, d, mp, t0, nt, vis_idx,       \
+                       anchor, feat, offset, scaling_raw, cam_center, slot_row, gr, partials)
+#define LAUNCH_DB_NT(KS, HD) \
+    do {                                                               \
+        if (nt <= 1) LAUNCH_DB(KS, HD, 1);                             \
+        else if (nt <= 2) LAUNCH_DB(KS, HD, 2);                        \
+        else if (nt <= 3) LAUNCH_DB(KS, HD, 3);                        \
+        else LAUNCH_DB(KS, HD, 5);                                     \
+    } while (0)
             if (view_dim == 3) {
-                if (head == 0) LAUNCH_DB(9, 0);
-                else if (head == 1) LAUNCH_DB(9, 1);
-                else LAUNCH_DB(9, 2);
+                if (head == 0) LAUNCH_DB(9, 0, 1);
+                else if (head == 1) LAUNCH_DB_NT(9, 1);
+                else LAUNCH_DB_NT(9, 2);
             } else {
-                if (head == 0) LAUNCH_DB(8, 0);
-                else if (head == 1) LAUNCH_DB(8, 1);
-                else LAUNCH_DB(8, 2);
+                if (head == 0) LAUNCH_DB(8, 0, 1);
+                else if (head == 1) LAUNCH_DB_NT(8, 1);
+                else LAUNCH_DB_NT(8, 2);
             }
+#undef LAUNCH_DB_NT
 #undef LAUNCH_DB
             if (int st = check_launch("decode_bwd")) return st;
             const int pf = bwd_partial_floats(nt);
