@@ -290,6 +290,23 @@ int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
                     float* d_offset, float* d_scaling, float* const* d_mlp, void* ws,
                     size_t ws_bytes, hgsr_stream_t stream);
 
+/* ---- K15: fused training loss ---------------------------
+ * replaces reference train.py:153-178 with utils/loss_utils.py:17-60: x = image*mask,
+ * y = gt*mask (image, gt [C,H,W]; mask [H,W] nullable); out[5] (device) =
+ * {loss, l1, ssim, sky, entropy} with loss = (1-l)*mean|x-y| + l*(1-mean SSIM(x,y)) +
+ * l_sky*mean(-(1-mask) log(1-a)) + l_ent*mean(-a log a), a = clamp(alpha, 1e-6, 1-1e-6)
+ * (alpha [H,W] nullable when both l_sky and l_ent are 0).  ws (hgsr_loss_ws_bytes) holds
+ * the SSIM derivative maps for hgsr_loss_bwd, which writes g_image [C,H,W] and g_alpha
+ * [H,W] (nullable) from g_out[5], the upstream gradients of the five outputs (device). */
+size_t hgsr_loss_ws_bytes(int C, int H, int W);
+int hgsr_loss_fwd(int C, int H, int W, const float* image, const float* gt, const float* mask,
+                  const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
+                  float* out, void* ws, size_t ws_bytes, hgsr_stream_t stream);
+int hgsr_loss_bwd(int C, int H, int W, const float* image, const float* gt, const float* mask,
+                  const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
+                  const float* g_out, float* g_image, float* g_alpha, const void* ws, size_t ws_bytes,
+                  hgsr_stream_t stream);
+
 /* ---- measurement ----------------------------------------------------------
  * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):
  * when enabled, the main kernel of every entry point is bracketed by

@@ -1,0 +1,65 @@
+"""GPU parity of the fused loss (horizongs_amd.loss) -- SURVEY 8(f) rank 2.
+
+Values against tests/golden/losses.npz (the reference's own l1 / ssim) and the oracle
+restatement oracle/loss_ref.py; gradients of every output against torch autograd of the
+oracle in fp64 (fp32 for the conditioning-aware check).  Tolerance 1e-5 abs / 1e-4 rel."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import loss_ref as L
+from oracle.checks import cond_close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def test_loss_matches_reference_golden():
+    from horizongs_amd.loss import fused_loss
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "losses.npz"))
+    img, gt = torch.from_numpy(g["img"]).to(DEV), torch.from_numpy(g["gt"]).to(DEV)
+    loss, l1, s, _, _ = fused_loss(img, gt, lambda_dssim=0.2)
+    assert abs(float(l1) - float(g["l1"])) <= 1e-6
+    assert abs(float(s) - float(g["ssim"])) <= 1e-5
+    assert abs(float(loss) - (0.8 * float(g["l1"]) + 0.2 * (1 - float(g["ssim"])))) <= 1e-5
+
+
+@pytest.mark.parametrize("H,W,masked,alpha_terms", [(64, 80, False, False), (67, 93, True, True),
+                                                    (1080 // 4, 1920 // 4, True, True)])
+def test_loss_gradients(H, W, masked, alpha_terms):
+    from horizongs_amd.loss import fused_loss
+    gen = torch.Generator().manual_seed(H * 7 + W)
+    img = torch.rand(3, H, W, generator=gen)
+    gt = (img + 0.1 * torch.randn(3, H, W, generator=gen)).clamp(0, 1)
+    mask = (torch.rand(H, W, generator=gen) > 0.2).float() if masked else None
+    alpha = torch.rand(H, W, generator=gen) if alpha_terms else None
+    lam = dict(lambda_dssim=0.2, lambda_sky=0.05 if alpha_terms else 0.0, lambda_ent=0.01 if alpha_terms else 0.0)
+    ups = torch.randn(5, generator=gen)
+
+    def ref(dtype):
+        i = img.to(dtype).clone().requires_grad_(True)
+        a = alpha.to(dtype).clone().requires_grad_(True) if alpha is not None else None
+        outs = L.loss(i, gt.to(dtype), None if mask is None else mask.to(dtype), alpha=a, **lam)
+        sum(o * u for o, u in zip(outs, ups.to(dtype))).backward()
+        return [o.detach().numpy() for o in outs], i.grad.numpy(), (a.grad.numpy() if a is not None else None)
+
+    o32, gi32, ga32 = ref(torch.float32)
+    o64, gi64, ga64 = ref(torch.float64)
+    i = img.to(DEV).clone().requires_grad_(True)
+    a = alpha.to(DEV).clone().requires_grad_(True) if alpha is not None else None
+    outs = fused_loss(i, gt.to(DEV), None if mask is None else mask.to(DEV), lam["lambda_dssim"], a,
+                      lam["lambda_sky"], lam["lambda_ent"])
+    for o, r32, r64, name in zip(outs, o32, o64, ("loss", "l1", "ssim", "sky", "entropy")):
+        cond_close(o.detach().cpu().numpy(), r32, r64, name)
+    sum(o * u for o, u in zip(outs, ups.to(DEV))).backward()
+    cond_close(i.grad.cpu().numpy(), gi32, gi64, "d_image")
+    if a is not None:
+        cond_close(a.grad.cpu().numpy(), ga32, ga64, "d_alpha")
