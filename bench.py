@@ -35,6 +35,7 @@ sys.path.insert(0, ROOT)
 from horizongs_amd import _native as NAT  # noqa: E402
 from horizongs_amd import decode as HD  # noqa: E402
 from horizongs_amd import gsplat_api as G  # noqa: E402
+from horizongs_amd.loss import fused_loss  # noqa: E402
 from horizongs_amd.multigpu import GradientAllReduce  # noqa: E402
 from horizongs_amd.synthetic import make_scene  # noqa: E402
 
@@ -44,7 +45,7 @@ HBM_PEAK_GBS = 8000.0      # HBM3E spec
 FLOP_PER_PAIR = {"raster3d_fwd": 20.0, "raster3d_bwd": 60.0, "raster2d_fwd": 40.0, "raster2d_bwd": 120.0}
 KERNELS = ["project3d_fwd", "isect_count", "isect_emit", "tile_sort", "raster3d_fwd", "raster3d_bwd",
            "project3d_bwd", "project2d_fwd", "raster2d_fwd", "raster2d_bwd", "project2d_bwd", "sh_fwd", "sh_bwd",
-           "decode_count", "decode_fwd", "decode_bwd"]
+           "decode_count", "decode_fwd", "decode_bwd", "loss_fwd", "loss_bwd"]
 
 
 def parse():
@@ -128,8 +129,11 @@ class Workload:
             (out, alpha, normals, nfd, distort, median), meta = G.rasterization_2dgs(
                 xyz, quats, scales, opac, cols, self.viewmats, self.Ks, W, H,
                 packed=False, backgrounds=self.bg, render_mode="RGB+ED")
+        # the reference fine-stage loss head (train.py:153-178, config/base/small_scene/fine.yaml:50-57):
+        # 0.8 L1 + 0.2 D-SSIM + 0.05 sky opacity + 0.05 opacity entropy (fused HIP loss) + 0.01 scale reg
         rgb = out[0, ..., :3].permute(2, 0, 1)
-        loss = (rgb - self.target).abs().mean() + 0.01 * alpha.mean()
+        loss = fused_loss(rgb, self.target, None, 0.2, alpha[0, ..., 0], 0.05, 0.05)[0]
+        loss = loss + 0.01 * scales.prod(dim=1).mean()
         if self.args.gs == "2d":
             n = normals[0].permute(2, 0, 1)
             nd = (nfd * alpha.detach())[0].permute(2, 0, 1)
@@ -324,7 +328,8 @@ def main():
             "data": "synthetic (seeded c2 scene, SURVEY 8(d); no dataset in the environment)",
             "config": {"workload": (f"c2 {'3DGS' if args.gs == '3d' else '2DGS'} train step: "
                                     + (f"fused anchor decode ({args.anchors} anchors) + " if args.anchors else "")
-                                    + "rasterization fwd + L1/alpha loss + bwd, RGB+ED"),
+                                    + "rasterization fwd + reference loss (L1 + D-SSIM + alpha/scale regs) + bwd, "
+                                      "RGB+ED"),
                        "gaussians": int(wl.last_colors.shape[0]), "width": args.width, "height": args.height,
                        "parallelism": ("per-chunk, one scene per GPU, no collectives" if args.mode == "chunk"
                                        else "DDP over views, RCCL all-reduce of Gaussian grads")},
