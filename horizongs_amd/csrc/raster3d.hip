@@ -350,16 +350,9 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
             // the list comes back into registers once per batch; the loop reads
             // entries with readlane so no LDS index read sits on the critical path
             const int lst0 = my_list[lane], lst1 = my_list[64 + lane];
-            int tn = __builtin_amdgcn_readfirstlane(lst0);
-            float4 g0n = s_g0[cur][tn], g1n = s_g1[cur][tn], cn = s_col[cur][tn];
             for (int i = 0; i < n_mine; ++i) {
-                const int t = tn;
-                const float4 g0 = g0n, g1 = g1n, c = cn;
-                const int inext = min(i + 1, n_mine - 1);
-                tn = __builtin_amdgcn_readlane(inext < 64 ? lst0 : lst1, inext & 63);
-                g0n = s_g0[cur][tn];
-                g1n = s_g1[cur][tn];
-                cn = s_col[cur][tn];
+                const int t = __builtin_amdgcn_readlane(i < 64 ? lst0 : lst1, i & 63);
+                const float4 g0 = s_g0[cur][t], g1 = s_g1[cur][t], c = s_col[cur][t];
                 const float dx = g0.x - tc.px, dy = g0.y - tc.py;
                 const float sigma = 0.5f * (g0.z * dx * dx + g1.x * dy * dy) + g0.w * dx * dy;
                 const float vis = __expf(-sigma);
