@@ -357,13 +357,23 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
     const int32_t end = min(tc.end, blk_final + 1);
     const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
-    float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0, n3 = n0, n4 = n0, n5 = n0;
+    // records are staged with LDS-DMA (global_load_lds_dwordx4: per-lane source, LDS
+    // destination base + 16 B x lane), one batch ahead, so they cost no VGPRs (89 -> 59);
+    // the 64 loader lanes are exactly wave 0
+    float4* const stage_arr[6] = {&s_r0[0][0], &s_r1[0][0], &s_r2[0][0], &s_col[0][0], &s_r4[0][0], &s_box[0][0]};
     int32_t cid = 0, nid = 0;
     const bool loader = tid < NB;
+    auto dma_batch = [&](int buf, int32_t id) {
+        const float4* r = reinterpret_cast<const float4*>(rec + id);
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + q),
+                                             (void __attribute__((address_space(3)))*)(stage_arr[q] + buf * NB), 16,
+                                             0, 0);
+    };
     if (nb > 0 && loader) {
         cid = flatten_ids[max(end - 1 - tid, tc.start)];
-        const float4* r = reinterpret_cast<const float4*>(rec + cid);
-        n0 = r[0]; n1 = r[1]; n2 = r[2]; n3 = r[3]; n4 = r[4]; n5 = r[5];
+        dma_batch(0, cid);
         nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
     }
     using TR = TransposeReduce<KV>;
@@ -374,16 +384,14 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
         const int cur = b & 1, prv = cur ^ 1;
         const int32_t batch_end = end - 1 - b * NB;
         const int bsz = b < nb ? min(NB, batch_end + 1 - tc.start) : 0;
-        // stage batch b, issue batch b+1's loads, then combine batch b-1 (atomics last)
-        if (tid < bsz) {
-            s_id[cur][tid] = cid;
-            s_r0[cur][tid] = n0; s_r1[cur][tid] = n1; s_r2[cur][tid] = n2;
-            s_col[cur][tid] = n3; s_r4[cur][tid] = n4; s_box[cur][tid] = n5;
-        }
-        if (b < nb && loader) {
+        // batch b's DMA (issued one iteration ago, together with one batch-old atomics) lands
+        // before the barrier below publishes it; then DMA batch b+1 into the other buffer
+        // (its previous records were last read before the previous barrier) and combine b-1
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+        if (tid < bsz) s_id[cur][tid] = cid;
+        if (b + 1 < nb && loader) {
             cid = nid;
-            const float4* r = reinterpret_cast<const float4*>(rec + cid);
-            n0 = r[0]; n1 = r[1]; n2 = r[2]; n3 = r[3]; n4 = r[4]; n5 = r[5];
+            dma_batch(prv, cid);
             nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
         if (b > 0) {
