@@ -25,12 +25,18 @@ struct LossWin {
     float w[11];
 };
 
-__device__ __forceinline__ float masked(const float* __restrict__ img, const float* __restrict__ mask, int c, int H,
-                                        int W, int yy, int xx) {
+// a [C,H,W] image with arbitrary element strides (contiguous CHW, or the channels-last
+// [H,W,C] render output viewed through permute(2,0,1) without a copy)
+struct Img {
+    const float* p;
+    int64_t sc, sy, sx;
+    __device__ __forceinline__ int64_t at(int c, int y, int x) const { return c * sc + y * sy + x * sx; }
+};
+
+__device__ __forceinline__ float masked(Img img, const float* __restrict__ mask, int c, int H, int W, int yy, int xx) {
     if (yy < 0 || yy >= H || xx < 0 || xx >= W) return 0.f;  // conv2d zero padding
-    const int64_t p = (int64_t)yy * W + xx;
-    const float v = img[(int64_t)c * H * W + p];
-    return mask ? v * mask[p] : v;
+    const float v = img.p[img.at(c, yy, xx)];
+    return mask ? v * mask[(int64_t)yy * W + xx] : v;
 }
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
@@ -45,8 +51,8 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 // forward: SSIM map statistics + derivative maps, L1, alpha terms; per-tile partials
 // partial layout per tile: [sum |x-y|, sum S, sum sky, sum entropy]
-__global__ __launch_bounds__(256) void loss_fwd_kernel(int C, int H, int W, const float* __restrict__ img,
-                                                       const float* __restrict__ gt, const float* __restrict__ mask,
+__global__ __launch_bounds__(256) void loss_fwd_kernel(int C, int H, int W, Img img, Img gt,
+                                                       const float* __restrict__ mask,
                                                        const float* __restrict__ alpha, LossWin win,
                                                        float* __restrict__ dmaps, float* __restrict__ partials) {
     __shared__ float s_x[kLH][kLH + 1], s_y[kLH][kLH + 1];
@@ -169,13 +175,13 @@ __global__ __launch_bounds__(256) void loss_reduce_kernel(int n_tiles, int C, in
 }
 
 // backward: d loss / d image (and d alpha), scaled by the upstream scalar gradient
-__global__ __launch_bounds__(256) void loss_bwd_kernel(int C, int H, int W, const float* __restrict__ img,
-                                                       const float* __restrict__ gt, const float* __restrict__ mask,
+__global__ __launch_bounds__(256) void loss_bwd_kernel(int C, int H, int W, Img img, Img gt,
+                                                       const float* __restrict__ mask,
                                                        const float* __restrict__ alpha, LossWin win, float lam_dssim,
                                                        float lam_sky, float lam_ent,
                                                        const float* __restrict__ dmaps,
                                                        const float* __restrict__ g_out, float* __restrict__ g_img,
-                                                       float* __restrict__ g_alpha) {
+                                                       int extra_ch, float* __restrict__ g_alpha) {
     __shared__ float s_m[3][kLH][kLH + 1];
     __shared__ float s_h[3][kLH][kLT + 1];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
@@ -223,13 +229,15 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(int C, int H, int W, cons
             gb += w * s_h[1][ty + k][tx];
             gc += w * s_h[2][ty + k][tx];
         }
-        const int64_t p = (int64_t)c * HW + pp;
-        const float x = img[p] * mk, y = gt[p] * mk;
+        const float x = img.p[img.at(c, py, px)] * mk, y = gt.p[gt.at(c, py, px)] * mk;
         const float d = x - y;
         const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
         const float gx = k_l1 * sgn + k_ss * (ga + 2.f * x * gb + y * gc);
-        g_img[p] = gx * mk;
+        g_img[img.at(c, py, px)] = gx * mk;
     }
+    // trailing image channels the loss does not read (e.g. the ED channel of RGB+ED)
+    if (inside)
+        for (int c = C; c < C + extra_ch; ++c) g_img[img.at(c, py, px)] = 0.f;
     if (g_alpha && inside) {
         float ga = 0.f;
         if (alpha) {
@@ -268,20 +276,34 @@ extern "C" size_t hgsr_loss_ws_bytes(int C, int H, int W) {
     return maps + (size_t)loss_tiles(H, W) * 4 * sizeof(float);
 }
 
-extern "C" int hgsr_loss_fwd(int C, int H, int W, const float* image, const float* gt, const float* mask,
+static int check_strides(const int64_t* st, const char* what) {
+    HGSR_REQUIRE(st == nullptr || (st[0] >= 0 && st[1] >= 0 && st[2] >= 0), "negative %s strides", what);
+    return HGSR_OK;
+}
+
+static Img make_img(const float* p, const int64_t* st, int H, int W) {
+    if (!st) return Img{p, (int64_t)H * W, W, 1};
+    return Img{p, st[0], st[1], st[2]};
+}
+
+extern "C" int hgsr_loss_fwd(int C, int H, int W, const float* image, const int64_t* image_strides,
+                             const float* gt, const int64_t* gt_strides, const float* mask,
                              const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
                              float* out, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
     HGSR_REQUIRE(C >= 1 && H > 0 && W > 0, "bad dims");
     HGSR_REQUIRE(image && gt && out && ws, "null pointer");
     HGSR_REQUIRE(ws_bytes >= hgsr_loss_ws_bytes(C, H, W), "loss workspace too small");
     HGSR_REQUIRE(alpha || (lambda_sky_opa == 0.f && lambda_entropy == 0.f), "alpha terms need alpha");
+    if (int st = check_strides(image_strides, "image")) return st;
+    if (int st = check_strides(gt_strides, "gt")) return st;
     hipStream_t s = as_stream(stream);
     float* dmaps = (float*)ws;
     float* partials = (float*)((char*)ws + (((size_t)3 * C * H * W * sizeof(float) + 255) & ~(size_t)255));
     const int nt = loss_tiles(H, W);
     {
         KernelTimer kt("loss_fwd", s);
-        hipLaunchKernelGGL(loss_fwd_kernel, dim3(nt), dim3(256), 0, s, C, H, W, image, gt, mask, alpha,
+        hipLaunchKernelGGL(loss_fwd_kernel, dim3(nt), dim3(256), 0, s, C, H, W, make_img(image, image_strides, H, W),
+                           make_img(gt, gt_strides, H, W), mask, alpha,
                            gaussian_window(), dmaps, partials);
     }
     if (int st = check_launch("loss_fwd")) return st;
@@ -290,17 +312,22 @@ extern "C" int hgsr_loss_fwd(int C, int H, int W, const float* image, const floa
     return check_launch("loss_reduce");
 }
 
-extern "C" int hgsr_loss_bwd(int C, int H, int W, const float* image, const float* gt, const float* mask,
+extern "C" int hgsr_loss_bwd(int C, int H, int W, const float* image, const int64_t* image_strides,
+                             const float* gt, const int64_t* gt_strides, const float* mask,
                              const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
-                             const float* g_out, float* g_image, float* g_alpha, const void* ws, size_t ws_bytes,
-                             hgsr_stream_t stream) {
+                             const float* g_out, float* g_image, int extra_channels, float* g_alpha,
+                             const void* ws, size_t ws_bytes, hgsr_stream_t stream) {
     HGSR_REQUIRE(C >= 1 && H > 0 && W > 0, "bad dims");
     HGSR_REQUIRE(image && gt && g_out && g_image && ws, "null pointer");
     HGSR_REQUIRE(ws_bytes >= hgsr_loss_ws_bytes(C, H, W), "loss workspace too small");
+    if (int st = check_strides(image_strides, "image")) return st;
+    if (int st = check_strides(gt_strides, "gt")) return st;
+    HGSR_REQUIRE(extra_channels >= 0, "negative extra_channels");
     hipStream_t s = as_stream(stream);
     KernelTimer kt("loss_bwd", s);
-    hipLaunchKernelGGL(loss_bwd_kernel, dim3(loss_tiles(H, W)), dim3(256), 0, s, C, H, W, image, gt, mask, alpha,
+    hipLaunchKernelGGL(loss_bwd_kernel, dim3(loss_tiles(H, W)), dim3(256), 0, s, C, H, W,
+                       make_img(image, image_strides, H, W), make_img(gt, gt_strides, H, W), mask, alpha,
                        gaussian_window(), lambda_dssim, lambda_sky_opa, lambda_entropy, (const float*)ws, g_out,
-                       g_image, g_alpha);
+                       g_image, extra_channels, g_alpha);
     return check_launch("loss_bwd");
 }

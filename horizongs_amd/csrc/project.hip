@@ -316,15 +316,13 @@ __global__ __launch_bounds__(256) void project3d_bwd_kernel(
         const float4 vq = quat_to_rotmat_vjp(q, vRq);
         vq_acc.x += vq.x; vq_acc.y += vq.y; vq_acc.z += vq.z; vq_acc.w += vq.w;
     }
-    if (!any) return;
+    // overwrite semantics: a Gaussian culled in every camera gets zeros
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        v_means[(int64_t)g * 3 + j] += vm_acc[j];
-        v_scales[(int64_t)g * 3 + j] += vs_acc[j];
+        v_means[(int64_t)g * 3 + j] = vm_acc[j];
+        v_scales[(int64_t)g * 3 + j] = vs_acc[j];
     }
-    float4 t = v_quats[g];
-    t.x += vq_acc.x; t.y += vq_acc.y; t.z += vq_acc.z; t.w += vq_acc.w;
-    v_quats[g] = t;
+    v_quats[g] = vq_acc;
 }
 
 // ---------------------------------------------------------------- 2DGS fwd
@@ -436,11 +434,9 @@ __global__ __launch_bounds__(256) void project2d_bwd_kernel(
     float vm_acc[3] = {0.f, 0.f, 0.f};
     float vs0 = 0.f, vs1 = 0.f;
     float4 vq_acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    bool any = false;
     for (int c = 0; c < C; ++c) {
         const int64_t o = (int64_t)c * N + g;
         if (radii[o] <= 0) continue;
-        any = true;
         const View v = load_view(viewmats + c * 16, Ks + c * 9);
         const Surfel f = surfel_frame(v, m, q, s);
         const float* M = ray_transforms + o * 9;
@@ -488,14 +484,13 @@ __global__ __launch_bounds__(256) void project2d_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 3; ++j) vm_acc[j] += v.R.m[0][j] * vmc[0] + v.R.m[1][j] * vmc[1] + v.R.m[2][j] * vmc[2];
     }
-    if (!any) return;
+    // overwrite semantics: a Gaussian culled in every camera gets zeros
 #pragma unroll
-    for (int j = 0; j < 3; ++j) v_means[(int64_t)g * 3 + j] += vm_acc[j];
-    v_scales[(int64_t)g * 3 + 0] += vs0;
-    v_scales[(int64_t)g * 3 + 1] += vs1;
-    float4 t = v_quats[g];
-    t.x += vq_acc.x; t.y += vq_acc.y; t.z += vq_acc.z; t.w += vq_acc.w;
-    v_quats[g] = t;
+    for (int j = 0; j < 3; ++j) v_means[(int64_t)g * 3 + j] = vm_acc[j];
+    v_scales[(int64_t)g * 3 + 0] = vs0;
+    v_scales[(int64_t)g * 3 + 1] = vs1;
+    v_scales[(int64_t)g * 3 + 2] = 0.f;
+    v_quats[g] = vq_acc;
 }
 
 }  // namespace hgsr

@@ -72,9 +72,9 @@ class _Project3D(torch.autograd.Function):
         means, quats, scales, viewmats, Ks, radii, conics = ctx.saved_tensors
         width, height, eps2d = ctx.cfg
         C, Ng = viewmats.shape[0], means.shape[0]
-        v_means = torch.zeros_like(means)
-        v_quats = torch.zeros_like(quats)
-        v_scales = torch.zeros_like(scales)
+        v_means = torch.empty_like(means)
+        v_quats = torch.empty_like(quats)
+        v_scales = torch.empty_like(scales)
         N.call("hgsr_project3d_bwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks), width,
                height, eps2d, ptr(radii), ptr(conics), ptr(_f32(v_means2d)), ptr(_f32(v_depths)),
                ptr(_f32(v_conics)), ptr(v_means), ptr(v_quats), ptr(v_scales), N.stream(means.device))
@@ -125,9 +125,9 @@ class _Project2D(torch.autograd.Function):
         means, quats, scales, viewmats, Ks, radii, rt = ctx.saved_tensors
         width, height = ctx.cfg
         C, Ng = viewmats.shape[0], means.shape[0]
-        v_means = torch.zeros_like(means)
-        v_quats = torch.zeros_like(quats)
-        v_scales = torch.zeros_like(scales)
+        v_means = torch.empty_like(means)
+        v_quats = torch.empty_like(quats)
+        v_scales = torch.empty_like(scales)
         N.call("hgsr_project2d_bwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks), width,
                height, ptr(radii), ptr(rt), ptr(_f32(v_means2d)), ptr(_f32(v_depths)), ptr(_f32(v_rt)),
                ptr(_f32(v_normals)), ptr(v_means), ptr(v_quats), ptr(v_scales), N.stream(means.device))

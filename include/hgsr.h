@@ -52,7 +52,7 @@ int hgsr_project3d_fwd(int C, int N, const float* means, const float* quats,
                        float far_plane, float radius_clip, int32_t* radii, float* means2d,
                        float* depths, float* conics, hgsr_stream_t stream);
 
-/* vjp of the above: accumulates v_means [N,3], v_quats [N,4], v_scales [N,3]. */
+/* vjp of the above: writes (overwrites) v_means [N,3], v_quats [N,4], v_scales [N,3]. */
 int hgsr_project3d_bwd(int C, int N, const float* means, const float* quats,
                        const float* scales, const float* viewmats, const float* Ks,
                        int width, int height, float eps2d, const int32_t* radii,
@@ -71,6 +71,7 @@ int hgsr_project2d_fwd(int C, int N, const float* means, const float* quats,
                        float radius_clip, int32_t* radii, float* means2d, float* depths,
                        float* ray_transforms, float* normals, hgsr_stream_t stream);
 
+/* vjp of the above: writes (overwrites) v_means, v_quats, v_scales (v_scales[:,2] = 0). */
 int hgsr_project2d_bwd(int C, int N, const float* means, const float* quats,
                        const float* scales, const float* viewmats, const float* Ks,
                        int width, int height, const int32_t* radii,
@@ -297,15 +298,20 @@ int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
  * l_sky*mean(-(1-mask) log(1-a)) + l_ent*mean(-a log a), a = clamp(alpha, 1e-6, 1-1e-6)
  * (alpha [H,W] nullable when both l_sky and l_ent are 0).  ws (hgsr_loss_ws_bytes) holds
  * the SSIM derivative maps for hgsr_loss_bwd, which writes g_image [C,H,W] and g_alpha
- * [H,W] (nullable) from g_out[5], the upstream gradients of the five outputs (device). */
+ * [H,W] (nullable) from g_out[5], the upstream gradients of the five outputs (device).
+ * *_strides (host, nullable = contiguous CHW): element strides {channel, row, column} of
+ * image / gt, e.g. {1, 3W, 3} for the channels-last render output seen through
+ * permute(2,0,1) (render.py:81-95); g_image is written with image's strides, and its
+ * channels C..C+extra_channels-1 (trailing render channels the loss ignores, e.g. the
+ * depth of RGB+ED) are written as zero so the caller needs no slice/fill. */
 size_t hgsr_loss_ws_bytes(int C, int H, int W);
-int hgsr_loss_fwd(int C, int H, int W, const float* image, const float* gt, const float* mask,
-                  const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
+int hgsr_loss_fwd(int C, int H, int W, const float* image, const int64_t* image_strides,
+                  const float* gt, const int64_t* gt_strides, const float* mask, const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
                   float* out, void* ws, size_t ws_bytes, hgsr_stream_t stream);
-int hgsr_loss_bwd(int C, int H, int W, const float* image, const float* gt, const float* mask,
-                  const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
-                  const float* g_out, float* g_image, float* g_alpha, const void* ws, size_t ws_bytes,
-                  hgsr_stream_t stream);
+int hgsr_loss_bwd(int C, int H, int W, const float* image, const int64_t* image_strides,
+                  const float* gt, const int64_t* gt_strides, const float* mask, const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
+                  const float* g_out, float* g_image, int extra_channels, float* g_alpha,
+                  const void* ws, size_t ws_bytes, hgsr_stream_t stream);
 
 /* ---- measurement ----------------------------------------------------------
  * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):

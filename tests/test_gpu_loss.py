@@ -63,3 +63,31 @@ def test_loss_gradients(H, W, masked, alpha_terms):
     cond_close(i.grad.cpu().numpy(), gi32, gi64, "d_image")
     if a is not None:
         cond_close(a.grad.cpu().numpy(), ga32, ga64, "d_alpha")
+
+
+@pytest.mark.parametrize("extra", [0, 1])
+def test_loss_channels_last_view(extra):
+    """render_colors[0].permute(2, 0, 1) of a channels-last [H,W,3+extra] render (render.py:81-95)
+    is read in place: outputs and the RGB gradient are bit-identical to the contiguous CHW
+    call, and trailing channels (RGB+ED depth) get an exact zero gradient."""
+    from horizongs_amd.loss import fused_loss
+    H, W = 75, 131
+    gen = torch.Generator().manual_seed(31 + extra)
+    hwc = torch.rand(H, W, 3 + extra, generator=gen).to(DEV)
+    gt = torch.rand(3, H, W, generator=gen).to(DEV)
+    mask = (torch.rand(H, W, generator=gen) > 0.3).float().to(DEV)
+    alpha = torch.rand(H, W, generator=gen).to(DEV)
+    ups = torch.randn(5, generator=gen).to(DEV)
+
+    a = hwc.clone().requires_grad_(True)
+    outs = fused_loss(a.permute(2, 0, 1), gt, mask, 0.2, alpha, 0.05, 0.01)
+    sum(o * u for o, u in zip(outs, ups)).backward()
+    b = hwc[..., :3].permute(2, 0, 1).contiguous().requires_grad_(True)
+    ref = fused_loss(b, gt, mask, 0.2, alpha, 0.05, 0.01)
+    sum(o * u for o, u in zip(ref, ups)).backward()
+    for o, r in zip(outs, ref):
+        assert torch.equal(o, r)
+    assert a.grad.is_contiguous()
+    assert torch.equal(a.grad[..., :3].permute(2, 0, 1), b.grad)
+    if extra:
+        assert torch.equal(a.grad[..., 3:], torch.zeros_like(a.grad[..., 3:]))
