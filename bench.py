@@ -130,13 +130,11 @@ class Workload:
                 xyz, quats, scales, opac, cols, self.viewmats, self.Ks, W, H,
                 packed=False, backgrounds=self.bg, render_mode="RGB+ED")
         # the reference fine-stage loss head (train.py:153-178, config/base/small_scene/fine.yaml:50-57):
-        # 0.8 L1 + 0.2 D-SSIM + 0.05 sky opacity + 0.05 opacity entropy (fused HIP loss) + 0.01 scale reg
+        # 0.8 L1 + 0.2 D-SSIM + 0.01 scale reg + 0.05 sky opacity + 0.05 opacity entropy, all in the fused HIP loss
         # C == 1: reshape/permute are views, so the loss reads the channels-last render in place and
         # its backward writes the full RGB+ED gradient (zero ED channel) with no slice/copy/fill glue
         img = out.reshape(H, W, -1).permute(2, 0, 1)
-        loss = fused_loss(img, self.target, None, 0.2, alpha.reshape(H, W), 0.05, 0.05)[0]
-        s0, s1, s2 = scales.unbind(1)  # == scales.prod(dim=1), without prod's zero-count backward
-        loss = loss + 0.01 * (s0 * s1 * s2).mean()
+        loss = fused_loss(img, self.target, None, 0.2, alpha.reshape(H, W), 0.05, 0.05, scales, 0.01)[0]
         if self.args.gs == "2d":
             n = normals[0].permute(2, 0, 1)
             nd = (nfd * alpha.detach())[0].permute(2, 0, 1)

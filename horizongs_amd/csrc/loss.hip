@@ -1,18 +1,21 @@
-// K15: fused training loss: masked L1 + D-SSIM and the alpha
-// regularisers of reference train.py:153-178 with utils/loss_utils.py:17-60
+// K15: fused training loss: masked L1 + D-SSIM, the scale regulariser
+// and the alpha regularisers of reference train.py:153-178 with utils/loss_utils.py:17-60
 // (Gaussian window 11, sigma 1.5, zero padding, C1 = 0.01^2, C2 = 0.03^2).
 //
 //   x = image * mask, y = gt * mask (mask [H,W] broadcast over channels, nullable)
-//   loss = (1 - l) * mean|x - y| + l * (1 - mean SSIM(x, y))
+//   loss = (1 - l) * mean|x - y| + l * (1 - mean SSIM(x, y)) + l_dreg * mean_i prod_j s_ij
 //        + l_sky * mean(-(1 - mask) log(1 - a)) + l_ent * mean(-a log a),  a = clamp(alpha, 1e-6, 1 - 1e-6)
 //
-// CDNA4 mapping: one 256-lane workgroup per 16x16 pixel tile; the tile plus its 5-pixel
-// halo is staged in LDS and the 11x11 window is applied separably (horizontal pass into
-// LDS, vertical pass in registers) for the five moments.  The forward also writes the
-// three per-pixel derivative maps the SSIM gradient needs,
+// CDNA4 mapping: one 256-lane workgroup per 16x16 pixel tile, all channels of a group of
+// NC (3 for RGB) at once.  The tile plus its 5-pixel halo is staged in LDS, the 11-tap
+// window is applied separably: a horizontal pass producing two adjacent columns per lane
+// (12 LDS reads for 2 outputs) and a vertical pass producing four rows per lane from a
+// 14-row register window, i.e. ~4x fewer LDS reads than one output per lane.  The forward
+// writes the three per-pixel derivative maps the SSIM gradient needs,
 //   dS/dx(q) = G*(S_mu1 - 2 mu1 S_s11 - mu2 S_s12)(q) + 2 x(q) G*S_s11(q) + y(q) G*S_s12(q),
-// and the backward pass filters them the same way; everything is HBM-streaming, with
-// per-tile partial sums reduced in a fixed order (deterministic).
+// and the backward filters them the same way.  The scale regulariser rides along: tile
+// block b also reduces Gaussians [b*per, (b+1)*per).  Per-tile partial sums are reduced
+// in a fixed order in f64 (deterministic).
 #include "common.h"
 
 namespace hgsr {
@@ -20,10 +23,16 @@ namespace hgsr {
 constexpr int kLT = 16;            // tile edge
 constexpr int kLR = 5;             // window radius
 constexpr int kLH = kLT + 2 * kLR;  // 26: tile + halo
+constexpr int kLP = kLH + 1;       // staged row pitch
+constexpr int kHP = 24;            // filtered row pitch: rows 2 apart land 16 banks apart
+constexpr int kLQ = 5;             // partial sums per tile: l1, ssim, sky, entropy, scale-prod
 
-struct LossWin {
-    float w[11];
-};
+// utils/loss_utils.py:20-22 window, exp(-(x - 5)^2 / (2 * 1.5^2)) normalised, rounded to
+// fp32; compile-time literals so the unrolled filters carry them as instruction constants
+// (no SGPRs).  check_window() verifies them against the f64 formula at first use.
+constexpr float kWin[11] = {0x1.0d956cp-10f, 0x1.f1fe02p-8f, 0x1.26eb18p-5f, 0x1.bff0fep-4f,
+                            0x1.b43c40p-3f,  0x1.106560p-2f, 0x1.b43c40p-3f, 0x1.bff0fep-4f,
+                            0x1.26eb18p-5f,  0x1.f1fe02p-8f, 0x1.0d956cp-10f};
 
 // a [C,H,W] image with arbitrary element strides (contiguous CHW, or the channels-last
 // [H,W,C] render output viewed through permute(2,0,1) without a copy)
@@ -33,14 +42,19 @@ struct Img {
     __device__ __forceinline__ int64_t at(int c, int y, int x) const { return c * sc + y * sy + x * sx; }
 };
 
-__device__ __forceinline__ float masked(Img img, const float* __restrict__ mask, int c, int H, int W, int yy, int xx) {
-    if (yy < 0 || yy >= H || xx < 0 || xx >= W) return 0.f;  // conv2d zero padding
-    const float v = img.p[img.at(c, yy, xx)];
-    return mask ? v * mask[(int64_t)yy * W + xx] : v;
+struct ScaleReg {  // scale regulariser operand: scaling [n, k] contiguous (nullable)
+    const float* s;
+    int64_t n;
+    int k;
+};
+
+__device__ __forceinline__ float row_prod(const float* __restrict__ s, int k) {
+    float p = s[0];
+    for (int j = 1; j < k; ++j) p *= s[j];
+    return p;
 }
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
-    // wave sum via DPP/shuffles, then 4 waves through LDS
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
     const int wave = threadIdx.x >> 6;
     __syncthreads();
@@ -49,220 +63,400 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
     return red[0] + red[1] + red[2] + red[3];
 }
 
-// forward: SSIM map statistics + derivative maps, L1, alpha terms; per-tile partials
-// partial layout per tile: [sum |x-y|, sum S, sum sky, sum entropy]
+// Per-thread share of the 26x26 staged window: positions e = tid + 256 i, i < 3.
+constexpr int kLS = (kLH * kLH + 255) / 256;  // 3
+
+struct StagePos {
+    int lds[kLS];        // r * kLP + q, or -1 past the window
+    bool in[kLS];        // inside the image (else zero padding)
+    unsigned pix[kLS];   // y * W + x
+    unsigned oi[kLS];    // element offsets in image / gt at channel 0 (32-bit: uniform base + lane offset)
+    unsigned og[kLS];
+};
+
+__device__ __forceinline__ StagePos stage_positions(int H, int W, int x0, int y0, const Img& a, const Img& b) {
+    StagePos sp;
+#pragma unroll
+    for (int i = 0; i < kLS; ++i) {
+        const int e = threadIdx.x + 256 * i;
+        const int r = e / kLH, q = e - r * kLH;
+        const int yy = y0 + r, xx = x0 + q;
+        const bool in = e < kLH * kLH && yy >= 0 && yy < H && xx >= 0 && xx < W;
+        sp.lds[i] = e < kLH * kLH ? r * kLP + q : -1;
+        sp.in[i] = in;
+        sp.pix[i] = in ? (unsigned)(yy * W + xx) : 0u;
+        sp.oi[i] = in ? (unsigned)a.at(0, yy, xx) : 0u;
+        sp.og[i] = in ? (unsigned)b.at(0, yy, xx) : 0u;
+    }
+    return sp;
+}
+
+// keeps the compiler from hoisting every LDS read of a filter pass to the top (which
+// costs ~60 live VGPRs and halves occupancy); LDS latency is hidden by the other waves
+__device__ __forceinline__ void sched_fence() { asm volatile("" ::: "memory"); }
+
+struct LossFwdSmem {
+    float x[kLH * kLP];
+    float y[kLH * kLP];
+    float h[5][kLH * kHP];  // horizontally filtered mu1, mu2, x^2, y^2, xy
+    float red[4];
+};
+
+// SSIM at one pixel from the five filtered moments, with the derivative-map terms
+struct SsimPix {
+    float S, dm0, ds11, ds12;
+};
+
+__device__ __forceinline__ SsimPix ssim_pix(float mu1, float mu2, float ex2, float ey2, float exy) {
+    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
+    const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu12 = mu1 * mu2;
+    const float s11 = ex2 - mu1_sq, s22 = ey2 - mu2_sq, s12 = exy - mu12;
+    const float A1 = 2.f * mu12 + C1, A2 = 2.f * s12 + C2;
+    const float B1 = mu1_sq + mu2_sq + C1, B2 = s11 + s22 + C2;
+    const float rB1 = __builtin_amdgcn_rcpf(B1), rB2 = __builtin_amdgcn_rcpf(B2);
+    const float inv = rB1 * rB2;
+    SsimPix o;
+    o.S = A1 * A2 * inv;
+    const float dmu1 = 2.f * mu2 * A2 * inv - 2.f * mu1 * o.S * rB1;
+    o.ds11 = -o.S * rB2;
+    o.ds12 = 2.f * A1 * inv;
+    o.dm0 = dmu1 - 2.f * mu1 * o.ds11 - mu2 * o.ds12;
+    return o;
+}
+
+// forward: SSIM statistics + derivative maps, L1, alpha terms, scale products; per-tile
+// partials, layout [kLQ][n_tiles].  Channels are processed one at a time with the next
+// channel's window already in flight in registers (LDS-only barriers keep it in flight).
 __global__ __launch_bounds__(256) void loss_fwd_kernel(int C, int H, int W, Img img, Img gt,
                                                        const float* __restrict__ mask,
-                                                       const float* __restrict__ alpha, LossWin win,
+                                                       const float* __restrict__ alpha, ScaleReg sr,
                                                        float* __restrict__ dmaps, float* __restrict__ partials) {
-    __shared__ float s_x[kLH][kLH + 1], s_y[kLH][kLH + 1];
-    __shared__ float s_h[5][kLH][kLT + 1];
-    __shared__ float s_red[4];
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    __shared__ LossFwdSmem sm;
     const int tiles_x = (W + kLT - 1) / kLT;
     const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
     const int x0 = bx * kLT - kLR, y0 = by * kLT - kLR;
-    const int px = bx * kLT + tx, py = by * kLT + ty;
-    const bool inside = px < W && py < H;
     const int64_t HW = (int64_t)H * W;
-    float l1 = 0.f, ss = 0.f;
-    for (int c = 0; c < C; ++c) {
-        __syncthreads();
-        for (int e = threadIdx.x; e < kLH * kLH; e += 256) {
-            const int r = e / kLH, q = e - r * kLH;
-            s_x[r][q] = masked(img, mask, c, H, W, y0 + r, x0 + q);
-            s_y[r][q] = masked(gt, mask, c, H, W, y0 + r, x0 + q);
-        }
-        __syncthreads();
-        // horizontal pass: 26 rows x 16 output columns x 5 moments
-        for (int e = threadIdx.x; e < kLH * kLT; e += 256) {
-            const int r = e / kLT, q = e - r * kLT;
-            float m1 = 0.f, m2 = 0.f, a = 0.f, b = 0.f, xy = 0.f;
+    const int tid = threadIdx.x;
+    const StagePos sp = stage_positions(H, W, x0, y0, img, gt);
+    float nx[kLS], ny[kLS], mk[kLS];
+    auto fetch = [&](int c) {
+        const float* __restrict__ bi = img.p + c * img.sc;
+        const float* __restrict__ bg = gt.p + c * gt.sc;
 #pragma unroll
-            for (int k = 0; k < 11; ++k) {
-                const float xv = s_x[r][q + k], yv = s_y[r][q + k], w = win.w[k];
-                m1 += w * xv;
-                m2 += w * yv;
-                a += w * xv * xv;
-                b += w * yv * yv;
-                xy += w * xv * yv;
-            }
-            s_h[0][r][q] = m1;
-            s_h[1][r][q] = m2;
-            s_h[2][r][q] = a;
-            s_h[3][r][q] = b;
-            s_h[4][r][q] = xy;
+        for (int i = 0; i < kLS; ++i) {
+            nx[i] = sp.in[i] ? bi[sp.oi[i]] : 0.f;
+            ny[i] = sp.in[i] ? bg[sp.og[i]] : 0.f;
         }
-        __syncthreads();
-        float mu1 = 0.f, mu2 = 0.f, ex2 = 0.f, ey2 = 0.f, exy = 0.f;
+    };
+    fetch(0);
 #pragma unroll
-        for (int k = 0; k < 11; ++k) {
-            const float w = win.w[k];
-            mu1 += w * s_h[0][ty + k][tx];
-            mu2 += w * s_h[1][ty + k][tx];
-            ex2 += w * s_h[2][ty + k][tx];
-            ey2 += w * s_h[3][ty + k][tx];
-            exy += w * s_h[4][ty + k][tx];
-        }
-        if (inside) {
-            const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
-            const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu12 = mu1 * mu2;
-            const float s11 = ex2 - mu1_sq, s22 = ey2 - mu2_sq, s12 = exy - mu12;
-            const float A1 = 2.f * mu12 + C1, A2 = 2.f * s12 + C2;
-            const float B1 = mu1_sq + mu2_sq + C1, B2 = s11 + s22 + C2;
-            const float inv = 1.0f / (B1 * B2);
-            const float S = A1 * A2 * inv;
-            const float dmu1 = 2.f * mu2 * A2 * inv - 2.f * mu1 * S / B1;
-            const float ds11 = -S / B2;
-            const float ds12 = 2.f * A1 * inv;
-            const int64_t p = (int64_t)c * HW + (int64_t)py * W + px;
-            dmaps[p] = dmu1 - 2.f * mu1 * ds11 - mu2 * ds12;
-            dmaps[(int64_t)C * HW + p] = ds11;
-            dmaps[2 * (int64_t)C * HW + p] = ds12;
-            ss += S;
-            l1 += fabsf(s_x[ty + kLR][tx + kLR] - s_y[ty + kLR][tx + kLR]);
-        }
-    }
+    for (int i = 0; i < kLS; ++i) mk[i] = (sp.in[i] && mask) ? mask[sp.pix[i]] : 1.f;
+    // per-pixel alpha terms and this block's share of the scale products, issued up front
+    const int px1 = bx * kLT + (tid & 15), py1 = by * kLT + (tid >> 4);
+    const bool inside1 = px1 < W && py1 < H;
     float sky = 0.f, ent = 0.f;
-    if (alpha && inside) {
-        const int64_t p = (int64_t)py * W + px;
+    if (alpha && inside1) {
+        const int64_t p = (int64_t)py1 * W + px1;
         const float o = fminf(fmaxf(alpha[p], 1e-6f), 1.f - 1e-6f);
         const float sk = mask ? mask[p] : 1.f;
         sky = -(1.f - sk) * logf(1.f - o);
         ent = -o * logf(o);
     }
-    l1 = block_sum(l1, s_red);
-    ss = block_sum(ss, s_red);
-    sky = block_sum(sky, s_red);
-    ent = block_sum(ent, s_red);
-    if (threadIdx.x == 0) {
-        float* o = partials + (int64_t)blockIdx.x * 4;
-        o[0] = l1;
-        o[1] = ss;
-        o[2] = sky;
-        o[3] = ent;
+    float dreg = 0.f;
+    if (sr.s) {
+        const int64_t per = (sr.n + gridDim.x - 1) / gridDim.x;
+        const int64_t g0 = (int64_t)blockIdx.x * per, g1 = min(sr.n, g0 + per);
+        for (int64_t g = g0 + tid; g < g1; g += 256) dreg += row_prod(sr.s + g * sr.k, sr.k);
+    }
+    float l1 = 0.f, ss = 0.f;
+    for (int c = 0; c < C; ++c) {
+        lds_barrier();  // previous channel's vertical pass is done with sm.x / sm.h
+#pragma unroll
+        for (int i = 0; i < kLS; ++i)
+            if (sp.lds[i] >= 0) {
+                sm.x[sp.lds[i]] = nx[i] * mk[i];
+                sm.y[sp.lds[i]] = ny[i] * mk[i];
+            }
+        if (c + 1 < C) fetch(c + 1);
+        lds_barrier();
+        // horizontal: (row, column pair) items, 12-wide register window
+        if (tid < kLH * (kLT / 2)) {
+            const int qp = tid & 7, r = tid >> 3;
+            // scatter form: each input sample feeds both outputs, so only the 10
+            // accumulators stay live
+            float acc[2][5] = {};
+#pragma unroll
+            for (int t = 0; t < 12; ++t) {
+                sched_fence();
+                const float xk = sm.x[r * kLP + 2 * qp + t], yk = sm.y[r * kLP + 2 * qp + t];
+                const float v[5] = {xk, yk, xk * xk, yk * yk, xk * yk};
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {
+                    if (t - o < 0 || t - o > 10) continue;
+#pragma unroll
+                    for (int m = 0; m < 5; ++m) acc[o][m] += kWin[t - o] * v[m];
+                }
+            }
+#pragma unroll
+            for (int o = 0; o < 2; ++o)
+#pragma unroll
+                for (int m = 0; m < 5; ++m) sm.h[m][r * kHP + 2 * qp + o] = acc[o][m];
+        }
+        lds_barrier();
+        // vertical: (column, row pair) items, 12-row register window per moment
+        if (tid < kLT * (kLT / 2)) {
+            const int tx = tid & 15, pr = tid >> 4;
+            float acc[5][2] = {};
+#pragma unroll
+            for (int t = 0; t < 12; ++t) {
+                sched_fence();
+#pragma unroll
+                for (int m = 0; m < 5; ++m) {
+                    const float v = sm.h[m][(2 * pr + t) * kHP + tx];
+                    if (t <= 10) acc[m][0] += kWin[t] * v;
+                    if (t >= 1) acc[m][1] += kWin[t - 1] * v;
+                }
+            }
+            const int px = bx * kLT + tx;
+#pragma unroll
+            for (int o = 0; o < 2; ++o) {
+                const int ty = 2 * pr + o, py = by * kLT + ty;
+                if (px >= W || py >= H) continue;
+                const SsimPix sp2 = ssim_pix(acc[0][o], acc[1][o], acc[2][o], acc[3][o], acc[4][o]);
+                const int64_t p = (int64_t)c * HW + (int64_t)py * W + px;
+                dmaps[p] = sp2.dm0;
+                dmaps[(int64_t)C * HW + p] = sp2.ds11;
+                dmaps[2 * (int64_t)C * HW + p] = sp2.ds12;
+                ss += sp2.S;
+                const int li = (ty + kLR) * kLP + tx + kLR;
+                l1 += fabsf(sm.x[li] - sm.y[li]);
+            }
+        }
+    }
+    l1 = block_sum(l1, sm.red);
+    ss = block_sum(ss, sm.red);
+    sky = block_sum(sky, sm.red);
+    ent = block_sum(ent, sm.red);
+    dreg = block_sum(dreg, sm.red);
+    if (tid == 0) {
+        const int64_t nt = gridDim.x;
+        partials[blockIdx.x] = l1;
+        partials[nt + blockIdx.x] = ss;
+        partials[2 * nt + blockIdx.x] = sky;
+        partials[3 * nt + blockIdx.x] = ent;
+        partials[4 * nt + blockIdx.x] = dreg;
     }
 }
 
-// fixed-order f64 reduction of the tile partials -> [loss, l1, ssim, sky, entropy]
-__global__ __launch_bounds__(256) void loss_reduce_kernel(int n_tiles, int C, int64_t HW, float lam_dssim,
-                                                          float lam_sky, float lam_ent,
-                                                          const float* __restrict__ partials, float* __restrict__ out) {
-    __shared__ double s[4][256];
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
+// fixed-order f64 reduction of the tile partials -> [loss, l1, ssim, sky, entropy, scale_reg]
+__global__ __launch_bounds__(256) void loss_reduce_kernel(int n_tiles, int C, int64_t HW, int64_t n_sc,
+                                                          float lam_dssim, float lam_sky, float lam_ent,
+                                                          float lam_dreg, const float* __restrict__ partials,
+                                                          float* __restrict__ out) {
+    __shared__ double s[kLQ][256];
+    double a[kLQ] = {0.0, 0.0, 0.0, 0.0, 0.0};
     for (int t = threadIdx.x; t < n_tiles; t += 256)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a[q] += partials[(int64_t)t * 4 + q];
+        for (int q = 0; q < kLQ; ++q) a[q] += partials[(int64_t)q * n_tiles + t];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) s[q][threadIdx.x] = a[q];
+    for (int q = 0; q < kLQ; ++q) s[q][threadIdx.x] = a[q];
     __syncthreads();
     for (int d = 128; d > 0; d >>= 1) {
         if (threadIdx.x < d)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) s[q][threadIdx.x] += s[q][threadIdx.x + d];
+            for (int q = 0; q < kLQ; ++q) s[q][threadIdx.x] += s[q][threadIdx.x + d];
         __syncthreads();
     }
     if (threadIdx.x == 0) {
         const double n = (double)C * (double)HW;
         const double l1 = s[0][0] / n, ssim = s[1][0] / n, sky = s[2][0] / (double)HW, ent = s[3][0] / (double)HW;
-        const double loss = (1.0 - lam_dssim) * l1 + lam_dssim * (1.0 - ssim) + lam_sky * sky + lam_ent * ent;
+        const double dreg = n_sc > 0 ? s[4][0] / (double)n_sc : 0.0;  // train.py:163-166: 0 when empty
+        const double loss =
+            (1.0 - lam_dssim) * l1 + lam_dssim * (1.0 - ssim) + lam_dreg * dreg + lam_sky * sky + lam_ent * ent;
         out[0] = (float)loss;
         out[1] = (float)l1;
         out[2] = (float)ssim;
         out[3] = (float)sky;
         out[4] = (float)ent;
+        out[5] = (float)dreg;
     }
 }
 
-// backward: d loss / d image (and d alpha), scaled by the upstream scalar gradient
+struct LossBwdSmem {
+    float m[3][kLH * kLP];  // staged derivative maps
+    float h[3][kLH * kHP];  // horizontally filtered
+};
+
+struct LossCoef {
+    float l1, ss, sky, ent, dreg;
+};
+
+__device__ __forceinline__ LossCoef loss_coef(const float* __restrict__ g_out, int C, int64_t HW, int64_t n_sc,
+                                              float lam_dssim, float lam_sky, float lam_ent, float lam_dreg) {
+    // upstream gradients of [loss, l1, ssim, sky, entropy, scale_reg] folded into per-term factors
+    const float g0 = g_out[0], g1 = g_out[1], g2 = g_out[2], g3 = g_out[3], g4 = g_out[4], g5 = g_out[5];
+    const float n = (float)C * (float)HW;
+    LossCoef k;
+    k.l1 = (g0 * (1.f - lam_dssim) + g1) / n;
+    k.ss = (g2 - g0 * lam_dssim) / n;
+    k.sky = (g0 * lam_sky + g3) / (float)HW;
+    k.ent = (g0 * lam_ent + g4) / (float)HW;
+    k.dreg = n_sc > 0 ? (g0 * lam_dreg + g5) / (float)n_sc : 0.f;
+    return k;
+}
+
+// backward: d loss / d image (and d alpha, d scaling); same channel pipeline as the forward
 __global__ __launch_bounds__(256) void loss_bwd_kernel(int C, int H, int W, Img img, Img gt,
                                                        const float* __restrict__ mask,
-                                                       const float* __restrict__ alpha, LossWin win, float lam_dssim,
-                                                       float lam_sky, float lam_ent,
+                                                       const float* __restrict__ alpha, ScaleReg sr,
+                                                       float lam_dssim, float lam_sky, float lam_ent, float lam_dreg,
                                                        const float* __restrict__ dmaps,
                                                        const float* __restrict__ g_out, float* __restrict__ g_img,
-                                                       int extra_ch, float* __restrict__ g_alpha) {
-    __shared__ float s_m[3][kLH][kLH + 1];
-    __shared__ float s_h[3][kLH][kLT + 1];
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+                                                       int extra_ch, float* __restrict__ g_alpha,
+                                                       float* __restrict__ g_scaling) {
+    __shared__ LossBwdSmem sm;
+    const int tid = threadIdx.x;
     const int tiles_x = (W + kLT - 1) / kLT;
     const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
     const int x0 = bx * kLT - kLR, y0 = by * kLT - kLR;
-    const int px = bx * kLT + tx, py = by * kLT + ty;
-    const bool inside = px < W && py < H;
     const int64_t HW = (int64_t)H * W;
-    // upstream gradients of [loss, l1, ssim, sky, entropy] folded into per-term coefficients
-    const float g0 = g_out[0], g1 = g_out[1], g2 = g_out[2], g3 = g_out[3], g4 = g_out[4];
-    const float n = (float)C * (float)HW;
-    const float k_l1 = (g0 * (1.f - lam_dssim) + g1) / n, k_ss = (g2 - g0 * lam_dssim) / n;
-    const float k_sky = (g0 * lam_sky + g3) / (float)HW, k_ent = (g0 * lam_ent + g4) / (float)HW;
-    const int64_t pp = (int64_t)py * W + px;
-    const float mk = (mask && inside) ? mask[pp] : 1.f;
-    for (int c = 0; c < C; ++c) {
-        __syncthreads();
-        for (int e = threadIdx.x; e < kLH * kLH; e += 256) {
-            const int r = e / kLH, q = e - r * kLH;
-            const int yy = y0 + r, xx = x0 + q;
-            const bool in = yy >= 0 && yy < H && xx >= 0 && xx < W;
-            const int64_t p = (int64_t)c * HW + (int64_t)yy * W + xx;
+    const StagePos sp = stage_positions(H, W, x0, y0, img, gt);
+    // vertical-pass pixels of this lane: column tx, rows 2 pr + {0, 1}
+    const int tx = tid & 15, pr = (tid >> 4) & 7;
+    const bool vlane = tid < kLT * (kLT / 2);
+    const int vx = bx * kLT + tx;
+    bool vin[2];
+    float vmk[2];
 #pragma unroll
-            for (int m = 0; m < 3; ++m) s_m[m][r][q] = in ? dmaps[(int64_t)m * C * HW + p] : 0.f;
-        }
-        __syncthreads();
-        for (int e = threadIdx.x; e < kLH * kLT; e += 256) {
-            const int r = e / kLT, q = e - r * kLT;
-            float v[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < 11; ++k)
-#pragma unroll
-                for (int m = 0; m < 3; ++m) v[m] += win.w[k] * s_m[m][r][q + k];
-#pragma unroll
-            for (int m = 0; m < 3; ++m) s_h[m][r][q] = v[m];
-        }
-        __syncthreads();
-        if (!inside) continue;
-        float ga = 0.f, gb = 0.f, gc = 0.f;
-#pragma unroll
-        for (int k = 0; k < 11; ++k) {
-            const float w = win.w[k];
-            ga += w * s_h[0][ty + k][tx];
-            gb += w * s_h[1][ty + k][tx];
-            gc += w * s_h[2][ty + k][tx];
-        }
-        const float x = img.p[img.at(c, py, px)] * mk, y = gt.p[gt.at(c, py, px)] * mk;
-        const float d = x - y;
-        const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-        const float gx = k_l1 * sgn + k_ss * (ga + 2.f * x * gb + y * gc);
-        g_img[img.at(c, py, px)] = gx * mk;
+    for (int o = 0; o < 2; ++o) {
+        const int vy = by * kLT + 2 * pr + o;
+        vin[o] = vlane && vx < W && vy < H;
+        vmk[o] = (vin[o] && mask) ? mask[(int64_t)vy * W + vx] : 1.f;
     }
-    // trailing image channels the loss does not read (e.g. the ED channel of RGB+ED)
-    if (inside)
-        for (int c = C; c < C + extra_ch; ++c) g_img[img.at(c, py, px)] = 0.f;
-    if (g_alpha && inside) {
-        float ga = 0.f;
-        if (alpha) {
-            const float a = alpha[pp];
-            const bool pass = a >= 1e-6f && a <= 1.f - 1e-6f;  // clamp passes the gradient inside
-            const float o = fminf(fmaxf(a, 1e-6f), 1.f - 1e-6f);
-            const float sk = mask ? mask[pp] : 1.f;
-            const float d_sky = (1.f - sk) / (1.f - o);
-            const float d_ent = -(logf(o) + 1.f);
-            ga = pass ? k_sky * d_sky + k_ent * d_ent : 0.f;
+    unsigned voi[2], vog[2];
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+        const int vy = by * kLT + 2 * pr + o;
+        voi[o] = vin[o] ? (unsigned)img.at(0, vy, vx) : 0u;
+        vog[o] = vin[o] ? (unsigned)gt.at(0, vy, vx) : 0u;
+    }
+    float nm[3][kLS], nx[2], ny[2];
+    auto fetch = [&](int c) {
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            const float* __restrict__ bm = dmaps + ((int64_t)m * C + c) * HW;
+#pragma unroll
+            for (int i = 0; i < kLS; ++i) nm[m][i] = sp.in[i] ? bm[sp.pix[i]] : 0.f;
         }
-        g_alpha[pp] = ga;
+        const float* __restrict__ bi = img.p + c * img.sc;
+        const float* __restrict__ bg = gt.p + c * gt.sc;
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+            nx[o] = vin[o] ? bi[voi[o]] : 0.f;
+            ny[o] = vin[o] ? bg[vog[o]] : 0.f;
+        }
+    };
+    fetch(0);
+    const LossCoef k = loss_coef(g_out, C, HW, sr.n, lam_dssim, lam_sky, lam_ent, lam_dreg);
+    Img gi = img;
+    gi.p = g_img;
+    {
+        const int px = bx * kLT + (tid & 15), py = by * kLT + (tid >> 4);
+        const bool inside = px < W && py < H;
+        const int64_t pp = (int64_t)py * W + px;
+        // trailing image channels the loss does not read (e.g. the ED channel of RGB+ED)
+        if (inside)
+            for (int c = C; c < C + extra_ch; ++c) g_img[gi.at(c, py, px)] = 0.f;
+        if (g_alpha && inside) {
+            float ga = 0.f;
+            if (alpha) {
+                const float a = alpha[pp];
+                const bool pass = a >= 1e-6f && a <= 1.f - 1e-6f;  // clamp passes the gradient inside
+                const float o = fminf(fmaxf(a, 1e-6f), 1.f - 1e-6f);
+                const float sk = mask ? mask[pp] : 1.f;
+                const float d_sky = (1.f - sk) / (1.f - o);
+                const float d_ent = -(logf(o) + 1.f);
+                ga = pass ? k.sky * d_sky + k.ent * d_ent : 0.f;
+            }
+            g_alpha[pp] = ga;
+        }
+    }
+    if (g_scaling) {  // d mean_i prod_j s_ij / d s_ij = prod_{l != j} s_il / n
+        const int64_t per = (sr.n + gridDim.x - 1) / gridDim.x;
+        const int64_t g0 = (int64_t)blockIdx.x * per, g1 = min(sr.n, g0 + per);
+        for (int64_t g = g0 + tid; g < g1; g += 256) {
+            const float* s = sr.s + g * sr.k;
+            for (int j = 0; j < sr.k; ++j) {
+                float p = 1.f;
+                for (int l = 0; l < sr.k; ++l)
+                    if (l != j) p *= s[l];
+                g_scaling[g * sr.k + j] = k.dreg * p;
+            }
+        }
+    }
+    for (int c = 0; c < C; ++c) {
+        lds_barrier();
+#pragma unroll
+        for (int i = 0; i < kLS; ++i)
+            if (sp.lds[i] >= 0)
+#pragma unroll
+                for (int m = 0; m < 3; ++m) sm.m[m][sp.lds[i]] = nm[m][i];
+        const float cx[2] = {nx[0], nx[1]}, cy[2] = {ny[0], ny[1]};
+        if (c + 1 < C) fetch(c + 1);
+        lds_barrier();
+        if (tid < kLH * (kLT / 2)) {
+            const int qp = tid & 7, r = tid >> 3;
+            float acc[3][2] = {};
+#pragma unroll
+            for (int t = 0; t < 12; ++t) {
+                sched_fence();
+#pragma unroll
+                for (int m = 0; m < 3; ++m) {
+                    const float v = sm.m[m][r * kLP + 2 * qp + t];
+                    if (t <= 10) acc[m][0] += kWin[t] * v;
+                    if (t >= 1) acc[m][1] += kWin[t - 1] * v;
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < 3; ++m)
+#pragma unroll
+                for (int o = 0; o < 2; ++o) sm.h[m][r * kHP + 2 * qp + o] = acc[m][o];
+        }
+        lds_barrier();
+        if (vlane) {
+            float acc[3][2] = {};
+#pragma unroll
+            for (int t = 0; t < 12; ++t) {
+                sched_fence();
+#pragma unroll
+                for (int m = 0; m < 3; ++m) {
+                    const float v = sm.h[m][(2 * pr + t) * kHP + tx];
+                    if (t <= 10) acc[m][0] += kWin[t] * v;
+                    if (t >= 1) acc[m][1] += kWin[t - 1] * v;
+                }
+            }
+#pragma unroll
+            for (int o = 0; o < 2; ++o) {
+                if (!vin[o]) continue;
+                const float x = cx[o] * vmk[o], y = cy[o] * vmk[o];
+                const float d = x - y;
+                const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+                const float gx = k.l1 * sgn + k.ss * (acc[0][o] + 2.f * x * acc[1][o] + y * acc[2][o]);
+                g_img[c * img.sc + voi[o]] = gx * vmk[o];
+            }
+        }
     }
 }
 
-static LossWin gaussian_window() {
-    // utils/loss_utils.py:20-22: exp(-(x - 5)^2 / (2 * 1.5^2)), normalised; f64 then rounded
-    LossWin w;
+static bool check_window() {
     double g[11], s = 0.0;
     for (int k = 0; k < 11; ++k) {
         g[k] = exp(-(double)((k - 5) * (k - 5)) / (2.0 * 1.5 * 1.5));
         s += g[k];
     }
-    for (int k = 0; k < 11; ++k) w.w[k] = (float)(g[k] / s);
-    return w;
+    for (int k = 0; k < 11; ++k)
+        if ((float)(g[k] / s) != kWin[k]) return false;
+    return true;
 }
 
 }  // namespace hgsr
@@ -271,13 +465,19 @@ using namespace hgsr;
 
 static int loss_tiles(int H, int W) { return ((W + kLT - 1) / kLT) * ((H + kLT - 1) / kLT); }
 
-extern "C" size_t hgsr_loss_ws_bytes(int C, int H, int W) {
-    const size_t maps = ((size_t)3 * C * H * W * sizeof(float) + 255) & ~(size_t)255;
-    return maps + (size_t)loss_tiles(H, W) * 4 * sizeof(float);
+static size_t loss_maps_bytes(int C, int H, int W) {
+    return ((size_t)3 * C * H * W * sizeof(float) + 255) & ~(size_t)255;
 }
 
-static int check_strides(const int64_t* st, const char* what) {
+extern "C" size_t hgsr_loss_ws_bytes(int C, int H, int W) {
+    return loss_maps_bytes(C, H, W) + (size_t)loss_tiles(H, W) * kLQ * sizeof(float);
+}
+
+static int check_strides(const int64_t* st, const char* what, int C, int H, int W) {
     HGSR_REQUIRE(st == nullptr || (st[0] >= 0 && st[1] >= 0 && st[2] >= 0), "negative %s strides", what);
+    const int64_t sc = st ? st[0] : (int64_t)H * W, sy = st ? st[1] : W, sx = st ? st[2] : 1;
+    HGSR_REQUIRE((C - 1) * sc + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx < ((int64_t)1 << 31),
+                 "%s spans >= 2^31 elements", what);
     return HGSR_OK;
 }
 
@@ -286,48 +486,64 @@ static Img make_img(const float* p, const int64_t* st, int H, int W) {
     return Img{p, st[0], st[1], st[2]};
 }
 
+static int check_scale_reg(int64_t n_sc, int k_sc, const float* scaling, float lam_dreg) {
+    HGSR_REQUIRE(n_sc >= 0 && (n_sc == 0 || (k_sc >= 1 && scaling)), "bad scaling operand (n=%lld k=%d)",
+                 (long long)n_sc, k_sc);
+    (void)lam_dreg;  // an absent or empty scaling contributes 0 (train.py:163-166)
+    return HGSR_OK;
+}
+
 extern "C" int hgsr_loss_fwd(int C, int H, int W, const float* image, const int64_t* image_strides,
                              const float* gt, const int64_t* gt_strides, const float* mask,
-                             const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
+                             const float* alpha, const float* scaling, int64_t n_scaling, int k_scaling,
+                             float lambda_dssim, float lambda_sky_opa, float lambda_entropy, float lambda_dreg,
                              float* out, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
     HGSR_REQUIRE(C >= 1 && H > 0 && W > 0, "bad dims");
     HGSR_REQUIRE(image && gt && out && ws, "null pointer");
+    static const bool win_ok = check_window();
+    HGSR_REQUIRE(win_ok, "SSIM window constants disagree with utils/loss_utils.py's formula");
     HGSR_REQUIRE(ws_bytes >= hgsr_loss_ws_bytes(C, H, W), "loss workspace too small");
     HGSR_REQUIRE(alpha || (lambda_sky_opa == 0.f && lambda_entropy == 0.f), "alpha terms need alpha");
-    if (int st = check_strides(image_strides, "image")) return st;
-    if (int st = check_strides(gt_strides, "gt")) return st;
+    if (int st = check_strides(image_strides, "image", C, H, W)) return st;
+    if (int st = check_strides(gt_strides, "gt", C, H, W)) return st;
+    if (int st = check_scale_reg(n_scaling, k_scaling, scaling, lambda_dreg)) return st;
     hipStream_t s = as_stream(stream);
     float* dmaps = (float*)ws;
-    float* partials = (float*)((char*)ws + (((size_t)3 * C * H * W * sizeof(float) + 255) & ~(size_t)255));
+    float* partials = (float*)((char*)ws + loss_maps_bytes(C, H, W));
     const int nt = loss_tiles(H, W);
+    const Img im = make_img(image, image_strides, H, W), gm = make_img(gt, gt_strides, H, W);
+    const ScaleReg sr{n_scaling > 0 ? scaling : nullptr, n_scaling, k_scaling};
     {
         KernelTimer kt("loss_fwd", s);
-        hipLaunchKernelGGL(loss_fwd_kernel, dim3(nt), dim3(256), 0, s, C, H, W, make_img(image, image_strides, H, W),
-                           make_img(gt, gt_strides, H, W), mask, alpha,
-                           gaussian_window(), dmaps, partials);
+        hipLaunchKernelGGL(loss_fwd_kernel, dim3(nt), dim3(256), 0, s, C, H, W, im, gm, mask, alpha, sr, dmaps,
+                           partials);
     }
     if (int st = check_launch("loss_fwd")) return st;
-    hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, s, nt, C, (int64_t)H * W, lambda_dssim,
-                       lambda_sky_opa, lambda_entropy, partials, out);
+    hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, s, nt, C, (int64_t)H * W, n_scaling,
+                       lambda_dssim, lambda_sky_opa, lambda_entropy, lambda_dreg, partials, out);
     return check_launch("loss_reduce");
 }
 
 extern "C" int hgsr_loss_bwd(int C, int H, int W, const float* image, const int64_t* image_strides,
                              const float* gt, const int64_t* gt_strides, const float* mask,
-                             const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
+                             const float* alpha, const float* scaling, int64_t n_scaling, int k_scaling,
+                             float lambda_dssim, float lambda_sky_opa, float lambda_entropy, float lambda_dreg,
                              const float* g_out, float* g_image, int extra_channels, float* g_alpha,
-                             const void* ws, size_t ws_bytes, hgsr_stream_t stream) {
+                             float* g_scaling, const void* ws, size_t ws_bytes, hgsr_stream_t stream) {
     HGSR_REQUIRE(C >= 1 && H > 0 && W > 0, "bad dims");
     HGSR_REQUIRE(image && gt && g_out && g_image && ws, "null pointer");
     HGSR_REQUIRE(ws_bytes >= hgsr_loss_ws_bytes(C, H, W), "loss workspace too small");
-    if (int st = check_strides(image_strides, "image")) return st;
-    if (int st = check_strides(gt_strides, "gt")) return st;
+    if (int st = check_strides(image_strides, "image", C, H, W)) return st;
+    if (int st = check_strides(gt_strides, "gt", C, H, W)) return st;
+    if (int st = check_scale_reg(n_scaling, k_scaling, scaling, lambda_dreg)) return st;
     HGSR_REQUIRE(extra_channels >= 0, "negative extra_channels");
     hipStream_t s = as_stream(stream);
+    const Img im = make_img(image, image_strides, H, W), gm = make_img(gt, gt_strides, H, W);
+    const ScaleReg sr{n_scaling > 0 ? scaling : nullptr, n_scaling, k_scaling};
+    float* gsc = n_scaling > 0 ? g_scaling : nullptr;
     KernelTimer kt("loss_bwd", s);
-    hipLaunchKernelGGL(loss_bwd_kernel, dim3(loss_tiles(H, W)), dim3(256), 0, s, C, H, W,
-                       make_img(image, image_strides, H, W), make_img(gt, gt_strides, H, W), mask, alpha,
-                       gaussian_window(), lambda_dssim, lambda_sky_opa, lambda_entropy, (const float*)ws, g_out,
-                       g_image, extra_channels, g_alpha);
+    hipLaunchKernelGGL(loss_bwd_kernel, dim3(loss_tiles(H, W)), dim3(256), 0, s, C, H, W, im, gm, mask, alpha, sr,
+                       lambda_dssim, lambda_sky_opa, lambda_entropy, lambda_dreg, (const float*)ws,
+                       g_out, g_image, extra_channels, g_alpha, gsc);
     return check_launch("loss_bwd");
 }

@@ -292,13 +292,16 @@ int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
                     size_t ws_bytes, hgsr_stream_t stream);
 
 /* ---- K15: fused training loss ---------------------------
- * replaces reference train.py:153-178 with utils/loss_utils.py:17-60: x = image*mask,
- * y = gt*mask (image, gt [C,H,W]; mask [H,W] nullable); out[5] (device) =
- * {loss, l1, ssim, sky, entropy} with loss = (1-l)*mean|x-y| + l*(1-mean SSIM(x,y)) +
- * l_sky*mean(-(1-mask) log(1-a)) + l_ent*mean(-a log a), a = clamp(alpha, 1e-6, 1-1e-6)
- * (alpha [H,W] nullable when both l_sky and l_ent are 0).  ws (hgsr_loss_ws_bytes) holds
- * the SSIM derivative maps for hgsr_loss_bwd, which writes g_image [C,H,W] and g_alpha
- * [H,W] (nullable) from g_out[5], the upstream gradients of the five outputs (device).
+ * replaces the loss head of reference train.py:153-178 with utils/loss_utils.py:17-60:
+ * x = image*mask, y = gt*mask (image, gt [C,H,W]; mask [H,W] nullable); out[6] (device) =
+ * {loss, l1, ssim, sky, entropy, scale_reg} with
+ *   loss = (1-l)*mean|x-y| + l*(1-mean SSIM(x,y)) + l_dreg*mean_i prod_j scaling[i,j]
+ *        + l_sky*mean(-(1-mask) log(1-a)) + l_ent*mean(-a log a),  a = clamp(alpha, 1e-6, 1-1e-6)
+ * (alpha [H,W] nullable when both l_sky and l_ent are 0; scaling [n_scaling, k_scaling]
+ * contiguous, nullable, scale_reg = 0 when n_scaling = 0 as train.py:163-166).
+ * ws (hgsr_loss_ws_bytes) holds the SSIM derivative maps for hgsr_loss_bwd, which writes
+ * g_image, g_alpha [H,W] (nullable) and g_scaling [n_scaling, k_scaling] (nullable) from
+ * g_out[6], the upstream gradients of the six outputs (device).
  * *_strides (host, nullable = contiguous CHW): element strides {channel, row, column} of
  * image / gt, e.g. {1, 3W, 3} for the channels-last render output seen through
  * permute(2,0,1) (render.py:81-95); g_image is written with image's strides, and its
@@ -306,11 +309,15 @@ int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
  * depth of RGB+ED) are written as zero so the caller needs no slice/fill. */
 size_t hgsr_loss_ws_bytes(int C, int H, int W);
 int hgsr_loss_fwd(int C, int H, int W, const float* image, const int64_t* image_strides,
-                  const float* gt, const int64_t* gt_strides, const float* mask, const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
-                  float* out, void* ws, size_t ws_bytes, hgsr_stream_t stream);
+                  const float* gt, const int64_t* gt_strides, const float* mask, const float* alpha,
+                  const float* scaling, int64_t n_scaling, int k_scaling, float lambda_dssim,
+                  float lambda_sky_opa, float lambda_entropy, float lambda_dreg, float* out, void* ws,
+                  size_t ws_bytes, hgsr_stream_t stream);
 int hgsr_loss_bwd(int C, int H, int W, const float* image, const int64_t* image_strides,
-                  const float* gt, const int64_t* gt_strides, const float* mask, const float* alpha, float lambda_dssim, float lambda_sky_opa, float lambda_entropy,
-                  const float* g_out, float* g_image, int extra_channels, float* g_alpha,
+                  const float* gt, const int64_t* gt_strides, const float* mask, const float* alpha,
+                  const float* scaling, int64_t n_scaling, int k_scaling, float lambda_dssim,
+                  float lambda_sky_opa, float lambda_entropy, float lambda_dreg, const float* g_out,
+                  float* g_image, int extra_channels, float* g_alpha, float* g_scaling,
                   const void* ws, size_t ws_bytes, hgsr_stream_t stream);
 
 /* ---- measurement ----------------------------------------------------------

@@ -2,7 +2,7 @@
 
 Only tests/ may import this module.  Follows reference utils/loss_utils.py:17-60 (l1_loss,
 gaussian/create_window, _ssim with conv2d, zero padding, C1 = 0.01^2, C2 = 0.03^2) and the
-alpha regularisers of train.py:169-178, in torch ops so autograd gives the reference
+scale / alpha regularisers of train.py:162-178, in torch ops so autograd gives the reference
 gradients.  Pinned by tests/golden/losses.npz (l1 and ssim of the reference module itself).
 """
 from __future__ import annotations
@@ -34,13 +34,19 @@ def ssim(img1, img2):
     return m.mean()
 
 
-def loss(image, gt, mask=None, lambda_dssim=0.2, alpha=None, lambda_sky=0.0, lambda_ent=0.0):
+def loss(image, gt, mask=None, lambda_dssim=0.2, alpha=None, lambda_sky=0.0, lambda_ent=0.0, scaling=None,
+         lambda_dreg=0.0):
+    """train.py:153-178 (the normal term excluded): returns (loss, l1, ssim, sky, entropy, scale_reg)."""
     if mask is not None:
         image = image * mask
         gt = gt * mask
     l1 = (image - gt).abs().mean()
     s = ssim(image, gt)
     total = (1 - lambda_dssim) * l1 + lambda_dssim * (1 - s)
+    dreg = torch.zeros((), dtype=image.dtype)
+    if scaling is not None and scaling.shape[0] > 0:  # train.py:163-167
+        dreg = scaling.prod(dim=1).mean()
+        total = total + lambda_dreg * dreg
     sky = ent = torch.zeros((), dtype=image.dtype)
     if alpha is not None:
         o = alpha.clamp(1e-6, 1 - 1e-6)
@@ -48,4 +54,4 @@ def loss(image, gt, mask=None, lambda_dssim=0.2, alpha=None, lambda_sky=0.0, lam
         sky = (-(1 - skym) * torch.log(1 - o)).mean()
         ent = -(o * torch.log(o)).mean()
         total = total + lambda_sky * sky + lambda_ent * ent
-    return total, l1, s, sky, ent
+    return total, l1, s, sky, ent, dreg

@@ -26,43 +26,53 @@ def test_loss_matches_reference_golden():
     from horizongs_amd.loss import fused_loss
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "losses.npz"))
     img, gt = torch.from_numpy(g["img"]).to(DEV), torch.from_numpy(g["gt"]).to(DEV)
-    loss, l1, s, _, _ = fused_loss(img, gt, lambda_dssim=0.2)
+    loss, l1, s, _, _, _ = fused_loss(img, gt, lambda_dssim=0.2)
     assert abs(float(l1) - float(g["l1"])) <= 1e-6
     assert abs(float(s) - float(g["ssim"])) <= 1e-5
     assert abs(float(loss) - (0.8 * float(g["l1"]) + 0.2 * (1 - float(g["ssim"])))) <= 1e-5
 
 
-@pytest.mark.parametrize("H,W,masked,alpha_terms", [(64, 80, False, False), (67, 93, True, True),
-                                                    (1080 // 4, 1920 // 4, True, True)])
-def test_loss_gradients(H, W, masked, alpha_terms):
+@pytest.mark.parametrize("H,W,masked,alpha_terms,n_sc", [(64, 80, False, False, 0), (67, 93, True, True, 1000),
+                                                         (1080 // 4, 1920 // 4, True, True, 300007),
+                                                         (40, 50, False, True, 0)])
+def test_loss_gradients(H, W, masked, alpha_terms, n_sc):
+    """n_sc = 0 with a scaling tensor is the reference's empty-model branch (train.py:163-166)."""
     from horizongs_amd.loss import fused_loss
     gen = torch.Generator().manual_seed(H * 7 + W)
     img = torch.rand(3, H, W, generator=gen)
     gt = (img + 0.1 * torch.randn(3, H, W, generator=gen)).clamp(0, 1)
     mask = (torch.rand(H, W, generator=gen) > 0.2).float() if masked else None
     alpha = torch.rand(H, W, generator=gen) if alpha_terms else None
-    lam = dict(lambda_dssim=0.2, lambda_sky=0.05 if alpha_terms else 0.0, lambda_ent=0.01 if alpha_terms else 0.0)
-    ups = torch.randn(5, generator=gen)
+    scaling = (0.02 * torch.rand(n_sc, 3, generator=gen)) if (n_sc or alpha_terms) else None
+    lam = dict(lambda_dssim=0.2, lambda_sky=0.05 if alpha_terms else 0.0, lambda_ent=0.01 if alpha_terms else 0.0,
+               lambda_dreg=0.01 if scaling is not None else 0.0)
+    ups = torch.randn(6, generator=gen)
 
     def ref(dtype):
         i = img.to(dtype).clone().requires_grad_(True)
         a = alpha.to(dtype).clone().requires_grad_(True) if alpha is not None else None
-        outs = L.loss(i, gt.to(dtype), None if mask is None else mask.to(dtype), alpha=a, **lam)
+        sc = scaling.to(dtype).clone().requires_grad_(True) if scaling is not None else None
+        outs = L.loss(i, gt.to(dtype), None if mask is None else mask.to(dtype), alpha=a, scaling=sc, **lam)
         sum(o * u for o, u in zip(outs, ups.to(dtype))).backward()
-        return [o.detach().numpy() for o in outs], i.grad.numpy(), (a.grad.numpy() if a is not None else None)
+        g_sc = sc.grad.numpy() if (sc is not None and sc.grad is not None) else None
+        return [o.detach().numpy() for o in outs], i.grad.numpy(), (a.grad.numpy() if a is not None else None), g_sc
 
-    o32, gi32, ga32 = ref(torch.float32)
-    o64, gi64, ga64 = ref(torch.float64)
+    o32, gi32, ga32, gs32 = ref(torch.float32)
+    o64, gi64, ga64, gs64 = ref(torch.float64)
     i = img.to(DEV).clone().requires_grad_(True)
     a = alpha.to(DEV).clone().requires_grad_(True) if alpha is not None else None
+    sc = scaling.to(DEV).clone().requires_grad_(True) if scaling is not None else None
     outs = fused_loss(i, gt.to(DEV), None if mask is None else mask.to(DEV), lam["lambda_dssim"], a,
-                      lam["lambda_sky"], lam["lambda_ent"])
-    for o, r32, r64, name in zip(outs, o32, o64, ("loss", "l1", "ssim", "sky", "entropy")):
+                      lam["lambda_sky"], lam["lambda_ent"], sc, lam["lambda_dreg"])
+    assert len(outs) == 6
+    for o, r32, r64, name in zip(outs, o32, o64, ("loss", "l1", "ssim", "sky", "entropy", "scale_reg")):
         cond_close(o.detach().cpu().numpy(), r32, r64, name)
     sum(o * u for o, u in zip(outs, ups.to(DEV))).backward()
     cond_close(i.grad.cpu().numpy(), gi32, gi64, "d_image")
     if a is not None:
         cond_close(a.grad.cpu().numpy(), ga32, ga64, "d_alpha")
+    if gs32 is not None:
+        cond_close(sc.grad.cpu().numpy(), gs32, gs64, "d_scaling")
 
 
 @pytest.mark.parametrize("extra", [0, 1])
@@ -77,7 +87,7 @@ def test_loss_channels_last_view(extra):
     gt = torch.rand(3, H, W, generator=gen).to(DEV)
     mask = (torch.rand(H, W, generator=gen) > 0.3).float().to(DEV)
     alpha = torch.rand(H, W, generator=gen).to(DEV)
-    ups = torch.randn(5, generator=gen).to(DEV)
+    ups = torch.randn(6, generator=gen).to(DEV)
 
     a = hwc.clone().requires_grad_(True)
     outs = fused_loss(a.permute(2, 0, 1), gt, mask, 0.2, alpha, 0.05, 0.01)
