@@ -24,7 +24,7 @@ namespace hgsr {
 
 constexpr int kFwdBatch = 256;
 constexpr int kBwdBatch = 128;
-constexpr int kRec3 = 16;  // floats per accumulator row: xy(2) conic(3) opac(1) color(D<=4) absxy(2)
+constexpr int kRec3 = 16;  // floats per accumulator row: sigma moments(5) opac(1) color(D<=4) absxy(2)
 
 struct TileCtx {
     int cam, tile, i, j;
@@ -55,12 +55,26 @@ __device__ __forceinline__ TileCtx tile_ctx(int C, int W, int H, int tw, int th,
     return t;
 }
 
-// 48-B raster record of one (camera, Gaussian)
+// 48-B raster record of one (camera, Gaussian).  The conic is stored pre-scaled,
+// {a', b', c'} = log2(e) * {a/2, b, c/2}, so that
+//   sigma' = a' dx^2 + c' dy^2 + b' dx dy = log2(e) * sigma,  vis = exp2(-sigma')
+// costs three products and two FMAs and feeds v_exp_f32 directly (same value as
+// gsplat's exp(-sigma) up to the last ulp; forward and backward share sigma2()).
+constexpr float kLog2e = 1.4426950408889634f;
 struct Rec3 {
-    float4 g0;  // x, y, conic a, conic b
-    float4 g1;  // conic c, opacity, footprint half-extent x, half-extent y
+    float4 g0;  // x, y, a', b'
+    float4 g1;  // c', opacity, footprint half-extent x, half-extent y
     float4 col; // colour (D <= 4, zero padded)
 };
+
+// sigma' of a record at offset (dx, dy); xx, yy, xy are returned for the backward
+__device__ __forceinline__ float sigma2(const float4 g0, const float4 g1, float dx, float dy, float& xx, float& yy,
+                                        float& xy) {
+    xx = dx * dx;
+    yy = dy * dy;
+    xy = dx * dy;
+    return __builtin_fmaf(g0.w, xy, __builtin_fmaf(g1.x, yy, g0.z * xx));
+}
 
 // Exact screen-space half-extents of the region where alpha = o*exp(-sigma) can
 // reach 1/255: 0.5 d^T Conic d <= L, L = ln(255 o); the ellipse's bounding box
@@ -88,8 +102,8 @@ __global__ __launch_bounds__(256) void pack3_kernel(int64_t n, int N, const floa
     const float o = cs.opac[c * cs.op_cstride + g];
     const float2 ext = footprint(a, b, cc, o);
     Rec3 r;
-    r.g0 = make_float4(m.x, m.y, a, b);
-    r.g1 = make_float4(cc, o, ext.x, ext.y);
+    r.g0 = make_float4(m.x, m.y, (0.5f * kLog2e) * a, kLog2e * b);
+    r.g1 = make_float4((0.5f * kLog2e) * cc, o, ext.x, ext.y);
     float col[4] = {0.f, 0.f, 0.f, 0.f};
     const float* src = cs.colors + c * cs.col_cstride + g * cs.dc;
 #pragma unroll
@@ -112,8 +126,9 @@ template <int D>
 __device__ __forceinline__ void fwd_step(const float4 g0, const float4 g1, const float4 c, int32_t idx, float px,
                                          float py, float& T, float (&acc)[4], int32_t& cur, bool& done) {
     const float dx = g0.x - px, dy = g0.y - py;
-    const float sigma = 0.5f * (g0.z * dx * dx + g1.x * dy * dy) + g0.w * dx * dy;
-    const float alpha = fminf(0.999f, g1.y * __expf(-sigma));
+    float xx, yy, xy;
+    const float sigma = sigma2(g0, g1, dx, dy, xx, yy, xy);
+    const float alpha = fminf(0.999f, g1.y * __builtin_amdgcn_exp2f(-sigma));
     const float nT = T * (1.0f - alpha);
     const bool valid = (sigma >= 0.f) & (alpha >= 1.0f / 255.0f) & !done;
     const bool keep = nT > 1e-4f;
@@ -243,9 +258,7 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     constexpr int NB = kBwdBatch;
     // double-buffered staging: batch b+1 is staged while batch b's partials are
     // combined, so each batch costs two barriers
-    __shared__ float4 s_g0[2][NB];
-    __shared__ float4 s_g1[2][NB];
-    __shared__ float4 s_col[2][NB];
+    __shared__ float4 s_rec[2][NB][3];  // interleaved {g0, g1, col}: one address per record
     __shared__ int32_t s_id[2][NB];
     __shared__ float s_part[NB * KV];  // the four waves' partials merged with LDS float atomics
     __shared__ uint8_t s_list[4][NB];
@@ -313,9 +326,9 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
         // them a whole batch old.
         if (tid < bsz) {
             s_id[cur][tid] = cid;
-            s_g0[cur][tid] = n0;
-            s_g1[cur][tid] = n1;
-            s_col[cur][tid] = n2;
+            s_rec[cur][tid][0] = n0;
+            s_rec[cur][tid][1] = n1;
+            s_rec[cur][tid][2] = n2;
         }
         if (b < nb && loader) {
             cid = nid;
@@ -341,7 +354,7 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
 #pragma unroll
         for (int k = 0; k < NB / 64; ++k) {
             const int t = k * 64 + lane;
-            const bool rel = t < bsz && t >= t0 && reaches(s_g0[cur][t], s_g1[cur][t], qx, qy);
+            const bool rel = t < bsz && t >= t0 && reaches(s_rec[cur][t][0], s_rec[cur][t][1], qx, qy);
             const uint64_t m = __ballot(rel);
             if (rel) my_list[n_mine + lanes_below(m)] = (uint8_t)t;
             n_mine += __popcll(m);
@@ -352,17 +365,23 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
             const int lst0 = my_list[lane], lst1 = my_list[64 + lane];
             for (int i = 0; i < n_mine; ++i) {
                 const int t = __builtin_amdgcn_readlane(i < 64 ? lst0 : lst1, i & 63);
-                const float4 g0 = s_g0[cur][t], g1 = s_g1[cur][t], c = s_col[cur][t];
+                const float4* rp = s_rec[cur][t];
+                const float4 g0 = rp[0], g1 = rp[1];
                 const float dx = g0.x - tc.px, dy = g0.y - tc.py;
-                const float sigma = 0.5f * (g0.z * dx * dx + g1.x * dy * dy) + g0.w * dx * dy;
-                const float vis = __expf(-sigma);
-                const float alpha = fminf(0.999f, g1.y * vis);
+                float xx, yy, xy;
+                const float sigma = sigma2(g0, g1, dx, dy, xx, yy, xy);
+                const float vis = __builtin_amdgcn_exp2f(-sigma);
+                const float araw = g1.y * vis;
+                const float alpha = fminf(0.999f, araw);
                 const bool valid = (batch_end - t <= bin_final) & (sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
                 if (!__any(valid)) continue;
+                const float4 c = rp[2];
                 const float ck[4] = {c.x, c.y, c.z, c.w};
-                const float ra = __builtin_amdgcn_rcpf(1.0f - alpha);
-                const float Tn = valid ? T * ra : T;
-                const float fac = valid ? alpha * Tn : 0.f;
+                // an invalid lane composites alpha = 0: T, fac and B come out unchanged
+                const float al = valid ? alpha : 0.f;
+                const float ra = __builtin_amdgcn_rcpf(1.0f - al);
+                const float Tn = T * ra;
+                const float fac = al * Tn;
                 float gv[KV];
                 float cv = ck[0] * vo[0];
 #pragma unroll
@@ -371,17 +390,21 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
                 for (int k = 0; k < D; ++k) gv[6 + k] = fac * vo[k];
                 const float v_alpha = Tn * cv + ra * (va_term - B);
                 B += fac * cv;
-                const bool ok2 = valid & (g1.y * vis <= 0.999f);
-                const float v_sigma = ok2 ? -g1.y * vis * v_alpha : 0.f;
-                gv[0] = v_sigma * (g0.z * dx + g0.w * dy);
-                gv[1] = v_sigma * (g0.w * dx + g1.x * dy);
-                gv[2] = 0.5f * v_sigma * dx * dx;
-                gv[3] = v_sigma * dx * dy;
-                gv[4] = 0.5f * v_sigma * dy * dy;
-                gv[5] = ok2 ? vis * v_alpha : 0.f;
-                if (ABS) {
-                    gv[6 + D] = fabsf(gv[0]);
-                    gv[7 + D] = fabsf(gv[1]);
+                // alpha clamped at 0.999 (or not composited): no gradient through it
+                const float va2 = (valid & (araw <= 0.999f)) ? v_alpha : 0.f;
+                const float v_sigma = -araw * va2;  // dL/dsigma (unscaled sigma)
+                // sigma moments; split3 turns them into v_means2d = Q (Sx, Sy) and
+                // v_conic = (Sxx / 2, Sxy, Syy / 2), Q the conic
+                gv[0] = v_sigma * dx;
+                gv[1] = v_sigma * dy;
+                gv[2] = v_sigma * xx;
+                gv[3] = v_sigma * xy;
+                gv[4] = v_sigma * yy;
+                gv[5] = vis * va2;
+                if (ABS) {  // |per-pixel v_means2d|: Q d = (2 a' dx + b' dy, b' dx + 2 c' dy) / log2(e)
+                    constexpr float kLn2 = 0.6931471805599453f;
+                    gv[6 + D] = fabsf(v_sigma * kLn2 * (2.f * g0.z * dx + g0.w * dy));
+                    gv[7 + D] = fabsf(v_sigma * kLn2 * (g0.w * dx + 2.f * g1.x * dy));
                 }
                 T = Tn;
                 float u[TR::G];
@@ -404,9 +427,12 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
 }
 
 // scatter accumulator rows into gsplat's separate gradient tensors (overwrite);
-// one lane per Gaussian, looping cameras in order (deterministic sums)
+// one lane per Gaussian, looping cameras in order (deterministic sums).  The rows
+// hold sigma moments (Sx, Sy, Sxx, Sxy, Syy) = sum_p v_sigma (dx, dy, dx^2, dx dy, dy^2):
+// v_means2d = Q (Sx, Sy) with Q the conic, v_conic = (Sxx / 2, Sxy, Syy / 2).
 template <int D, bool ABS>
 __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* __restrict__ rows,
+                                                     const float* __restrict__ conics,
                                                      float2* __restrict__ v_means2d, float* __restrict__ v_conics,
                                                      ChanDst cd, float2* __restrict__ v_abs) {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -421,10 +447,11 @@ __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* 
             const float4 v = r4[q];
             r[q * 4] = v.x; r[q * 4 + 1] = v.y; r[q * 4 + 2] = v.z; r[q * 4 + 3] = v.w;
         }
-        v_means2d[i] = make_float2(r[0], r[1]);
-        v_conics[i * 3] = r[2];
+        const float qa = conics[i * 3], qb = conics[i * 3 + 1], qc = conics[i * 3 + 2];
+        v_means2d[i] = make_float2(qa * r[0] + qb * r[1], qb * r[0] + qc * r[1]);
+        v_conics[i * 3] = 0.5f * r[2];
         v_conics[i * 3 + 1] = r[3];
-        v_conics[i * 3 + 2] = r[4];
+        v_conics[i * 3 + 2] = 0.5f * r[4];
         if (cd.op_shared) op_sum += r[5];
         else cd.opac[i] = r[5];
 #pragma unroll
@@ -599,7 +626,7 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                            flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows);        \
     }                                                                                                          \
     hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, \
-                       N, rows, reinterpret_cast<float2*>(v_means2d), v_conics, cd,                             \
+                       N, rows, conics, reinterpret_cast<float2*>(v_means2d), v_conics, cd,                     \
                        reinterpret_cast<float2*>(v_means2d_abs))
     switch (D * 2 + (abs ? 1 : 0)) {
         case 2: LAUNCH_B(1, false); break;
