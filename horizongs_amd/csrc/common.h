@@ -111,11 +111,14 @@ __device__ __forceinline__ void wave_sum_many_to_lane63(float (&v)[K]) {
 //           value i+H in lanes 32-63;
 //   step B: v_permlane16_swap pairs those registers again; each 16-lane row now
 //           holds a different value summed over the 4 rows;
-//   step C: 4 DPP row steps finish the 16-lane sums.
+//   step C: ROW_STEPS DPP row steps finish the 16-lane sums: with 4, every lane of
+//           row r holds the row total; with 3 (the last, row_ror:8, left out), lanes
+//           0 and 8 of each row hold two halves whose sum is the total, for callers
+//           that add both halves into memory anyway (LDS atomics from 2 lanes/row).
 // ~2.6 instructions per value instead of 6+ for independent full reductions.
-// Afterwards register u[j] holds, in every lane of row r, the total of value
+// Afterwards register u[j] holds, in row r, (a part of) the total of value
 // transpose_index<K>(j, r) (or -1 = padding).
-template <int K>
+template <int K, int ROW_STEPS = 4>
 struct TransposeReduce {
     static constexpr int H = (K + 1) / 2;  // registers after step A
     static constexpr int G = (H + 1) / 2;  // registers after step B
@@ -149,8 +152,12 @@ struct TransposeReduce {
         HGSR_ROW_STEP(0xB1)   // quad_perm [1,0,3,2]
         HGSR_ROW_STEP(0x4E)   // quad_perm [2,3,0,1]
         HGSR_ROW_STEP(0x124)  // row_ror:4
-        HGSR_ROW_STEP(0x128)  // row_ror:8
+        if constexpr (ROW_STEPS == 4) HGSR_ROW_STEP(0x128)  // row_ror:8
 #undef HGSR_ROW_STEP
+        // materialise the sums in every lane: otherwise the compiler sinks the last
+        // add into the caller's lane-predicated branch as mov 0 + mov_dpp + add
+#pragma unroll
+        for (int j = 0; j < G; ++j) asm volatile("" : "+v"(u[j]));
     }
 };
 

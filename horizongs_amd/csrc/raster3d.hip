@@ -260,7 +260,8 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     // combined, so each batch costs two barriers
     __shared__ float4 s_rec[2][NB][3];  // interleaved {g0, g1, col}: one address per record
     __shared__ int32_t s_id[2][NB];
-    __shared__ float s_part[NB * KV];  // the four waves' partials merged with LDS float atomics
+    constexpr int KVP = KV + 1;        // + a never-read slot that absorbs padding lanes' atomics
+    __shared__ float s_part[NB * KVP];  // the four waves' partials merged with LDS float atomics
     __shared__ uint8_t s_list[4][NB];
     __shared__ int32_t s_last[4];
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
@@ -295,7 +296,7 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
     const int32_t wave_final = wave_max_i32(bin_final);
     if (lane == 0) s_last[wave] = wave_final;
-    for (int e = tid; e < NB * KV; e += 256) s_part[e] = 0.f;
+    for (int e = tid; e < NB * KVP; e += 256) s_part[e] = 0.f;
     lds_barrier();
     const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
     // Gaussians after the block's last contributor are never reached
@@ -314,6 +315,13 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     }
     using TR = TransposeReduce<KV>;
     const int row = lane >> 4;
+    int slot[TR::G];  // accumulator slot of this row's reduced value j (KV = padding)
+#pragma unroll
+    for (int j = 0; j < TR::G; ++j) {
+        const int idx = row == 0 ? TR::index(j, 0) : row == 1 ? TR::index(j, 1) : row == 2 ? TR::index(j, 2)
+                                                                                        : TR::index(j, 3);
+        slot[j] = idx >= 0 ? idx : KV;
+    }
     uint8_t* my_list = s_list[wave];
     int prev_bsz = 0;
     for (int b = 0; b <= nb; ++b) {
@@ -339,8 +347,8 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
         if (b > 0) {
             for (int e = tid; e < prev_bsz * KV; e += 256) {
                 const int t = e / KV, k = e - t * KV;
-                const float sv = s_part[e];
-                s_part[e] = 0.f;
+                const float sv = s_part[t * KVP + k];
+                s_part[t * KVP + k] = 0.f;
                 if (sv != 0.f) atomicAdd(acc_rows + (int64_t)s_id[prv][t] * kRec3 + k, sv);
             }
         }
@@ -363,8 +371,7 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
             // the list comes back into registers once per batch; the loop reads
             // entries with readlane so no LDS index read sits on the critical path
             const int lst0 = my_list[lane], lst1 = my_list[64 + lane];
-            for (int i = 0; i < n_mine; ++i) {
-                const int t = __builtin_amdgcn_readlane(i < 64 ? lst0 : lst1, i & 63);
+            auto step = [&](const int t) {
                 const float4* rp = s_rec[cur][t];
                 const float4 g0 = rp[0], g1 = rp[1];
                 const float dx = g0.x - tc.px, dy = g0.y - tc.py;
@@ -374,7 +381,7 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
                 const float araw = g1.y * vis;
                 const float alpha = fminf(0.999f, araw);
                 const bool valid = (batch_end - t <= bin_final) & (sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
-                if (!__any(valid)) continue;
+                if (!__any(valid)) return;
                 const float4 c = rp[2];
                 const float ck[4] = {c.x, c.y, c.z, c.w};
                 // an invalid lane composites alpha = 0: T, fac and B come out unchanged
@@ -410,16 +417,15 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
                 float u[TR::G];
                 TR::run(gv, u);
                 if ((lane & 15) == 0) {
-                    float* dst = s_part + t * KV;
+                    float* dst = s_part + t * KVP;
 #pragma unroll
-                    for (int j = 0; j < TR::G; ++j) {
-                        const int i0 = TR::index(j, 0), i1 = TR::index(j, 1), i2 = TR::index(j, 2),
-                                  i3 = TR::index(j, 3);
-                        const int idx = row == 0 ? i0 : row == 1 ? i1 : row == 2 ? i2 : i3;
-                        if (idx >= 0) atomicAdd(dst + idx, u[j]);  // ds_add_f32
-                    }
+                    for (int j = 0; j < TR::G; ++j) atomicAdd(dst + slot[j], u[j]);  // ds_add_f32
                 }
-            }
+            };
+            // two loops instead of a per-step select between the list halves
+            const int n0 = min(n_mine, 64);
+            for (int i = 0; i < n0; ++i) step(__builtin_amdgcn_readlane(lst0, i));
+            for (int i = 64; i < n_mine; ++i) step(__builtin_amdgcn_readlane(lst1, i - 64));
         }
         prev_bsz = bsz;
         lds_barrier();
