@@ -121,25 +121,26 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
-// one front-to-back compositing step, branch-free (predicated per lane)
+// one front-to-back compositing step, branch-free (predicated per lane).  A lane
+// that has stopped (gsplat: the Gaussian that would push T to <= 1e-4 ends the pixel,
+// exclusively) carries T negated, so "done" costs no separate flag: its next T is
+// negative, never kept, and |T| is the final transmittance.
 template <int D>
 __device__ __forceinline__ void fwd_step(const float4 g0, const float4 g1, const float4 c, int32_t idx, float px,
-                                         float py, float& T, float (&acc)[4], int32_t& cur, bool& done) {
+                                         float py, float& T, float (&acc)[4], int32_t& cur) {
     const float dx = g0.x - px, dy = g0.y - py;
     float xx, yy, xy;
     const float sigma = sigma2(g0, g1, dx, dy, xx, yy, xy);
     const float alpha = fminf(0.999f, g1.y * __builtin_amdgcn_exp2f(-sigma));
     const float nT = T * (1.0f - alpha);
-    const bool valid = (sigma >= 0.f) & (alpha >= 1.0f / 255.0f) & !done;
-    const bool keep = nT > 1e-4f;
-    const bool ok = valid & keep;
-    done = done | (valid & !keep);  // this Gaussian would push T <= 1e-4: stop, exclusive
+    const bool valid = (sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
+    const bool ok = valid & (nT > 1e-4f);  // T < 0 (stopped) gives nT < 0
     const float vis = ok ? alpha * T : 0.f;
     acc[0] += c.x * vis;
     if (D > 1) acc[1] += c.y * vis;
     if (D > 2) acc[2] += c.z * vis;
     if (D > 3) acc[3] += c.w * vis;
-    T = ok ? nT : T;
+    T = ok ? nT : (valid ? -fabsf(T) : T);
     cur = ok ? idx : cur;
 }
 
@@ -164,10 +165,9 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
         s_g1[kFwdBatch] = make_float4(0.f, 0.f, -1e30f, -1e30f);
         s_col[kFwdBatch] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    float T = 1.0f;
+    float T = tc.inside ? 1.0f : -1.0f;  // negative = stopped
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     int32_t cur = 0;
-    bool done = !tc.inside;
     const int nb = (tc.end - tc.start + kFwdBatch - 1) / kFwdBatch;
     // two-deep software pipeline of the batch loads: ids two batches ahead,
     // records one batch ahead; indices are clamped so every load is unconditional
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     for (int b = 0; b < nb; ++b) {
         // workgroup early-out vote (double-buffered slots; LDS-only barriers so the
         // prefetch loads stay in flight)
-        const bool wave_done = __all(done);
+        const bool wave_done = __all(T < 0.f);
         if (lane == 0) s_vote[b & 1][wave] = wave_done;
         lds_barrier();
         if (s_vote[b & 1][0] & s_vote[b & 1][1] & s_vote[b & 1][2] & s_vote[b & 1][3]) break;
@@ -221,14 +221,15 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
             const float4 a0 = s_g0[t0], a1 = s_g0[t1], a2 = s_g0[t2], a3 = s_g0[t3];
             const float4 b0 = s_g1[t0], b1 = s_g1[t1], b2 = s_g1[t2], b3 = s_g1[t3];
             const float4 c0 = s_col[t0], c1 = s_col[t1], c2 = s_col[t2], c3 = s_col[t3];
-            fwd_step<D>(a0, b0, c0, bs + t0, tc.px, tc.py, T, acc, cur, done);
-            fwd_step<D>(a1, b1, c1, bs + t1, tc.px, tc.py, T, acc, cur, done);
-            fwd_step<D>(a2, b2, c2, bs + t2, tc.px, tc.py, T, acc, cur, done);
-            fwd_step<D>(a3, b3, c3, bs + t3, tc.px, tc.py, T, acc, cur, done);
-            if (__all(done)) break;
+            fwd_step<D>(a0, b0, c0, bs + t0, tc.px, tc.py, T, acc, cur);
+            fwd_step<D>(a1, b1, c1, bs + t1, tc.px, tc.py, T, acc, cur);
+            fwd_step<D>(a2, b2, c2, bs + t2, tc.px, tc.py, T, acc, cur);
+            fwd_step<D>(a3, b3, c3, bs + t3, tc.px, tc.py, T, acc, cur);
+            if (__all(T < 0.f)) break;
         }
     }
     if (tc.inside) {
+        T = fabsf(T);
         const float alpha = 1.0f - T;
         render_alphas[tc.pix] = alpha;
 #pragma unroll
