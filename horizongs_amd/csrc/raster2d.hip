@@ -185,7 +185,8 @@ __device__ __forceinline__ Hit2 hit2(const float4 r0, const float4 r1, const flo
     h.sy = cy * h.iz;
     h.g3 = h.sx * h.sx + h.sy * h.sy;
     h.g2 = 2.0f * (h.dx * h.dx + h.dy * h.dy);
-    h.sigma = 0.5f * fminf(h.g3, h.g2);
+    // log2(e) * sigma, sigma = min(g3, g2) / 2: feeds v_exp_f32 directly (vis = exp2(-sigma'))
+    h.sigma = (0.5f * 1.4426950408889634f) * fminf(h.g3, h.g2);
     return h;
 }
 
@@ -205,10 +206,10 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
-    float T = 1.0f, distort = 0.f, acc_vd = 0.f, median = 0.f;
+    // a stopped lane (exclusive stop at T <= 1e-4) carries T negated: no separate flag
+    float T = tc.inside ? 1.0f : -1.0f, distort = 0.f, acc_vd = 0.f, median = 0.f;
     float acc[4] = {0.f, 0.f, 0.f, 0.f}, nacc[3] = {0.f, 0.f, 0.f};
     int32_t cur = 0, med_idx = 0;
-    bool done = !tc.inside;
     const int nb = (tc.end - tc.start + NB - 1) / NB;
     const int32_t last = tc.end - 1;
     const bool loader = tid < NB;
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     }
     uint8_t* my_list = s_list[wave];
     for (int b = 0; b < nb; ++b) {
-        const bool wave_done = __all(done);
+        const bool wave_done = __all(T < 0.f);
         if (lane == 0) s_vote[b & 1][wave] = wave_done;
         lds_barrier();
         if (s_vote[b & 1][0] & s_vote[b & 1][1] & s_vote[b & 1][2] & s_vote[b & 1][3]) break;
@@ -249,16 +250,13 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
         }
         if (n_mine == 0) continue;
         const int lst0 = my_list[lane], lst1 = my_list[64 + lane];
-        for (int i = 0; i < n_mine; ++i) {
-            const int t = __builtin_amdgcn_readlane(i < 64 ? lst0 : lst1, i & 63);
+        auto step = [&](const int t) {
             const float4 r0 = s_r0[t], r1 = s_r1[t], r2 = s_r2[t], c = s_col[t], r4 = s_r4[t];
             const Hit2 h = hit2(r0, r1, r2, tc.px, tc.py);
-            const float alpha = fminf(0.999f, r2.w * __expf(-h.sigma));
-            const bool valid = h.ok & (h.sigma >= 0.f) & (alpha >= 1.0f / 255.0f) & !done;
+            const float alpha = fminf(0.999f, r2.w * __builtin_amdgcn_exp2f(-h.sigma));
+            const bool valid = h.ok & (h.sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
             const float nT = T * (1.0f - alpha);
-            const bool keep = nT > 1e-4f;
-            const bool ok = valid & keep;
-            done = done | (valid & !keep);  // exclusive stop at T <= 1e-4
+            const bool ok = valid & (nT > 1e-4f);  // a stopped lane's nT is negative
             const float vis = ok ? alpha * T : 0.f;
             const float ck[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
@@ -273,11 +271,22 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
             median = med ? depth : median;
             med_idx = med ? bs + t : med_idx;
             cur = ok ? bs + t : cur;
-            T = ok ? nT : T;
-            if (__all(done)) break;
+            T = ok ? nT : (valid ? -fabsf(T) : T);
+        };
+        const int n0 = min(n_mine, 64);
+        int i = 0;
+        for (; i < n0; ++i) {
+            step(__builtin_amdgcn_readlane(lst0, i));
+            if (__all(T < 0.f)) break;
         }
+        if (i == n0)
+            for (; i < n_mine; ++i) {
+                step(__builtin_amdgcn_readlane(lst1, i - 64));
+                if (__all(T < 0.f)) break;
+            }
     }
     if (tc.inside) {
+        T = fabsf(T);
         const float alpha = 1.0f - T;
         render_alphas[tc.pix] = alpha;
 #pragma unroll
@@ -315,7 +324,8 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     constexpr int NB = kBwd2Batch;
     __shared__ float4 s_r0[2][NB], s_r1[2][NB], s_r2[2][NB], s_col[2][NB], s_r4[2][NB], s_box[2][NB];
     __shared__ int32_t s_id[2][NB];
-    __shared__ float s_part[NB * KV];  // the four waves' partials merged with LDS float atomics
+    constexpr int KVP = KV + 1;        // + a never-read slot that absorbs padding lanes' atomics
+    __shared__ float s_part[NB * KVP];  // the four waves' partials merged with LDS float atomics
     __shared__ uint8_t s_list[4][NB];
     __shared__ int32_t s_last[4];
     const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects);
@@ -352,7 +362,7 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
     const int32_t wave_final = wave_max2(bin_final);
     if (lane == 0) s_last[wave] = wave_final;
-    for (int e = tid; e < NB * KV; e += 256) s_part[e] = 0.f;
+    for (int e = tid; e < NB * KVP; e += 256) s_part[e] = 0.f;
     lds_barrier();
     const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
     const int32_t end = min(tc.end, blk_final + 1);
@@ -378,6 +388,13 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     }
     using TR = TransposeReduce<KV>;
     const int row = lane >> 4;
+    int slot[TR::G];  // accumulator slot of this row's reduced value j (KV = padding)
+#pragma unroll
+    for (int j = 0; j < TR::G; ++j) {
+        const int idx = row == 0 ? TR::index(j, 0) : row == 1 ? TR::index(j, 1) : row == 2 ? TR::index(j, 2)
+                                                                                        : TR::index(j, 3);
+        slot[j] = idx >= 0 ? idx : KV;
+    }
     uint8_t* my_list = s_list[wave];
     int prev_bsz = 0;
     for (int b = 0; b <= nb; ++b) {
@@ -397,8 +414,8 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
         if (b > 0) {
             for (int e = tid; e < prev_bsz * KV; e += 256) {
                 const int t = e / KV, k = e - t * KV;
-                const float sv = s_part[e];
-                s_part[e] = 0.f;
+                const float sv = s_part[t * KVP + k];
+                s_part[t * KVP + k] = 0.f;
                 if (sv != 0.f) atomicAdd(acc_rows + (int64_t)s_id[prv][t] * kRec2 + k, sv);
             }
         }
@@ -417,13 +434,16 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
                 const float4 r0 = s_r0[cur][t], r1 = s_r1[cur][t], r2 = s_r2[cur][t], c = s_col[cur][t],
                              r4 = s_r4[cur][t];
                 const Hit2 h = hit2(r0, r1, r2, tc.px, tc.py);
-                const float vis = __expf(-h.sigma);
-                const float alpha = fminf(0.999f, r2.w * vis);
+                const float vis = __builtin_amdgcn_exp2f(-h.sigma);
+                const float araw = r2.w * vis;
+                const float alpha = fminf(0.999f, araw);
                 const bool valid = (batch_end - t <= bin_final) & h.ok & (h.sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
                 if (!__any(valid)) continue;
-                const float ra = __builtin_amdgcn_rcpf(1.0f - alpha);
-                const float Tn = valid ? T * ra : T;
-                const float fac = valid ? alpha * Tn : 0.f;
+                // an invalid lane composites alpha = 0: T, fac and Bsum come out unchanged
+                const float al = valid ? alpha : 0.f;
+                const float ra = __builtin_amdgcn_rcpf(1.0f - al);
+                const float Tn = T * ra;
+                const float fac = al * Tn;
                 const float ck[4] = {c.x, c.y, c.z, c.w};
                 float gv[KV];
                 float cv = r4.x * vn[0] + r4.y * vn[1] + r4.z * vn[2];
@@ -436,8 +456,8 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
                 for (int k = 0; k < 3; ++k) gv[12 + k] = fac * vn[k];
                 const float v_alpha = Tn * cv + ra * (va_term - Bsum);
                 Bsum += fac * cv;
-                const bool ok2 = valid & (r2.w * vis <= 0.999f);
-                const float v_sigma = ok2 ? -r2.w * vis * v_alpha : 0.f;
+                const float va2 = (valid & (araw <= 0.999f)) ? v_alpha : 0.f;  // clamped: no gradient
+                const float v_sigma = -araw * va2;
                 // sigma = |s|^2/2 (ray-plane hit) or |m - p|^2 (low-pass), whichever is smaller
                 const bool ell = h.g3 <= h.g2;
                 const float ve = ell ? v_sigma : 0.f, vp = ell ? 0.f : v_sigma;
@@ -449,7 +469,7 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
                 gv[2] = -h.dx * vc0; gv[3] = -h.dx * vc1; gv[4] = -h.dx * vc2;
                 gv[5] = -h.dy * vc0; gv[6] = -h.dy * vc1; gv[7] = -h.dy * vc2;
                 gv[8] = vc0; gv[9] = vc1; gv[10] = vc2;
-                gv[11] = ok2 ? vis * v_alpha : 0.f;
+                gv[11] = vis * va2;
                 if constexpr (ABS) {
                     gv[15 + D] = fabsf(vx);
                     gv[16 + D] = fabsf(vy);
@@ -458,14 +478,9 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
                 float u[TR::G];
                 TR::run(gv, u);
                 if ((lane & 15) == 0) {
-                    float* dst = s_part + t * KV;
+                    float* dst = s_part + t * KVP;
 #pragma unroll
-                    for (int j = 0; j < TR::G; ++j) {
-                        const int i0 = TR::index(j, 0), i1 = TR::index(j, 1), i2 = TR::index(j, 2),
-                                  i3 = TR::index(j, 3);
-                        const int idx = row == 0 ? i0 : row == 1 ? i1 : row == 2 ? i2 : i3;
-                        if (idx >= 0) atomicAdd(dst + idx, u[j]);  // ds_add_f32
-                    }
+                    for (int j = 0; j < TR::G; ++j) atomicAdd(dst + slot[j], u[j]);  // ds_add_f32
                 }
             }
         }
