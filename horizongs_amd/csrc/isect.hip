@@ -7,7 +7,8 @@
 //
 //   1. isect_count  : per-block LDS histogram of (camera, tile) bins, written as
 //                     a dense [blocks][bins] matrix (no global atomics);
-//   2. isect_colscan: per-bin exclusive prefix over blocks (coalesced across bins);
+//   2. isect_colscan: per-bin exclusive prefix over blocks (coalesced across bins,
+//                     two levels over chunks of 64 block rows);
 //   3. isect_binscan: exclusive scan over bins -> isect_offsets (= gsplat
 //                     isect_offset_encode) and {n_isects, largest bin};
 //   4. isect_emit   : each block scatters 8-byte (depth_bits<<32 | flatten_id)
@@ -24,6 +25,7 @@ namespace hgsr {
 
 constexpr int kLdsBins = 16384;   // <= 64 KiB of LDS per block for the histogram / cursors
 constexpr int kSortCap = 2048;    // keys sorted entirely in LDS by one 256-lane workgroup
+constexpr int kIsectBatch = 8;    // Gaussians per lane whose loads are issued together (count / emit)
 
 __host__ __device__ inline int nbits64(int64_t v) {
     int b = 0;
@@ -80,19 +82,31 @@ __global__ __launch_bounds__(256) void isect_count_lds_kernel(
     __syncthreads();
     const int64_t g0 = (int64_t)blockIdx.x * per_block;
     const int64_t g1 = min(g0 + per_block, CN);
-    for (int64_t o = g0 + threadIdx.x; o < g1; o += 256) {
-        const int32_t r = radii[o];
-        if (r <= 0) {
-            tiles_per_gauss[o] = 0;
-            continue;
+    // kIsectBatch Gaussians per lane per round, all loads issued before any is used
+    for (int64_t ob = g0 + threadIdx.x; ob < g1; ob += 256 * kIsectBatch) {
+        int32_t r[kIsectBatch];
+        float2 m[kIsectBatch];
+#pragma unroll
+        for (int k = 0; k < kIsectBatch; ++k) {
+            const int64_t o = ob + 256 * k;
+            r[k] = o < g1 ? radii[o] : 0;
+            m[k] = o < g1 ? means2d[o] : make_float2(0.f, 0.f);
         }
-        const float2 m = means2d[o];
-        int x0, y0, x1, y1;
-        tile_rect(m.x, m.y, r, tile_size, tw, th, x0, y0, x1, y1);
-        tiles_per_gauss[o] = (y1 - y0) * (x1 - x0);
-        const int base = (int)(o / N) * n_tiles;
-        for (int y = y0; y < y1; ++y)
-            for (int x = x0; x < x1; ++x) atomicAdd(&s_hist[base + y * tw + x], 1);
+#pragma unroll
+        for (int k = 0; k < kIsectBatch; ++k) {
+            const int64_t o = ob + 256 * k;
+            if (o >= g1) break;
+            if (r[k] <= 0) {
+                tiles_per_gauss[o] = 0;
+                continue;
+            }
+            int x0, y0, x1, y1;
+            tile_rect(m[k].x, m[k].y, r[k], tile_size, tw, th, x0, y0, x1, y1);
+            tiles_per_gauss[o] = (y1 - y0) * (x1 - x0);
+            const int base = (int)(o / N) * n_tiles;
+            for (int y = y0; y < y1; ++y)
+                for (int x = x0; x < x1; ++x) atomicAdd(&s_hist[base + y * tw + x], 1);
+        }
     }
     __syncthreads();
     int32_t* row = blockhist + (int64_t)blockIdx.x * n_bins;
@@ -120,14 +134,22 @@ __global__ __launch_bounds__(256) void isect_count_global_kernel(
 }
 
 // ---------------------------------------------------------------- stage 2
+// Per-bin exclusive prefix over the block rows, in two levels so that enough
+// workgroups run: (a) each (bin, chunk of kColRows rows) is scanned in place and
+// its total written to chunk_pre[chunk][bin]; (b) per bin, the chunk totals are
+// scanned in place into chunk offsets and the bin total.  The emit adds
+// chunk_pre[row / kColRows] to its row's prefix.
+constexpr int kColRows = 64;
+
 __global__ __launch_bounds__(256) void isect_colscan_kernel(int n_blocks, int n_bins,
                                                             int32_t* __restrict__ blockhist,
-                                                            int32_t* __restrict__ totals) {
+                                                            int32_t* __restrict__ chunk_pre) {
     const int bin = blockIdx.x * 256 + threadIdx.x;
     if (bin >= n_bins) return;
+    const int b0 = blockIdx.y * kColRows, b1 = min(b0 + kColRows, n_blocks);
     int32_t run = 0;
-    int b = 0;
-    for (; b + 8 <= n_blocks; b += 8) {
+    int b = b0;
+    for (; b + 8 <= b1; b += 8) {
         int32_t v[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = blockhist[(int64_t)(b + k) * n_bins + bin];
@@ -137,9 +159,23 @@ __global__ __launch_bounds__(256) void isect_colscan_kernel(int n_blocks, int n_
             run += v[k];
         }
     }
-    for (; b < n_blocks; ++b) {
+    for (; b < b1; ++b) {
         const int32_t v = blockhist[(int64_t)b * n_bins + bin];
         blockhist[(int64_t)b * n_bins + bin] = run;
+        run += v;
+    }
+    chunk_pre[(int64_t)blockIdx.y * n_bins + bin] = run;
+}
+
+__global__ __launch_bounds__(256) void isect_chunkscan_kernel(int n_chunks, int n_bins,
+                                                              int32_t* __restrict__ chunk_pre,
+                                                              int32_t* __restrict__ totals) {
+    const int bin = blockIdx.x * 256 + threadIdx.x;
+    if (bin >= n_bins) return;
+    int32_t run = 0;
+    for (int c = 0; c < n_chunks; ++c) {
+        const int32_t v = chunk_pre[(int64_t)c * n_bins + bin];
+        chunk_pre[(int64_t)c * n_bins + bin] = run;
         run += v;
     }
     totals[bin] = run;
@@ -189,26 +225,40 @@ __global__ __launch_bounds__(256) void isect_emit_lds_kernel(
     int64_t CN, int N, int per_block, const float2* __restrict__ means2d,
     const int32_t* __restrict__ radii, const float* __restrict__ depths, int tile_size, int tw,
     int th, int n_tiles, int n_bins, const int32_t* __restrict__ offsets,
-    const int32_t* __restrict__ blockhist, uint64_t* __restrict__ keys) {
+    const int32_t* __restrict__ blockhist, const int32_t* __restrict__ chunk_pre, uint64_t* __restrict__ keys) {
     extern __shared__ __attribute__((aligned(16))) int s_cur[];
     const int32_t* row = blockhist + (int64_t)blockIdx.x * n_bins;
-    for (int i = threadIdx.x; i < n_bins; i += 256) s_cur[i] = offsets[i] + row[i];
+    const int32_t* cpre = chunk_pre + (int64_t)(blockIdx.x / kColRows) * n_bins;
+    for (int i = threadIdx.x; i < n_bins; i += 256) s_cur[i] = offsets[i] + cpre[i] + row[i];
     __syncthreads();
     const int64_t g0 = (int64_t)blockIdx.x * per_block;
     const int64_t g1 = min(g0 + per_block, CN);
-    for (int64_t o = g0 + threadIdx.x; o < g1; o += 256) {
-        const int32_t r = radii[o];
-        if (r <= 0) continue;
-        const float2 m = means2d[o];
-        int x0, y0, x1, y1;
-        tile_rect(m.x, m.y, r, tile_size, tw, th, x0, y0, x1, y1);
-        const uint64_t key = ((uint64_t)__float_as_uint(depths[o]) << 32) | (uint32_t)o;
-        const int base = (int)(o / N) * n_tiles;
-        for (int y = y0; y < y1; ++y)
-            for (int x = x0; x < x1; ++x) {
-                const int pos = atomicAdd(&s_cur[base + y * tw + x], 1);
-                keys[pos] = key;
-            }
+    for (int64_t ob = g0 + threadIdx.x; ob < g1; ob += 256 * kIsectBatch) {
+        int32_t r[kIsectBatch];
+        float2 m[kIsectBatch];
+        float d[kIsectBatch];
+#pragma unroll
+        for (int k = 0; k < kIsectBatch; ++k) {
+            const int64_t o = ob + 256 * k;
+            r[k] = o < g1 ? radii[o] : 0;
+            m[k] = o < g1 ? means2d[o] : make_float2(0.f, 0.f);
+            d[k] = o < g1 ? depths[o] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < kIsectBatch; ++k) {
+            const int64_t o = ob + 256 * k;
+            if (o >= g1) break;
+            if (r[k] <= 0) continue;
+            int x0, y0, x1, y1;
+            tile_rect(m[k].x, m[k].y, r[k], tile_size, tw, th, x0, y0, x1, y1);
+            const uint64_t key = ((uint64_t)__float_as_uint(d[k]) << 32) | (uint32_t)o;
+            const int base = (int)(o / N) * n_tiles;
+            for (int y = y0; y < y1; ++y)
+                for (int x = x0; x < x1; ++x) {
+                    const int pos = atomicAdd(&s_cur[base + y * tw + x], 1);
+                    keys[pos] = key;
+                }
+        }
     }
 }
 
@@ -530,7 +580,10 @@ extern "C" size_t hgsr_isect_ws1_bytes(int C, int N, int tile_w, int tile_h) {
     const IsectGeom g = isect_geom(C, N, tile_w, tile_h);
     size_t b = align256((size_t)g.n_bins * 4);  // totals (or global counters)
     b += align256((size_t)g.n_bins * 4);        // cursors (global path)
-    if (g.lds) b += align256((size_t)g.n_blocks * g.n_bins * 4);
+    if (g.lds) {
+        b += align256((size_t)g.n_blocks * g.n_bins * 4);
+        b += align256((size_t)((g.n_blocks + kColRows - 1) / kColRows) * g.n_bins * 4);  // chunk prefixes
+    }
     return b;
 }
 
@@ -544,6 +597,7 @@ struct Ws1 {
     int32_t* totals;
     int32_t* cursor;
     int32_t* blockhist;
+    int32_t* chunk_pre;
 };
 static Ws1 carve_ws1(const IsectGeom& g, void* ws) {
     Ws1 w;
@@ -553,6 +607,7 @@ static Ws1 carve_ws1(const IsectGeom& g, void* ws) {
     w.cursor = (int32_t*)p;
     p += align256((size_t)g.n_bins * 4);
     w.blockhist = g.lds ? (int32_t*)p : nullptr;
+    w.chunk_pre = g.lds ? (int32_t*)(p + align256((size_t)g.n_blocks * g.n_bins * 4)) : nullptr;
     return w;
 }
 
@@ -574,8 +629,11 @@ extern "C" int hgsr_isect_count(int C, int N, const float* means2d, const int32_
                                g.per_block, reinterpret_cast<const float2*>(means2d), radii, tile_size, tile_w,
                                tile_h, g.n_tiles, g.n_bins, tiles_per_gauss, w.blockhist);
             if (int st = check_launch("isect_count")) return st;
-            hipLaunchKernelGGL(isect_colscan_kernel, dim3((g.n_bins + 255) / 256), dim3(256), 0, s,
-                               g.n_blocks, g.n_bins, w.blockhist, w.totals);
+            const int n_chunks = (g.n_blocks + kColRows - 1) / kColRows;
+            hipLaunchKernelGGL(isect_colscan_kernel, dim3((g.n_bins + 255) / 256, n_chunks), dim3(256), 0, s,
+                               g.n_blocks, g.n_bins, w.blockhist, w.chunk_pre);
+            hipLaunchKernelGGL(isect_chunkscan_kernel, dim3((g.n_bins + 255) / 256), dim3(256), 0, s, n_chunks,
+                               g.n_bins, w.chunk_pre, w.totals);
         } else {
             if (int st = memset_async(w.totals, (size_t)g.n_bins * 4, s, "isect_count")) return st;
         }
@@ -611,7 +669,7 @@ extern "C" int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const 
         KernelTimer kt("isect_emit", s);
         hipLaunchKernelGGL(isect_emit_lds_kernel, dim3(g.n_blocks), dim3(256), g.n_bins * 4, s, g.CN, N,
                            g.per_block, reinterpret_cast<const float2*>(means2d), radii, depths, tile_size,
-                           tile_w, tile_h, g.n_tiles, g.n_bins, isect_offsets, w.blockhist, keys);
+                           tile_w, tile_h, g.n_tiles, g.n_bins, isect_offsets, w.blockhist, w.chunk_pre, keys);
     } else {
         hipLaunchKernelGGL(copy_i32_kernel, dim3((g.n_bins + 255) / 256), dim3(256), 0, s, g.n_bins,
                            isect_offsets, w.cursor);
