@@ -134,11 +134,11 @@ class Workload:
         # C == 1: reshape/permute are views, so the loss reads the channels-last render in place and
         # its backward writes the full RGB+ED gradient (zero ED channel) with no slice/copy/fill glue
         img = out.reshape(H, W, -1).permute(2, 0, 1)
-        loss = fused_loss(img, self.target, None, 0.2, alpha.reshape(H, W), 0.05, 0.05, scales, 0.01)[0]
-        if self.args.gs == "2d":
-            n = normals[0].permute(2, 0, 1)
-            nd = (nfd * alpha.detach())[0].permute(2, 0, 1)
-            loss = loss + 0.05 * (1 - (n * nd).sum(0)).mean()
+        # 2DGS adds the normal-consistency term (config/our_2d/*/fine.yaml: lambda_normal 0.05), fused too
+        aux = {} if self.args.gs == "3d" else dict(normals=normals.reshape(H, W, 3).permute(2, 0, 1),
+                                                 normals_from_depth=nfd.reshape(H, W, 3).permute(2, 0, 1),
+                                                 lambda_normal=0.05)
+        loss = fused_loss(img, self.target, None, 0.2, alpha.reshape(H, W), 0.05, 0.05, scales, 0.01, **aux)[0]
         loss.backward()
         if self.args.mode == "ddp":
             self.allreduce()

@@ -65,8 +65,8 @@ _SIGS = {
     "hgsr_decode_bwd_ws_bytes": (SZ, [I]),
     "hgsr_decode_bwd": (I, [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P]),
     "hgsr_loss_ws_bytes": (SZ, [I, I, I]),
-    "hgsr_loss_fwd": (I, [I, I, I, P, P, P, P, P, P, P, I64, I, F, F, F, F, P, P, SZ, P]),
-    "hgsr_loss_bwd": (I, [I, I, I, P, P, P, P, P, P, P, I64, I, F, F, F, F, P, P, I, P, P, P, SZ, P]),
+    "hgsr_loss_fwd": (I, [I, I, I, P, P, P, P, P, P, P, I64, I, P, P, P, SZ, P]),
+    "hgsr_loss_bwd": (I, [I, I, I, P, P, P, P, P, P, P, I64, I, P, P, P, I, P, P, P, P, SZ, P]),
     "hgsr_timing_enable": (I, [I]),
     "hgsr_timing_reset": (I, []),
     "hgsr_timing_query": (I, [ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(I64)]),

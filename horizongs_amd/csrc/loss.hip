@@ -25,7 +25,7 @@ constexpr int kLR = 5;             // window radius
 constexpr int kLH = kLT + 2 * kLR;  // 26: tile + halo
 constexpr int kLP = kLH + 1;       // staged row pitch
 constexpr int kHP = 24;            // filtered row pitch: rows 2 apart land 16 banks apart
-constexpr int kLQ = 5;             // partial sums per tile: l1, ssim, sky, entropy, scale-prod
+constexpr int kLQ = 8;  // partial sums per tile: l1, ssim, sky, entropy, scale-prod, normal, distortion, inv-depth
 
 // utils/loss_utils.py:20-22 window, exp(-(x - 5)^2 / (2 * 1.5^2)) normalised, rounded to
 // fp32; compile-time literals so the unrolled filters carry them as instruction constants
@@ -47,6 +47,52 @@ struct ScaleReg {  // scale regulariser operand: scaling [n, k] contiguous (null
     int64_t n;
     int k;
 };
+
+// per-pixel terms of train.py:180-202 (all nullable): normal consistency (2DGS),
+// distortion, inverse-depth L1.  Strided views like Img; gradients use the same strides.
+struct LossAux {
+    const float* nrm;  // render_normals [3,H,W]
+    int64_t ns[3];
+    const float* nfd;  // render_normals_from_depth [3,H,W] (times alpha.detach() here)
+    int64_t fs[3];
+    const float* dist;  // render_distort [H,W]
+    int64_t dst[2];
+    const float* depth;  // render_depth [H,W]
+    int64_t dps[2];
+    const float* mono;   // mono inverse depth [H,W] contiguous
+    const float* dmask;  // depth mask [H,W] contiguous (nullable = 1)
+    float* g_nrm;
+    float* g_nfd;
+    float* g_dist;
+    float* g_depth;
+};
+
+struct LossLam {
+    float dssim, sky, ent, dreg, normal, dist, depth;
+};
+
+// the aux terms' per-pixel values {normal error * mask, distortion * mask, |invD - mono| * dmask}
+__device__ __forceinline__ void aux_terms(const LossAux& ax, const float* __restrict__ alpha,
+                                          const float* __restrict__ mask, int W, int y, int x, float (&t)[3]) {
+    const int64_t p = (int64_t)y * W + x;
+    const float mk = mask ? mask[p] : 1.f;
+    t[0] = t[1] = t[2] = 0.f;
+    if (ax.nrm) {
+        const float a = alpha ? alpha[p] : 1.f;
+        float dot = 0.f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            dot += ax.nrm[c * ax.ns[0] + y * ax.ns[1] + x * ax.ns[2]] *
+                   (ax.nfd[c * ax.fs[0] + y * ax.fs[1] + x * ax.fs[2]] * a);
+        t[0] = (1.f - dot) * mk;
+    }
+    if (ax.dist) t[1] = ax.dist[y * ax.dst[0] + x * ax.dst[1]] * mk;
+    if (ax.depth) {
+        const float d = ax.depth[y * ax.dps[0] + x * ax.dps[1]];
+        const float inv = d > 0.f ? 1.f / d : 0.f;
+        t[2] = fabsf((inv - ax.mono[p]) * (ax.dmask ? ax.dmask[p] : 1.f));
+    }
+}
 
 __device__ __forceinline__ float row_prod(const float* __restrict__ s, int k) {
     float p = s[0];
@@ -129,7 +175,7 @@ __device__ __forceinline__ SsimPix ssim_pix(float mu1, float mu2, float ex2, flo
 // channel's window already in flight in registers (LDS-only barriers keep it in flight).
 __global__ __launch_bounds__(256) void loss_fwd_kernel(int C, int H, int W, Img img, Img gt,
                                                        const float* __restrict__ mask,
-                                                       const float* __restrict__ alpha, ScaleReg sr,
+                                                       const float* __restrict__ alpha, ScaleReg sr, LossAux ax,
                                                        float* __restrict__ dmaps, float* __restrict__ partials) {
     __shared__ LossFwdSmem sm;
     const int tiles_x = (W + kLT - 1) / kLT;
@@ -162,6 +208,8 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(int C, int H, int W, Img 
         sky = -(1.f - sk) * logf(1.f - o);
         ent = -o * logf(o);
     }
+    float aux[3] = {0.f, 0.f, 0.f};
+    if (inside1) aux_terms(ax, alpha, mask, W, py1, px1, aux);
     float dreg = 0.f;
     if (sr.s) {
         const int64_t per = (sr.n + gridDim.x - 1) / gridDim.x;
@@ -238,6 +286,8 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(int C, int H, int W, Img 
     sky = block_sum(sky, sm.red);
     ent = block_sum(ent, sm.red);
     dreg = block_sum(dreg, sm.red);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) aux[q] = block_sum(aux[q], sm.red);
     if (tid == 0) {
         const int64_t nt = gridDim.x;
         partials[blockIdx.x] = l1;
@@ -245,16 +295,17 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(int C, int H, int W, Img 
         partials[2 * nt + blockIdx.x] = sky;
         partials[3 * nt + blockIdx.x] = ent;
         partials[4 * nt + blockIdx.x] = dreg;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) partials[(5 + q) * nt + blockIdx.x] = aux[q];
     }
 }
 
 // fixed-order f64 reduction of the tile partials -> [loss, l1, ssim, sky, entropy, scale_reg]
 __global__ __launch_bounds__(256) void loss_reduce_kernel(int n_tiles, int C, int64_t HW, int64_t n_sc,
-                                                          float lam_dssim, float lam_sky, float lam_ent,
-                                                          float lam_dreg, const float* __restrict__ partials,
+                                                          LossLam lam, const float* __restrict__ partials,
                                                           float* __restrict__ out) {
     __shared__ double s[kLQ][256];
-    double a[kLQ] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    double a[kLQ] = {};
     for (int t = threadIdx.x; t < n_tiles; t += 256)
 #pragma unroll
         for (int q = 0; q < kLQ; ++q) a[q] += partials[(int64_t)q * n_tiles + t];
@@ -271,14 +322,18 @@ __global__ __launch_bounds__(256) void loss_reduce_kernel(int n_tiles, int C, in
         const double n = (double)C * (double)HW;
         const double l1 = s[0][0] / n, ssim = s[1][0] / n, sky = s[2][0] / (double)HW, ent = s[3][0] / (double)HW;
         const double dreg = n_sc > 0 ? s[4][0] / (double)n_sc : 0.0;  // train.py:163-166: 0 when empty
-        const double loss =
-            (1.0 - lam_dssim) * l1 + lam_dssim * (1.0 - ssim) + lam_dreg * dreg + lam_sky * sky + lam_ent * ent;
+        const double nrm = s[5][0] / (double)HW, dist = s[6][0] / (double)HW, dep = s[7][0] / (double)HW;
+        const double loss = (1.0 - lam.dssim) * l1 + lam.dssim * (1.0 - ssim) + lam.dreg * dreg + lam.sky * sky +
+                            lam.ent * ent + lam.normal * nrm + lam.dist * dist + lam.depth * dep;
         out[0] = (float)loss;
         out[1] = (float)l1;
         out[2] = (float)ssim;
         out[3] = (float)sky;
         out[4] = (float)ent;
         out[5] = (float)dreg;
+        out[6] = (float)nrm;
+        out[7] = (float)dist;
+        out[8] = (float)dep;
     }
 }
 
@@ -288,29 +343,31 @@ struct LossBwdSmem {
 };
 
 struct LossCoef {
-    float l1, ss, sky, ent, dreg;
+    float l1, ss, sky, ent, dreg, nrm, dist, dep;
 };
 
 __device__ __forceinline__ LossCoef loss_coef(const float* __restrict__ g_out, int C, int64_t HW, int64_t n_sc,
-                                              float lam_dssim, float lam_sky, float lam_ent, float lam_dreg) {
-    // upstream gradients of [loss, l1, ssim, sky, entropy, scale_reg] folded into per-term factors
-    const float g0 = g_out[0], g1 = g_out[1], g2 = g_out[2], g3 = g_out[3], g4 = g_out[4], g5 = g_out[5];
-    const float n = (float)C * (float)HW;
+                                              const LossLam& lam) {
+    // upstream gradients of the nine outputs folded into per-term factors
+    const float g0 = g_out[0];
+    const float n = (float)C * (float)HW, hw = (float)HW;
     LossCoef k;
-    k.l1 = (g0 * (1.f - lam_dssim) + g1) / n;
-    k.ss = (g2 - g0 * lam_dssim) / n;
-    k.sky = (g0 * lam_sky + g3) / (float)HW;
-    k.ent = (g0 * lam_ent + g4) / (float)HW;
-    k.dreg = n_sc > 0 ? (g0 * lam_dreg + g5) / (float)n_sc : 0.f;
+    k.l1 = (g0 * (1.f - lam.dssim) + g_out[1]) / n;
+    k.ss = (g_out[2] - g0 * lam.dssim) / n;
+    k.sky = (g0 * lam.sky + g_out[3]) / hw;
+    k.ent = (g0 * lam.ent + g_out[4]) / hw;
+    k.dreg = n_sc > 0 ? (g0 * lam.dreg + g_out[5]) / (float)n_sc : 0.f;
+    k.nrm = (g0 * lam.normal + g_out[6]) / hw;
+    k.dist = (g0 * lam.dist + g_out[7]) / hw;
+    k.dep = (g0 * lam.depth + g_out[8]) / hw;
     return k;
 }
 
 // backward: d loss / d image (and d alpha, d scaling); same channel pipeline as the forward
 __global__ __launch_bounds__(256) void loss_bwd_kernel(int C, int H, int W, Img img, Img gt,
                                                        const float* __restrict__ mask,
-                                                       const float* __restrict__ alpha, ScaleReg sr,
-                                                       float lam_dssim, float lam_sky, float lam_ent, float lam_dreg,
-                                                       const float* __restrict__ dmaps,
+                                                       const float* __restrict__ alpha, ScaleReg sr, LossAux ax,
+                                                       LossLam lam, const float* __restrict__ dmaps,
                                                        const float* __restrict__ g_out, float* __restrict__ g_img,
                                                        int extra_ch, float* __restrict__ g_alpha,
                                                        float* __restrict__ g_scaling) {
@@ -357,7 +414,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(int C, int H, int W, Img 
         }
     };
     fetch(0);
-    const LossCoef k = loss_coef(g_out, C, HW, sr.n, lam_dssim, lam_sky, lam_ent, lam_dreg);
+    const LossCoef k = loss_coef(g_out, C, HW, sr.n, lam);
     Img gi = img;
     gi.p = g_img;
     {
@@ -379,6 +436,33 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(int C, int H, int W, Img 
                 ga = pass ? k.sky * d_sky + k.ent * d_ent : 0.f;
             }
             g_alpha[pp] = ga;
+        }
+        if (inside) {
+            const float mk = mask ? mask[pp] : 1.f;
+            if (ax.nrm) {  // d/dn = -mask nfd a, d/dnfd = -mask n a (alpha detached, train.py:183)
+                const float a = alpha ? alpha[pp] : 1.f;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const int64_t in = c * ax.ns[0] + py * ax.ns[1] + px * ax.ns[2];
+                    const int64_t iF = c * ax.fs[0] + py * ax.fs[1] + px * ax.fs[2];
+                    const float n = ax.nrm[in], f = ax.nfd[iF];
+                    if (ax.g_nrm) ax.g_nrm[in] = -k.nrm * mk * f * a;
+                    if (ax.g_nfd) ax.g_nfd[iF] = -k.nrm * mk * n * a;
+                }
+            }
+            if (ax.dist && ax.g_dist) ax.g_dist[py * ax.dst[0] + px * ax.dst[1]] = k.dist * mk;
+            if (ax.depth && ax.g_depth) {
+                const int64_t id = py * ax.dps[0] + px * ax.dps[1];
+                const float d = ax.depth[id];
+                float g = 0.f;
+                if (d > 0.f) {
+                    const float dm = ax.dmask ? ax.dmask[pp] : 1.f;
+                    const float e = (1.f / d - ax.mono[pp]) * dm;
+                    const float sg = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+                    g = k.dep * sg * dm * (-1.f / (d * d));
+                }
+                ax.g_depth[id] = g;
+            }
         }
     }
     if (g_scaling) {  // d mean_i prod_j s_ij / d s_ij = prod_{l != j} s_il / n
@@ -493,20 +577,58 @@ static int check_scale_reg(int64_t n_sc, int k_sc, const float* scaling, float l
     return HGSR_OK;
 }
 
+static int make_terms(const hgsr_loss_terms* t, const hgsr_loss_aux_grads* g, int H, int W, LossLam& lam,
+                      LossAux& ax) {
+    HGSR_REQUIRE(t, "null loss terms");
+    lam = LossLam{t->lambda_dssim, t->lambda_sky_opa, t->lambda_entropy, t->lambda_dreg,
+                  t->lambda_normal, t->lambda_dist, t->lambda_depth};
+    HGSR_REQUIRE(!t->normals == !t->normals_from_depth, "normal term needs normals and normals_from_depth");
+    HGSR_REQUIRE(t->lambda_normal == 0.f || t->normals, "lambda_normal needs normals");
+    HGSR_REQUIRE(t->lambda_dist == 0.f || t->distort, "lambda_dist needs distort");
+    HGSR_REQUIRE(!t->depth == !t->mono_invdepth, "depth term needs depth and mono_invdepth");
+    HGSR_REQUIRE(t->lambda_depth == 0.f || t->depth, "lambda_depth needs depth");
+    ax = LossAux{};
+    ax.nrm = t->normals;
+    ax.nfd = t->normals_from_depth;
+    const int64_t def3[3] = {(int64_t)H * W, W, 1}, def2[2] = {W, 1};
+    for (int k = 0; k < 3; ++k) {
+        ax.ns[k] = t->normals_strides[k] ? t->normals_strides[k] : def3[k];
+        ax.fs[k] = t->nfd_strides[k] ? t->nfd_strides[k] : def3[k];
+    }
+    ax.dist = t->distort;
+    ax.depth = t->depth;
+    for (int k = 0; k < 2; ++k) {
+        ax.dst[k] = t->distort_strides[k] ? t->distort_strides[k] : def2[k];
+        ax.dps[k] = t->depth_strides[k] ? t->depth_strides[k] : def2[k];
+    }
+    ax.mono = t->mono_invdepth;
+    ax.dmask = t->depth_mask;
+    if (g) {
+        ax.g_nrm = g->g_normals;
+        ax.g_nfd = g->g_normals_from_depth;
+        ax.g_dist = g->g_distort;
+        ax.g_depth = g->g_depth;
+    }
+    return HGSR_OK;
+}
+
 extern "C" int hgsr_loss_fwd(int C, int H, int W, const float* image, const int64_t* image_strides,
                              const float* gt, const int64_t* gt_strides, const float* mask,
                              const float* alpha, const float* scaling, int64_t n_scaling, int k_scaling,
-                             float lambda_dssim, float lambda_sky_opa, float lambda_entropy, float lambda_dreg,
-                             float* out, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
+                             const hgsr_loss_terms* terms, float* out, void* ws, size_t ws_bytes,
+                             hgsr_stream_t stream) {
     HGSR_REQUIRE(C >= 1 && H > 0 && W > 0, "bad dims");
     HGSR_REQUIRE(image && gt && out && ws, "null pointer");
     static const bool win_ok = check_window();
     HGSR_REQUIRE(win_ok, "SSIM window constants disagree with utils/loss_utils.py's formula");
     HGSR_REQUIRE(ws_bytes >= hgsr_loss_ws_bytes(C, H, W), "loss workspace too small");
-    HGSR_REQUIRE(alpha || (lambda_sky_opa == 0.f && lambda_entropy == 0.f), "alpha terms need alpha");
+    LossLam lam;
+    LossAux ax;
+    if (int st = make_terms(terms, nullptr, H, W, lam, ax)) return st;
+    HGSR_REQUIRE(alpha || (lam.sky == 0.f && lam.ent == 0.f), "alpha terms need alpha");
     if (int st = check_strides(image_strides, "image", C, H, W)) return st;
     if (int st = check_strides(gt_strides, "gt", C, H, W)) return st;
-    if (int st = check_scale_reg(n_scaling, k_scaling, scaling, lambda_dreg)) return st;
+    if (int st = check_scale_reg(n_scaling, k_scaling, scaling, lam.dreg)) return st;
     hipStream_t s = as_stream(stream);
     float* dmaps = (float*)ws;
     float* partials = (float*)((char*)ws + loss_maps_bytes(C, H, W));
@@ -515,27 +637,30 @@ extern "C" int hgsr_loss_fwd(int C, int H, int W, const float* image, const int6
     const ScaleReg sr{n_scaling > 0 ? scaling : nullptr, n_scaling, k_scaling};
     {
         KernelTimer kt("loss_fwd", s);
-        hipLaunchKernelGGL(loss_fwd_kernel, dim3(nt), dim3(256), 0, s, C, H, W, im, gm, mask, alpha, sr, dmaps,
+        hipLaunchKernelGGL(loss_fwd_kernel, dim3(nt), dim3(256), 0, s, C, H, W, im, gm, mask, alpha, sr, ax, dmaps,
                            partials);
     }
     if (int st = check_launch("loss_fwd")) return st;
-    hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, s, nt, C, (int64_t)H * W, n_scaling,
-                       lambda_dssim, lambda_sky_opa, lambda_entropy, lambda_dreg, partials, out);
+    hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, s, nt, C, (int64_t)H * W, n_scaling, lam,
+                       partials, out);
     return check_launch("loss_reduce");
 }
 
 extern "C" int hgsr_loss_bwd(int C, int H, int W, const float* image, const int64_t* image_strides,
                              const float* gt, const int64_t* gt_strides, const float* mask,
                              const float* alpha, const float* scaling, int64_t n_scaling, int k_scaling,
-                             float lambda_dssim, float lambda_sky_opa, float lambda_entropy, float lambda_dreg,
-                             const float* g_out, float* g_image, int extra_channels, float* g_alpha,
-                             float* g_scaling, const void* ws, size_t ws_bytes, hgsr_stream_t stream) {
+                             const hgsr_loss_terms* terms, const float* g_out, float* g_image, int extra_channels,
+                             float* g_alpha, float* g_scaling, const hgsr_loss_aux_grads* aux_grads,
+                             const void* ws, size_t ws_bytes, hgsr_stream_t stream) {
     HGSR_REQUIRE(C >= 1 && H > 0 && W > 0, "bad dims");
     HGSR_REQUIRE(image && gt && g_out && g_image && ws, "null pointer");
     HGSR_REQUIRE(ws_bytes >= hgsr_loss_ws_bytes(C, H, W), "loss workspace too small");
+    LossLam lam;
+    LossAux ax;
+    if (int st = make_terms(terms, aux_grads, H, W, lam, ax)) return st;
     if (int st = check_strides(image_strides, "image", C, H, W)) return st;
     if (int st = check_strides(gt_strides, "gt", C, H, W)) return st;
-    if (int st = check_scale_reg(n_scaling, k_scaling, scaling, lambda_dreg)) return st;
+    if (int st = check_scale_reg(n_scaling, k_scaling, scaling, lam.dreg)) return st;
     HGSR_REQUIRE(extra_channels >= 0, "negative extra_channels");
     hipStream_t s = as_stream(stream);
     const Img im = make_img(image, image_strides, H, W), gm = make_img(gt, gt_strides, H, W);
@@ -543,7 +668,6 @@ extern "C" int hgsr_loss_bwd(int C, int H, int W, const float* image, const int6
     float* gsc = n_scaling > 0 ? g_scaling : nullptr;
     KernelTimer kt("loss_bwd", s);
     hipLaunchKernelGGL(loss_bwd_kernel, dim3(loss_tiles(H, W)), dim3(256), 0, s, C, H, W, im, gm, mask, alpha, sr,
-                       lambda_dssim, lambda_sky_opa, lambda_entropy, lambda_dreg, (const float*)ws,
-                       g_out, g_image, extra_channels, g_alpha, gsc);
+                       ax, lam, (const float*)ws, g_out, g_image, extra_channels, g_alpha, gsc);
     return check_launch("loss_bwd");
 }

@@ -292,33 +292,56 @@ int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
                     size_t ws_bytes, hgsr_stream_t stream);
 
 /* ---- K15: fused training loss ---------------------------
- * replaces the loss head of reference train.py:153-178 with utils/loss_utils.py:17-60:
- * x = image*mask, y = gt*mask (image, gt [C,H,W]; mask [H,W] nullable); out[6] (device) =
- * {loss, l1, ssim, sky, entropy, scale_reg} with
+ * replaces the loss head of reference train.py:153-202 with utils/loss_utils.py:17-60:
+ * x = image*mask, y = gt*mask (image, gt [C,H,W]; mask [H,W] nullable); out[9] (device) =
+ * {loss, l1, ssim, sky, entropy, scale_reg, normal, distortion, inv_depth} with
  *   loss = (1-l)*mean|x-y| + l*(1-mean SSIM(x,y)) + l_dreg*mean_i prod_j scaling[i,j]
- *        + l_sky*mean(-(1-mask) log(1-a)) + l_ent*mean(-a log a),  a = clamp(alpha, 1e-6, 1-1e-6)
+ *        + l_sky*mean(-(1-mask) log(1-a)) + l_ent*mean(-a log a)       (a = clamp(alpha, 1e-6, 1-1e-6))
+ *        + l_normal*mean((1 - sum_c n_c nfd_c alpha) * mask)          (train.py:180-188, alpha detached)
+ *        + l_dist*mean(distort * mask)                                  (train.py:190-191)
+ *        + l_depth*mean(|(invD - mono) * depth_mask|), invD = depth > 0 ? 1/depth : 0  (train.py:193-199)
  * (alpha [H,W] nullable when both l_sky and l_ent are 0; scaling [n_scaling, k_scaling]
- * contiguous, nullable, scale_reg = 0 when n_scaling = 0 as train.py:163-166).
+ * contiguous, nullable, scale_reg = 0 when n_scaling = 0 as train.py:163-166; the aux
+ * inputs are nullable and their terms 0 when absent).
  * ws (hgsr_loss_ws_bytes) holds the SSIM derivative maps for hgsr_loss_bwd, which writes
- * g_image, g_alpha [H,W] (nullable) and g_scaling [n_scaling, k_scaling] (nullable) from
- * g_out[6], the upstream gradients of the six outputs (device).
- * *_strides (host, nullable = contiguous CHW): element strides {channel, row, column} of
- * image / gt, e.g. {1, 3W, 3} for the channels-last render output seen through
- * permute(2,0,1) (render.py:81-95); g_image is written with image's strides, and its
- * channels C..C+extra_channels-1 (trailing render channels the loss ignores, e.g. the
- * depth of RGB+ED) are written as zero so the caller needs no slice/fill. */
+ * g_image, g_alpha [H,W] (nullable), g_scaling (nullable) and the aux gradients
+ * (nullable) from g_out[9], the upstream gradients of the nine outputs (device).
+ * *_strides (host, nullable / zero = contiguous): element strides {channel, row, column}
+ * ({row, column} for [H,W] maps), e.g. {1, 3W, 3} for the channels-last render output
+ * seen through permute(2,0,1) (render.py:81-95); every gradient is written with its
+ * input's strides.  g_image channels C..C+extra_channels-1 (trailing render channels the
+ * loss ignores, e.g. the depth of RGB+ED) are written as zero. */
+typedef struct hgsr_loss_terms {
+    float lambda_dssim, lambda_sky_opa, lambda_entropy, lambda_dreg;
+    float lambda_normal, lambda_dist, lambda_depth;
+    const float* normals;            /* render_normals [3,H,W] view */
+    int64_t normals_strides[3];
+    const float* normals_from_depth; /* render_normals_from_depth [3,H,W] view */
+    int64_t nfd_strides[3];
+    const float* distort;            /* render_distort [H,W] view */
+    int64_t distort_strides[2];
+    const float* depth;              /* render_depth [H,W] view */
+    int64_t depth_strides[2];
+    const float* mono_invdepth;      /* [H,W] contiguous */
+    const float* depth_mask;         /* [H,W] contiguous, nullable */
+} hgsr_loss_terms;
+typedef struct hgsr_loss_aux_grads {
+    float* g_normals;
+    float* g_normals_from_depth;
+    float* g_distort;
+    float* g_depth;
+} hgsr_loss_aux_grads;
 size_t hgsr_loss_ws_bytes(int C, int H, int W);
 int hgsr_loss_fwd(int C, int H, int W, const float* image, const int64_t* image_strides,
                   const float* gt, const int64_t* gt_strides, const float* mask, const float* alpha,
-                  const float* scaling, int64_t n_scaling, int k_scaling, float lambda_dssim,
-                  float lambda_sky_opa, float lambda_entropy, float lambda_dreg, float* out, void* ws,
-                  size_t ws_bytes, hgsr_stream_t stream);
+                  const float* scaling, int64_t n_scaling, int k_scaling, const hgsr_loss_terms* terms,
+                  float* out, void* ws, size_t ws_bytes, hgsr_stream_t stream);
 int hgsr_loss_bwd(int C, int H, int W, const float* image, const int64_t* image_strides,
                   const float* gt, const int64_t* gt_strides, const float* mask, const float* alpha,
-                  const float* scaling, int64_t n_scaling, int k_scaling, float lambda_dssim,
-                  float lambda_sky_opa, float lambda_entropy, float lambda_dreg, const float* g_out,
-                  float* g_image, int extra_channels, float* g_alpha, float* g_scaling,
-                  const void* ws, size_t ws_bytes, hgsr_stream_t stream);
+                  const float* scaling, int64_t n_scaling, int k_scaling, const hgsr_loss_terms* terms,
+                  const float* g_out, float* g_image, int extra_channels, float* g_alpha,
+                  float* g_scaling, const hgsr_loss_aux_grads* aux_grads, const void* ws,
+                  size_t ws_bytes, hgsr_stream_t stream);
 
 /* ---- measurement ----------------------------------------------------------
  * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):

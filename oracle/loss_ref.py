@@ -2,7 +2,8 @@
 
 Only tests/ may import this module.  Follows reference utils/loss_utils.py:17-60 (l1_loss,
 gaussian/create_window, _ssim with conv2d, zero padding, C1 = 0.01^2, C2 = 0.03^2) and the
-scale / alpha regularisers of train.py:162-178, in torch ops so autograd gives the reference
+scale / alpha regularisers and per-pixel normal / distortion / inverse-depth terms of
+train.py:162-202, in torch ops so autograd gives the reference
 gradients.  Pinned by tests/golden/losses.npz (l1 and ssim of the reference module itself).
 """
 from __future__ import annotations
@@ -35,8 +36,11 @@ def ssim(img1, img2):
 
 
 def loss(image, gt, mask=None, lambda_dssim=0.2, alpha=None, lambda_sky=0.0, lambda_ent=0.0, scaling=None,
-         lambda_dreg=0.0):
-    """train.py:153-178 (the normal term excluded): returns (loss, l1, ssim, sky, entropy, scale_reg)."""
+         lambda_dreg=0.0, normals=None, nfd=None, lambda_normal=0.0, distort=None, lambda_dist=0.0, depth=None,
+         mono=None, dmask=None, lambda_depth=0.0):
+    """train.py:153-202: returns (loss, l1, ssim, sky, entropy, scale_reg, normal, distortion, inv_depth).
+    normals / nfd [3,H,W], distort / depth / mono / dmask [H,W]; mask [H,W] or None."""
+    mask_hw = mask
     if mask is not None:
         image = image * mask
         gt = gt * mask
@@ -54,4 +58,23 @@ def loss(image, gt, mask=None, lambda_dssim=0.2, alpha=None, lambda_sky=0.0, lam
         sky = (-(1 - skym) * torch.log(1 - o)).mean()
         ent = -(o * torch.log(o)).mean()
         total = total + lambda_sky * sky + lambda_ent * ent
-    return total, l1, s, sky, ent, dreg
+    z = torch.zeros((), dtype=image.dtype)
+    mk = mask_hw if mask_hw is not None else torch.ones(image.shape[-2:], dtype=image.dtype)
+    nrm = dist = dep = z
+    if normals is not None:  # train.py:180-188 (alpha detached)
+        a = alpha.detach() if alpha is not None else torch.ones_like(mk)
+        err = 1 - (normals * (nfd * a[None])).sum(0)
+        nrm = (err * mk).mean()
+        total = total + lambda_normal * nrm
+    if distort is not None:  # train.py:190-191
+        dist = (distort * mk).mean()
+        total = total + lambda_dist * dist
+    if depth is not None:  # train.py:193-199
+        # train.py:195 uses where(depth > 0, 1/depth, 0), whose backward is NaN at depth == 0
+        # (0 * -inf); the inner where keeps that gradient 0, as the HIP kernel defines it
+        pos = depth > 0.0
+        inv = torch.where(pos, 1.0 / torch.where(pos, depth, torch.ones_like(depth)), torch.zeros_like(depth))
+        dm = dmask if dmask is not None else torch.ones_like(depth)
+        dep = torch.abs((inv - mono) * dm).mean()
+        total = total + lambda_depth * dep
+    return total, l1, s, sky, ent, dreg, nrm, dist, dep

@@ -26,7 +26,7 @@ def test_loss_matches_reference_golden():
     from horizongs_amd.loss import fused_loss
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "losses.npz"))
     img, gt = torch.from_numpy(g["img"]).to(DEV), torch.from_numpy(g["gt"]).to(DEV)
-    loss, l1, s, _, _, _ = fused_loss(img, gt, lambda_dssim=0.2)
+    loss, l1, s = fused_loss(img, gt, lambda_dssim=0.2)[:3]
     assert abs(float(l1) - float(g["l1"])) <= 1e-6
     assert abs(float(s) - float(g["ssim"])) <= 1e-5
     assert abs(float(loss) - (0.8 * float(g["l1"]) + 0.2 * (1 - float(g["ssim"])))) <= 1e-5
@@ -46,7 +46,7 @@ def test_loss_gradients(H, W, masked, alpha_terms, n_sc):
     scaling = (0.02 * torch.rand(n_sc, 3, generator=gen)) if (n_sc or alpha_terms) else None
     lam = dict(lambda_dssim=0.2, lambda_sky=0.05 if alpha_terms else 0.0, lambda_ent=0.01 if alpha_terms else 0.0,
                lambda_dreg=0.01 if scaling is not None else 0.0)
-    ups = torch.randn(6, generator=gen)
+    ups = torch.randn(9, generator=gen)
 
     def ref(dtype):
         i = img.to(dtype).clone().requires_grad_(True)
@@ -64,7 +64,7 @@ def test_loss_gradients(H, W, masked, alpha_terms, n_sc):
     sc = scaling.to(DEV).clone().requires_grad_(True) if scaling is not None else None
     outs = fused_loss(i, gt.to(DEV), None if mask is None else mask.to(DEV), lam["lambda_dssim"], a,
                       lam["lambda_sky"], lam["lambda_ent"], sc, lam["lambda_dreg"])
-    assert len(outs) == 6
+    assert len(outs) == 9
     for o, r32, r64, name in zip(outs, o32, o64, ("loss", "l1", "ssim", "sky", "entropy", "scale_reg")):
         cond_close(o.detach().cpu().numpy(), r32, r64, name)
     sum(o * u for o, u in zip(outs, ups.to(DEV))).backward()
@@ -87,7 +87,7 @@ def test_loss_channels_last_view(extra):
     gt = torch.rand(3, H, W, generator=gen).to(DEV)
     mask = (torch.rand(H, W, generator=gen) > 0.3).float().to(DEV)
     alpha = torch.rand(H, W, generator=gen).to(DEV)
-    ups = torch.randn(6, generator=gen).to(DEV)
+    ups = torch.randn(9, generator=gen).to(DEV)
 
     a = hwc.clone().requires_grad_(True)
     outs = fused_loss(a.permute(2, 0, 1), gt, mask, 0.2, alpha, 0.05, 0.01)
@@ -101,3 +101,54 @@ def test_loss_channels_last_view(extra):
     assert torch.equal(a.grad[..., :3].permute(2, 0, 1), b.grad)
     if extra:
         assert torch.equal(a.grad[..., 3:], torch.zeros_like(a.grad[..., 3:]))
+
+
+@pytest.mark.parametrize("H,W,masked", [(48, 70, True), (1080 // 4, 1920 // 4, False)])
+def test_loss_aux_terms(H, W, masked):
+    """Normal consistency, distortion and inverse-depth L1 (train.py:180-199) on channels-last
+    render views, every gradient vs fp64 / fp32 autograd of the oracle."""
+    from horizongs_amd.loss import fused_loss
+    gen = torch.Generator().manual_seed(H + 3 * W)
+    img = torch.rand(3, H, W, generator=gen)
+    gt = torch.rand(3, H, W, generator=gen)
+    mask = (torch.rand(H, W, generator=gen) > 0.25).float() if masked else None
+    alpha = torch.rand(H, W, generator=gen)
+    nrm = torch.nn.functional.normalize(torch.randn(H, W, 3, generator=gen), dim=-1)
+    nfd = torch.nn.functional.normalize(torch.randn(H, W, 3, generator=gen), dim=-1)
+    dist = torch.rand(H, W, 1, generator=gen) * 0.1
+    depth = torch.where(torch.rand(H, W, generator=gen) > 0.1, 1.0 + 9.0 * torch.rand(H, W, generator=gen),
+                        torch.zeros(H, W))
+    mono = 1.0 / (1.0 + 9.0 * torch.rand(H, W, generator=gen))
+    dmask = (torch.rand(H, W, generator=gen) > 0.2).float()
+    lam = dict(lambda_normal=0.05, lambda_dist=100.0, lambda_depth=0.3)
+    ups = torch.randn(9, generator=gen)
+
+    def ref(dtype):
+        t = {k: v.to(dtype).clone().requires_grad_(True) for k, v in
+             dict(img=img, alpha=alpha, nrm=nrm, nfd=nfd, dist=dist, depth=depth).items()}
+        outs = L.loss(t["img"], gt.to(dtype), None if mask is None else mask.to(dtype), 0.2, t["alpha"], 0.0, 0.0,
+                      None, 0.0, t["nrm"].permute(2, 0, 1), t["nfd"].permute(2, 0, 1), lam["lambda_normal"],
+                      t["dist"][..., 0], lam["lambda_dist"], t["depth"], mono.to(dtype), dmask.to(dtype),
+                      lam["lambda_depth"])
+        sum(o * u for o, u in zip(outs, ups.to(dtype))).backward()
+        return [o.detach().numpy() for o in outs], {k: (v.grad.numpy() if v.grad is not None else None)
+                                                    for k, v in t.items()}
+
+    o32, g32 = ref(torch.float32)
+    o64, g64 = ref(torch.float64)
+    d = {k: v.to(DEV).clone().requires_grad_(True) for k, v in
+         dict(img=img, alpha=alpha, nrm=nrm, nfd=nfd, dist=dist, depth=depth).items()}
+    outs = fused_loss(d["img"], gt.to(DEV), None if mask is None else mask.to(DEV), 0.2, d["alpha"],
+                      normals=d["nrm"].permute(2, 0, 1), normals_from_depth=d["nfd"].permute(2, 0, 1),
+                      distort=d["dist"], depth=d["depth"], mono_invdepth=mono.to(DEV), depth_mask=dmask.to(DEV),
+                      **lam)
+    names = ("loss", "l1", "ssim", "sky", "entropy", "scale_reg", "normal", "distortion", "inv_depth")
+    for o, r32, r64, name in zip(outs, o32, o64, names):
+        cond_close(o.detach().cpu().numpy(), r32, r64, name)
+    sum(o * u for o, u in zip(outs, ups.to(DEV))).backward()
+    for k in ("img", "alpha", "nrm", "nfd", "dist", "depth"):
+        assert d[k].grad is not None, k
+        if g32[k] is None:  # alpha only reaches the normal term, detached: zero gradient
+            assert torch.count_nonzero(d[k].grad) == 0, k
+            continue
+        cond_close(d[k].grad.cpu().numpy(), g32[k], g64[k], "d_" + k)
