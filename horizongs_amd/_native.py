@@ -65,6 +65,11 @@ _SIGS = {
     "hgsr_decode_bwd_ws_bytes": (SZ, [I]),
     "hgsr_decode_bwd": (I, [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P]),
     "hgsr_loss_ws_bytes": (SZ, [I, I, I]),
+    "hgsr_training_statis": (I, [I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "hgsr_voxel_dedup_ws_bytes": (SZ, [I64]),
+    "hgsr_voxel_dedup": (I, [I64, P, I64, P, P, P, P, SZ, P]),
+    "hgsr_scatter_max": (I, [I64, I, P, P, I64, P, P]),
+    "hgsr_weed_out": (I, [I64, P, P, I, P, F, F, I, I, F, P, P]),
     "hgsr_loss_fwd": (I, [I, I, I, P, P, P, P, P, P, P, I64, I, P, P, P, SZ, P]),
     "hgsr_loss_bwd": (I, [I, I, I, P, P, P, P, P, P, P, I64, I, P, P, P, I, P, P, P, P, SZ, P]),
     "hgsr_timing_enable": (I, [I]),

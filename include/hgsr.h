@@ -343,6 +343,41 @@ int hgsr_loss_bwd(int C, int H, int W, const float* image, const int64_t* image_
                   float* g_scaling, const hgsr_loss_aux_grads* aux_grads, const void* ws,
                   size_t ws_bytes, hgsr_stream_t stream);
 
+/* ---- K16: densification on device ----------------------
+ * hgsr_training_statis replaces BasicModel.training_statis (scene/basic_model.py:96-144):
+ * vis_idx [Av] = nonzero(visible_mask) (ascending); selection [Av*n_offsets] = the decode's
+ * opacity > 0 mask; selection_rank [Av*n_offsets] its exclusive prefix (= output row);
+ * visibility_filter [M] (radii > 0), viewspace_grad [M,2] (means2d.grad), opacity [M],
+ * radii [M] (max growing only) for the M decoded Gaussians.  Updates in place (float32):
+ * anchor_opacity_accum / anchor_demon [A], offset_gradient_accum / offset_denom /
+ * max_radii2D / offset_opacity_accum [A*n_offsets] ("mean" or "max" pruning / growing
+ * types; the reference scales the gradient by (W/2, H/2) before the norm).
+ * One lane per visible anchor, slots in order: deterministic. */
+int hgsr_training_statis(int Av, int n_offsets, int width, int height, int pruning_max, int growing_max,
+                         const int32_t* vis_idx, const uint8_t* selection, const int32_t* selection_rank,
+                         const uint8_t* visibility_filter, const float* viewspace_grad,
+                         const float* opacity, const int32_t* radii, float* anchor_opacity_accum,
+                         float* anchor_demon, float* offset_gradient_accum, float* offset_denom,
+                         float* max_radii2D, float* offset_opacity_accum, hgsr_stream_t stream);
+/* replaces get_remove_duplicates (scene/basic_model.py:179-190): found[i] = 1 iff
+ * cand_coords[i] (int32 xyz voxel) equals some grid_coords row.  Hash set in ws
+ * (hgsr_voxel_dedup_ws_bytes); coordinates must lie in [-(2^20-1), 2^20-1] (bit 0 of
+ * *overflow, device int32, is set otherwise). */
+size_t hgsr_voxel_dedup_ws_bytes(int64_t n_grid);
+int hgsr_voxel_dedup(int64_t n_grid, const int32_t* grid_coords, int64_t n_cand, const int32_t* cand_coords,
+                     uint8_t* found, int32_t* overflow, void* ws, size_t ws_bytes, hgsr_stream_t stream);
+/* torch_scatter.scatter_max(src [n,F], index [n] int64, dim=0, dim_size=n_out)[0]
+ * (scene/lod_model.py:559): out [n_out,F]; rows no index reaches are 0. */
+int hgsr_scatter_max(int64_t n, int F, const float* src, const int64_t* index, int64_t n_out, float* out,
+                     hgsr_stream_t stream);
+/* GaussianLoDModel.weed_out (scene/lod_model.py:236-249, weed_ratio > 0 branch):
+ * mask[i] = mean over cameras (cam_infos [n_cams,4] = centre xyz, resolution scale) of
+ * levels[i] <= map_to_int_level(log2(standard_dist / dist) / log2(fork), street_levels-1)
+ * > weed_ratio.  dist2level_mode: 0 floor, 1 round, 2 ceil, 3 progressive. */
+int hgsr_weed_out(int64_t n, const float* positions, const int32_t* levels, int n_cams,
+                  const float* cam_infos, float standard_dist, float fork, int street_levels,
+                  int dist2level_mode, float weed_ratio, uint8_t* mask, hgsr_stream_t stream);
+
 /* ---- measurement ----------------------------------------------------------
  * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):
  * when enabled, the main kernel of every entry point is bracketed by

@@ -11,9 +11,12 @@ Pinned here:
   * scene/basic_model.py:297-371 generate_neural_gaussians (anchor -> Gaussian decode),
     RGB (view_dim=3) and SH2 (view_dim=0) variants, MLP shapes of scene/lod_model.py:67-84
   * utils/loss_utils.py:17-60 l1_loss / ssim and utils/image_utils.py:18-20 psnr
+  * scene/basic_model.py:96-144 training_statis, :179-190 get_remove_duplicates and
+    scene/lod_model.py:236-249 weed_out (their device="cuda" allocations mapped to the CPU)
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import sys
 import types
@@ -138,6 +141,89 @@ def golden_losses():
              psnr=psnr(a[None], b[None]).numpy())
 
 
+@contextlib.contextmanager
+def _cuda_as_cpu():
+    """Run reference code that allocates with device="cuda" / calls .cuda() on the CPU."""
+    names = ["zeros", "ones", "empty", "full", "tensor", "arange", "zeros_like", "ones_like"]
+    saved = {n: getattr(torch, n) for n in names}
+
+    def wrap(orig):
+        def f(*a, **k):
+            if "device" in k and str(k["device"]).startswith("cuda"):
+                k["device"] = "cpu"
+            return orig(*a, **k)
+        return f
+
+    for n in names:
+        setattr(torch, n, wrap(saved[n]))
+    saved_cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    try:
+        yield
+    finally:
+        for n in names:
+            setattr(torch, n, saved[n])
+        torch.Tensor.cuda = saved_cuda
+
+
+def golden_densify():
+    """scene/basic_model.py:96-144 training_statis (mean/mean and max/max), :179-190
+    get_remove_duplicates, scene/lod_model.py:236-249 weed_out."""
+    from types import SimpleNamespace
+    out = {}
+    g = torch.Generator().manual_seed(41)
+    A, k = 300, 10
+    model = _make_lod_model(A, 3, "RGB", seed=41)
+    vis = torch.rand(A, generator=g) < 0.7
+    Av = int(vis.sum())
+    sel = torch.rand(Av * k, generator=g) < 0.6
+    M = int(sel.sum())
+    radii = torch.randint(0, 12, (M,), generator=g, dtype=torch.int32)
+    filt = radii > 0
+    grad = torch.randn(1, M, 2, generator=g) * 1e-3
+    opac = torch.rand(M, 1, generator=g)
+    W, H = 640, 360
+    out.update(vis=vis.numpy(), sel=sel.numpy(), radii=radii.numpy(), filt=filt.numpy(), grad=grad.numpy(),
+               opacity=opac.numpy(), W=np.int32(W), H=np.int32(H), n_offsets=np.int32(k))
+    for tag, ptype, gtype in [("mean", "mean", "mean"), ("max", "max", "max")]:
+        st = dict(anchor_opacity_accum=torch.rand(A, 1, generator=g), anchor_demon=torch.randint(0, 5, (A, 1), generator=g).float(),
+                  offset_gradient_accum=torch.rand(A * k, 1, generator=g) * 1e-2,
+                  offset_denom=torch.randint(0, 5, (A * k, 1), generator=g).float(),
+                  max_radii2D=torch.randint(0, 8, (A * k,), generator=g).float(),
+                  offset_opacity_accum=torch.rand(A * k, 1, generator=g))
+        for n, v in st.items():
+            out[f"{tag}_in_{n}"] = v.numpy().copy()
+            setattr(model, n, v.clone())
+        vsp = grad.clone().requires_grad_(True)
+        vsp.grad = grad.clone()
+        pkg = dict(selection_mask=sel, visible_mask=vis, viewspace_points=vsp, visibility_filter=filt,
+                   opacity=opac, radii=radii)
+        with _cuda_as_cpu():
+            model.training_statis(SimpleNamespace(pruning_type=ptype, growing_type=gtype), pkg, W, H)
+        for n in st:
+            out[f"{tag}_out_{n}"] = getattr(model, n).numpy()
+    # get_remove_duplicates: existing voxels and candidates with a known overlap
+    grid = torch.unique(torch.randint(-300, 300, (5000, 3), generator=g, dtype=torch.int32), dim=0)
+    cand = torch.cat([grid[torch.randperm(grid.shape[0], generator=g)[:700]],
+                      torch.randint(-300, 300, (900, 3), generator=g, dtype=torch.int32)])
+    cand = torch.unique(cand, dim=0)
+    with _cuda_as_cpu():
+        dup = model.get_remove_duplicates(grid, cand)
+    out.update(grid_coords=grid.numpy(), cand_coords=cand.numpy(), duplicates=dup.numpy())
+    # weed_out over 137 cameras
+    model.weed_ratio = 0.3
+    model.cam_infos = torch.cat([torch.rand(137, 3, generator=g) * 40 - 20, 0.5 + torch.rand(137, 1, generator=g)], 1)
+    pos = torch.rand(2000, 3, generator=g) * 60 - 30
+    lev = torch.randint(0, 8, (2000,), generator=g, dtype=torch.int32)
+    with _cuda_as_cpu():
+        wm = model.weed_out(pos, lev)
+    out.update(weed_pos=pos.numpy(), weed_levels=lev.numpy(), weed_cams=model.cam_infos.numpy(),
+               weed_ratio=np.float32(model.weed_ratio), weed_mask=wm.numpy(),
+               standard_dist=np.float32(model.standard_dist), fork=np.int32(model.fork),
+               street_levels=np.int32(model.street_levels))
+    np.savez(os.path.join(OUT, "densify.npz"), **out)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     sys.path.insert(0, REF)
@@ -145,6 +231,7 @@ def main():
     golden_sh()
     golden_decode()
     golden_losses()
+    golden_densify()
     print("wrote", sorted(os.listdir(OUT)))
 
 
