@@ -13,6 +13,8 @@ Pinned here:
   * utils/loss_utils.py:17-60 l1_loss / ssim and utils/image_utils.py:18-20 psnr
   * scene/basic_model.py:96-144 training_statis, :179-190 get_remove_duplicates and
     scene/lod_model.py:236-249 weed_out (their device="cuda" allocations mapped to the CPU)
+  * scene/lod_model.py:487-596 anchor_growing (fine stage), with torch_scatter.scatter_max
+    (absent third-party dependency, torch_scatter 2.x) restated in _scatter_max_restated
 """
 from __future__ import annotations
 
@@ -224,6 +226,54 @@ def golden_densify():
     np.savez(os.path.join(OUT, "densify.npz"), **out)
 
 
+def _scatter_max_restated(src, index, dim=0, out=None, dim_size=None):
+    """torch_scatter 2.x scatter_max (the reference's dependency, absent here), restated:
+    out[i] = elementwise max of the src rows with index i, 0 for rows no index reaches;
+    the argmax output is not used by the reference (lod_model.py:559 takes [0])."""
+    n = int(index.max()) + 1 if dim_size is None else dim_size
+    res = torch.full((n,) + tuple(src.shape[1:]), float("-inf"), dtype=src.dtype)
+    res = res.scatter_reduce(0, index, src, reduce="amax", include_self=True)
+    res[torch.isinf(res) & (res < 0)] = 0
+    return res, None
+
+
+def golden_anchor_growing():
+    """scene/lod_model.py:487-596 anchor_growing (fine stage, weed_out active) on the CPU."""
+    import torch.nn as nn
+    from types import SimpleNamespace
+    import scene.lod_model as LM
+    LM.scatter_max = _scatter_max_restated
+    g = torch.Generator().manual_seed(51)
+    A, k = 400, 10
+    model = _make_lod_model(A, 3, "RGB", seed=51)
+    model._level = torch.randint(0, 4, (A, 1), generator=g).float()
+    model.training_stage, model.aerial_levels, model.street_levels = "fine", 1, 4
+    model.voxel_size, model.padding = 0.5, 0.0
+    model.weed_ratio = 0.05
+    model.cam_infos = torch.cat([torch.rand(64, 3, generator=g) * 40 - 20, 0.5 + torch.rand(64, 1, generator=g)], 1)
+    model.anchor_demon = torch.rand(A, 1, generator=g)
+    model.anchor_opacity_accum = torch.rand(A, 1, generator=g)
+    for n in ("_anchor", "_offset", "_anchor_feat", "_scaling", "_rotation"):
+        setattr(model, n, nn.Parameter(getattr(model, n).clone()))
+    model.optimizer = torch.optim.Adam([
+        {"params": [model._anchor], "name": "anchor"}, {"params": [model._offset], "name": "offset"},
+        {"params": [model._anchor_feat], "name": "anchor_feat"}, {"params": [model._scaling], "name": "scaling"},
+        {"params": [model._rotation], "name": "rotation"}], lr=0.0)
+    before = {n: getattr(model, n).detach().numpy().copy() for n in
+              ("_anchor", "_offset", "_anchor_feat", "_scaling", "_rotation", "_level", "_extra_level",
+               "anchor_demon", "anchor_opacity_accum")}
+    grads = torch.rand(A * k, generator=g) * 0.0004
+    offset_mask = torch.rand(A * k, generator=g) < 0.7
+    opt = SimpleNamespace(update_ratio=0.5, densify_grad_threshold=0.0002, extra_ratio=0.25, extra_up=0.01,
+                          overlap=False)
+    with _cuda_as_cpu():
+        model.anchor_growing(grads.clone(), opt, offset_mask, 1000)
+    after = {n: getattr(model, n).detach().numpy() for n in before}
+    np.savez(os.path.join(OUT, "anchor_growing.npz"), grads=grads.numpy(), offset_mask=offset_mask.numpy(),
+             cam_infos=model.cam_infos.numpy(), standard_dist=np.float32(model.standard_dist),
+             **{"in" + n: v for n, v in before.items()}, **{"out" + n: v for n, v in after.items()})
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     sys.path.insert(0, REF)
@@ -232,6 +282,7 @@ def main():
     golden_decode()
     golden_losses()
     golden_densify()
+    golden_anchor_growing()
     print("wrote", sorted(os.listdir(OUT)))
 
 

@@ -112,3 +112,42 @@ def test_weed_out_modes_vs_oracle(mode):
     # per-camera levels can flip at exact integer boundaries by one ulp of log2: allow a
     # handful of candidates whose visible fraction sits on the ratio
     assert int((m != ref).sum()) <= 2
+
+
+class _LoDShim:
+    """The attributes GaussianLoDModel.anchor_growing touches (scene/lod_model.py:487-596),
+    with cat_tensors_to_optimizer reduced to the concatenation (no optimizer state)."""
+
+    def __init__(self, g):
+        t = lambda k: torch.from_numpy(g[k]).to(DEV)
+        self._anchor, self._offset, self._anchor_feat = t("in_anchor"), t("in_offset"), t("in_anchor_feat")
+        self._scaling, self._rotation = t("in_scaling"), t("in_rotation")
+        self._level, self._extra_level = t("in_level"), t("in_extra_level")
+        self.anchor_demon, self.anchor_opacity_accum = t("inanchor_demon"), t("inanchor_opacity_accum")
+        self.feat_dim, self.n_offsets, self.street_levels, self.fork = 32, 10, 4, 2
+        self.training_stage, self.aerial_levels, self.voxel_size, self.padding = "fine", 1, 0.5, 0.0
+        self.weed_ratio, self.cam_infos = 0.05, t("cam_infos")
+        self.standard_dist, self.dist2level = float(g["standard_dist"]), "floor"
+
+    get_anchor = property(lambda self: self._anchor)
+    get_level = property(lambda self: self._level)
+    get_scaling = property(lambda self: torch.exp(self._scaling))
+
+    def cat_tensors_to_optimizer(self, d):
+        return {k: torch.cat([getattr(self, "_" + k), v], 0) for k, v in d.items()}
+
+
+def test_anchor_growing_matches_reference():
+    """End to end against the reference's own anchor_growing (fine stage, weed-out on):
+    the same new anchors in the same order, with the same scatter-max features."""
+    from horizongs_amd import densify as HD
+    g = np.load(os.path.join(GOLD, "anchor_growing.npz"))
+    m = _LoDShim(g)
+    opt = SimpleNamespace(update_ratio=0.5, densify_grad_threshold=0.0002, extra_ratio=0.25, extra_up=0.01,
+                          overlap=False)
+    HD.anchor_growing(m, torch.from_numpy(g["grads"]).to(DEV), opt, torch.from_numpy(g["offset_mask"]).to(DEV), 1000)
+    for n in ("_anchor", "_offset", "_anchor_feat", "_scaling", "_rotation", "_level", "_extra_level",
+              "anchor_demon", "anchor_opacity_accum"):
+        got = getattr(m, n).cpu().numpy()
+        assert got.shape == g["out" + n].shape, n
+        np.testing.assert_allclose(got, g["out" + n], rtol=1e-6, atol=1e-7, err_msg=n)
