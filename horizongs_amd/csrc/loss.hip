@@ -20,11 +20,14 @@
 
 namespace hgsr {
 
-constexpr int kLT = 16;            // tile edge
+constexpr int kLT = 32;            // tile edge (1024 pixels per 256-lane workgroup)
 constexpr int kLR = 5;             // window radius
-constexpr int kLH = kLT + 2 * kLR;  // 26: tile + halo
-constexpr int kLP = kLH + 1;       // staged row pitch
-constexpr int kHP = 24;            // filtered row pitch: rows 2 apart land 16 banks apart
+constexpr int kLH = kLT + 2 * kLR;  // 42: tile + halo
+constexpr int kLP = kLH + 1;       // staged row pitch (43: 4 rows x 8 column quads hit 32 banks)
+constexpr int kHP = kLT + 1;       // filtered row pitch (33: same for the quad writes)
+constexpr int kLS = (kLH * kLH + 255) / 256;  // 7 staged positions per lane
+constexpr int kLQ4 = kLT / 4;      // column / row quads per tile edge
+constexpr int kLC = 3;             // channels held in registers (the loss is defined on RGB)
 constexpr int kLQ = 8;  // partial sums per tile: l1, ssim, sky, entropy, scale-prod, normal, distortion, inv-depth
 
 // utils/loss_utils.py:20-22 window, exp(-(x - 5)^2 / (2 * 1.5^2)) normalised, rounded to
@@ -109,37 +112,73 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
     return red[0] + red[1] + red[2] + red[3];
 }
 
-// Per-thread share of the 26x26 staged window: positions e = tid + 256 i, i < 3.
-constexpr int kLS = (kLH * kLH + 255) / 256;  // 3
-
-struct StagePos {
-    int lds[kLS];        // r * kLP + q, or -1 past the window
-    bool in[kLS];        // inside the image (else zero padding)
-    unsigned pix[kLS];   // y * W + x
-    unsigned oi[kLS];    // element offsets in image / gt at channel 0 (32-bit: uniform base + lane offset)
-    unsigned og[kLS];
-};
-
-__device__ __forceinline__ StagePos stage_positions(int H, int W, int x0, int y0, const Img& a, const Img& b) {
-    StagePos sp;
-#pragma unroll
-    for (int i = 0; i < kLS; ++i) {
-        const int e = threadIdx.x + 256 * i;
-        const int r = e / kLH, q = e - r * kLH;
-        const int yy = y0 + r, xx = x0 + q;
-        const bool in = e < kLH * kLH && yy >= 0 && yy < H && xx >= 0 && xx < W;
-        sp.lds[i] = e < kLH * kLH ? r * kLP + q : -1;
-        sp.in[i] = in;
-        sp.pix[i] = in ? (unsigned)(yy * W + xx) : 0u;
-        sp.oi[i] = in ? (unsigned)a.at(0, yy, xx) : 0u;
-        sp.og[i] = in ? (unsigned)b.at(0, yy, xx) : 0u;
-    }
-    return sp;
+// staged position i of this lane: LDS index, image coordinates, inside-image flag
+__device__ __forceinline__ bool stage_pos(int i, int H, int W, int x0, int y0, int& lds, int& yy, int& xx) {
+    const int e = threadIdx.x + 256 * i;
+    const int r = e / kLH, q = e - r * kLH;
+    lds = e < kLH * kLH ? r * kLP + q : -1;
+    yy = y0 + r;
+    xx = x0 + q;
+    return e < kLH * kLH && yy >= 0 && yy < H && xx >= 0 && xx < W;
 }
 
 // keeps the compiler from hoisting every LDS read of a filter pass to the top (which
 // costs ~60 live VGPRs and halves occupancy); LDS latency is hidden by the other waves
 __device__ __forceinline__ void sched_fence() { asm volatile("" ::: "memory"); }
+
+// horizontal pass over NM staged maps: (row, column quad) items, 14-sample scatter form
+// (each sample feeds up to four outputs, so only the accumulators stay live); map m of
+// item (r, q4) -> hout[m][r * kHP + 4 q4 + o].  PROD adds x^2, y^2, xy of maps 0 and 1.
+template <int NM, bool PROD>
+__device__ __forceinline__ void hpass(const float* const (&in)[NM], float* const (&hout)[PROD ? 5 : NM]) {
+    constexpr int NO = PROD ? 5 : NM;
+    for (int item = threadIdx.x; item < kLH * kLQ4; item += 256) {
+        const int q4 = item & (kLQ4 - 1), r = item / kLQ4;
+        float acc[4][NO] = {};
+#pragma unroll
+        for (int t = 0; t < 14; ++t) {
+            sched_fence();
+            float v[NO];
+#pragma unroll
+            for (int m = 0; m < NM; ++m) v[m] = in[m][r * kLP + 4 * q4 + t];
+            if constexpr (PROD) {
+                v[2] = v[0] * v[0];
+                v[3] = v[1] * v[1];
+                v[4] = v[0] * v[1];
+            }
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                if (t - o < 0 || t - o > 10) continue;
+#pragma unroll
+                for (int m = 0; m < NO; ++m) acc[o][m] += kWin[t - o] * v[m];
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < 4; ++o)
+#pragma unroll
+            for (int m = 0; m < NO; ++m) hout[m][r * kHP + 4 * q4 + o] = acc[o][m];
+    }
+}
+
+// vertical pass: lane (column tx, row quad qd) filters 14 rows of each map into 4 outputs
+template <int NO>
+__device__ __forceinline__ void vpass(float* const (&h)[NO], int tx, int qd, float (&acc)[NO][4]) {
+#pragma unroll
+    for (int m = 0; m < NO; ++m)
+#pragma unroll
+        for (int o = 0; o < 4; ++o) acc[m][o] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 14; ++t) {
+        sched_fence();
+#pragma unroll
+        for (int m = 0; m < NO; ++m) {
+            const float v = h[m][(4 * qd + t) * kHP + tx];
+#pragma unroll
+            for (int o = 0; o < 4; ++o)
+                if (t - o >= 0 && t - o <= 10) acc[m][o] += kWin[t - o] * v;
+        }
+    }
+}
 
 struct LossFwdSmem {
     float x[kLH * kLP];
@@ -170,10 +209,10 @@ __device__ __forceinline__ SsimPix ssim_pix(float mu1, float mu2, float ex2, flo
     return o;
 }
 
-// forward: SSIM statistics + derivative maps, L1, alpha terms, scale products; per-tile
-// partials, layout [kLQ][n_tiles].  Channels are processed one at a time with the next
-// channel's window already in flight in registers (LDS-only barriers keep it in flight).
-__global__ __launch_bounds__(256) void loss_fwd_kernel(int C, int H, int W, Img img, Img gt,
+// forward: SSIM statistics + derivative maps, L1, alpha / aux terms, scale products;
+// per-tile partials, layout [kLQ][n_tiles].  Channels are processed one at a time with
+// the next channel's window already in flight in registers (LDS-only barriers keep it so).
+__global__ __launch_bounds__(256, 3) void loss_fwd_kernel(int C, int H, int W, Img img, Img gt,
                                                        const float* __restrict__ mask,
                                                        const float* __restrict__ alpha, ScaleReg sr, LossAux ax,
                                                        float* __restrict__ dmaps, float* __restrict__ partials) {
@@ -183,102 +222,86 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(int C, int H, int W, Img 
     const int x0 = bx * kLT - kLR, y0 = by * kLT - kLR;
     const int64_t HW = (int64_t)H * W;
     const int tid = threadIdx.x;
-    const StagePos sp = stage_positions(H, W, x0, y0, img, gt);
-    float nx[kLS], ny[kLS], mk[kLS];
-    auto fetch = [&](int c) {
-        const float* __restrict__ bi = img.p + c * img.sc;
-        const float* __restrict__ bg = gt.p + c * gt.sc;
+    // the whole window for every channel is loaded up front: a pixel's channels are read
+    // together (channels-last renders are not re-fetched once per channel)
+    float nx[kLC][kLS], ny[kLC][kLS], nm[kLS];
 #pragma unroll
-        for (int i = 0; i < kLS; ++i) {
-            nx[i] = sp.in[i] ? bi[sp.oi[i]] : 0.f;
-            ny[i] = sp.in[i] ? bg[sp.og[i]] : 0.f;
+    for (int i = 0; i < kLS; ++i) {
+        int l, yy, xx;
+        const bool in = stage_pos(i, H, W, x0, y0, l, yy, xx);
+#pragma unroll
+        for (int c = 0; c < kLC; ++c) {
+            const bool ok = in && c < C;
+            nx[c][i] = ok ? img.p[(unsigned)(c * img.sc + yy * img.sy + xx * img.sx)] : 0.f;
+            ny[c][i] = ok ? gt.p[(unsigned)(c * gt.sc + yy * gt.sy + xx * gt.sx)] : 0.f;
         }
-    };
-    fetch(0);
-#pragma unroll
-    for (int i = 0; i < kLS; ++i) mk[i] = (sp.in[i] && mask) ? mask[sp.pix[i]] : 1.f;
-    // per-pixel alpha terms and this block's share of the scale products, issued up front
-    const int px1 = bx * kLT + (tid & 15), py1 = by * kLT + (tid >> 4);
-    const bool inside1 = px1 < W && py1 < H;
-    float sky = 0.f, ent = 0.f;
-    if (alpha && inside1) {
-        const int64_t p = (int64_t)py1 * W + px1;
-        const float o = fminf(fmaxf(alpha[p], 1e-6f), 1.f - 1e-6f);
-        const float sk = mask ? mask[p] : 1.f;
-        sky = -(1.f - sk) * logf(1.f - o);
-        ent = -o * logf(o);
+        nm[i] = (in && mask) ? mask[(unsigned)(yy * W + xx)] : 1.f;
     }
-    float aux[3] = {0.f, 0.f, 0.f};
-    if (inside1) aux_terms(ax, alpha, mask, W, py1, px1, aux);
+    // per-pixel alpha / aux terms and this block's share of the scale products
+    float sky = 0.f, ent = 0.f, aux[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < kLT * kLT / 256; ++j) {
+        const int pl = tid + 256 * j;
+        const int px = bx * kLT + (pl & (kLT - 1)), py = by * kLT + pl / kLT;
+        if (px >= W || py >= H) continue;
+        const int64_t p = (int64_t)py * W + px;
+        if (alpha) {
+            const float o = fminf(fmaxf(alpha[p], 1e-6f), 1.f - 1e-6f);
+            const float sk = mask ? mask[p] : 1.f;
+            sky += -(1.f - sk) * logf(1.f - o);
+            ent += -o * logf(o);
+        }
+        float t[3];
+        aux_terms(ax, alpha, mask, W, py, px, t);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) aux[q] += t[q];
+    }
     float dreg = 0.f;
     if (sr.s) {
         const int64_t per = (sr.n + gridDim.x - 1) / gridDim.x;
         const int64_t g0 = (int64_t)blockIdx.x * per, g1 = min(sr.n, g0 + per);
         for (int64_t g = g0 + tid; g < g1; g += 256) dreg += row_prod(sr.s + g * sr.k, sr.k);
     }
+    const int tx = tid & (kLT - 1), qd = tid / kLT;  // vertical pass: column, row quad
+    const int vx = bx * kLT + tx;
     float l1 = 0.f, ss = 0.f;
-    for (int c = 0; c < C; ++c) {
-        lds_barrier();  // previous channel's vertical pass is done with sm.x / sm.h
 #pragma unroll
-        for (int i = 0; i < kLS; ++i)
-            if (sp.lds[i] >= 0) {
-                sm.x[sp.lds[i]] = nx[i] * mk[i];
-                sm.y[sp.lds[i]] = ny[i] * mk[i];
+    for (int c = 0; c < kLC; ++c) {
+        if (c >= C) break;
+        lds_barrier();  // previous channel's passes are done with sm.x / sm.h
+#pragma unroll
+        for (int i = 0; i < kLS; ++i) {
+            int l, yy, xx;
+            stage_pos(i, H, W, x0, y0, l, yy, xx);
+            if (l >= 0) {
+                sm.x[l] = nx[c][i] * nm[i];
+                sm.y[l] = ny[c][i] * nm[i];
             }
-        if (c + 1 < C) fetch(c + 1);
-        lds_barrier();
-        // horizontal: (row, column pair) items, 12-wide register window
-        if (tid < kLH * (kLT / 2)) {
-            const int qp = tid & 7, r = tid >> 3;
-            // scatter form: each input sample feeds both outputs, so only the 10
-            // accumulators stay live
-            float acc[2][5] = {};
-#pragma unroll
-            for (int t = 0; t < 12; ++t) {
-                sched_fence();
-                const float xk = sm.x[r * kLP + 2 * qp + t], yk = sm.y[r * kLP + 2 * qp + t];
-                const float v[5] = {xk, yk, xk * xk, yk * yk, xk * yk};
-#pragma unroll
-                for (int o = 0; o < 2; ++o) {
-                    if (t - o < 0 || t - o > 10) continue;
-#pragma unroll
-                    for (int m = 0; m < 5; ++m) acc[o][m] += kWin[t - o] * v[m];
-                }
-            }
-#pragma unroll
-            for (int o = 0; o < 2; ++o)
-#pragma unroll
-                for (int m = 0; m < 5; ++m) sm.h[m][r * kHP + 2 * qp + o] = acc[o][m];
         }
         lds_barrier();
-        // vertical: (column, row pair) items, 12-row register window per moment
-        if (tid < kLT * (kLT / 2)) {
-            const int tx = tid & 15, pr = tid >> 4;
-            float acc[5][2] = {};
+        {
+            const float* const in[2] = {sm.x, sm.y};
+            float* const ho[5] = {sm.h[0], sm.h[1], sm.h[2], sm.h[3], sm.h[4]};
+            hpass<2, true>(in, ho);
+        }
+        lds_barrier();
+        float acc[5][4];
+        {
+            float* const hh[5] = {sm.h[0], sm.h[1], sm.h[2], sm.h[3], sm.h[4]};
+            vpass<5>(hh, tx, qd, acc);
+        }
 #pragma unroll
-            for (int t = 0; t < 12; ++t) {
-                sched_fence();
-#pragma unroll
-                for (int m = 0; m < 5; ++m) {
-                    const float v = sm.h[m][(2 * pr + t) * kHP + tx];
-                    if (t <= 10) acc[m][0] += kWin[t] * v;
-                    if (t >= 1) acc[m][1] += kWin[t - 1] * v;
-                }
-            }
-            const int px = bx * kLT + tx;
-#pragma unroll
-            for (int o = 0; o < 2; ++o) {
-                const int ty = 2 * pr + o, py = by * kLT + ty;
-                if (px >= W || py >= H) continue;
-                const SsimPix sp2 = ssim_pix(acc[0][o], acc[1][o], acc[2][o], acc[3][o], acc[4][o]);
-                const int64_t p = (int64_t)c * HW + (int64_t)py * W + px;
-                dmaps[p] = sp2.dm0;
-                dmaps[(int64_t)C * HW + p] = sp2.ds11;
-                dmaps[2 * (int64_t)C * HW + p] = sp2.ds12;
-                ss += sp2.S;
-                const int li = (ty + kLR) * kLP + tx + kLR;
-                l1 += fabsf(sm.x[li] - sm.y[li]);
-            }
+        for (int o = 0; o < 4; ++o) {
+            const int ty = 4 * qd + o, py = by * kLT + ty;
+            if (vx >= W || py >= H) continue;
+            const SsimPix sp2 = ssim_pix(acc[0][o], acc[1][o], acc[2][o], acc[3][o], acc[4][o]);
+            const int64_t p = (int64_t)c * HW + (int64_t)py * W + vx;
+            dmaps[p] = sp2.dm0;
+            dmaps[(int64_t)C * HW + p] = sp2.ds11;
+            dmaps[2 * (int64_t)C * HW + p] = sp2.ds12;
+            ss += sp2.S;
+            const int li = (ty + kLR) * kLP + tx + kLR;
+            l1 += fabsf(sm.x[li] - sm.y[li]);
         }
     }
     l1 = block_sum(l1, sm.red);
@@ -300,7 +323,8 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(int C, int H, int W, Img 
     }
 }
 
-// fixed-order f64 reduction of the tile partials -> [loss, l1, ssim, sky, entropy, scale_reg]
+// fixed-order f64 reduction of the tile partials -> [loss, l1, ssim, sky, entropy, scale_reg, normal,
+// distortion, inv_depth]
 __global__ __launch_bounds__(256) void loss_reduce_kernel(int n_tiles, int C, int64_t HW, int64_t n_sc,
                                                           LossLam lam, const float* __restrict__ partials,
                                                           float* __restrict__ out) {
@@ -363,8 +387,52 @@ __device__ __forceinline__ LossCoef loss_coef(const float* __restrict__ g_out, i
     return k;
 }
 
-// backward: d loss / d image (and d alpha, d scaling); same channel pipeline as the forward
-__global__ __launch_bounds__(256) void loss_bwd_kernel(int C, int H, int W, Img img, Img gt,
+// per-pixel gradients of the alpha and aux terms (and the zero trailing channels)
+__device__ __forceinline__ void pixel_grads(const LossCoef& k, const LossAux& ax, const float* __restrict__ alpha,
+                                            const float* __restrict__ mask, float* __restrict__ g_img, const Img& gi,
+                                            int C, int extra_ch, float* __restrict__ g_alpha, int W, int py, int px) {
+    const int64_t pp = (int64_t)py * W + px;
+    const float mk = mask ? mask[pp] : 1.f;
+    if (g_alpha) {
+        float ga = 0.f;
+        if (alpha) {
+            const float a = alpha[pp];
+            const bool pass = a >= 1e-6f && a <= 1.f - 1e-6f;  // clamp passes the gradient inside
+            const float o = fminf(fmaxf(a, 1e-6f), 1.f - 1e-6f);
+            const float d_sky = (1.f - mk) / (1.f - o);
+            const float d_ent = -(logf(o) + 1.f);
+            ga = pass ? k.sky * d_sky + k.ent * d_ent : 0.f;
+        }
+        g_alpha[pp] = ga;
+    }
+    if (ax.nrm) {  // d/dn = -mask nfd a, d/dnfd = -mask n a (alpha detached, train.py:183)
+        const float a = alpha ? alpha[pp] : 1.f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int64_t in = c * ax.ns[0] + py * ax.ns[1] + px * ax.ns[2];
+            const int64_t iF = c * ax.fs[0] + py * ax.fs[1] + px * ax.fs[2];
+            const float n = ax.nrm[in], f = ax.nfd[iF];
+            if (ax.g_nrm) ax.g_nrm[in] = -k.nrm * mk * f * a;
+            if (ax.g_nfd) ax.g_nfd[iF] = -k.nrm * mk * n * a;
+        }
+    }
+    if (ax.dist && ax.g_dist) ax.g_dist[py * ax.dst[0] + px * ax.dst[1]] = k.dist * mk;
+    if (ax.depth && ax.g_depth) {
+        const int64_t id = py * ax.dps[0] + px * ax.dps[1];
+        const float d = ax.depth[id];
+        float g = 0.f;
+        if (d > 0.f) {
+            const float dm = ax.dmask ? ax.dmask[pp] : 1.f;
+            const float e = (1.f / d - ax.mono[pp]) * dm;
+            const float sg = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+            g = k.dep * sg * dm * (-1.f / (d * d));
+        }
+        ax.g_depth[id] = g;
+    }
+}
+
+// backward: d loss / d image (and d alpha, d scaling, aux); same channel pipeline as the forward
+__global__ __launch_bounds__(256, 3) void loss_bwd_kernel(int C, int H, int W, Img img, Img gt,
                                                        const float* __restrict__ mask,
                                                        const float* __restrict__ alpha, ScaleReg sr, LossAux ax,
                                                        LossLam lam, const float* __restrict__ dmaps,
@@ -377,93 +445,42 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(int C, int H, int W, Img 
     const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
     const int x0 = bx * kLT - kLR, y0 = by * kLT - kLR;
     const int64_t HW = (int64_t)H * W;
-    const StagePos sp = stage_positions(H, W, x0, y0, img, gt);
-    // vertical-pass pixels of this lane: column tx, rows 2 pr + {0, 1}
-    const int tx = tid & 15, pr = (tid >> 4) & 7;
-    const bool vlane = tid < kLT * (kLT / 2);
+    const int tx = tid & (kLT - 1), qd = tid / kLT;
     const int vx = bx * kLT + tx;
-    bool vin[2];
-    float vmk[2];
+    float nd[3][kLS];
+    auto fetch = [&](int c) {  // planar derivative maps: one channel ahead
 #pragma unroll
-    for (int o = 0; o < 2; ++o) {
-        const int vy = by * kLT + 2 * pr + o;
-        vin[o] = vlane && vx < W && vy < H;
-        vmk[o] = (vin[o] && mask) ? mask[(int64_t)vy * W + vx] : 1.f;
-    }
-    unsigned voi[2], vog[2];
+        for (int i = 0; i < kLS; ++i) {
+            int l, yy, xx;
+            const bool in = stage_pos(i, H, W, x0, y0, l, yy, xx);
 #pragma unroll
-    for (int o = 0; o < 2; ++o) {
-        const int vy = by * kLT + 2 * pr + o;
-        voi[o] = vin[o] ? (unsigned)img.at(0, vy, vx) : 0u;
-        vog[o] = vin[o] ? (unsigned)gt.at(0, vy, vx) : 0u;
-    }
-    float nm[3][kLS], nx[2], ny[2];
-    auto fetch = [&](int c) {
-#pragma unroll
-        for (int m = 0; m < 3; ++m) {
-            const float* __restrict__ bm = dmaps + ((int64_t)m * C + c) * HW;
-#pragma unroll
-            for (int i = 0; i < kLS; ++i) nm[m][i] = sp.in[i] ? bm[sp.pix[i]] : 0.f;
-        }
-        const float* __restrict__ bi = img.p + c * img.sc;
-        const float* __restrict__ bg = gt.p + c * gt.sc;
-#pragma unroll
-        for (int o = 0; o < 2; ++o) {
-            nx[o] = vin[o] ? bi[voi[o]] : 0.f;
-            ny[o] = vin[o] ? bg[vog[o]] : 0.f;
+            for (int m = 0; m < 3; ++m)
+                nd[m][i] = in ? dmaps[((int64_t)m * C + c) * HW + (unsigned)(yy * W + xx)] : 0.f;
         }
     };
     fetch(0);
+    // this lane's four output pixels, every channel read together (channels-last renders)
+    float cx[kLC][4], cy[kLC][4], gimg[kLC][4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const int vy = by * kLT + 4 * qd + o;
+        const bool in = vx < W && vy < H;
+#pragma unroll
+        for (int c = 0; c < kLC; ++c) {
+            const bool ok = in && c < C;
+            cx[c][o] = ok ? img.p[(unsigned)(c * img.sc + vy * img.sy + vx * img.sx)] : 0.f;
+            cy[c][o] = ok ? gt.p[(unsigned)(c * gt.sc + vy * gt.sy + vx * gt.sx)] : 0.f;
+            gimg[c][o] = 0.f;
+        }
+    }
     const LossCoef k = loss_coef(g_out, C, HW, sr.n, lam);
     Img gi = img;
     gi.p = g_img;
-    {
-        const int px = bx * kLT + (tid & 15), py = by * kLT + (tid >> 4);
-        const bool inside = px < W && py < H;
-        const int64_t pp = (int64_t)py * W + px;
-        // trailing image channels the loss does not read (e.g. the ED channel of RGB+ED)
-        if (inside)
-            for (int c = C; c < C + extra_ch; ++c) g_img[gi.at(c, py, px)] = 0.f;
-        if (g_alpha && inside) {
-            float ga = 0.f;
-            if (alpha) {
-                const float a = alpha[pp];
-                const bool pass = a >= 1e-6f && a <= 1.f - 1e-6f;  // clamp passes the gradient inside
-                const float o = fminf(fmaxf(a, 1e-6f), 1.f - 1e-6f);
-                const float sk = mask ? mask[pp] : 1.f;
-                const float d_sky = (1.f - sk) / (1.f - o);
-                const float d_ent = -(logf(o) + 1.f);
-                ga = pass ? k.sky * d_sky + k.ent * d_ent : 0.f;
-            }
-            g_alpha[pp] = ga;
-        }
-        if (inside) {
-            const float mk = mask ? mask[pp] : 1.f;
-            if (ax.nrm) {  // d/dn = -mask nfd a, d/dnfd = -mask n a (alpha detached, train.py:183)
-                const float a = alpha ? alpha[pp] : 1.f;
 #pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const int64_t in = c * ax.ns[0] + py * ax.ns[1] + px * ax.ns[2];
-                    const int64_t iF = c * ax.fs[0] + py * ax.fs[1] + px * ax.fs[2];
-                    const float n = ax.nrm[in], f = ax.nfd[iF];
-                    if (ax.g_nrm) ax.g_nrm[in] = -k.nrm * mk * f * a;
-                    if (ax.g_nfd) ax.g_nfd[iF] = -k.nrm * mk * n * a;
-                }
-            }
-            if (ax.dist && ax.g_dist) ax.g_dist[py * ax.dst[0] + px * ax.dst[1]] = k.dist * mk;
-            if (ax.depth && ax.g_depth) {
-                const int64_t id = py * ax.dps[0] + px * ax.dps[1];
-                const float d = ax.depth[id];
-                float g = 0.f;
-                if (d > 0.f) {
-                    const float dm = ax.dmask ? ax.dmask[pp] : 1.f;
-                    const float e = (1.f / d - ax.mono[pp]) * dm;
-                    const float sg = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
-                    g = k.dep * sg * dm * (-1.f / (d * d));
-                }
-                ax.g_depth[id] = g;
-            }
-        }
+    for (int j = 0; j < kLT * kLT / 256; ++j) {
+        const int pl = tid + 256 * j;
+        const int px = bx * kLT + (pl & (kLT - 1)), py = by * kLT + pl / kLT;
+        if (px < W && py < H) pixel_grads(k, ax, alpha, mask, g_img, gi, C, extra_ch, g_alpha, W, py, px);
     }
     if (g_scaling) {  // d mean_i prod_j s_ij / d s_ij = prod_{l != j} s_il / n
         const int64_t per = (sr.n + gridDim.x - 1) / gridDim.x;
@@ -478,57 +495,54 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(int C, int H, int W, Img 
             }
         }
     }
-    for (int c = 0; c < C; ++c) {
+    float vmk[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const int vy = by * kLT + 4 * qd + o;
+        vmk[o] = (mask && vx < W && vy < H) ? mask[(int64_t)vy * W + vx] : 1.f;
+    }
+#pragma unroll
+    for (int c = 0; c < kLC; ++c) {
+        if (c >= C) break;
         lds_barrier();
 #pragma unroll
-        for (int i = 0; i < kLS; ++i)
-            if (sp.lds[i] >= 0)
+        for (int i = 0; i < kLS; ++i) {
+            int l, yy, xx;
+            stage_pos(i, H, W, x0, y0, l, yy, xx);
+            if (l >= 0)
 #pragma unroll
-                for (int m = 0; m < 3; ++m) sm.m[m][sp.lds[i]] = nm[m][i];
-        const float cx[2] = {nx[0], nx[1]}, cy[2] = {ny[0], ny[1]};
+                for (int m = 0; m < 3; ++m) sm.m[m][l] = nd[m][i];
+        }
         if (c + 1 < C) fetch(c + 1);
         lds_barrier();
-        if (tid < kLH * (kLT / 2)) {
-            const int qp = tid & 7, r = tid >> 3;
-            float acc[3][2] = {};
-#pragma unroll
-            for (int t = 0; t < 12; ++t) {
-                sched_fence();
-#pragma unroll
-                for (int m = 0; m < 3; ++m) {
-                    const float v = sm.m[m][r * kLP + 2 * qp + t];
-                    if (t <= 10) acc[m][0] += kWin[t] * v;
-                    if (t >= 1) acc[m][1] += kWin[t - 1] * v;
-                }
-            }
-#pragma unroll
-            for (int m = 0; m < 3; ++m)
-#pragma unroll
-                for (int o = 0; o < 2; ++o) sm.h[m][r * kHP + 2 * qp + o] = acc[m][o];
+        {
+            const float* const in[3] = {sm.m[0], sm.m[1], sm.m[2]};
+            float* const ho[3] = {sm.h[0], sm.h[1], sm.h[2]};
+            hpass<3, false>(in, ho);
         }
         lds_barrier();
-        if (vlane) {
-            float acc[3][2] = {};
-#pragma unroll
-            for (int t = 0; t < 12; ++t) {
-                sched_fence();
-#pragma unroll
-                for (int m = 0; m < 3; ++m) {
-                    const float v = sm.h[m][(2 * pr + t) * kHP + tx];
-                    if (t <= 10) acc[m][0] += kWin[t] * v;
-                    if (t >= 1) acc[m][1] += kWin[t - 1] * v;
-                }
-            }
-#pragma unroll
-            for (int o = 0; o < 2; ++o) {
-                if (!vin[o]) continue;
-                const float x = cx[o] * vmk[o], y = cy[o] * vmk[o];
-                const float d = x - y;
-                const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-                const float gx = k.l1 * sgn + k.ss * (acc[0][o] + 2.f * x * acc[1][o] + y * acc[2][o]);
-                g_img[c * img.sc + voi[o]] = gx * vmk[o];
-            }
+        float acc[3][4];
+        {
+            float* const hh[3] = {sm.h[0], sm.h[1], sm.h[2]};
+            vpass<3>(hh, tx, qd, acc);
         }
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+            const float x = cx[c][o] * vmk[o], y = cy[c][o] * vmk[o];
+            const float d = x - y;
+            const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+            gimg[c][o] = (k.l1 * sgn + k.ss * (acc[0][o] + 2.f * x * acc[1][o] + y * acc[2][o])) * vmk[o];
+        }
+    }
+    // all channels of a pixel written together (plus the zero trailing channels)
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const int vy = by * kLT + 4 * qd + o;
+        if (vx >= W || vy >= H) continue;
+#pragma unroll
+        for (int c = 0; c < kLC; ++c)
+            if (c < C) g_img[(unsigned)(c * img.sc + vy * img.sy + vx * img.sx)] = gimg[c][o];
+        for (int c = C; c < C + extra_ch; ++c) g_img[(unsigned)(c * img.sc + vy * img.sy + vx * img.sx)] = 0.f;
     }
 }
 
@@ -617,7 +631,7 @@ extern "C" int hgsr_loss_fwd(int C, int H, int W, const float* image, const int6
                              const float* alpha, const float* scaling, int64_t n_scaling, int k_scaling,
                              const hgsr_loss_terms* terms, float* out, void* ws, size_t ws_bytes,
                              hgsr_stream_t stream) {
-    HGSR_REQUIRE(C >= 1 && H > 0 && W > 0, "bad dims");
+    HGSR_REQUIRE(C >= 1 && C <= kLC && H > 0 && W > 0, "bad dims (C must be 1..3)");
     HGSR_REQUIRE(image && gt && out && ws, "null pointer");
     static const bool win_ok = check_window();
     HGSR_REQUIRE(win_ok, "SSIM window constants disagree with utils/loss_utils.py's formula");
@@ -652,7 +666,7 @@ extern "C" int hgsr_loss_bwd(int C, int H, int W, const float* image, const int6
                              const hgsr_loss_terms* terms, const float* g_out, float* g_image, int extra_channels,
                              float* g_alpha, float* g_scaling, const hgsr_loss_aux_grads* aux_grads,
                              const void* ws, size_t ws_bytes, hgsr_stream_t stream) {
-    HGSR_REQUIRE(C >= 1 && H > 0 && W > 0, "bad dims");
+    HGSR_REQUIRE(C >= 1 && C <= kLC && H > 0 && W > 0, "bad dims (C must be 1..3)");
     HGSR_REQUIRE(image && gt && g_out && g_image && ws, "null pointer");
     HGSR_REQUIRE(ws_bytes >= hgsr_loss_ws_bytes(C, H, W), "loss workspace too small");
     LossLam lam;

@@ -293,7 +293,7 @@ int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
 
 /* ---- K15: fused training loss ---------------------------
  * replaces the loss head of reference train.py:153-202 with utils/loss_utils.py:17-60:
- * x = image*mask, y = gt*mask (image, gt [C,H,W]; mask [H,W] nullable); out[9] (device) =
+ * x = image*mask, y = gt*mask (image, gt [C,H,W], C <= 3; mask [H,W] nullable); out[9] (device) =
  * {loss, l1, ssim, sky, entropy, scale_reg, normal, distortion, inv_depth} with
  *   loss = (1-l)*mean|x-y| + l*(1-mean SSIM(x,y)) + l_dreg*mean_i prod_j scaling[i,j]
  *        + l_sky*mean(-(1-mask) log(1-a)) + l_ent*mean(-a log a)       (a = clamp(alpha, 1e-6, 1-1e-6))
