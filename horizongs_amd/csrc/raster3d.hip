@@ -117,6 +117,28 @@ __device__ __forceinline__ bool reaches(const float4 g0, const float4 g1, float 
     return fabsf(g0.x - qx) <= g1.z + 3.5f && fabsf(g0.y - qy) <= g1.w + 3.5f;
 }
 
+// Exact refinement of reaches(): the minimum of sigma' = a'dx^2 + b'dx dy + c'dy^2 over
+// the quadrant's pixel-centre rectangle (dx = x - px, px in qx +- 3.5) against the alpha
+// >= 1/255 level sigma' <= log2(255 o).  A convex quadratic attains its minimum over a
+// rectangle at the origin (if inside) or on an edge, where it is a 1-D parabola minimised
+// in closed form.  Conservative: a relative + absolute slack covers the rounding of the
+// per-pixel evaluation and of v_exp_f32, so a skipped record has alpha < 1/255 at every
+// pixel of the quadrant (forward and backward skip the same records).
+__device__ __forceinline__ bool ellipse_reaches(const float4 g0, const float4 g1, float qx, float qy) {
+    const float cx = g0.x - qx, cy = g0.y - qy;
+    const float x0 = cx - 3.5f, x1 = cx + 3.5f, y0 = cy - 3.5f, y1 = cy + 3.5f;
+    const float a = g0.z, b = g0.w, c = g1.x;
+    const float lim = __builtin_amdgcn_logf(255.0f * g1.y);  // log2
+    const float ia = -0.5f * __builtin_amdgcn_rcpf(a), ic = -0.5f * __builtin_amdgcn_rcpf(c);
+    auto q = [&](float dx, float dy) { return a * dx * dx + b * dx * dy + c * dy * dy; };
+    const float dya = fminf(fmaxf(b * x0 * ic, y0), y1), dyb = fminf(fmaxf(b * x1 * ic, y0), y1);
+    const float dxa = fminf(fmaxf(b * y0 * ia, x0), x1), dxb = fminf(fmaxf(b * y1 * ia, x0), x1);
+    float m = fminf(fminf(q(x0, dya), q(x1, dyb)), fminf(q(dxa, y0), q(dxb, y1)));
+    const bool inside = x0 <= 0.f && x1 >= 0.f && y0 <= 0.f && y1 >= 0.f;
+    m = inside ? 0.f : m;
+    return m <= lim + 1e-3f * fabsf(lim) + 1e-3f;
+}
+
 __device__ __forceinline__ int lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
@@ -210,7 +232,7 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
 #pragma unroll
         for (int k = 0; k < kFwdBatch / 64; ++k) {
             const int t = k * 64 + lane;
-            const bool rel = t < cnt && reaches(s_g0[t], s_g1[t], qx, qy);
+            const bool rel = t < cnt && reaches(s_g0[t], s_g1[t], qx, qy) && ellipse_reaches(s_g0[t], s_g1[t], qx, qy);
             const uint64_t m = __ballot(rel);
             if (rel) my_list[n_mine + lanes_below(m)] = (uint16_t)t;
             n_mine += __popcll(m);
@@ -363,7 +385,8 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
 #pragma unroll
         for (int k = 0; k < NB / 64; ++k) {
             const int t = k * 64 + lane;
-            const bool rel = t < bsz && t >= t0 && reaches(s_rec[cur][t][0], s_rec[cur][t][1], qx, qy);
+            const bool rel = t < bsz && t >= t0 && reaches(s_rec[cur][t][0], s_rec[cur][t][1], qx, qy) &&
+                             ellipse_reaches(s_rec[cur][t][0], s_rec[cur][t][1], qx, qy);
             const uint64_t m = __ballot(rel);
             if (rel) my_list[n_mine + lanes_below(m)] = (uint8_t)t;
             n_mine += __popcll(m);
