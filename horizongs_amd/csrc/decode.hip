@@ -28,6 +28,9 @@ constexpr int kDecTile = 64;      // visible anchors per workgroup iteration (4 
 constexpr int kDecF = 32;         // feat_dim (every reference config)
 constexpr int kDecS = 38;         // LDS row stride (floats) of W1 / W2 / X: conflict-free 16x4 fragment reads
 constexpr int kDecYS = 20;        // LDS row stride of the Y^T tiles: conflict-free accumulator stores
+// backward Y^T / dY^T / H^T stride: the MFMA fragment reads (rows i, columns 4kk+g) and the
+// per-row sums (one row per lane) dominate there, both conflict-free at an odd stride
+constexpr int kDecBS = 17;
 constexpr int kDecMaxRows = 368;  // W2 rows (opacity + cov + colour heads, padded to 16): SH2 x 10 offsets
 
 struct MlpPtrs {
@@ -379,6 +382,12 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
 // that decode_wgrad_reduce_kernel sums in a fixed order (deterministic).
 constexpr int kBwdChunk = 5;  // output tiles per launch
 
+// the backward only needs 1 - tanh^2 (absolute accuracy of tanh suffices): exp-based
+__device__ __forceinline__ float fast_tanh(float x) {
+    const float e = __expf(-2.0f * fabsf(x));
+    return copysignf((1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e), x);
+}
+
 struct DecodeGrads {
     const float* g_xyz;      // [M,3]
     const float* g_offsets;  // [M,3] nullable
@@ -401,8 +410,8 @@ struct DecodeBwdSmem {
     float w2[YR * kDecS];  // YR >= R rows: the cov head stages (and recomputes) all of its rows
     float b2[YR];
     float x[4][16 * kDecS];
-    float dy[4][YR * kDecYS];  // recomputed pre-activations Y^T, overwritten in place by dY^T[o][anchor]
-    float h[4][32 * kDecYS];                 // H^T, then dH^T [hidden][anchor]
+    float dy[4][YR * kDecBS];  // recomputed pre-activations Y^T, overwritten in place by dY^T[o][anchor]
+    float h[4][32 * kDecBS];                 // H^T, then dH^T [hidden][anchor]
     float acc[4][16 * 9];                    // per-anchor d scaling_raw (6) + d anchor (3)
 };
 
@@ -471,8 +480,8 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
         for (int r = 0; r < 4; ++r) {
             h0[r] = fmaxf(h0[r] + sm.b1[4 * g + r], 0.f);
             h1[r] = fmaxf(h1[r] + sm.b1[16 + 4 * g + r], 0.f);
-            sh[(4 * g + r) * kDecYS + i] = h0[r];
-            sh[(16 + 4 * g + r) * kDecYS + i] = h1[r];
+            sh[(4 * g + r) * kDecBS + i] = h0[r];
+            sh[(16 + 4 * g + r) * kDecBS + i] = h1[r];
         }
         // recompute the pre-activations the derivative needs
         if (head < 2) {
@@ -484,16 +493,16 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
 #pragma unroll
                 for (int r = 0; r < 4; ++r) y = mfma4(w[16 + 4 * r], h1[r], y);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) sy[(ot * 16 + 4 * g + r) * kDecYS + i] = y[r] + sm.b2[ot * 16 + 4 * g + r];
+                for (int r = 0; r < 4; ++r) sy[(ot * 16 + 4 * g + r) * kDecBS + i] = y[r] + sm.b2[ot * 16 + 4 * g + r];
             }
         }
         // dY^T for the chunk, in place over Y^T for the opacity / cov heads: every slot writes
         // all of its rows (zeros when dropped or absent), padding rows are zeroed separately
         if (head == 2) {
-            for (int e = lane; e < rows * 16; e += 64) sdy[(e >> 4) * kDecYS + (e & 15)] = 0.f;
+            for (int e = lane; e < rows * 16; e += 64) sdy[(e >> 4) * kDecBS + (e & 15)] = 0.f;
         } else {
             const int used = head == 0 ? noff : 7 * noff;
-            for (int e = lane; e < (srows - used) * 16; e += 64) sdy[(used + (e >> 4)) * kDecYS + (e & 15)] = 0.f;
+            for (int e = lane; e < (srows - used) * 16; e += 64) sdy[(used + (e >> 4)) * kDecBS + (e & 15)] = 0.f;
         }
         if (head == 0) {
             for (int s = lane; s < 16 * noff; s += 64) {
@@ -501,10 +510,10 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 const int p = a0 + a < d.Av ? slot_row[(int64_t)(a0 + a) * noff + k] : -1;
                 float v = 0.f;
                 if (p >= 0 && gr.g_opacity) {
-                    const float th = tanhf(sy[k * kDecYS + a]);
+                    const float th = fast_tanh(sy[k * kDecBS + a]);
                     v = gr.g_opacity[p] * (1.0f - th * th);
                 }
-                sdy[k * kDecYS + a] = v;
+                sdy[k * kDecBS + a] = v;
             }
         } else if (head == 1) {
             for (int s = lane; s < 16 * noff; s += 64) {
@@ -515,12 +524,12 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 float cv[7], dv[7];
 #pragma unroll
                 for (int q = 0; q < 7; ++q) {
-                    cv[q] = sy[(7 * k + q) * kDecYS + a];
+                    cv[q] = sy[(7 * k + q) * kDecBS + a];
                     dv[q] = 0.f;
                 }
                 if (p < 0) {
 #pragma unroll
-                    for (int q = 0; q < 7; ++q) sdy[(7 * k + q) * kDecYS + a] = 0.f;
+                    for (int q = 0; q < 7; ++q) sdy[(7 * k + q) * kDecBS + a] = 0.f;
                     if (present && t0 == 0) {
                         float* dof = gr.d_offset + ((int64_t)id * noff + k) * 3;
                         dof[0] = dof[1] = dof[2] = 0.f;
@@ -533,7 +542,7 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 if (gr.g_scaling) {
 #pragma unroll
                     for (int q = 0; q < 3; ++q) {
-                        const float es = expf(sr[3 + q]), sg = 1.0f / (1.0f + expf(-cv[q]));
+                        const float es = __expf(sr[3 + q]), sg = __builtin_amdgcn_rcpf(1.0f + __expf(-cv[q]));
                         const float gs = gr.g_scaling[(int64_t)p * 3 + q];
                         dv[q] = gs * es * sg * (1.0f - sg);
                         if (t0 == 0) atomicAdd(&sacc[a * 9 + 3 + q], gs * es * sg);
@@ -541,10 +550,10 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 }
                 // rot = v / max(|v|, 1e-12)
                 if (gr.g_rot) {
-                    const float nr = sqrtf(cv[3] * cv[3] + cv[4] * cv[4] + cv[5] * cv[5] + cv[6] * cv[6]);
+                    const float n2 = cv[3] * cv[3] + cv[4] * cv[4] + cv[5] * cv[5] + cv[6] * cv[6];
                     const float* gq = gr.g_rot + (int64_t)p * 4;
-                    if (nr > 1e-12f) {
-                        const float inv = 1.0f / nr;
+                    if (n2 > 1e-24f) {  // |v| > 1e-12
+                        const float inv = __builtin_amdgcn_rsqf(n2);
                         float dot = 0.f;
 #pragma unroll
                         for (int q = 0; q < 4; ++q) dot += cv[3 + q] * inv * gq[q];
@@ -556,7 +565,7 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                     }
                 }
 #pragma unroll
-                for (int q = 0; q < 7; ++q) sdy[(7 * k + q) * kDecYS + a] = dv[q];
+                for (int q = 0; q < 7; ++q) sdy[(7 * k + q) * kDecBS + a] = dv[q];
                 if (t0 != 0) continue;  // the position / offset chain belongs to the first cov chunk
                 // xyz = anchor + offset * exp(sr[0:3]); offsets_out = offset * exp(sr[0:3])
                 const float* of = offset + ((int64_t)id * noff + k) * 3;
@@ -564,7 +573,7 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 for (int q = 0; q < 3; ++q) {
                     const float gx = gr.g_xyz ? gr.g_xyz[(int64_t)p * 3 + q] : 0.f;
                     const float gt = gx + (gr.g_offsets ? gr.g_offsets[(int64_t)p * 3 + q] : 0.f);
-                    const float es = expf(sr[q]);
+                    const float es = __expf(sr[q]);
                     dof[q] = gt * es;
                     atomicAdd(&sacc[a * 9 + q], gt * of[q] * es);
                     atomicAdd(&sacc[a * 9 + 6 + q], gx);
@@ -577,7 +586,7 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 if (o >= O || a0 + a >= d.Av) continue;
                 const int k = o / cd, c = o - k * cd;
                 const int p = slot_row[(int64_t)(a0 + a) * noff + k];
-                if (p >= 0) sdy[ol * kDecYS + a] = gr.g_color[(int64_t)p * cd + c];
+                if (p >= 0) sdy[ol * kDecBS + a] = gr.g_color[(int64_t)p * cd + c];
             }
         }
         // per-anchor d scaling_raw / d anchor of the cov head (xyz and scaling outputs)
@@ -597,8 +606,8 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 for (int ht = 0; ht < 2; ++ht) {
 #pragma unroll
                     for (int kk = 0; kk < 4; ++kk)
-                        aw2[ot][ht] = mfma4(sdy[(co + ot * 16 + i) * kDecYS + 4 * kk + g],
-                                            sh[(ht * 16 + i) * kDecYS + 4 * kk + g], aw2[ot][ht]);
+                        aw2[ot][ht] = mfma4(sdy[(co + ot * 16 + i) * kDecBS + 4 * kk + g],
+                                            sh[(ht * 16 + i) * kDecBS + 4 * kk + g], aw2[ot][ht]);
                 }
             }
         }
@@ -608,7 +617,7 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
             if (ol < rows) {
                 float sum = 0.f;
 #pragma unroll
-                for (int a = 0; a < 16; ++a) sum += sdy[(co + ol) * kDecYS + a];
+                for (int a = 0; a < 16; ++a) sum += sdy[(co + ol) * kDecBS + a];
                 ab2[q] += sum;
             }
         }
@@ -616,7 +625,7 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
         f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
         for (int kk = 0; kk < rows / 4; ++kk) {
             const int o = co + 4 * kk + g;
-            const float b = sdy[o * kDecYS + i];
+            const float b = sdy[o * kDecBS + i];
             d0 = mfma4(sm.w2[o * kDecS + w2_col(i)], b, d0);
             d1 = mfma4(sm.w2[o * kDecS + w2_col(16 + i)], b, d1);
         }
@@ -627,8 +636,8 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            sh[(4 * g + r) * kDecYS + i] = d0[r];
-            sh[(16 + 4 * g + r) * kDecYS + i] = d1[r];
+            sh[(4 * g + r) * kDecBS + i] = d0[r];
+            sh[(16 + 4 * g + r) * kDecBS + i] = d1[r];
         }
         // dW1 += dH X^T (k = anchors), db1 += row sums of dH
 #pragma unroll
@@ -638,13 +647,13 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 if (kt * 16 >= K1) break;
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk)
-                    aw1[ht][kt] = mfma4(sh[(ht * 16 + i) * kDecYS + 4 * kk + g], sx[(4 * kk + g) * kDecS + kt * 16 + i],
+                    aw1[ht][kt] = mfma4(sh[(ht * 16 + i) * kDecBS + 4 * kk + g], sx[(4 * kk + g) * kDecS + kt * 16 + i],
                                         aw1[ht][kt]);
             }
         if (lane < 32) {
             float sum = 0.f;
 #pragma unroll
-            for (int a = 0; a < 16; ++a) sum += sh[lane * kDecYS + a];
+            for (int a = 0; a < 16; ++a) sum += sh[lane * kDecBS + a];
             ab1 += sum;
         }
         // dX = W1^T dH -> d feat (k < 32), d ob_view (k = 32..34) -> d anchor.  The MFMAs run
