@@ -28,6 +28,7 @@ constexpr int kHP = kLT + 1;       // filtered row pitch (33: same for the quad 
 constexpr int kLS = (kLH * kLH + 255) / 256;  // 7 staged positions per lane
 constexpr int kLQ4 = kLT / 4;      // column / row quads per tile edge
 constexpr int kLC = 3;             // channels held in registers (the loss is defined on RGB)
+constexpr int kLossOuts = 9;       // loss, l1, ssim, sky, entropy, scale_reg, normal, distortion, inv_depth
 constexpr int kLQ = 8;  // partial sums per tile: l1, ssim, sky, entropy, scale-prod, normal, distortion, inv-depth
 
 // utils/loss_utils.py:20-22 window, exp(-(x - 5)^2 / (2 * 1.5^2)) normalised, rounded to
@@ -370,20 +371,28 @@ struct LossCoef {
     float l1, ss, sky, ent, dreg, nrm, dist, dep;
 };
 
-__device__ __forceinline__ LossCoef loss_coef(const float* __restrict__ g_out, int C, int64_t HW, int64_t n_sc,
+// upstream gradients of the nine 0-dim outputs: one device pointer each, NULL = zero
+// (autograd hands None for outputs the loss graph does not use: no zero tensors built)
+struct GradOuts {
+    const float* p[kLossOuts];
+};
+
+__device__ __forceinline__ LossCoef loss_coef(const GradOuts& go, int C, int64_t HW, int64_t n_sc,
                                               const LossLam& lam) {
-    // upstream gradients of the nine outputs folded into per-term factors
-    const float g0 = g_out[0];
+    float g[kLossOuts];
+#pragma unroll
+    for (int i = 0; i < kLossOuts; ++i) g[i] = go.p[i] ? *go.p[i] : 0.f;
+    const float g0 = g[0];
     const float n = (float)C * (float)HW, hw = (float)HW;
     LossCoef k;
-    k.l1 = (g0 * (1.f - lam.dssim) + g_out[1]) / n;
-    k.ss = (g_out[2] - g0 * lam.dssim) / n;
-    k.sky = (g0 * lam.sky + g_out[3]) / hw;
-    k.ent = (g0 * lam.ent + g_out[4]) / hw;
-    k.dreg = n_sc > 0 ? (g0 * lam.dreg + g_out[5]) / (float)n_sc : 0.f;
-    k.nrm = (g0 * lam.normal + g_out[6]) / hw;
-    k.dist = (g0 * lam.dist + g_out[7]) / hw;
-    k.dep = (g0 * lam.depth + g_out[8]) / hw;
+    k.l1 = (g0 * (1.f - lam.dssim) + g[1]) / n;
+    k.ss = (g[2] - g0 * lam.dssim) / n;
+    k.sky = (g0 * lam.sky + g[3]) / hw;
+    k.ent = (g0 * lam.ent + g[4]) / hw;
+    k.dreg = n_sc > 0 ? (g0 * lam.dreg + g[5]) / (float)n_sc : 0.f;
+    k.nrm = (g0 * lam.normal + g[6]) / hw;
+    k.dist = (g0 * lam.dist + g[7]) / hw;
+    k.dep = (g0 * lam.depth + g[8]) / hw;
     return k;
 }
 
@@ -436,7 +445,7 @@ __global__ __launch_bounds__(256, 3) void loss_bwd_kernel(int C, int H, int W, I
                                                        const float* __restrict__ mask,
                                                        const float* __restrict__ alpha, ScaleReg sr, LossAux ax,
                                                        LossLam lam, const float* __restrict__ dmaps,
-                                                       const float* __restrict__ g_out, float* __restrict__ g_img,
+                                                       GradOuts g_out, float* __restrict__ g_img,
                                                        int extra_ch, float* __restrict__ g_alpha,
                                                        float* __restrict__ g_scaling) {
     __shared__ LossBwdSmem sm;
@@ -663,11 +672,14 @@ extern "C" int hgsr_loss_fwd(int C, int H, int W, const float* image, const int6
 extern "C" int hgsr_loss_bwd(int C, int H, int W, const float* image, const int64_t* image_strides,
                              const float* gt, const int64_t* gt_strides, const float* mask,
                              const float* alpha, const float* scaling, int64_t n_scaling, int k_scaling,
-                             const hgsr_loss_terms* terms, const float* g_out, float* g_image, int extra_channels,
+                             const hgsr_loss_terms* terms, const float* const* g_outs, float* g_image,
+                             int extra_channels,
                              float* g_alpha, float* g_scaling, const hgsr_loss_aux_grads* aux_grads,
                              const void* ws, size_t ws_bytes, hgsr_stream_t stream) {
     HGSR_REQUIRE(C >= 1 && C <= kLC && H > 0 && W > 0, "bad dims (C must be 1..3)");
-    HGSR_REQUIRE(image && gt && g_out && g_image && ws, "null pointer");
+    HGSR_REQUIRE(image && gt && g_outs && g_image && ws, "null pointer");
+    GradOuts go;
+    for (int i = 0; i < kLossOuts; ++i) go.p[i] = g_outs[i];
     HGSR_REQUIRE(ws_bytes >= hgsr_loss_ws_bytes(C, H, W), "loss workspace too small");
     LossLam lam;
     LossAux ax;
@@ -682,6 +694,6 @@ extern "C" int hgsr_loss_bwd(int C, int H, int W, const float* image, const int6
     float* gsc = n_scaling > 0 ? g_scaling : nullptr;
     KernelTimer kt("loss_bwd", s);
     hipLaunchKernelGGL(loss_bwd_kernel, dim3(loss_tiles(H, W)), dim3(256), 0, s, C, H, W, im, gm, mask, alpha, sr,
-                       ax, lam, (const float*)ws, g_out, g_image, extra_channels, g_alpha, gsc);
+                       ax, lam, (const float*)ws, go, g_image, extra_channels, g_alpha, gsc);
     return check_launch("loss_bwd");
 }

@@ -93,11 +93,16 @@ class _Decode(torch.autograd.Function):
         dev = anchor.device
         Av = vis_idx.numel()
         F = feat.shape[1]
-        d_anchor = torch.zeros_like(anchor) if ctx.needs_input_grad[0] else None
-        d_feat = torch.zeros_like(feat)
-        d_offset = torch.zeros_like(offset)
-        d_scaling = torch.zeros_like(scaling_raw)
-        d_w = [torch.zeros_like(t) for t in w]
+        # every accumulated gradient carved from ONE zero-filled buffer (one fill launch, not 16)
+        like = ([anchor] if ctx.needs_input_grad[0] else []) + [feat, offset, scaling_raw] + list(w)
+        flat = torch.zeros(sum(t.numel() for t in like), dtype=torch.float32, device=dev)
+        views, o = [], 0
+        for t in like:
+            views.append(flat[o:o + t.numel()].view(t.shape))
+            o += t.numel()
+        if not ctx.needs_input_grad[0]:
+            views.insert(0, None)
+        d_anchor, d_feat, d_offset, d_scaling, *d_w = views
         arr, mlp = _ptr_array(w)
         darr, dmlp = _ptr_array(d_w)
         ws_b = N.size_query("hgsr_decode_bwd_ws_bytes", Av)

@@ -89,10 +89,13 @@ class _FusedLoss(torch.autograd.Function):
                ptr(alpha), ptr(scaling), n_sc, k_sc, ct.byref(terms), ptr(out), ptr(ws), ws_b, N.stream(dev))
         ctx.save_for_backward(image, gt, mask, alpha, scaling, normals, nfd, distort, depth, mono, dmask, ws)
         ctx.lams = lams
-        return out
+        # nine separate 0-dim outputs: an output the caller never uses gets no gradient
+        # tensor at all (None below), so the backward builds no zeros / stack glue
+        ctx.set_materialize_grads(False)
+        return tuple(out.unbind(0))
 
     @staticmethod
-    def backward(ctx, g_out):
+    def backward(ctx, *g_outs):
         image, gt, mask, alpha, scaling, normals, nfd, distort, depth, mono, dmask, ws = ctx.saved_tensors
         C, H, W = gt.shape
         dev = image.device
@@ -108,8 +111,10 @@ class _FusedLoss(torch.autograd.Function):
                        _dptr(distort), _strides(distort, 2), _dptr(depth), _strides(depth, 2), ptr(mono), ptr(dmask))
         aux = _AuxGrads(_dptr(g_n), _dptr(g_f), _dptr(g_d), _dptr(g_z))
         n_sc, k_sc = (0, 0) if scaling is None else scaling.shape
+        gs = [None if g is None else _f32(g) for g in g_outs]
+        gptrs = (ct.c_void_p * len(OUTPUTS))(*[None if g is None else g.data_ptr() for g in gs])
         N.call("hgsr_loss_bwd", C, H, W, _dptr(image), _strides(image, 3), _dptr(gt), _strides(gt, 3), ptr(mask),
-               ptr(alpha), ptr(scaling), n_sc, k_sc, ct.byref(terms), ptr(_f32(g_out)), _dptr(g_img),
+               ptr(alpha), ptr(scaling), n_sc, k_sc, ct.byref(terms), gptrs, _dptr(g_img),
                image.shape[0] - C, ptr(g_alpha), ptr(g_sc), ct.byref(aux), ptr(ws), ws.numel(), N.stream(dev))
         if g_alpha is not None:
             g_alpha = g_alpha.reshape(alpha.shape)
@@ -150,4 +155,4 @@ def fused_loss(image, gt, alpha_mask=None, lambda_dssim=0.2, alpha=None, lambda_
                                                                                   alpha.reshape(H, W)),
                            _f32(scaling), _view(normals, (3, H, W)), _view(normals_from_depth, (3, H, W)),
                            _view(distort, (H, W)), _view(depth, (H, W)), hw(mono_invdepth), hw(depth_mask), lams)
-    return tuple(out.unbind(0))
+    return out

@@ -305,7 +305,8 @@ int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
  * inputs are nullable and their terms 0 when absent).
  * ws (hgsr_loss_ws_bytes) holds the SSIM derivative maps for hgsr_loss_bwd, which writes
  * g_image, g_alpha [H,W] (nullable), g_scaling (nullable) and the aux gradients
- * (nullable) from g_out[9], the upstream gradients of the nine outputs (device).
+ * (nullable) from g_outs[9] (host array of device pointers to the upstream gradients of the
+ * nine 0-dim outputs; a NULL entry is a zero gradient).
  * *_strides (host, nullable / zero = contiguous): element strides {channel, row, column}
  * ({row, column} for [H,W] maps), e.g. {1, 3W, 3} for the channels-last render output
  * seen through permute(2,0,1) (render.py:81-95); every gradient is written with its
@@ -339,7 +340,7 @@ int hgsr_loss_fwd(int C, int H, int W, const float* image, const int64_t* image_
 int hgsr_loss_bwd(int C, int H, int W, const float* image, const int64_t* image_strides,
                   const float* gt, const int64_t* gt_strides, const float* mask, const float* alpha,
                   const float* scaling, int64_t n_scaling, int k_scaling, const hgsr_loss_terms* terms,
-                  const float* g_out, float* g_image, int extra_channels, float* g_alpha,
+                  const float* const* g_outs, float* g_image, int extra_channels, float* g_alpha,
                   float* g_scaling, const hgsr_loss_aux_grads* aux_grads, const void* ws,
                   size_t ws_bytes, hgsr_stream_t stream);
 
