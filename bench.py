@@ -211,6 +211,23 @@ def pmc_traffic(args):
     return out, os.path.basename(files[-1]) + ": 2*FETCH_SIZE + WRITE_SIZE"
 
 
+def psnr_parity(args):
+    """The "PSNR delta vs ref" half of the metric: equal-iteration training parity measured
+    by tests/test_gpu_training_parity.py (HIP path vs the autograd torch restatement of
+    gsplat, same init / target / Adam steps) and committed as profiles/rNN_psnr_parity_*.json.
+    Training to convergence cannot run inside a timed bench step, so the newest recorded
+    figure for this path is quoted."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          f"r*_psnr_parity_{args.gs}dgs.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    return {"psnr_delta_db": d["psnr_delta_db"], "psnr_hip_db": d["psnr_hip_db"], "psnr_ref_db": d["psnr_ref_db"],
+            "iterations": d["iterations"], "source": os.path.basename(files[-1]) +
+            " (tests/test_gpu_training_parity.py)"}
+
+
 def cpu_baseline(args, wl):
     """The C oracle (scalar, 1 thread) on a bounded sample of the same workload."""
     from oracle import oracle as O
@@ -334,7 +351,7 @@ def main():
                        "gaussians": int(wl.last_colors.shape[0]), "width": args.width, "height": args.height,
                        "parallelism": ("per-chunk, one scene per GPU, no collectives" if args.mode == "chunk"
                                        else "DDP over views, RCCL all-reduce of Gaussian grads")},
-            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+            "roofline": roof, "cpu_baseline": cpu, "quality": psnr_parity(args), "kernels": kernels,
         }
         print(json.dumps(line))
     if world > 1:

@@ -1,0 +1,119 @@
+"""Training parity (BASELINE "PSNR delta vs ref"): the same small
+synthetic scene is fitted for the same number of Adam iterations through (a) the HIP
+rasterizer (horizongs_amd.gsplat_api.rasterization) and (b) the autograd torch
+restatement of gsplat's rasterization (oracle/torch_ref.py, CPU, fp32), from the same
+perturbed initialisation towards the same ground-truth render.  The two final PSNRs
+must agree within 0.05 dB.  The measured numbers are written to
+gpurun_out/psnr_parity.json (copied into profiles/ and quoted by bench.py)."""
+import json
+import math
+import os
+
+import pytest
+import torch
+
+from horizongs_amd.synthetic import make_scene
+from oracle import torch_ref as TR
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _params(sc, seed):
+    g = torch.Generator().manual_seed(seed)
+    z = sc.means[:, 2:3]
+    fx = float(sc.Ks[0, 0, 0])
+    jitter = torch.cat([torch.randn(sc.means.shape[0], 2, generator=g) * 2.0 * z / fx,
+                        torch.zeros(sc.means.shape[0], 1)], 1)  # ~2 px
+    return dict(means=sc.means + jitter, log_scales=torch.log(sc.scales * 1.5), quats=sc.quats.clone(),
+                opac_logit=torch.full((sc.means.shape[0],), -0.5), colors=torch.full_like(sc.colors, 0.5))
+
+
+def _fit(render, p0, gt, iters):
+    p = {k: v.clone().requires_grad_(True) for k, v in p0.items()}
+    lr = dict(means=1e-3, log_scales=1e-2, quats=1e-2, opac_logit=5e-2, colors=2e-2)
+    opt = torch.optim.Adam([{"params": [p[k]], "lr": lr[k]} for k in p])
+    for _ in range(iters):
+        opt.zero_grad()
+        loss = (render(p) - gt).abs().mean()
+        loss.backward()
+        opt.step()
+    with torch.no_grad():
+        mse = ((render(p) - gt) ** 2).mean().item()
+    return 10 * math.log10(1.0 / mse)
+
+
+def test_psnr_parity_3dgs():
+    from horizongs_amd import gsplat_api as G
+    W, H, N, iters = 128, 96, 300, 200
+    sc = make_scene(N, W, H, seed=11)
+    vm, K = sc.viewmats[0], sc.Ks[0]
+
+    def render_cpu(p):
+        m2, con, dep, rad = TR.project3d(p["means"], p["quats"], torch.exp(p["log_scales"]), vm, K, W, H)
+        img, _ = TR.raster3d(m2, con, p["colors"], torch.sigmoid(p["opac_logit"]), dep, rad, W, H)
+        return img
+
+    vmd, Kd = sc.viewmats.cuda(), sc.Ks.cuda()
+
+    def render_gpu(p):
+        out, _, _ = G.rasterization(p["means"], p["quats"], torch.exp(p["log_scales"]), torch.sigmoid(p["opac_logit"]),
+                                    p["colors"], vmd, Kd, W, H, packed=False)
+        return out[0]
+
+    with torch.no_grad():
+        gt_cpu = render_cpu(dict(means=sc.means, quats=sc.quats, log_scales=torch.log(sc.scales),
+                                 opac_logit=torch.logit(sc.opacities), colors=sc.colors))
+    p0 = _params(sc, seed=12)
+    psnr_init = 10 * math.log10(1.0 / ((render_cpu(p0).detach() - gt_cpu) ** 2).mean().item())
+    psnr_cpu = _fit(render_cpu, p0, gt_cpu, iters)
+    psnr_gpu = _fit(render_gpu, {k: v.cuda() for k, v in p0.items()}, gt_cpu.cuda(), iters)
+    res = dict(psnr_init_db=round(psnr_init, 4), psnr_ref_db=round(psnr_cpu, 4), psnr_hip_db=round(psnr_gpu, 4),
+               psnr_delta_db=round(psnr_gpu - psnr_cpu, 4), iterations=iters, gaussians=N, width=W, height=H,
+               reference="oracle/torch_ref.py autograd restatement of gsplat rasterization (CPU, fp32)")
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "psnr_parity.json"), "w") as f:
+        json.dump(res, f)
+    print(res)
+    assert psnr_cpu > psnr_init + 3.0  # the fit actually fits
+    assert abs(psnr_gpu - psnr_cpu) <= 0.05, res
+
+
+def test_psnr_parity_2dgs():
+    from horizongs_amd import gsplat_api as G
+    W, H, N, iters = 128, 96, 300, 200
+    sc = make_scene(N, W, H, seed=13)
+    vm, K = sc.viewmats[0], sc.Ks[0]
+
+    def render_cpu(p):
+        m2, rt, dep, nrm, rad = TR.project2d(p["means"], p["quats"], torch.exp(p["log_scales"]), vm, K)
+        img, _, _ = TR.raster2d(m2, rt, p["colors"], torch.sigmoid(p["opac_logit"]), nrm, dep, rad, W, H)
+        return img
+
+    vmd, Kd = sc.viewmats.cuda(), sc.Ks.cuda()
+
+    def render_gpu(p):
+        (out, *_), _ = G.rasterization_2dgs(p["means"], p["quats"], torch.exp(p["log_scales"]),
+                                            torch.sigmoid(p["opac_logit"]), p["colors"], vmd, Kd, W, H, packed=False)
+        return out[0]
+
+    with torch.no_grad():
+        gt_cpu = render_cpu(dict(means=sc.means, quats=sc.quats, log_scales=torch.log(sc.scales),
+                                 opac_logit=torch.logit(sc.opacities), colors=sc.colors))
+    p0 = _params(sc, seed=14)
+    psnr_init = 10 * math.log10(1.0 / ((render_cpu(p0).detach() - gt_cpu) ** 2).mean().item())
+    psnr_cpu = _fit(render_cpu, p0, gt_cpu, iters)
+    psnr_gpu = _fit(render_gpu, {k: v.cuda() for k, v in p0.items()}, gt_cpu.cuda(), iters)
+    res = dict(psnr_init_db=round(psnr_init, 4), psnr_ref_db=round(psnr_cpu, 4), psnr_hip_db=round(psnr_gpu, 4),
+               psnr_delta_db=round(psnr_gpu - psnr_cpu, 4), iterations=iters, gaussians=N, width=W, height=H,
+               reference="oracle/torch_ref.py autograd restatement of gsplat rasterization_2dgs (CPU, fp32)")
+    with open(os.path.join("gpurun_out", "psnr_parity_2dgs.json"), "w") as f:
+        json.dump(res, f)
+    print(res)
+    assert psnr_cpu > psnr_init + 3.0
+    assert abs(psnr_gpu - psnr_cpu) <= 0.05, res
