@@ -516,11 +516,45 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 sdy[k * kDecBS + a] = v;
             }
         } else if (head == 1) {
-            for (int s = lane; s < 16 * noff; s += 64) {
+            // Two phases: every slot's global operands (slot row first, then the output
+            // gradients, offsets and scaling) are issued for all of this lane's slots before
+            // any is used -- one exposed memory latency per tile instead of one per slot.
+            constexpr int kSI = 3;  // 16 anchors x n_offsets <= 11 -> <= 192 slots = 3 per lane
+            int sa[kSI], sk[kSI], sid[kSI], sp[kSI];
+#pragma unroll
+            for (int it = 0; it < kSI; ++it) {
+                const int s = lane + 64 * it;
                 const int a = s / noff, k = s - a * noff;
-                const bool present = a0 + a < d.Av;
-                const int id = present ? (vis_idx ? vis_idx[a0 + a] : a0 + a) : 0;
-                const int p = present ? slot_row[(int64_t)(a0 + a) * noff + k] : -1;
+                const bool present = s < 16 * noff && a0 + a < d.Av;
+                sa[it] = a;
+                sk[it] = k;
+                sid[it] = present ? (vis_idx ? vis_idx[a0 + a] : a0 + a) : -1;
+                sp[it] = present ? slot_row[(int64_t)(a0 + a) * noff + k] : -1;
+            }
+            float gsc[kSI][3], grt[kSI][4], gxy[kSI][3], gof[kSI][3], ofs[kSI][3], srw[kSI][6];
+#pragma unroll
+            for (int it = 0; it < kSI; ++it) {
+                const int64_t p = sp[it] < 0 ? 0 : sp[it];
+                const bool live = sp[it] >= 0;
+                const int64_t id = sid[it] < 0 ? 0 : sid[it];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    gsc[it][q] = (live && gr.g_scaling) ? gr.g_scaling[p * 3 + q] : 0.f;
+                    gxy[it][q] = (live && gr.g_xyz && t0 == 0) ? gr.g_xyz[p * 3 + q] : 0.f;
+                    gof[it][q] = (live && gr.g_offsets && t0 == 0) ? gr.g_offsets[p * 3 + q] : 0.f;
+                    ofs[it][q] = (live && t0 == 0) ? offset[(id * noff + sk[it]) * 3 + q] : 0.f;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) grt[it][q] = (live && gr.g_rot) ? gr.g_rot[p * 4 + q] : 0.f;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) srw[it][q] = live ? scaling_raw[id * 6 + q] : 0.f;
+            }
+#pragma unroll
+            for (int it = 0; it < kSI; ++it) {
+                const int a = sa[it], k = sk[it];
+                if (lane + 64 * it >= 16 * noff) continue;
+                const int64_t id = sid[it];
+                const int p = sp[it];
                 float cv[7], dv[7];
 #pragma unroll
                 for (int q = 0; q < 7; ++q) {
@@ -530,20 +564,18 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 if (p < 0) {
 #pragma unroll
                     for (int q = 0; q < 7; ++q) sdy[(7 * k + q) * kDecBS + a] = 0.f;
-                    if (present && t0 == 0) {
-                        float* dof = gr.d_offset + ((int64_t)id * noff + k) * 3;
+                    if (id >= 0 && t0 == 0) {
+                        float* dof = gr.d_offset + (id * noff + k) * 3;
                         dof[0] = dof[1] = dof[2] = 0.f;
                     }
                     continue;
                 }
-                float* dof = gr.d_offset + ((int64_t)id * noff + k) * 3;
-                const float* sr = scaling_raw + (int64_t)id * 6;
                 // scaling = exp(sr[3:6]) * sigmoid(cv[0:3])
                 if (gr.g_scaling) {
 #pragma unroll
                     for (int q = 0; q < 3; ++q) {
-                        const float es = __expf(sr[3 + q]), sg = __builtin_amdgcn_rcpf(1.0f + __expf(-cv[q]));
-                        const float gs = gr.g_scaling[(int64_t)p * 3 + q];
+                        const float es = __expf(srw[it][3 + q]), sg = __builtin_amdgcn_rcpf(1.0f + __expf(-cv[q]));
+                        const float gs = gsc[it][q];
                         dv[q] = gs * es * sg * (1.0f - sg);
                         if (t0 == 0) atomicAdd(&sacc[a * 9 + 3 + q], gs * es * sg);
                     }
@@ -551,31 +583,30 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 // rot = v / max(|v|, 1e-12)
                 if (gr.g_rot) {
                     const float n2 = cv[3] * cv[3] + cv[4] * cv[4] + cv[5] * cv[5] + cv[6] * cv[6];
-                    const float* gq = gr.g_rot + (int64_t)p * 4;
                     if (n2 > 1e-24f) {  // |v| > 1e-12
                         const float inv = __builtin_amdgcn_rsqf(n2);
                         float dot = 0.f;
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) dot += cv[3 + q] * inv * gq[q];
+                        for (int q = 0; q < 4; ++q) dot += cv[3 + q] * inv * grt[it][q];
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) dv[3 + q] = (gq[q] - cv[3 + q] * inv * dot) * inv;
+                        for (int q = 0; q < 4; ++q) dv[3 + q] = (grt[it][q] - cv[3 + q] * inv * dot) * inv;
                     } else {
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) dv[3 + q] = gq[q] * 1e12f;
+                        for (int q = 0; q < 4; ++q) dv[3 + q] = grt[it][q] * 1e12f;
                     }
                 }
 #pragma unroll
                 for (int q = 0; q < 7; ++q) sdy[(7 * k + q) * kDecBS + a] = dv[q];
                 if (t0 != 0) continue;  // the position / offset chain belongs to the first cov chunk
                 // xyz = anchor + offset * exp(sr[0:3]); offsets_out = offset * exp(sr[0:3])
-                const float* of = offset + ((int64_t)id * noff + k) * 3;
+                float* dof = gr.d_offset + (id * noff + k) * 3;
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
-                    const float gx = gr.g_xyz ? gr.g_xyz[(int64_t)p * 3 + q] : 0.f;
-                    const float gt = gx + (gr.g_offsets ? gr.g_offsets[(int64_t)p * 3 + q] : 0.f);
-                    const float es = __expf(sr[q]);
+                    const float gx = gxy[it][q];
+                    const float gt = gx + gof[it][q];
+                    const float es = __expf(srw[it][q]);
                     dof[q] = gt * es;
-                    atomicAdd(&sacc[a * 9 + q], gt * of[q] * es);
+                    atomicAdd(&sacc[a * 9 + q], gt * ofs[it][q] * es);
                     atomicAdd(&sacc[a * 9 + 6 + q], gx);
                 }
             }
