@@ -373,6 +373,10 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
 }
 
 // ---------------------------------------------------------------- backward
+// wave-level LDS ordering point: all of this wave's LDS operations have completed and the
+// compiler may not move memory operations across it (no workgroup barrier)
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // One launch per (head, chunk of <= 5 output tiles): the colour head of an SH model
 // has 17 tiles, whose dW2 accumulators would not fit registers in one pass.  Every
 // launch recomputes its head's hidden layer, forms dY from the output gradients,
@@ -463,12 +467,16 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
     float* sh = sm.h[wave];
     float* sacc = sm.acc[wave];
     const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
+    __syncthreads();  // weights staged
+    // Every per-tile LDS array (x, Y / dY, H / dH, per-anchor sums) belongs to one wave, so
+    // the waves of a block run their tiles independently: a wave's LDS operations complete
+    // in order, and the waits below only keep the compiler from reordering across phases.
     for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-        __syncthreads();  // weights staged / previous tile's LDS reads done
+        wave_lds_sync();  // this wave's previous tile is done with its LDS arrays
         const int a0 = t * kDecTile + wave * 16;
         stage_x(sx, vis_idx, a0, d.Av, d.vd, anchor, feat, cam);
         for (int e = lane; e < 16 * 9; e += 64) sacc[e] = 0.f;
-        __syncthreads();
+        wave_lds_sync();
         // hidden layer of this head (rows 0..31 of sm.w1)
         f32x4 h0 = {0.f, 0.f, 0.f, 0.f}, h1 = h0;
 #pragma unroll
