@@ -31,6 +31,16 @@ constexpr int kDecYS = 20;        // LDS row stride of the Y^T tiles: conflict-f
 // backward Y^T / dY^T / H^T stride: the MFMA fragment reads (rows i, columns 4kk+g) and the
 // per-row sums (one row per lane) dominate there, both conflict-free at an odd stride
 constexpr int kDecBS = 17;
+
+// tanh to a few ulp for the opacity head: exp-based, and x itself below |x| < 2^-8 (error
+// < x^3/3, keeps the sign and never rounds a positive input to 0, so the opacity > 0 mask
+// is exactly the reference's)
+__device__ __forceinline__ float tanh_fast(float x) {
+    const float ax = fabsf(x);
+    const float e = __expf(-2.0f * ax);
+    const float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
+    return ax < 0.00390625f ? x : copysignf(t, x);
+}
 constexpr int kDecMaxRows = 368;  // W2 rows (opacity + cov + colour heads, padded to 16): SH2 x 10 offsets
 
 struct MlpPtrs {
@@ -208,7 +218,7 @@ __device__ int opacity_head(S& sm, int wave, int a0, int Av, const DecodeDims& d
     const f32x4 y = layer2_tile(sm, d.row0[0], h0, h1);
     float* sy = sm.y[wave];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sy[(4 * g + r) * kDecYS + i] = tanhf(y[r]);
+    for (int r = 0; r < 4; ++r) sy[(4 * g + r) * kDecYS + i] = tanh_fast(y[r]);
     // order-preserving keep positions over slots s = a * noff + k
     const int nslots = 16 * d.noff;
     int cnt = 0;
@@ -344,14 +354,16 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
             const float* sr = scaling_raw + (int64_t)id * 6;
 #pragma unroll
             for (int q = 0; q < 3; ++q)
-                out.scaling[(int64_t)p * 3 + q] = expf(sr[3 + q]) * (1.0f / (1.0f + expf(-cv[q])));
-            const float nrm = fmaxf(sqrtf(cv[3] * cv[3] + cv[4] * cv[4] + cv[5] * cv[5] + cv[6] * cv[6]), 1e-12f);
+                out.scaling[(int64_t)p * 3 + q] = __expf(sr[3 + q]) * __builtin_amdgcn_rcpf(1.0f + __expf(-cv[q]));
+            const float nrm = fmaxf(__builtin_amdgcn_sqrtf(cv[3] * cv[3] + cv[4] * cv[4] + cv[5] * cv[5] + cv[6] * cv[6]),
+                                    1e-12f);
+            const float inrm = __builtin_amdgcn_rcpf(nrm);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) out.rot[(int64_t)p * 4 + q] = cv[3 + q] / nrm;
+            for (int q = 0; q < 4; ++q) out.rot[(int64_t)p * 4 + q] = cv[3 + q] * inrm;
             const float* of = offset + ((int64_t)id * noff + k) * 3;
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
-                const float o = of[q] * expf(sr[q]);
+                const float o = of[q] * __expf(sr[q]);
                 out.offsets[(int64_t)p * 3 + q] = o;
                 out.xyz[(int64_t)p * 3 + q] = anchor[(int64_t)id * 3 + q] + o;
             }
