@@ -13,7 +13,8 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libhgsr.so")
+# HGSR_LIB: developer override (benchmarking alternative builds of the same sources)
+LIB_PATH = os.environ.get("HGSR_LIB") or os.path.join(_HERE, "_lib", "libhgsr.so")
 
 _lock = threading.Lock()
 _lib = None
