@@ -219,7 +219,7 @@ def psnr_parity(args):
     figure for this path is quoted."""
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                          f"r*_psnr_parity_{args.gs}dgs.json")))
+                                          f"r*_psnr_parity_{args.gs}gs.json")))
     if not files:
         return None
     d = json.load(open(files[-1]))
