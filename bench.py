@@ -2,9 +2,9 @@
 
 One "step" = one training view through the rasterizer path Horizon-GS runs at
 train.py:150-206: gsplat.rasterization(..., packed=False, render_mode="RGB+ED")
-(projection -> tile binning + depth sort -> raster forward), an L1 photometric
-loss plus an alpha term, and loss.backward() (raster backward -> projection
-backward), on a synthetic c2 scene: 2,000,000 Gaussians at
+(projection -> tile binning + depth sort -> raster forward), the reference loss
+head (fused HIP loss), loss.backward() (raster backward -> projection backward)
+and the optimizer step (Adam, eps=1e-15, one fused HIP launch), on a synthetic c2 scene: 2,000,000 Gaussians at
 1920x1080, fp32, inputs resident in HBM.
 
 Multi-GPU: one process per GPU (torchrun); the path shards per chunk (reference
@@ -34,9 +34,11 @@ sys.path.insert(0, ROOT)
 
 from horizongs_amd import _native as NAT  # noqa: E402
 from horizongs_amd import decode as HD  # noqa: E402
+from horizongs_amd import densify as HDn  # noqa: E402
 from horizongs_amd import gsplat_api as G  # noqa: E402
 from horizongs_amd.loss import fused_loss  # noqa: E402
 from horizongs_amd.multigpu import GradientAllReduce  # noqa: E402
+from horizongs_amd.optim import Adam  # noqa: E402
 from horizongs_amd.synthetic import make_scene  # noqa: E402
 
 METRIC = "train-step views/sec (fwd+bwd raster) @2M Gaussians/1080p; PSNR delta vs ref"
@@ -45,7 +47,7 @@ HBM_PEAK_GBS = 8000.0      # HBM3E spec
 FLOP_PER_PAIR = {"raster3d_fwd": 20.0, "raster3d_bwd": 60.0, "raster2d_fwd": 40.0, "raster2d_bwd": 120.0}
 KERNELS = ["project3d_fwd", "isect_count", "isect_emit", "tile_sort", "raster3d_fwd", "raster3d_bwd",
            "project3d_bwd", "project2d_fwd", "raster2d_fwd", "raster2d_bwd", "project2d_bwd", "sh_fwd", "sh_bwd",
-           "decode_count", "decode_fwd", "decode_bwd", "loss_fwd", "loss_bwd"]
+           "decode_count", "decode_fwd", "decode_bwd", "loss_fwd", "loss_bwd", "adam"]
 
 
 def parse():
@@ -72,10 +74,11 @@ class Workload:
         seed = rank if args.mode == "chunk" else 0
         sc = make_scene(args.n, args.width, args.height, seed=seed)
         self.sc = sc
+        # trained in the 3DGS parametrisation: log scales and opacity logits, activated each step
         self.means = sc.means.to(dev).requires_grad_(True)
         self.quats = sc.quats.to(dev).requires_grad_(True)
-        self.scales = sc.scales.to(dev).requires_grad_(True)
-        self.opac = sc.opacities.to(dev).requires_grad_(True)
+        self.log_scales = torch.log(sc.scales).to(dev).requires_grad_(True)
+        self.opac_logit = torch.logit(sc.opacities).to(dev).requires_grad_(True)
         self.colors = sc.colors.to(dev).requires_grad_(True)
         vm = sc.viewmats.clone()
         if args.mode == "ddp" and rank > 0:  # a different view of the same scene per rank
@@ -87,9 +90,15 @@ class Workload:
         self.bg = torch.zeros(1, 3, device=dev)
         g = torch.Generator().manual_seed(1000 + rank)
         self.target = torch.rand(3, args.height, args.width, generator=g).to(dev)
-        self.params = [self.means, self.quats, self.scales, self.opac, self.colors]
+        self.params = [self.means, self.quats, self.log_scales, self.opac_logit, self.colors]
+        # 3DGS per-attribute learning rates for the explicit Gaussians
+        groups = [(self.means, 1.6e-4), (self.quats, 1e-3), (self.log_scales, 5e-3), (self.opac_logit, 5e-2),
+                  (self.colors, 2.5e-3)]
         if args.anchors:
-            self._init_anchors(args, seed, dev)
+            groups = self._init_anchors(args, seed, dev)
+        # the reference optimizer (scene/lod_model.py:320): Adam(eps=1e-15), one group per tensor,
+        # stepped every iteration (train.py:274-277) -- one fused HIP launch here
+        self.optimizer = Adam([{"params": [p], "lr": lr} for p, lr in groups], lr=0.0, eps=1e-15)
         self.allreduce = GradientAllReduce(self.params, bucket_mb=64.0)
 
     def _init_anchors(self, args, seed, dev):
@@ -109,17 +118,38 @@ class Workload:
         self.cam_center = torch.zeros(3, device=dev)
         self.params = [self.anchor, self.feat, self.offset, self.scaling_raw] + [
             p for m in self.mlps for p in m.parameters()]
+        self.anchor_quats = torch.zeros(A, 4, device=dev)
+        self.anchor_quats[:, 0] = 1.0  # get_rotation at init (_rotation is not trained)
+        # densification statistics updated every step by training_statis (train.py:258-262)
+        k = 10
+        self.stats = dict(anchor_opacity_accum=torch.zeros(A, 1, device=dev), anchor_demon=torch.zeros(A, 1, device=dev),
+                          offset_gradient_accum=torch.zeros(A * k, 1, device=dev),
+                          offset_denom=torch.zeros(A * k, 1, device=dev))
+        self.stats_model = type("Stats", (), dict(n_offsets=k, **self.stats))
+        self.stats_opt = type("Opt", (), dict(pruning_type="mean", growing_type="mean"))
+        # config/base/small_scene/coarse.yaml learning rates (position lr 0: still an Adam group)
+        return [(p, lr) for p, lr in zip([self.anchor, self.feat, self.offset, self.scaling_raw] + [
+            p for m in self.mlps for p in m.parameters()], [0.0, 0.0075, 0.01, 0.007] + [0.002] * 4 + [0.004] * 4
+            + [0.008] * 4)]
 
     def step(self):
         for p in self.params:
             p.grad = None
         W, H = self.args.width, self.args.height
         if self.args.anchors:
-            xyz, _, cols, opac, scales, quats, _ = HD.decode(self.anchor, self.feat, self.offset, self.scaling_raw,
-                                                             self.cam_center, self.mlps, None, 3, 10, 3)
+            # prefilter_voxel (gaussian_renderer/render.py:120-197): project the anchors with their
+            # offset scale, keep radii > 0
+            with torch.no_grad():
+                radii_a = G.fully_fused_projection(self.anchor.detach(), None, self.anchor_quats,
+                                                   torch.exp(self.scaling_raw.detach()[:, :3]), self.viewmats, self.Ks,
+                                                   W, H, eps2d=0.3, packed=False)[0]
+                visible = radii_a[0] > 0
+            xyz, _, cols, opac, scales, quats, sel = HD.decode(self.anchor, self.feat, self.offset, self.scaling_raw,
+                                                               self.cam_center, self.mlps, visible, 3, 10, 3)
             opac = opac.reshape(-1)
         else:
-            xyz, quats, scales, opac, cols = self.means, self.quats, self.scales, self.opac, self.colors
+            xyz, quats, cols = self.means, self.quats, self.colors
+            scales, opac = torch.exp(self.log_scales), torch.sigmoid(self.opac_logit)
         self.last_colors = cols
         if self.args.gs == "3d":
             out, alpha, meta = G.rasterization(xyz, quats, scales, opac, cols, self.viewmats, self.Ks, W, H,
@@ -142,6 +172,12 @@ class Workload:
         loss.backward()
         if self.args.mode == "ddp":
             self.allreduce()
+        if self.args.anchors:  # densification statistics of this view (train.py:258-262)
+            HDn.training_statis(self.stats_model, self.stats_opt,
+                                dict(selection_mask=sel, visible_mask=visible, viewspace_points=meta["means2d"],
+                                     visibility_filter=meta["radii"][0] > 0, opacity=opac, radii=meta["radii"][0]),
+                                W, H)
+        self.optimizer.step()  # train.py:274-277 (zero_grad(set_to_none) = the grad reset above)
         self.meta = meta
         return loss
 
@@ -284,6 +320,8 @@ def main():
     for _ in range(args.warmup):
         wl.step()
     torch.cuda.synchronize(dev)
+    # the optimizer moves the scene: intersections before / after the timed steps show the drift
+    isects_before = wl.meta["flatten_ids"].numel() if args.warmup else None
     timing = not args.no_timing
     if timing:
         NAT.call("hgsr_timing_reset")
@@ -334,6 +372,7 @@ def main():
             roof["traffic_source"] = traffic_src
         roof["aggregate_hbm_frac"] = round(b_step / (dt / args.steps) / (HBM_PEAK_GBS * 1e9), 4)
         roof["n_isects"] = n_isects
+        roof["n_isects_before_timed"] = isects_before
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.gs == "3d" and not args.anchors:
         cpu = cpu_baseline(args, wl)
@@ -345,9 +384,9 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (seeded c2 scene, SURVEY 8(d); no dataset in the environment)",
             "config": {"workload": (f"c2 {'3DGS' if args.gs == '3d' else '2DGS'} train step: "
-                                    + (f"fused anchor decode ({args.anchors} anchors) + " if args.anchors else "")
-                                    + "rasterization fwd + reference loss (L1 + D-SSIM + alpha/scale regs) + bwd, "
-                                      "RGB+ED"),
+                                    + (f"anchor prefilter + fused anchor decode ({args.anchors} anchors) + " if args.anchors else "")
+                                    + "rasterization fwd + reference loss (L1 + D-SSIM + alpha/scale regs) + bwd"
+                                    + (" + training_statis" if args.anchors else "") + " + Adam step, RGB+ED"),
                        "gaussians": int(wl.last_colors.shape[0]), "width": args.width, "height": args.height,
                        "parallelism": ("per-chunk, one scene per GPU, no collectives" if args.mode == "chunk"
                                        else "DDP over views, RCCL all-reduce of Gaussian grads")},

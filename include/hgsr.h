@@ -379,6 +379,27 @@ int hgsr_weed_out(int64_t n, const float* positions, const int32_t* levels, int 
                   const float* cam_infos, float standard_dist, float fork, int street_levels,
                   int dist2level_mode, float weed_ratio, uint8_t* mask, hgsr_stream_t stream);
 
+/* ---- K17: optimizer step ------------------------------------------------------
+ * replaces gaussians.optimizer.step() (reference train.py:274-277) of
+ * torch.optim.Adam(l, lr=0.0, eps=1e-15) (scene/lod_model.py:320; per-group lr from
+ * update_learning_rate, scene/lod_model.py:350-372), all parameters in one launch
+ * (chunks of 16 tensors).  Per tensor: param / grad / exp_avg / exp_avg_sq device
+ * pointers (fp32, numel elements each, updated in place), its group's lr and its
+ * 1-based step count (torch's per-parameter state["step"] after the increment).
+ * grad == NULL skips the tensor (torch skips parameters whose .grad is None).
+ * amsgrad, weight_decay and maximize are not used by the reference and not offered. */
+typedef struct {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t numel;
+    double lr;
+    int64_t step;
+} hgsr_adam_tensor;
+int hgsr_adam_step(int n_tensors, const hgsr_adam_tensor* tensors, double beta1, double beta2, double eps,
+                   hgsr_stream_t stream);
+
 /* ---- measurement ----------------------------------------------------------
  * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):
  * when enabled, the main kernel of every entry point is bracketed by

@@ -1,6 +1,6 @@
 """Training parity (BASELINE "PSNR delta vs ref"): the same small
 synthetic scene is fitted for the same number of Adam iterations through (a) the HIP
-rasterizer (horizongs_amd.gsplat_api.rasterization) and (b) the autograd torch
+rasterizer (horizongs_amd.gsplat_api.rasterization) + the fused HIP Adam and (b) the autograd torch
 restatement of gsplat's rasterization (oracle/torch_ref.py, CPU, fp32), from the same
 perturbed initialisation towards the same ground-truth render.  The two final PSNRs
 must agree within 0.05 dB.  The measured numbers are written to
@@ -35,9 +35,15 @@ def _params(sc, seed):
 
 
 def _fit(render, p0, gt, iters):
+    """Fit with the reference optimizer (torch.optim.Adam) on CPU tensors and with the
+    fused HIP Adam (horizongs_amd.optim.Adam) on device tensors."""
     p = {k: v.clone().requires_grad_(True) for k, v in p0.items()}
     lr = dict(means=1e-3, log_scales=1e-2, quats=1e-2, opac_logit=5e-2, colors=2e-2)
-    opt = torch.optim.Adam([{"params": [p[k]], "lr": lr[k]} for k in p])
+    if next(iter(p.values())).is_cuda:
+        from horizongs_amd.optim import Adam
+    else:
+        Adam = torch.optim.Adam
+    opt = Adam([{"params": [p[k]], "lr": lr[k]} for k in p])
     for _ in range(iters):
         opt.zero_grad()
         loss = (render(p) - gt).abs().mean()
