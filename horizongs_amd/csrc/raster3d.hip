@@ -148,8 +148,8 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
 // exclusively) carries T negated, so "done" costs no separate flag: its next T is
 // negative, never kept, and |T| is the final transmittance.
 template <int D>
-__device__ __forceinline__ void fwd_step(const float4 g0, const float4 g1, const float4 c, int32_t idx, float px,
-                                         float py, float& T, float (&acc)[4], int32_t& cur) {
+__device__ __forceinline__ void fwd_step(const float4 g0, const float4 g1, const float4 c, uint32_t idx, float px,
+                                         float py, float& T, float (&acc)[4], uint32_t& cur) {
     const float dx = g0.x - px, dy = g0.y - py;
     float xx, yy, xy;
     const float sigma = sigma2(g0, g1, dx, dy, xx, yy, xy);
@@ -176,7 +176,10 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     __shared__ float4 s_g0[kFwdBatch + 1];
     __shared__ float4 s_g1[kFwdBatch + 1];
     __shared__ float4 s_col[kFwdBatch + 1];
-    __shared__ uint16_t s_list[4][kFwdBatch + 4];
+    // per-wave compacted lists hold LDS byte offsets (16 x slot) of the records: the
+    // list read yields the record addresses directly and the last-contributor update
+    // keeps the offset, rebased once per batch
+    __shared__ uint32_t s_list[4][kFwdBatch + 4];
     __shared__ int s_vote[2][4];
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -203,7 +206,10 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
         n0 = r[0]; n1 = r[1]; n2 = r[2];
         nid = flatten_ids[min(tc.start + kFwdBatch + tid, last)];
     }
-    uint16_t* my_list = s_list[wave];
+    uint32_t* my_list = s_list[wave];
+    const char* lds_g0 = reinterpret_cast<const char*>(s_g0);
+    const char* lds_g1 = reinterpret_cast<const char*>(s_g1);
+    const char* lds_col = reinterpret_cast<const char*>(s_col);
     for (int b = 0; b < nb; ++b) {
         // workgroup early-out vote (double-buffered slots; LDS-only barriers so the
         // prefetch loads stay in flight)
@@ -234,21 +240,24 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
             const int t = k * 64 + lane;
             const bool rel = t < cnt && reaches(s_g0[t], s_g1[t], qx, qy) && ellipse_reaches(s_g0[t], s_g1[t], qx, qy);
             const uint64_t m = __ballot(rel);
-            if (rel) my_list[n_mine + lanes_below(m)] = (uint16_t)t;
+            if (rel) my_list[n_mine + lanes_below(m)] = (uint32_t)t * 16u;
             n_mine += __popcll(m);
         }
-        if (lane < 4) my_list[n_mine + lane] = (uint16_t)kFwdBatch;  // pad to a multiple of 4
+        if (lane < 4) my_list[n_mine + lane] = (uint32_t)kFwdBatch * 16u;  // pad to a multiple of 4
+        uint32_t cur_off = 0xffffffffu;  // byte offset of this batch's latest contributor, if any
         for (int i = 0; i < n_mine; i += 4) {
-            const int t0 = my_list[i], t1 = my_list[i + 1], t2 = my_list[i + 2], t3 = my_list[i + 3];
-            const float4 a0 = s_g0[t0], a1 = s_g0[t1], a2 = s_g0[t2], a3 = s_g0[t3];
-            const float4 b0 = s_g1[t0], b1 = s_g1[t1], b2 = s_g1[t2], b3 = s_g1[t3];
-            const float4 c0 = s_col[t0], c1 = s_col[t1], c2 = s_col[t2], c3 = s_col[t3];
-            fwd_step<D>(a0, b0, c0, bs + t0, tc.px, tc.py, T, acc, cur);
-            fwd_step<D>(a1, b1, c1, bs + t1, tc.px, tc.py, T, acc, cur);
-            fwd_step<D>(a2, b2, c2, bs + t2, tc.px, tc.py, T, acc, cur);
-            fwd_step<D>(a3, b3, c3, bs + t3, tc.px, tc.py, T, acc, cur);
+            const uint4 o = *reinterpret_cast<const uint4*>(my_list + i);
+            auto ld = [](const char* base, uint32_t off) { return *reinterpret_cast<const float4*>(base + off); };
+            const float4 a0 = ld(lds_g0, o.x), a1 = ld(lds_g0, o.y), a2 = ld(lds_g0, o.z), a3 = ld(lds_g0, o.w);
+            const float4 b0 = ld(lds_g1, o.x), b1 = ld(lds_g1, o.y), b2 = ld(lds_g1, o.z), b3 = ld(lds_g1, o.w);
+            const float4 c0 = ld(lds_col, o.x), c1 = ld(lds_col, o.y), c2 = ld(lds_col, o.z), c3 = ld(lds_col, o.w);
+            fwd_step<D>(a0, b0, c0, o.x, tc.px, tc.py, T, acc, cur_off);
+            fwd_step<D>(a1, b1, c1, o.y, tc.px, tc.py, T, acc, cur_off);
+            fwd_step<D>(a2, b2, c2, o.z, tc.px, tc.py, T, acc, cur_off);
+            fwd_step<D>(a3, b3, c3, o.w, tc.px, tc.py, T, acc, cur_off);
             if (__all(T < 0.f)) break;
         }
+        if (cur_off != 0xffffffffu) cur = bs + (int32_t)(cur_off >> 4);
     }
     if (tc.inside) {
         T = fabsf(T);
@@ -539,6 +548,11 @@ extern "C" size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D) {
     return rec_bytes(C, N);
 }
 
+static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backgrounds, int bg_ch, int ed_ch,
+                               int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
+                               int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
+                               float* render_alphas, int32_t* last_ids, hipStream_t s);
+
 static int raster3d_fwd_impl(int C, int N, int D, const float* means2d, const float* conics, const ChanSrc& cs,
                              const float* backgrounds, int bg_ch, int ed_ch, int width, int height, int tile_size,
                              int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
@@ -553,6 +567,14 @@ static int raster3d_fwd_impl(int C, int N, int D, const float* means2d, const fl
     Rec3* rec = (Rec3*)ws;
     if (n_isects > 0)
         if (int st = pack3(C, N, D, means2d, conics, cs, rec, s)) return st;
+    return raster3d_fwd_launch(C, D, rec, backgrounds, bg_ch, ed_ch, width, height, tile_w, tile_h, isect_offsets,
+                               n_isects, flatten_ids, render_colors, render_alphas, last_ids, s);
+}
+
+static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backgrounds, int bg_ch, int ed_ch,
+                               int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
+                               int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
+                               float* render_alphas, int32_t* last_ids, hipStream_t s) {
     const dim3 grid(C * tile_w * tile_h);
     KernelTimer kt("raster3d_fwd", s);
 #define LAUNCH_F(DD)                                                                                           \
@@ -596,6 +618,39 @@ extern "C" int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2
     return raster3d_fwd_impl(C, N, D, means2d, conics, cs, backgrounds, Dc, expected_depth ? Dc : -1, width,
                              height, tile_size, tile_w, tile_h, isect_offsets, n_isects, flatten_ids,
                              render_colors, render_alphas, last_ids, ws, ws_bytes, stream);
+}
+
+extern "C" int hgsr_raster3d_pack_fused(int C, int N, int Dc, const float* means2d, const float* conics,
+                                        const float* colors, int colors_shared, const float* depths,
+                                        const float* opacities, int opacities_shared, void* ws, size_t ws_bytes,
+                                        hgsr_stream_t stream) {
+    HGSR_REQUIRE(C >= 1 && N >= 0, "bad dims");
+    HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
+    const int D = Dc + (depths ? 1 : 0);
+    HGSR_REQUIRE(D <= 4, "channels per call must be 1..4 (got %d)", D);
+    HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_fwd_ws_bytes(C, N, D), "raster3d_pack workspace too small");
+    HGSR_REQUIRE(N == 0 || (means2d && conics && (colors || Dc == 0) && opacities && ws), "null pointer");
+    const ChanSrc cs{colors, colors_shared ? 0 : (int64_t)N * Dc, Dc, depths, opacities,
+                     opacities_shared ? 0 : (int64_t)N};
+    return pack3(C, N, D, means2d, conics, cs, (Rec3*)ws, as_stream(stream));
+}
+
+extern "C" int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_depth,
+                                        const float* backgrounds, int width, int height, int tile_size,
+                                        int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                                        const int32_t* flatten_ids, float* render_colors, float* render_alphas,
+                                        int32_t* last_ids, const void* records, size_t records_bytes,
+                                        hgsr_stream_t stream) {
+    HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || with_depth), "fused raster: 0..4 colour channels (got %d)", Dc);
+    HGSR_REQUIRE(!(expected_depth && !with_depth), "expected_depth needs depths");
+    const int D = Dc + (with_depth ? 1 : 0);
+    if (int st = check_raster(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
+    HGSR_REQUIRE(records_bytes >= hgsr_raster3d_fwd_ws_bytes(C, N, D), "raster3d_fwd_packed: records too small");
+    HGSR_REQUIRE(isect_offsets && render_colors && render_alphas && last_ids, "null pointer");
+    HGSR_REQUIRE(n_isects == 0 || (flatten_ids && records), "null pointer");
+    return raster3d_fwd_launch(C, D, (const Rec3*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
+                               tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
+                               last_ids, as_stream(stream));
 }
 
 extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {

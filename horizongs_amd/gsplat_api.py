@@ -20,6 +20,7 @@ RuntimeError, as gsplat's TORCH_CHECKs do.
 from __future__ import annotations
 
 import math
+import threading
 from typing import Optional, Tuple
 
 import torch
@@ -198,9 +199,22 @@ def _tile_grid(width, height, tile_size):
     return math.ceil(width / tile_size), math.ceil(height / tile_size)
 
 
+_pinned = threading.local()
+
+
+def _host_info_buffer():
+    """Per-thread pinned 2 x int64 landing buffer for the intersection count."""
+    buf = getattr(_pinned, "buf", None)
+    if buf is None:
+        buf = _pinned.buf = torch.empty(2, dtype=torch.int64, pin_memory=True)
+    return buf
+
+
 @torch.no_grad()
-def _isect_binned(means2d, radii, tile_size, tile_width, tile_height, depths):
-    """Binned tile intersection: (tiles_per_gauss, isect_ids, flatten_ids, isect_offsets)."""
+def _isect_count(means2d, radii, tile_size, tile_width, tile_height, depths):
+    """Stage 1 of the binned intersection: launches the count pass and an async copy of
+    {n_isects, largest bin} to pinned host memory.  Work enqueued before _isect_finish()
+    runs on the device while the host waits for that copy."""
     C, Ng = radii.shape
     dev = means2d.device
     m2 = _f32(means2d.detach())
@@ -214,7 +228,23 @@ def _isect_binned(means2d, radii, tile_size, tile_width, tile_height, depths):
     s = N.stream(dev)
     N.call("hgsr_isect_count", C, Ng, ptr(m2), ptr(radii), tile_size, tile_width, tile_height, ptr(tpg),
            ptr(offsets), ptr(info), ptr(ws1), ws1_b, s)
-    n_isects, max_bin = (int(v) for v in info.cpu().tolist())  # the one host sync (gsplat has it too)
+    host = _host_info_buffer()
+    host.copy_(info, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    return (m2, dep, radii, tpg, offsets, ws1, ws1_b, host, ev, tile_size, tile_width, tile_height)
+
+
+@torch.no_grad()
+def _isect_finish(st):
+    """Stage 2: wait for the count (the one host sync of a view; gsplat has it too), then
+    emit + sort -> (tiles_per_gauss, isect_ids, flatten_ids, isect_offsets)."""
+    m2, dep, radii, tpg, offsets, ws1, ws1_b, host, ev, tile_size, tile_width, tile_height = st
+    C, Ng = radii.shape
+    dev = m2.device
+    s = N.stream(dev)
+    ev.synchronize()
+    n_isects, max_bin = int(host[0]), int(host[1])
     isect_ids = torch.empty(n_isects, dtype=torch.int64, device=dev)
     flatten_ids = torch.empty(n_isects, dtype=torch.int32, device=dev)
     if n_isects > 0:
@@ -224,6 +254,11 @@ def _isect_binned(means2d, radii, tile_size, tile_width, tile_height, depths):
                tile_height, ptr(offsets), n_isects, max_bin, ptr(isect_ids), ptr(flatten_ids), ptr(ws1), ws1_b,
                ptr(ws2), ws2_b, s)
     return tpg, isect_ids, flatten_ids, offsets
+
+
+def _isect_binned(means2d, radii, tile_size, tile_width, tile_height, depths):
+    """Binned tile intersection: (tiles_per_gauss, isect_ids, flatten_ids, isect_offsets)."""
+    return _isect_finish(_isect_count(means2d, radii, tile_size, tile_width, tile_height, depths))
 
 
 @torch.no_grad()
@@ -324,8 +359,22 @@ class _Raster3DFused(torch.autograd.Function):
     kernels instead of torch cat / repeat / divide (gsplat rendering.py does those in torch)."""
 
     @staticmethod
+    def pack(means2d, conics, colors, depths, opacities):
+        """Raster records for forward(records=...): launched before the intersection
+        count is read back, so the packing overlaps the host sync."""
+        C, Ng = means2d.shape[:2]
+        Dc = 0 if colors is None else colors.shape[-1]
+        D = Dc + (0 if depths is None else 1)
+        ws_b = N.size_query("hgsr_raster3d_fwd_ws_bytes", C, Ng, D)
+        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=means2d.device)
+        N.call("hgsr_raster3d_pack_fused", C, Ng, Dc, ptr(means2d), ptr(conics), ptr(colors),
+               int(colors is not None and colors.dim() == 2), ptr(depths), ptr(opacities), int(opacities.dim() == 1),
+               ptr(ws), ws_b, N.stream(means2d.device))
+        return ws
+
+    @staticmethod
     def forward(ctx, means2d, conics, colors, depths, opacities, backgrounds, width, height, tile_size,
-                isect_offsets, flatten_ids, expected_depth, absgrad):
+                isect_offsets, flatten_ids, expected_depth, absgrad, records=None):
         C, Ng = means2d.shape[:2]
         Dc = 0 if colors is None else colors.shape[-1]
         D = Dc + (0 if depths is None else 1)
@@ -336,13 +385,20 @@ class _Raster3DFused(torch.autograd.Function):
         rc = torch.empty((C, height, width, D), dtype=torch.float32, device=dev)
         ra = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
         last = torch.empty((C, height, width), dtype=torch.int32, device=dev)
-        ws_b = N.size_query("hgsr_raster3d_fwd_ws_bytes", C, Ng, D)
-        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
-        N.call("hgsr_raster3d_fwd_fused", C, Ng, Dc, ptr(means2d), ptr(conics), ptr(colors), int(col_shared),
-               ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(backgrounds), width, height,
-               tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
-               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(ws), ws_b,
-               N.stream(dev))
+        if records is not None:
+            ws = records
+            N.call("hgsr_raster3d_fwd_packed", C, Ng, Dc, int(depths is not None), int(expected_depth),
+                   ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
+                   ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(ws),
+                   ws.numel(), N.stream(dev))
+        else:
+            ws_b = N.size_query("hgsr_raster3d_fwd_ws_bytes", C, Ng, D)
+            ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+            N.call("hgsr_raster3d_fwd_fused", C, Ng, Dc, ptr(means2d), ptr(conics), ptr(colors), int(col_shared),
+                   ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(backgrounds), width,
+                   height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
+                   ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(ws), ws_b,
+                   N.stream(dev))
         ctx.save_for_backward(means2d, conics, colors, depths, opacities, backgrounds, isect_offsets, flatten_ids,
                               rc, ra, last)
         ctx.cfg = (width, height, tile_size, expected_depth, absgrad, Dc, col_shared, op_shared)
@@ -378,7 +434,8 @@ class _Raster3DFused(torch.autograd.Function):
         v_bg = None
         if backgrounds is not None and ctx.needs_input_grad[5]:
             v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))
-        return (v_means2d, v_conics, v_colors, v_depths, v_opac, v_bg, None, None, None, None, None, None, None)
+        return (v_means2d, v_conics, v_colors, v_depths, v_opac, v_bg, None, None, None, None, None, None, None,
+                None)
 
 
 def rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_height, tile_size, isect_offsets,
@@ -609,19 +666,24 @@ def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, 
         calc_compensations=False, camera_model=camera_model)
     cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
     tw, th = _tile_grid(width, height, tile_size)
-    tpg, isect_ids, flatten_ids, isect_offsets = _isect_binned(means2d, radii, int(tile_size), tw, th, depths)
+    isect_state = _isect_count(means2d, radii, int(tile_size), tw, th, depths)
     with_depth = render_mode in ("RGB+D", "RGB+ED", "D", "ED")
     rgb = render_mode in ("RGB", "RGB+D", "RGB+ED")
     Dc = cols.shape[-1] if rgb else 0
     if Dc + int(with_depth) <= _MAX_CH:
-        # one fused native call each way: no cat / repeat / ED divide in torch
+        # one fused native call each way: no cat / repeat / ED divide in torch; the raster
+        # records are packed while the host waits for the intersection count
+        r_in = (_f32(means2d), _f32(conics), _f32(cols) if rgb else None, _f32(depths) if with_depth else None,
+                _f32(opacities))
+        records = _Raster3DFused.pack(*(t.detach() if t is not None else None for t in r_in))
+        tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
         bgs = None if (backgrounds is None or not rgb) else _f32(backgrounds)
         render_colors, render_alphas = _Raster3DFused.apply(
-            _f32(means2d), _f32(conics), _f32(cols) if rgb else None, _f32(depths) if with_depth else None,
-            _f32(opacities), bgs, int(width), int(height), int(tile_size), isect_offsets.contiguous(),
-            flatten_ids.contiguous(), render_mode in ("ED", "RGB+ED"), absgrad)
+            *r_in, bgs, int(width), int(height), int(tile_size), isect_offsets.contiguous(),
+            flatten_ids.contiguous(), render_mode in ("ED", "RGB+ED"), absgrad, records)
         opac = opacities.expand(C, -1)
     else:
+        tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
         opac = opacities.repeat(C, 1)
         if cols.dim() == 2:
             cols = cols.expand(C, -1, -1)

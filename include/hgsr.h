@@ -171,6 +171,22 @@ int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
                             const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                             int32_t* last_ids, void* ws, size_t ws_bytes, hgsr_stream_t stream);
+/* hgsr_raster3d_fwd_fused split in two, so the packing runs while the host reads the
+ * intersection count (the one host sync of a view): hgsr_raster3d_pack_fused writes the
+ * per-Gaussian raster records of the fused channel layout into ws (size as above; it
+ * needs no intersection data), hgsr_raster3d_fwd_packed composites from them (with_depth:
+ * the records carry the depth channel after the Dc colours).  The records stay valid for
+ * hgsr_raster3d_bwd_fused's fwd_ws. */
+int hgsr_raster3d_pack_fused(int C, int N, int Dc, const float* means2d, const float* conics,
+                             const float* colors, int colors_shared, const float* depths,
+                             const float* opacities, int opacities_shared, void* ws, size_t ws_bytes,
+                             hgsr_stream_t stream);
+int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_depth,
+                             const float* backgrounds, int width, int height, int tile_size,
+                             int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                             const int32_t* flatten_ids, float* render_colors, float* render_alphas,
+                             int32_t* last_ids, const void* records, size_t records_bytes,
+                             hgsr_stream_t stream);
 /* vjp of hgsr_raster3d_fwd_fused: v_colors in the colours' layout (shared colours
  * summed over cameras in camera order), v_depths [C,N] (when depths), v_opacities
  * in the opacities' layout; render_colors is the forward output (needed for ED). */
