@@ -602,6 +602,12 @@ extern "C" size_t hgsr_raster2d_fwd_ws_bytes(int C, int N, int D) {
     return rec2_bytes(C, N);
 }
 
+static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backgrounds, int bg_ch, int ed_ch,
+                               int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
+                               int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
+                               float* render_alphas, float* render_normals, float* render_distort,
+                               float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s);
+
 static int raster2d_fwd_impl(int C, int N, int D, const float* means2d, const float* rt, const ChanSrc& cs,
                              const float* normals, const float* backgrounds, int bg_ch, int ed_ch, int width,
                              int height, int tile_size, int tile_w, int tile_h, const int32_t* isect_offsets,
@@ -621,6 +627,16 @@ static int raster2d_fwd_impl(int C, int N, int D, const float* means2d, const fl
     Rec2* rec = (Rec2*)ws;
     if (n_isects > 0)
         if (int st = pack2(C, N, D, means2d, rt, cs, normals, rec, s)) return st;
+    return raster2d_fwd_launch(C, D, rec, backgrounds, bg_ch, ed_ch, width, height, tile_w, tile_h, isect_offsets,
+                               n_isects, flatten_ids, render_colors, render_alphas, render_normals, render_distort,
+                               render_median, last_ids, median_ids, s);
+}
+
+static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backgrounds, int bg_ch, int ed_ch,
+                               int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
+                               int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
+                               float* render_alphas, float* render_normals, float* render_distort,
+                               float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s) {
     const dim3 grid(C * tile_w * tile_h);
     KernelTimer kt("raster2d_fwd", s);
 #define LAUNCH_F2(DD)                                                                                            \
@@ -670,6 +686,44 @@ extern "C" int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2
                              expected_depth ? Dc : -1, width, height, tile_size, tile_w, tile_h, isect_offsets,
                              n_isects, flatten_ids, render_colors, render_alphas, render_normals, render_distort,
                              render_median, last_ids, median_ids, ws, ws_bytes, stream);
+}
+
+extern "C" int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
+                                        const float* colors, int colors_shared, const float* depths,
+                                        const float* opacities, int opacities_shared, const float* normals, void* ws,
+                                        size_t ws_bytes, hgsr_stream_t stream) {
+    HGSR_REQUIRE(C >= 1 && N >= 0, "bad dims");
+    HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
+    const int D = Dc + (depths ? 1 : 0);
+    HGSR_REQUIRE(D <= 4, "channels per call must be 1..4 (got %d)", D);
+    HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_fwd_ws_bytes(C, N, D), "raster2d_pack workspace too small");
+    HGSR_REQUIRE(N == 0 || (means2d && ray_transforms && (colors || Dc == 0) && opacities && normals && ws),
+                 "null pointer");
+    const ChanSrc cs{colors, colors_shared ? 0 : (int64_t)N * Dc, Dc, depths, opacities,
+                     opacities_shared ? 0 : (int64_t)N};
+    return pack2(C, N, D, means2d, ray_transforms, cs, normals, (Rec2*)ws, as_stream(stream));
+}
+
+extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_depth,
+                                        const float* backgrounds, int width, int height, int tile_size, int tile_w,
+                                        int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                                        const int32_t* flatten_ids, float* render_colors, float* render_alphas,
+                                        float* render_normals, float* render_distort, float* render_median,
+                                        int32_t* last_ids, int32_t* median_ids, const void* records,
+                                        size_t records_bytes, hgsr_stream_t stream) {
+    HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || with_depth), "fused raster: 0..4 colour channels (got %d)", Dc);
+    HGSR_REQUIRE(!(expected_depth && !with_depth), "expected_depth needs depths");
+    const int D = Dc + (with_depth ? 1 : 0);
+    if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
+    HGSR_REQUIRE(records_bytes >= hgsr_raster2d_fwd_ws_bytes(C, N, D), "raster2d_fwd_packed: records too small");
+    HGSR_REQUIRE(isect_offsets && render_colors && render_alphas && render_normals && render_distort &&
+                     render_median && last_ids && median_ids,
+                 "null pointer");
+    HGSR_REQUIRE(n_isects == 0 || (flatten_ids && records), "null pointer");
+    return raster2d_fwd_launch(C, D, (const Rec2*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
+                               tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
+                               render_normals, render_distort, render_median, last_ids, median_ids,
+                               as_stream(stream));
 }
 
 extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {

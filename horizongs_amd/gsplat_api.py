@@ -528,8 +528,21 @@ class _Raster2DFused(torch.autograd.Function):
     native call each way (hgsr_raster2d_{fwd,bwd}_fused); see _Raster3DFused."""
 
     @staticmethod
+    def pack(means2d, rt, colors, depths, opacities, normals):
+        """Surfel records for forward(records=...), packed while the host reads the count."""
+        C, Ng = means2d.shape[:2]
+        Dc = 0 if colors is None else colors.shape[-1]
+        D = Dc + (0 if depths is None else 1)
+        ws_b = N.size_query("hgsr_raster2d_fwd_ws_bytes", C, Ng, D)
+        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=means2d.device)
+        N.call("hgsr_raster2d_pack_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors),
+               int(colors is not None and colors.dim() == 2), ptr(depths), ptr(opacities), int(opacities.dim() == 1),
+               ptr(normals), ptr(ws), ws_b, N.stream(means2d.device))
+        return ws
+
+    @staticmethod
     def forward(ctx, means2d, rt, colors, depths, opacities, normals, densify, backgrounds, width, height,
-                tile_size, isect_offsets, flatten_ids, expected_depth):
+                tile_size, isect_offsets, flatten_ids, expected_depth, records=None):
         C, Ng = means2d.shape[:2]
         Dc = 0 if colors is None else colors.shape[-1]
         D = Dc + (0 if depths is None else 1)
@@ -544,13 +557,20 @@ class _Raster2DFused(torch.autograd.Function):
         rm = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
         last = torch.empty((C, height, width), dtype=torch.int32, device=dev)
         med = torch.empty((C, height, width), dtype=torch.int32, device=dev)
-        ws_b = N.size_query("hgsr_raster2d_fwd_ws_bytes", C, Ng, D)
-        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
-        N.call("hgsr_raster2d_fwd_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors), int(col_shared),
-               ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(normals), ptr(backgrounds),
-               width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
-               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(rn), ptr(rd), ptr(rm),
-               ptr(last), ptr(med), ptr(ws), ws_b, N.stream(dev))
+        if records is not None:
+            ws = records
+            N.call("hgsr_raster2d_fwd_packed", C, Ng, Dc, int(depths is not None), int(expected_depth),
+                   ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
+                   ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(rn), ptr(rd), ptr(rm),
+                   ptr(last), ptr(med), ptr(ws), ws.numel(), N.stream(dev))
+        else:
+            ws_b = N.size_query("hgsr_raster2d_fwd_ws_bytes", C, Ng, D)
+            ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+            N.call("hgsr_raster2d_fwd_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors), int(col_shared),
+                   ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(normals),
+                   ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
+                   ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(rn), ptr(rd), ptr(rm),
+                   ptr(last), ptr(med), ptr(ws), ws_b, N.stream(dev))
         ctx.save_for_backward(means2d, rt, colors, depths, opacities, normals, backgrounds, isect_offsets,
                               flatten_ids, rc, ra, last)
         ctx.cfg = (width, height, tile_size, expected_depth, Dc, col_shared, op_shared)
@@ -588,7 +608,7 @@ class _Raster2DFused(torch.autograd.Function):
         if backgrounds is not None and ctx.needs_input_grad[7]:
             v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))
         return (v_means2d, v_rt, v_colors, v_depths, v_opac, v_normals, v_dens, v_bg, None, None, None, None, None,
-                None)
+                None, None)
 
 
 def rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals, densify, image_width,
@@ -759,20 +779,24 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
         near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip, sparse_grad=sparse_grad)
     cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
     tw, th = _tile_grid(width, height, tile_size)
-    tpg, isect_ids, flatten_ids, isect_offsets = _isect_binned(means2d, radii, int(tile_size), tw, th, depths)
+    isect_state = _isect_count(means2d, radii, int(tile_size), tw, th, depths)
     with_depth = render_mode in ("RGB+D", "RGB+ED", "D", "ED")
     rgb = render_mode in ("RGB", "RGB+D", "RGB+ED")
     Dc = cols.shape[-1] if rgb else 0
     if Dc + int(with_depth) <= _MAX_CH and not absgrad:
-        # one fused native call each way: no cat / repeat / ED divide in torch
+        # one fused native call each way: no cat / repeat / ED divide in torch; the surfel
+        # records are packed while the host waits for the intersection count
+        r_in = (_f32(means2d), _f32(ray_transforms.reshape(C, Ng, 9)), _f32(cols) if rgb else None,
+                _f32(depths) if with_depth else None, _f32(opacities), _f32(normals))
+        records = _Raster2DFused.pack(*(t.detach() if t is not None else None for t in r_in))
+        tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
         bgs = None if (backgrounds is None or not rgb) else _f32(backgrounds)
         opac = opacities.expand(C, -1)
         render_colors, render_alphas, render_normals, render_distort, render_median = _Raster2DFused.apply(
-            _f32(means2d), _f32(ray_transforms.reshape(C, Ng, 9)), _f32(cols) if rgb else None,
-            _f32(depths) if with_depth else None, _f32(opacities), _f32(normals), densifications, bgs, int(width),
-            int(height), int(tile_size), isect_offsets.contiguous(), flatten_ids.contiguous(),
-            render_mode in ("ED", "RGB+ED"))
+            *r_in[:5], r_in[5], densifications, bgs, int(width), int(height), int(tile_size),
+            isect_offsets.contiguous(), flatten_ids.contiguous(), render_mode in ("ED", "RGB+ED"), records)
     else:
+        tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
         opac = opacities.repeat(C, 1)
         if cols.dim() == 2:
             cols = cols.expand(C, -1, -1)

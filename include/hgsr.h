@@ -244,6 +244,20 @@ int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             float* render_alphas, float* render_normals, float* render_distort,
                             float* render_median, int32_t* last_ids, int32_t* median_ids, void* ws,
                             size_t ws_bytes, hgsr_stream_t stream);
+/* hgsr_raster2d_fwd_fused split in two (as hgsr_raster3d_pack_fused / _fwd_packed): the
+ * surfel records (ws, hgsr_raster2d_fwd_ws_bytes) are packed while the host reads the
+ * intersection count, then composited; they stay valid as hgsr_raster2d_bwd_fused's fwd_ws. */
+int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
+                             const float* colors, int colors_shared, const float* depths,
+                             const float* opacities, int opacities_shared, const float* normals, void* ws,
+                             size_t ws_bytes, hgsr_stream_t stream);
+int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_depth,
+                             const float* backgrounds, int width, int height, int tile_size, int tile_w,
+                             int tile_h, const int32_t* isect_offsets, int64_t n_isects,
+                             const int32_t* flatten_ids, float* render_colors, float* render_alphas,
+                             float* render_normals, float* render_distort, float* render_median,
+                             int32_t* last_ids, int32_t* median_ids, const void* records,
+                             size_t records_bytes, hgsr_stream_t stream);
 int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                             const float* colors, int colors_shared, const float* depths,
                             int expected_depth, const float* opacities, int opacities_shared,
