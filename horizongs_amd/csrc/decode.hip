@@ -175,6 +175,57 @@ __device__ void stage_x(float* sx, const int32_t* __restrict__ vis_idx, int a0, 
     }
 }
 
+// X rows of a wave's 16 anchors fetched into registers one tile ahead (software pipeline:
+// the id loads, then the feat / anchor loads, are issued during the previous tile's MFMA
+// work, so stage-in costs no exposed memory latency).  Lane l holds the id of anchor
+// l & 15 (-1 past Av) and feat elements e = l + 64 j (row e >> 5, column e & 31).
+struct XPrefetch {
+    int id;
+    float f[8];
+    float ax, ay, az;  // lanes < 16: the anchor position (view direction)
+};
+
+__device__ __forceinline__ void x_issue_id(XPrefetch& p, const int32_t* __restrict__ vis_idx, int a0, int Av) {
+    const int v = a0 + (threadIdx.x & 15);
+    p.id = v < Av ? (vis_idx ? vis_idx[v] : v) : -1;
+}
+
+__device__ __forceinline__ void x_issue_data(XPrefetch& p, const float* __restrict__ feat,
+                                             const float* __restrict__ anchor, int vd) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int id = __shfl(p.id, (lane >> 5) + 2 * j);
+        p.f[j] = id >= 0 ? feat[(int64_t)id * kDecF + (lane & 31)] : 0.f;
+    }
+    const bool a = lane < 16 && p.id >= 0 && vd > 0;
+    p.ax = a ? anchor[(int64_t)p.id * 3] : 0.f;
+    p.ay = a ? anchor[(int64_t)p.id * 3 + 1] : 0.f;
+    p.az = a ? anchor[(int64_t)p.id * 3 + 2] : 0.f;
+}
+
+// same LDS image as stage_x from the prefetched registers
+// (lanes < 16 also return their anchor's view direction and distance for the backward)
+__device__ __forceinline__ void x_store(const XPrefetch& p, float* sx, int vd, const float* __restrict__ cam,
+                                        float (&ov)[3], float& dist) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sx[((lane >> 5) + 2 * j) * kDecS + (lane & 31)] = p.f[j];
+    ov[0] = ov[1] = ov[2] = 0.f;
+    dist = 1.f;
+    if (lane < 16) {
+        if (p.id >= 0 && vd > 0) {
+            const float dx = p.ax - cam[0], dy = p.ay - cam[1], dz = p.az - cam[2];
+            dist = sqrtf(dx * dx + dy * dy + dz * dz);
+            ov[0] = dx / dist;
+            ov[1] = dy / dist;
+            ov[2] = dz / dist;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sx[lane * kDecS + kDecF + k] = (k < 3 && vd > 0) ? ov[k] : 0.f;
+    }
+}
+
 // first layer of head `head` (or all three): H^T tiles [16 hidden x 16 anchors], bias + ReLU
 template <int KSTEPS, class S>
 __device__ __forceinline__ f32x4 layer1_tile(const S& sm, const float* sx, int mt) {
@@ -389,6 +440,24 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
 // compiler may not move memory operations across it (no workgroup barrier)
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Developer instrumentation (variant builds with -DHGSR_DECODE_PROF only): per-head, per-phase
+// shader-clock totals of the backward; every boundary drains the wave's memory counters so a
+// phase is charged the latency of the loads it issued.
+#ifdef HGSR_DECODE_PROF
+__device__ unsigned long long g_dprof[3][16];
+#define DPROF_INIT uint64_t _tp = __builtin_amdgcn_s_memtime();
+#define DPROF_T(k)                                                                  \
+    do {                                                                            \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                 \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();                           \
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_dprof[HEAD][k], (unsigned long long)(_t - _tp)); \
+        _tp = _t;                                                                   \
+    } while (0)
+#else
+#define DPROF_INIT
+#define DPROF_T(k)
+#endif
+
 // One launch per (head, chunk of <= 5 output tiles): the colour head of an SH model
 // has 17 tiles, whose dW2 accumulators would not fit registers in one pass.  Every
 // launch recomputes its head's hidden layer, forms dY from the output gradients,
@@ -435,7 +504,7 @@ struct DecodeBwdSmem {
 __host__ __device__ inline int bwd_partial_floats(int nt) { return nt * 16 * 32 + nt * 16 + 32 * 48 + 32; }
 
 template <int KSTEPS, int HEAD, int NT>
-__global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtrs mp, int t0, int nt,
+__global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtrs mp, int t0, int nt,
                                                          const int32_t* __restrict__ vis_idx,
                                                          const float* __restrict__ anchor,
                                                          const float* __restrict__ feat,
@@ -480,15 +549,61 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
     float* sacc = sm.acc[wave];
     const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
     __syncthreads();  // weights staged
+    DPROF_INIT
     // Every per-tile LDS array (x, Y / dY, H / dH, per-anchor sums) belongs to one wave, so
     // the waves of a block run their tiles independently: a wave's LDS operations complete
     // in order, and the waits below only keep the compiler from reordering across phases.
+    // software pipeline (one tile ahead): X rows of the next tile; this tile's slot rows,
+    // output-gradient gathers and the old values of the accumulated input gradients are
+    // issued before the MFMA phases that hide their latency
+    XPrefetch px;
+    if (blockIdx.x < (unsigned)n_tiles) {
+        x_issue_id(px, vis_idx, blockIdx.x * kDecTile + wave * 16, d.Av);
+        x_issue_data(px, feat, anchor, d.vd);
+    }
+    constexpr int kSI = 3;  // 16 anchors x n_offsets <= 11 -> <= 192 slots = 3 per lane
+    constexpr int kCI = NT * 4;  // colour head: rows * 16 / 64 (anchor, output) pairs per lane
     for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
         wave_lds_sync();  // this wave's previous tile is done with its LDS arrays
         const int a0 = t * kDecTile + wave * 16;
-        stage_x(sx, vis_idx, a0, d.Av, d.vd, anchor, feat, cam);
+        float my_ov[3], my_dist;
+        x_store(px, sx, d.vd, cam, my_ov, my_dist);
+        const int cur_id = px.id;  // lane i (= lane & 15): id of anchor i of this tile, -1 past Av
         for (int e = lane; e < 16 * 9; e += 64) sacc[e] = 0.f;
+        const int tn = t + gridDim.x;
+        if (tn < n_tiles) x_issue_id(px, vis_idx, tn * kDecTile + wave * 16, d.Av);
+        // old values of the accumulated input gradients of this tile (d feat rows of anchor i,
+        // columns kt*16 + 4g + r; d anchor / d scaling_raw on lanes < 16)
+        float old_feat[2][4], old_anc[3] = {0.f, 0.f, 0.f}, old_sc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                old_feat[kt][r] = cur_id >= 0 ? gr.d_feat[(int64_t)cur_id * kDecF + kt * 16 + 4 * g + r] : 0.f;
+        const bool anc_lane = lane < 16 && cur_id >= 0 && gr.d_anchor && (d.vd > 0 || (head == 1 && t0 == 0));
+        if (anc_lane)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) old_anc[q] = gr.d_anchor[(int64_t)cur_id * 3 + q];
+        if (head == 1 && t0 == 0 && lane < 16 && cur_id >= 0)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) old_sc[q] = gr.d_scaling[(int64_t)cur_id * 6 + q];
+        // slot rows of this tile's (anchor, offset) slots
+        int sp[kSI], cp[kCI];
+#pragma unroll
+        for (int it = 0; it < kSI; ++it) {
+            const int sl = lane + 64 * it;
+            const int a = sl / noff;
+            sp[it] = (head < 2 && sl < 16 * noff && a0 + a < d.Av) ? slot_row[(int64_t)a0 * noff + sl] : -1;
+        }
+#pragma unroll
+        for (int it = 0; it < kCI; ++it) {
+            const int e = lane + 64 * it, ol = e >> 4, a = e & 15, o = o0 + ol;
+            const int k = o / cd;
+            cp[it] = (head == 2 && gr.g_color && ol < rows && o < O && a0 + a < d.Av)
+                         ? slot_row[(int64_t)(a0 + a) * noff + k] : -1;
+        }
         wave_lds_sync();
+        DPROF_T(0);
         // hidden layer of this head (rows 0..31 of sm.w1)
         f32x4 h0 = {0.f, 0.f, 0.f, 0.f}, h1 = h0;
 #pragma unroll
@@ -503,59 +618,22 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
             sh[(4 * g + r) * kDecBS + i] = h0[r];
             sh[(16 + 4 * g + r) * kDecBS + i] = h1[r];
         }
-        // recompute the pre-activations the derivative needs
-        if (head < 2) {
-            for (int ot = 0; ot < srows / 16; ++ot) {
-                f32x4 y = {0.f, 0.f, 0.f, 0.f};
-                const float* w = sm.w2 + (ot * 16 + i) * kDecS + g;
+        // the next tile's X rows (its ids have arrived) and this tile's output-gradient gathers
+        if (tn < n_tiles) x_issue_data(px, feat, anchor, d.vd);
+        float gop[kSI], gcol[kCI];
+        int sk[kSI], sid[kSI];
+        float gsc[kSI][3], grt[kSI][4], gxy[kSI][3], gof[kSI][3], ofs[kSI][3], srw[kSI][6];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) y = mfma4(w[4 * r], h0[r], y);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) y = mfma4(w[16 + 4 * r], h1[r], y);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) sy[(ot * 16 + 4 * g + r) * kDecBS + i] = y[r] + sm.b2[ot * 16 + 4 * g + r];
-            }
-        }
-        // dY^T for the chunk, in place over Y^T for the opacity / cov heads: every slot writes
-        // all of its rows (zeros when dropped or absent), padding rows are zeroed separately
-        if (head == 2) {
-            for (int e = lane; e < rows * 16; e += 64) sdy[(e >> 4) * kDecBS + (e & 15)] = 0.f;
-        } else {
-            const int used = head == 0 ? noff : 7 * noff;
-            for (int e = lane; e < (srows - used) * 16; e += 64) sdy[(used + (e >> 4)) * kDecBS + (e & 15)] = 0.f;
-        }
-        if (head == 0) {
-            for (int s = lane; s < 16 * noff; s += 64) {
-                const int a = s / noff, k = s - a * noff;
-                const int p = a0 + a < d.Av ? slot_row[(int64_t)(a0 + a) * noff + k] : -1;
-                float v = 0.f;
-                if (p >= 0 && gr.g_opacity) {
-                    const float th = fast_tanh(sy[k * kDecBS + a]);
-                    v = gr.g_opacity[p] * (1.0f - th * th);
-                }
-                sdy[k * kDecBS + a] = v;
-            }
-        } else if (head == 1) {
-            // Two phases: every slot's global operands (slot row first, then the output
-            // gradients, offsets and scaling) are issued for all of this lane's slots before
-            // any is used -- one exposed memory latency per tile instead of one per slot.
-            constexpr int kSI = 3;  // 16 anchors x n_offsets <= 11 -> <= 192 slots = 3 per lane
-            int sa[kSI], sk[kSI], sid[kSI], sp[kSI];
-#pragma unroll
-            for (int it = 0; it < kSI; ++it) {
-                const int s = lane + 64 * it;
-                const int a = s / noff, k = s - a * noff;
-                const bool present = s < 16 * noff && a0 + a < d.Av;
-                sa[it] = a;
-                sk[it] = k;
-                sid[it] = present ? (vis_idx ? vis_idx[a0 + a] : a0 + a) : -1;
-                sp[it] = present ? slot_row[(int64_t)(a0 + a) * noff + k] : -1;
-            }
-            float gsc[kSI][3], grt[kSI][4], gxy[kSI][3], gof[kSI][3], ofs[kSI][3], srw[kSI][6];
-#pragma unroll
-            for (int it = 0; it < kSI; ++it) {
-                const int64_t p = sp[it] < 0 ? 0 : sp[it];
-                const bool live = sp[it] >= 0;
+        for (int it = 0; it < kSI; ++it) {
+            const int sl = lane + 64 * it;
+            const int a = sl / noff;
+            sk[it] = sl - a * noff;
+            const int aid = __shfl(cur_id, a < 16 ? a : 0);
+            sid[it] = (sl < 16 * noff && a0 + a < d.Av) ? aid : -1;
+            const int64_t p = sp[it] < 0 ? 0 : sp[it];
+            const bool live = sp[it] >= 0;
+            gop[it] = (head == 0 && live && gr.g_opacity) ? gr.g_opacity[p] : 0.f;
+            if (head == 1) {
                 const int64_t id = sid[it] < 0 ? 0 : sid[it];
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
@@ -569,9 +647,57 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
 #pragma unroll
                 for (int q = 0; q < 6; ++q) srw[it][q] = live ? scaling_raw[id * 6 + q] : 0.f;
             }
+        }
+#pragma unroll
+        for (int it = 0; it < kCI; ++it) {
+            const int e = lane + 64 * it, o = o0 + (e >> 4);
+            const int c = o - (o / cd) * cd;
+            gcol[it] = cp[it] >= 0 ? gr.g_color[(int64_t)cp[it] * cd + c] : 0.f;
+        }
+        DPROF_T(1);
+        // recompute the pre-activations the derivative needs
+        if (head < 2) {
+            for (int ot = 0; ot < srows / 16; ++ot) {
+                f32x4 y = {0.f, 0.f, 0.f, 0.f};
+                const float* w = sm.w2 + (ot * 16 + i) * kDecS + g;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) y = mfma4(w[4 * r], h0[r], y);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) y = mfma4(w[16 + 4 * r], h1[r], y);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sy[(ot * 16 + 4 * g + r) * kDecBS + i] = y[r] + sm.b2[ot * 16 + 4 * g + r];
+            }
+        }
+        DPROF_T(2);
+        // dY^T for the chunk, in place over Y^T for the opacity / cov heads: every slot writes
+        // all of its rows (zeros when dropped or absent), padding rows are zeroed separately
+        if (head == 2) {
+#pragma unroll
+            for (int it = 0; it < kCI; ++it) {
+                const int e = lane + 64 * it;
+                if ((e >> 4) < rows) sdy[(e >> 4) * kDecBS + (e & 15)] = gcol[it];
+            }
+        } else {
+            const int used = head == 0 ? noff : 7 * noff;
+            for (int e = lane; e < (srows - used) * 16; e += 64) sdy[(used + (e >> 4)) * kDecBS + (e & 15)] = 0.f;
+        }
+        if (head == 0) {
 #pragma unroll
             for (int it = 0; it < kSI; ++it) {
-                const int a = sa[it], k = sk[it];
+                const int sl = lane + 64 * it;
+                if (sl >= 16 * noff) continue;
+                const int a = sl / noff, k = sl - a * noff;
+                float v = 0.f;
+                if (sp[it] >= 0 && gr.g_opacity) {
+                    const float th = fast_tanh(sy[k * kDecBS + a]);
+                    v = gop[it] * (1.0f - th * th);
+                }
+                sdy[k * kDecBS + a] = v;
+            }
+        } else if (head == 1) {
+#pragma unroll
+            for (int it = 0; it < kSI; ++it) {
+                const int a = (lane + 64 * it) / noff, k = sk[it];
                 if (lane + 64 * it >= 16 * noff) continue;
                 const int64_t id = sid[it];
                 const int p = sp[it];
@@ -630,25 +756,24 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                     atomicAdd(&sacc[a * 9 + 6 + q], gx);
                 }
             }
-        } else if (gr.g_color) {
-            for (int e = lane; e < rows * 16; e += 64) {
-                const int ol = e >> 4, a = e & 15;
-                const int o = o0 + ol;
-                if (o >= O || a0 + a >= d.Av) continue;
-                const int k = o / cd, c = o - k * cd;
-                const int p = slot_row[(int64_t)(a0 + a) * noff + k];
-                if (p >= 0) sdy[ol * kDecBS + a] = gr.g_color[(int64_t)p * cd + c];
+        }
+        DPROF_T(3);
+        // per-anchor d scaling_raw / d anchor of the cov head (xyz and scaling outputs); the
+        // d anchor sum joins the view-direction term of dX below (one store per tile)
+        float anc_add[3] = {0.f, 0.f, 0.f};
+        if (head == 1 && t0 == 0) {
+            wave_lds_sync();
+            if (lane < 16 && cur_id >= 0) {
+#pragma unroll
+                for (int q = 0; q < 6; ++q) gr.d_scaling[(int64_t)cur_id * 6 + q] = old_sc[q] + sacc[lane * 9 + q];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) anc_add[q] = sacc[lane * 9 + 6 + q];
+                if (gr.d_anchor && d.vd == 0)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) gr.d_anchor[(int64_t)cur_id * 3 + q] = old_anc[q] + anc_add[q];
             }
         }
-        // per-anchor d scaling_raw / d anchor of the cov head (xyz and scaling outputs)
-        if (head == 1 && t0 == 0 && lane < 16 && a0 + lane < d.Av) {
-            const int id = vis_idx ? vis_idx[a0 + lane] : a0 + lane;
-#pragma unroll
-            for (int q = 0; q < 6; ++q) gr.d_scaling[(int64_t)id * 6 + q] += sacc[lane * 9 + q];
-            if (gr.d_anchor)
-#pragma unroll
-                for (int q = 0; q < 3; ++q) gr.d_anchor[(int64_t)id * 3 + q] += sacc[lane * 9 + 6 + q];
-        }
+        DPROF_T(4);
         // dW2 += dY H^T (k = anchors), db2 += row sums of dY
 #pragma unroll
         for (int ot = 0; ot < NT; ++ot) {
@@ -672,6 +797,7 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 ab2[q] += sum;
             }
         }
+        DPROF_T(5);
         // dH = W2^T dY, masked by ReLU; then stored transposed for dW1
         f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
         for (int kk = 0; kk < rows / 4; ++kk) {
@@ -690,6 +816,7 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
             sh[(4 * g + r) * kDecBS + i] = d0[r];
             sh[(16 + 4 * g + r) * kDecBS + i] = d1[r];
         }
+        DPROF_T(6);
         // dW1 += dH X^T (k = anchors), db1 += row sums of dH
 #pragma unroll
         for (int ht = 0; ht < 2; ++ht)
@@ -707,11 +834,12 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
             for (int a = 0; a < 16; ++a) sum += sh[lane * kDecBS + a];
             ab1 += sum;
         }
+        DPROF_T(7);
         // dX = W1^T dH -> d feat (k < 32), d ob_view (k = 32..34) -> d anchor.  The MFMAs run
         // with the whole wave (an MFMA consumes every lane's operands whatever EXEC says);
         // only the stores are predicated on the anchor being present.
-        const bool present = a0 + i < d.Av;
-        const int id = present ? (vis_idx ? vis_idx[a0 + i] : a0 + i) : 0;
+        const bool present = cur_id >= 0;
+#pragma unroll
         for (int kt = 0; kt < 3; ++kt) {
             if (kt * 16 >= K1) break;
             f32x4 dx = {0.f, 0.f, 0.f, 0.f};
@@ -722,40 +850,52 @@ __global__ __launch_bounds__(256, 3) void decode_bwd_kernel(DecodeDims d, MlpPtr
             if (!present) continue;
             if (kt < 2) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) gr.d_feat[(int64_t)id * kDecF + kt * 16 + 4 * g + r] += dx[r];
+                for (int r = 0; r < 4; ++r)
+                    gr.d_feat[(int64_t)cur_id * kDecF + kt * 16 + 4 * g + r] = old_feat[kt][r] + dx[r];
             } else if (g == 0 && gr.d_anchor) {
-                const float ex = anchor[id * 3] - cam[0], ey = anchor[id * 3 + 1] - cam[1], ez = anchor[id * 3 + 2] - cam[2];
-                const float dist = sqrtf(ex * ex + ey * ey + ez * ez);
-                const float ov[3] = {ex / dist, ey / dist, ez / dist};
-                const float dot = ov[0] * dx[0] + ov[1] * dx[1] + ov[2] * dx[2];
+                const float dot = my_ov[0] * dx[0] + my_ov[1] * dx[1] + my_ov[2] * dx[2];
 #pragma unroll
-                for (int q = 0; q < 3; ++q) gr.d_anchor[(int64_t)id * 3 + q] += (dx[q] - ov[q] * dot) / dist;
+                for (int q = 0; q < 3; ++q)
+                    gr.d_anchor[(int64_t)cur_id * 3 + q] = (old_anc[q] + anc_add[q]) + (dx[q] - my_ov[q] * dot) / my_dist;
             }
         }
+        DPROF_T(8);
     }
-    // flush this wave's weight-gradient partials
-    float* out = partials + (int64_t)(blockIdx.x * 4 + wave) * bwd_partial_floats(nt);
+    DPROF_T(9);
+    // the four waves' weight-gradient partials summed in LDS in wave order (deterministic),
+    // one partial per workgroup for decode_wgrad_sum_kernel
+    __syncthreads();  // every wave is done with its tile arrays: the LDS is reused
+    float* red = reinterpret_cast<float*>(&sm);
+    static_assert(sizeof(sm) >= sizeof(float) * (R * 32 + R + 32 * 48 + 32), "LDS too small for the combine");
+    for (int w = 0; w < 4; ++w) {
+        if (wave == w) {
+            auto put = [&](int idx, float v) { red[idx] = w == 0 ? v : red[idx] + v; };
 #pragma unroll
-    for (int ot = 0; ot < NT; ++ot) {
-        if (ot < nt) {
+            for (int ot = 0; ot < NT; ++ot) {
+                if (ot < nt) {
+#pragma unroll
+                    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) put((ot * 16 + 4 * g + r) * 32 + ht * 16 + i, aw2[ot][ht][r]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (lane + 64 * q < rows) put(rows * 32 + lane + 64 * q, (float)ab2[q]);
 #pragma unroll
             for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) out[(ot * 16 + 4 * g + r) * 32 + ht * 16 + i] = aw2[ot][ht][r];
+                for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        put(rows * 33 + (ht * 16 + 4 * g + r) * 48 + kt * 16 + i, aw1[ht][kt][r]);
+            if (lane < 32) put(rows * 33 + 32 * 48 + lane, (float)ab1);
         }
+        __syncthreads();
     }
-    float* ob2 = out + rows * 32;
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-        if (lane + 64 * q < rows) ob2[lane + 64 * q] = (float)ab2[q];
-    float* ow1 = ob2 + rows;
-#pragma unroll
-    for (int ht = 0; ht < 2; ++ht)
-#pragma unroll
-        for (int kt = 0; kt < 3; ++kt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) ow1[(ht * 16 + 4 * g + r) * 48 + kt * 16 + i] = aw1[ht][kt][r];
-    if (lane < 32) ow1[32 * 48 + lane] = (float)ab1;
+    const int pf = bwd_partial_floats(nt);
+    float* out = partials + (int64_t)blockIdx.x * pf;
+    for (int e = threadIdx.x; e < pf; e += 256) out[e] = red[e];
 }
 
 // sum the per-wave partials of one launch into the weight gradients (+=), in two
@@ -970,7 +1110,7 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
 #undef LAUNCH_DB
             if (int st = check_launch("decode_bwd")) return st;
             const int pf = bwd_partial_floats(nt);
-            hipLaunchKernelGGL(decode_wgrad_sum_kernel, dim3((pf + 255) / 256, kRedGroups), dim3(256), 0, s, grid * 4,
+            hipLaunchKernelGGL(decode_wgrad_sum_kernel, dim3((pf + 255) / 256, kRedGroups), dim3(256), 0, s, grid,
                                pf, partials, level2);
             if (int st = check_launch("decode_wgrad_sum")) return st;
             hipLaunchKernelGGL(decode_wgrad_reduce_kernel, dim3((pf + 255) / 256), dim3(256), 0, s, nt, t0 * 16,
@@ -981,3 +1121,14 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
     }
     return HGSR_OK;
 }
+
+#ifdef HGSR_DECODE_PROF
+extern "C" int hgsr_debug_decode_prof(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dprof), sizeof(unsigned long long) * 48) != hipSuccess) return -2;
+    if (reset) {
+        static const unsigned long long z[48] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_dprof), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
