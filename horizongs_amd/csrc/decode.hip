@@ -144,37 +144,6 @@ __device__ void stage_weights(S& sm, const MlpPtrs& mp, const DecodeDims& d, int
     }
 }
 
-// X rows of this wave's 16 anchors: feat (F) | ob_view (vd) | zero padding
-__device__ void stage_x(float* sx, const int32_t* __restrict__ vis_idx, int a0, int Av, int vd,
-                        const float* __restrict__ anchor, const float* __restrict__ feat,
-                        const float* __restrict__ cam) {
-    const int lane = threadIdx.x & 63;
-    for (int e = lane; e < 16 * kDecF; e += 64) {
-        const int a = e >> 5, k = e & 31;
-        const int v = a0 + a;
-        float val = 0.f;
-        if (v < Av) {
-            const int id = vis_idx ? vis_idx[v] : v;
-            val = feat[(int64_t)id * kDecF + k];
-        }
-        sx[a * kDecS + k] = val;
-    }
-    if (lane < 16) {
-        const int v = a0 + lane;
-        float ov[3] = {0.f, 0.f, 0.f};
-        if (v < Av && vd > 0) {
-            const int id = vis_idx ? vis_idx[v] : v;
-            const float dx = anchor[id * 3] - cam[0], dy = anchor[id * 3 + 1] - cam[1], dz = anchor[id * 3 + 2] - cam[2];
-            const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
-            ov[0] = dx / dist;
-            ov[1] = dy / dist;
-            ov[2] = dz / dist;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) sx[lane * kDecS + kDecF + k] = (k < 3 && vd > 0) ? ov[k] : 0.f;
-    }
-}
-
 // X rows of a wave's 16 anchors fetched into registers one tile ahead (software pipeline:
 // the id loads, then the feat / anchor loads, are issued during the previous tile's MFMA
 // work, so stage-in costs no exposed memory latency).  Lane l holds the id of anchor
@@ -296,12 +265,21 @@ __global__ __launch_bounds__(256) void decode_count_kernel(DecodeDims d, MlpPtrs
     stage_weights(sm, mp, d, 32, 16);  // opacity head only
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
+    XPrefetch px;  // X rows one tile ahead
+    if (blockIdx.x < (unsigned)n_tiles) {
+        x_issue_id(px, vis_idx, blockIdx.x * kDecTile + wave * 16, d.Av);
+        x_issue_data(px, feat, anchor, d.vd);
+    }
     for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
         __syncthreads();
         const int a0 = t * kDecTile + wave * 16;
-        stage_x(sm.x[wave], vis_idx, a0, d.Av, d.vd, anchor, feat, cam);
+        float ov[3], dist;
+        x_store(px, sm.x[wave], d.vd, cam, ov, dist);
+        const int tn = t + gridDim.x;
+        if (tn < n_tiles) x_issue_id(px, vis_idx, tn * kDecTile + wave * 16, d.Av);
         __syncthreads();
         const int c = opacity_head<KSTEPS>(sm, wave, a0, d.Av, d, false);
+        if (tn < n_tiles) x_issue_data(px, feat, anchor, d.vd);
         if (lane == 0) sm.wave_cnt[wave] = c;
         __syncthreads();
         if (threadIdx.x == 0) tile_cnt[t] = sm.wave_cnt[0] + sm.wave_cnt[1] + sm.wave_cnt[2] + sm.wave_cnt[3];
@@ -359,12 +337,41 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
     const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
     const int noff = d.noff, cd = d.cd;
+    XPrefetch px;  // X rows one tile ahead
+    if (blockIdx.x < (unsigned)n_tiles) {
+        x_issue_id(px, vis_idx, blockIdx.x * kDecTile + wave * 16, d.Av);
+        x_issue_data(px, feat, anchor, d.vd);
+    }
+    constexpr int kSI = 3;  // 16 anchors x n_offsets <= 12 -> <= 192 slots = 3 per lane
     for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
         __syncthreads();
         const int a0 = t * kDecTile + wave * 16;
-        stage_x(sm.x[wave], vis_idx, a0, d.Av, d.vd, anchor, feat, cam);
+        float ov[3], dist;
+        x_store(px, sm.x[wave], d.vd, cam, ov, dist);
+        const int cur_id = px.id;
+        const int tn = t + gridDim.x;
+        if (tn < n_tiles) x_issue_id(px, vis_idx, tn * kDecTile + wave * 16, d.Av);
+        // per-slot operands of this tile (scaling_raw, offset, anchor position), issued now and
+        // consumed after the MLPs
+        float srw[kSI][6], ofs[kSI][3], anc[kSI][3];
+#pragma unroll
+        for (int it = 0; it < kSI; ++it) {
+            const int sl = lane + 64 * it;
+            const int a = sl / noff, k = sl - a * noff;
+            const int aid = __shfl(cur_id, a < 16 ? a : 0);
+            const bool live = sl < 16 * noff && a0 + a < d.Av;
+            const int64_t id = live ? aid : 0;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) srw[it][q] = live ? scaling_raw[id * 6 + q] : 0.f;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                ofs[it][q] = live ? offset[(id * noff + k) * 3 + q] : 0.f;
+                anc[it][q] = live ? anchor[id * 3 + q] : 0.f;
+            }
+        }
         __syncthreads();
         const int c = opacity_head<KSTEPS>(sm, wave, a0, d.Av, d, true);
+        if (tn < n_tiles) x_issue_data(px, feat, anchor, d.vd);
         if (lane == 0) sm.wave_cnt[wave] = c;
         __syncthreads();
         int base = tile_off[t];
@@ -393,16 +400,18 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
 #pragma unroll
             for (int r = 0; r < 4; ++r) syw[(ot * 16 + 4 * g + r) * kDecYS + i] = y[r];
         }
-        for (int s = lane; s < 16 * noff; s += 64) {
+#pragma unroll
+        for (int it = 0; it < kSI; ++it) {
+            const int s = lane + 64 * it;
+            if (s >= 16 * noff) continue;
             const int a = s / noff, k = s - a * noff;
             if (a0 + a >= d.Av) continue;
             const int p = pos[s];
             if (p < 0) continue;
-            const int id = vis_idx ? vis_idx[a0 + a] : a0 + a;
             float cv[7];
 #pragma unroll
             for (int q = 0; q < 7; ++q) cv[q] = syw[(7 * k + q) * kDecYS + a];
-            const float* sr = scaling_raw + (int64_t)id * 6;
+            const float* sr = srw[it];
 #pragma unroll
             for (int q = 0; q < 3; ++q)
                 out.scaling[(int64_t)p * 3 + q] = __expf(sr[3 + q]) * __builtin_amdgcn_rcpf(1.0f + __expf(-cv[q]));
@@ -411,12 +420,11 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
             const float inrm = __builtin_amdgcn_rcpf(nrm);
 #pragma unroll
             for (int q = 0; q < 4; ++q) out.rot[(int64_t)p * 4 + q] = cv[3 + q] * inrm;
-            const float* of = offset + ((int64_t)id * noff + k) * 3;
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
-                const float o = of[q] * __expf(sr[q]);
+                const float o = ofs[it][q] * __expf(sr[q]);
                 out.offsets[(int64_t)p * 3 + q] = o;
-                out.xyz[(int64_t)p * 3 + q] = anchor[(int64_t)id * 3 + q] + o;
+                out.xyz[(int64_t)p * 3 + q] = anc[it][q] + o;
             }
         }
         // colour head straight from the accumulators (linear output)
@@ -561,7 +569,7 @@ __global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtr
         x_issue_id(px, vis_idx, blockIdx.x * kDecTile + wave * 16, d.Av);
         x_issue_data(px, feat, anchor, d.vd);
     }
-    constexpr int kSI = 3;  // 16 anchors x n_offsets <= 11 -> <= 192 slots = 3 per lane
+    constexpr int kSI = 3;  // 16 anchors x n_offsets <= 12 -> <= 192 slots = 3 per lane
     constexpr int kCI = NT * 4;  // colour head: rows * 16 / 64 (anchor, output) pairs per lane
     for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
         wave_lds_sync();  // this wave's previous tile is done with its LDS arrays
@@ -958,7 +966,8 @@ static int check_decode(int Av, int F, int vd, int noff, int cd, const DecodeDim
     HGSR_REQUIRE(Av >= 0, "bad dims");
     HGSR_REQUIRE(F == kDecF, "decode: feat_dim must be %d (got %d)", kDecF, F);
     HGSR_REQUIRE(vd == 0 || vd == 3, "decode: view_dim must be 0 or 3 (got %d)", vd);
-    HGSR_REQUIRE(noff >= 1 && noff <= 16, "decode: n_offsets must be 1..16 (got %d)", noff);
+    // 16 anchors x n_offsets slots per wave tile, 3 per lane (every reference config: 5 or 10)
+    HGSR_REQUIRE(noff >= 1 && noff <= 12, "decode: n_offsets must be 1..12 (got %d)", noff);
     HGSR_REQUIRE(cd >= 1 && cd % 3 == 0, "decode: color_dim must be a positive multiple of 3 (got %d)", cd);
     HGSR_REQUIRE(d.rows <= kDecMaxRows, "decode: %d second-layer rows exceed the LDS plan (%d)", d.rows, kDecMaxRows);
     HGSR_REQUIRE(d.T[1] <= 5, "decode: n_offsets too large for the cov head plan");
