@@ -37,41 +37,71 @@ struct StatisState {
     float* offset_opacity_accum;   // [A*noff] (max mode)
 };
 
+// One lane per visible anchor, its slots unrolled (noff <= kStatMaxOff) so that every
+// memory access of a level is issued for all slots before any is used: the selection
+// bytes and ranks, then the Gaussian gathers and the old accumulator values, then the
+// stores -- three exposed latencies per anchor instead of ~4 per slot.  Each slot's
+// accumulators are written by exactly one lane (deterministic).
+constexpr int kStatMaxOff = 16;
 __global__ __launch_bounds__(256) void training_statis_kernel(int Av, int noff, float half_w, float half_h,
                                                               int pruning_max, int growing_max, StatisIn in,
                                                               StatisState st) {
     const int a = blockIdx.x * 256 + threadIdx.x;
     if (a >= Av) return;
     const int64_t id = in.vis_idx[a];
+    bool sel[kStatMaxOff];
+    int64_t m[kStatMaxOff];
+#pragma unroll
+    for (int k = 0; k < kStatMaxOff; ++k) {
+        const int64_t j = (int64_t)a * noff + k;
+        sel[k] = k < noff && in.sel[j];
+        m[k] = k < noff ? in.sel_rank[j] : 0;
+    }
+    float o[kStatMaxOff], gx[kStatMaxOff], gy[kStatMaxOff], acc[kStatMaxOff], den[kStatMaxOff];
+    float mr[kStatMaxOff], oa[kStatMaxOff], rad[kStatMaxOff];
+    bool flt[kStatMaxOff];
+#pragma unroll
+    for (int k = 0; k < kStatMaxOff; ++k) {
+        const int64_t mk = sel[k] ? m[k] : 0;
+        const int64_t gslot = id * noff + k;
+        o[k] = sel[k] ? in.opacity[mk] : 0.f;
+        flt[k] = sel[k] && in.filt[mk];
+        gx[k] = flt[k] ? in.grad[mk * 2] : 0.f;
+        gy[k] = flt[k] ? in.grad[mk * 2 + 1] : 0.f;
+        acc[k] = flt[k] ? st.offset_gradient_accum[gslot] : 0.f;
+        den[k] = flt[k] ? st.offset_denom[gslot] : 0.f;
+        mr[k] = (flt[k] && growing_max) ? st.max_radii2D[gslot] : 0.f;
+        oa[k] = (flt[k] && growing_max) ? st.offset_opacity_accum[gslot] : 0.f;
+        rad[k] = (flt[k] && growing_max) ? (float)in.radii[mk] : 0.f;
+    }
+    const float a_old = st.anchor_opacity_accum[id], d_old = st.anchor_demon[id];
     float osum = 0.f;
     int cnt = 0;
-    for (int k = 0; k < noff; ++k) {
-        const int64_t j = (int64_t)a * noff + k;
-        if (!in.sel[j]) continue;
-        const int64_t m = in.sel_rank[j];
-        const float o = in.opacity[m];
-        osum += o;
+#pragma unroll
+    for (int k = 0; k < kStatMaxOff; ++k) {
+        if (!sel[k]) continue;
+        osum += o[k];
         ++cnt;
-        if (!in.filt[m]) continue;
+        if (!flt[k]) continue;
         const int64_t gslot = id * noff + k;
         // grad[:, 0] *= W/2, grad[:, 1] *= H/2, then the 2-norm (basic_model.py:128-131)
-        const float gx = in.grad[m * 2] * half_w, gy = in.grad[m * 2 + 1] * half_h;
-        const float gn = sqrtf(gx * gx + gy * gy);
+        const float sx = gx[k] * half_w, sy = gy[k] * half_h;
+        const float gn = sqrtf(sx * sx + sy * sy);
         if (growing_max) {
-            st.offset_gradient_accum[gslot] = fmaxf(st.offset_gradient_accum[gslot], fabsf(gn));
-            st.max_radii2D[gslot] = fmaxf(st.max_radii2D[gslot], (float)in.radii[m]);
-            st.offset_opacity_accum[gslot] += o;
+            st.offset_gradient_accum[gslot] = fmaxf(acc[k], fabsf(gn));
+            st.max_radii2D[gslot] = fmaxf(mr[k], rad[k]);
+            st.offset_opacity_accum[gslot] = oa[k] + o[k];
         } else {
-            st.offset_gradient_accum[gslot] += gn;
+            st.offset_gradient_accum[gslot] = acc[k] + gn;
         }
-        st.offset_denom[gslot] += 1.f;
+        st.offset_denom[gslot] = den[k] + 1.f;
     }
     if (pruning_max) {
-        st.anchor_opacity_accum[id] = fmaxf(st.anchor_opacity_accum[id], fabsf(osum));
+        st.anchor_opacity_accum[id] = fmaxf(a_old, fabsf(osum));
     } else {
-        st.anchor_opacity_accum[id] += cnt > 0 ? osum / (float)cnt : 0.f;  // clamp(count, 1); 0 if empty
+        st.anchor_opacity_accum[id] = a_old + (cnt > 0 ? osum / (float)cnt : 0.f);  // clamp(count, 1); 0 if empty
     }
-    st.anchor_demon[id] += 1.f;
+    st.anchor_demon[id] = d_old + 1.f;
 }
 
 // ------------------------------------------------------------ voxel hash set
@@ -233,6 +263,7 @@ extern "C" int hgsr_training_statis(int Av, int n_offsets, int width, int height
                                     float* anchor_demon, float* offset_gradient_accum, float* offset_denom,
                                     float* max_radii2D, float* offset_opacity_accum, hgsr_stream_t stream) {
     HGSR_REQUIRE(Av >= 0 && n_offsets > 0 && width > 0 && height > 0, "bad dims");
+    HGSR_REQUIRE(n_offsets <= kStatMaxOff, "training_statis: n_offsets must be <= %d (got %d)", kStatMaxOff, n_offsets);
     if (Av == 0) return HGSR_OK;
     HGSR_REQUIRE(vis_idx && selection && selection_rank && visibility_filter && viewspace_grad && opacity &&
                      anchor_opacity_accum && anchor_demon && offset_gradient_accum && offset_denom,
@@ -241,6 +272,7 @@ extern "C" int hgsr_training_statis(int Av, int n_offsets, int width, int height
     const StatisIn in{vis_idx, selection, selection_rank, visibility_filter, viewspace_grad, opacity, radii};
     const StatisState st{anchor_opacity_accum, anchor_demon, offset_gradient_accum, offset_denom, max_radii2D,
                          offset_opacity_accum};
+    KernelTimer kt("training_statis", as_stream(stream));
     hipLaunchKernelGGL(training_statis_kernel, dim3(blocks_for(Av)), dim3(256), 0, as_stream(stream), Av, n_offsets,
                        0.5f * (float)width, 0.5f * (float)height, pruning_max, growing_max, in, st);
     return check_launch("training_statis");

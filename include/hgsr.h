@@ -383,7 +383,7 @@ int hgsr_loss_bwd(int C, int H, int W, const float* image, const int64_t* image_
  * anchor_opacity_accum / anchor_demon [A], offset_gradient_accum / offset_denom /
  * max_radii2D / offset_opacity_accum [A*n_offsets] ("mean" or "max" pruning / growing
  * types; the reference scales the gradient by (W/2, H/2) before the norm).
- * One lane per visible anchor, slots in order: deterministic. */
+ * One lane per visible anchor, slots in order (n_offsets <= 16): deterministic. */
 int hgsr_training_statis(int Av, int n_offsets, int width, int height, int pruning_max, int growing_max,
                          const int32_t* vis_idx, const uint8_t* selection, const int32_t* selection_rank,
                          const uint8_t* visibility_filter, const float* viewspace_grad,
