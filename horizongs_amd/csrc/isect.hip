@@ -80,7 +80,8 @@ __global__ __launch_bounds__(256) void isect_count_lds_kernel(
     extern __shared__ __attribute__((aligned(16))) int s_hist[];
     for (int i = threadIdx.x; i < n_bins; i += 256) s_hist[i] = 0;
     __syncthreads();
-    const int64_t g0 = (int64_t)blockIdx.x * per_block;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);  // the same block <-> Gaussian range map as the emit
+    const int64_t g0 = (int64_t)blk * per_block;
     const int64_t g1 = min(g0 + per_block, CN);
     // kIsectBatch Gaussians per lane per round, all loads issued before any is used
     for (int64_t ob = g0 + threadIdx.x; ob < g1; ob += 256 * kIsectBatch) {
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(256) void isect_count_lds_kernel(
         }
     }
     __syncthreads();
-    int32_t* row = blockhist + (int64_t)blockIdx.x * n_bins;
+    int32_t* row = blockhist + (int64_t)blk * n_bins;
     for (int i = threadIdx.x; i < n_bins; i += 256) row[i] = s_hist[i];
 }
 
@@ -227,11 +228,15 @@ __global__ __launch_bounds__(256) void isect_emit_lds_kernel(
     int th, int n_tiles, int n_bins, const int32_t* __restrict__ offsets,
     const int32_t* __restrict__ blockhist, const int32_t* __restrict__ chunk_pre, uint64_t* __restrict__ keys) {
     extern __shared__ __attribute__((aligned(16))) int s_cur[];
-    const int32_t* row = blockhist + (int64_t)blockIdx.x * n_bins;
-    const int32_t* cpre = chunk_pre + (int64_t)(blockIdx.x / kColRows) * n_bins;
+    // Logical block = XCD-contiguous remap of the dispatch index: the blocks resident on one
+    // XCD hold consecutive slices of every bin, so their scattered 8-B key writes to a bin
+    // land in adjacent addresses of the same L2 and leave it as whole lines.
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int32_t* row = blockhist + (int64_t)blk * n_bins;
+    const int32_t* cpre = chunk_pre + (int64_t)(blk / kColRows) * n_bins;
     for (int i = threadIdx.x; i < n_bins; i += 256) s_cur[i] = offsets[i] + cpre[i] + row[i];
     __syncthreads();
-    const int64_t g0 = (int64_t)blockIdx.x * per_block;
+    const int64_t g0 = (int64_t)blk * per_block;
     const int64_t g1 = min(g0 + per_block, CN);
     for (int64_t ob = g0 + threadIdx.x; ob < g1; ob += 256 * kIsectBatch) {
         int32_t r[kIsectBatch];
