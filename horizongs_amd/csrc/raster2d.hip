@@ -154,11 +154,47 @@ __global__ __launch_bounds__(256) void pack2_kernel(int64_t n, int N, const floa
     rec[i] = r;
 }
 
-// does the surfel's skip geometry reach the 8x8 quadrant centred at (qx, qy)?
-__device__ __forceinline__ bool reaches2(const float4 r2, const float4 r4, const float4 box, float qx, float qy) {
+// Does the surfel reach the 8x8 quadrant centred at (qx, qy)?  Both passes use this test, so
+// they skip the same records.  The record's boxes give a cheap conservative answer; the
+// exact refinement follows.
+// With q = p - m (pixel centre relative to the projected mean) the hit is
+// c = q_x A + q_y B + C' and the UV-disk branch is valid iff |c_xy|^2 <= 2L c_z^2, i.e.
+// f(q) = a q_x^2 + b q_x q_y + c q_y^2 + d q_x + e q_y + f0 <= 0.  When the quadratic part
+// is positive definite that set is an ellipse and f is convex, so its minimum over the
+// quadrant's pixel-centre rectangle is at the unconstrained minimiser (if inside) or on an
+// edge (a 1-D parabola minimised in closed form).  Otherwise (the plane nearly through the
+// camera) the f64 bounding box of the record decides, as before.  The low-pass branch
+// (|q|^2 <= L) is tested against the nearest point of the rectangle.  Conservative: L is
+// inflated by 2 % + 0.02, far above the rounding of the per-pixel evaluation and of the
+// hardware exp / rcp, so a skipped record has alpha < 1/255 at every pixel of the quadrant.
+__device__ __forceinline__ bool reaches2_exact(const float4 r0, const float4 r1, const float4 r2, const float4 r4,
+                                               const float4 box, float qx, float qy) {
     const bool in_box = fabsf(box.x - qx) <= box.z + 3.5f && fabsf(box.y - qy) <= box.w + 3.5f;
-    const bool in_disk = fabsf(r2.y - qx) <= r4.w + 3.5f && fabsf(r2.z - qy) <= r4.w + 3.5f;
-    return in_box | in_disk;
+    const bool in_dbox = fabsf(r2.y - qx) <= r4.w + 3.5f && fabsf(r2.z - qy) <= r4.w + 3.5f;
+    const float X0 = qx - 3.5f - r2.y, X1 = qx + 3.5f - r2.y, Y0 = qy - 3.5f - r2.z, Y1 = qy + 3.5f - r2.z;
+    const float Lp = 1.02f * __logf(255.0f * r2.w) + 0.02f;
+    const float nx = fminf(fmaxf(0.f, X0), X1), ny = fminf(fmaxf(0.f, Y0), Y1);
+    const bool in_disk = in_dbox & (nx * nx + ny * ny <= Lp);
+    const float L2 = 2.0f * Lp;
+    const float Ax = r0.x, Ay = r0.y, Az = r0.z, Bx = r0.w, By = r1.x, Bz = r1.y, Cx = r1.z, Cy = r1.w, Cz = r2.x;
+    const float a = Ax * Ax + Ay * Ay - L2 * Az * Az;
+    const float b = 2.0f * (Ax * Bx + Ay * By - L2 * Az * Bz);
+    const float c = Bx * Bx + By * By - L2 * Bz * Bz;
+    const float d = 2.0f * (Ax * Cx + Ay * Cy - L2 * Az * Cz);
+    const float e = 2.0f * (Bx * Cx + By * Cy - L2 * Bz * Cz);
+    const float f0 = Cx * Cx + Cy * Cy - L2 * Cz * Cz;
+    const float det = 4.0f * a * c - b * b;
+    const bool pd = (a > 0.f) & (c > 0.f) & (det > 1e-3f * 4.0f * a * c);
+    const float i2a = 0.5f * __builtin_amdgcn_rcpf(a), i2c = 0.5f * __builtin_amdgcn_rcpf(c);
+    auto F = [&](float x, float y) { return fmaf(fmaf(a, x, fmaf(b, y, d)), x, fmaf(fmaf(c, y, e), y, f0)); };
+    const float yA = fminf(fmaxf(-(b * X0 + e) * i2c, Y0), Y1), yB = fminf(fmaxf(-(b * X1 + e) * i2c, Y0), Y1);
+    const float xA = fminf(fmaxf(-(b * Y0 + d) * i2a, X0), X1), xB = fminf(fmaxf(-(b * Y1 + d) * i2a, X0), X1);
+    const float m = fminf(fminf(F(X0, yA), F(X1, yB)), fminf(F(xA, Y0), F(xB, Y1)));
+    const float idet = __builtin_amdgcn_rcpf(det);
+    const float sx = (b * e - 2.0f * c * d) * idet, sy = (b * d - 2.0f * a * e) * idet;
+    const bool centre_in = (sx >= X0) & (sx <= X1) & (sy >= Y0) & (sy <= Y1);
+    const bool in_ell = pd ? (centre_in | (m <= 0.f)) : true;
+    return (in_box & in_ell) | in_disk;
 }
 
 __device__ __forceinline__ int lanes_below2(uint64_t m) {
@@ -243,7 +279,7 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
 #pragma unroll
         for (int k = 0; k < NB / 64; ++k) {
             const int t = k * 64 + lane;
-            const bool rel = t < cnt && reaches2(s_r2[t], s_r4[t], s_box[t], qx, qy);
+            const bool rel = t < cnt && reaches2_exact(s_r0[t], s_r1[t], s_r2[t], s_r4[t], s_box[t], qx, qy);
             const uint64_t m = __ballot(rel);
             if (rel) my_list[n_mine + lanes_below2(m)] = (uint8_t)t;
             n_mine += __popcll(m);
@@ -423,7 +459,8 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
         lds_barrier();
         const int t0 = max(0, batch_end - wave_final);
         const int t = lane;
-        const bool rel = t < bsz && t >= t0 && reaches2(s_r2[cur][t], s_r4[cur][t], s_box[cur][t], qx, qy);
+        const bool rel = t < bsz && t >= t0 &&
+                         reaches2_exact(s_r0[cur][t], s_r1[cur][t], s_r2[cur][t], s_r4[cur][t], s_box[cur][t], qx, qy);
         const uint64_t m = __ballot(rel);
         if (rel) my_list[lanes_below2(m)] = (uint8_t)t;
         const int n_mine = __popcll(m);
