@@ -235,7 +235,11 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     float* __restrict__ render_distort, float* __restrict__ render_median, int32_t* __restrict__ last_ids,
     int32_t* __restrict__ median_ids) {
     constexpr int NB = kFwd2Batch;
-    __shared__ float4 s_r0[NB], s_r1[NB], s_r2[NB], s_col[NB], s_r4[NB], s_box[NB];
+    // one LDS object: every component of record t sits at a compile-time offset from one address
+    __shared__ struct {
+        float4 r0[NB], r1[NB], r2[NB], col[NB], r4[NB], box[NB];
+    } sr;
+    float4 *s_r0 = sr.r0, *s_r1 = sr.r1, *s_r2 = sr.r2, *s_col = sr.col, *s_r4 = sr.r4, *s_box = sr.box;
     __shared__ uint8_t s_list[4][NB];
     __shared__ int s_vote[2][4];
     const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects);
@@ -358,9 +362,22 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     // 11 opac, 12-14 normal, 15.. colour, then abs xy; split2 maps v_c sums to u, v, w and densify
     constexpr int KV = 15 + D + (ABS ? 2 : 0);
     constexpr int NB = kBwd2Batch;
-    __shared__ float4 s_r0[2][NB], s_r1[2][NB], s_r2[2][NB], s_col[2][NB], s_r4[2][NB], s_box[2][NB];
+    // one LDS object: every component of record t sits at a compile-time offset from one address
+    __shared__ struct {
+        float4 r0[2][NB], r1[2][NB], r2[2][NB], col[2][NB], r4[2][NB], box[2][NB];
+    } sr;
+    auto& s_r0 = sr.r0;
+    auto& s_r1 = sr.r1;
+    auto& s_r2 = sr.r2;
+    auto& s_col = sr.col;
+    auto& s_r4 = sr.r4;
+    auto& s_box = sr.box;
     __shared__ int32_t s_id[2][NB];
-    constexpr int KVP = KV + 1;        // + a never-read slot that absorbs padding lanes' atomics
+    // row j of a lane row r lands in slot slot0(r) + 2j (TransposeReduce's pattern); the
+    // pattern's positions past KV are never read, and a padding position inside [0, KV) only
+    // ever receives an exact 0 (the padded values), so one base address serves every j
+    constexpr int KVP = (KV + 1) > (2 * TransposeReduce<KV>::G + TransposeReduce<KV>::H)
+                            ? (KV + 1) : (2 * TransposeReduce<KV>::G + TransposeReduce<KV>::H);
     __shared__ float s_part[NB * KVP];  // the four waves' partials merged with LDS float atomics
     __shared__ uint8_t s_list[4][NB];
     __shared__ int32_t s_last[4];
@@ -424,13 +441,8 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     }
     using TR = TransposeReduce<KV>;
     const int row = lane >> 4;
-    int slot[TR::G];  // accumulator slot of this row's reduced value j (KV = padding)
-#pragma unroll
-    for (int j = 0; j < TR::G; ++j) {
-        const int idx = row == 0 ? TR::index(j, 0) : row == 1 ? TR::index(j, 1) : row == 2 ? TR::index(j, 2)
-                                                                                        : TR::index(j, 3);
-        slot[j] = idx >= 0 ? idx : KV;
-    }
+    // first accumulator slot of this lane row's reduced values (slot0 + 2j for value j)
+    const int slot0 = row == 0 ? 0 : row == 1 ? 1 : row == 2 ? TR::H : TR::H + 1;
     uint8_t* my_list = s_list[wave];
     int prev_bsz = 0;
     for (int b = 0; b <= nb; ++b) {
@@ -517,7 +529,7 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
                 if ((lane & 15) == 0) {
                     float* dst = s_part + t * KVP;
 #pragma unroll
-                    for (int j = 0; j < TR::G; ++j) atomicAdd(dst + slot[j], u[j]);  // ds_add_f32
+                    for (int j = 0; j < TR::G; ++j) atomicAdd(dst + slot0 + 2 * j, u[j]);  // ds_add_f32
                 }
             }
         }

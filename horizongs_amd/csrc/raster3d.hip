@@ -292,7 +292,11 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     // combined, so each batch costs two barriers
     __shared__ float4 s_rec[2][NB][3];  // interleaved {g0, g1, col}: one address per record
     __shared__ int32_t s_id[2][NB];
-    constexpr int KVP = KV + 1;        // + a never-read slot that absorbs padding lanes' atomics
+    // row j of a lane row r lands in slot slot0(r) + 2j (TransposeReduce's pattern); the
+    // pattern's positions past KV are never read, and a padding position inside [0, KV) only
+    // ever receives an exact 0 (the padded values), so one base address serves every j
+    constexpr int KVP = (KV + 1) > (2 * TransposeReduce<KV>::G + TransposeReduce<KV>::H)
+                            ? (KV + 1) : (2 * TransposeReduce<KV>::G + TransposeReduce<KV>::H);
     __shared__ float s_part[NB * KVP];  // the four waves' partials merged with LDS float atomics
     __shared__ uint8_t s_list[4][NB];
     __shared__ int32_t s_last[4];
@@ -347,13 +351,8 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     }
     using TR = TransposeReduce<KV>;
     const int row = lane >> 4;
-    int slot[TR::G];  // accumulator slot of this row's reduced value j (KV = padding)
-#pragma unroll
-    for (int j = 0; j < TR::G; ++j) {
-        const int idx = row == 0 ? TR::index(j, 0) : row == 1 ? TR::index(j, 1) : row == 2 ? TR::index(j, 2)
-                                                                                        : TR::index(j, 3);
-        slot[j] = idx >= 0 ? idx : KV;
-    }
+    // first accumulator slot of this lane row's reduced values (slot0 + 2j for value j)
+    const int slot0 = row == 0 ? 0 : row == 1 ? 1 : row == 2 ? TR::H : TR::H + 1;
     uint8_t* my_list = s_list[wave];
     int prev_bsz = 0;
     for (int b = 0; b <= nb; ++b) {
@@ -452,7 +451,7 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
                 if ((lane & 15) == 0) {
                     float* dst = s_part + t * KVP;
 #pragma unroll
-                    for (int j = 0; j < TR::G; ++j) atomicAdd(dst + slot[j], u[j]);  // ds_add_f32
+                    for (int j = 0; j < TR::G; ++j) atomicAdd(dst + slot0 + 2 * j, u[j]);  // ds_add_f32
                 }
             };
             // two loops instead of a per-step select between the list halves
