@@ -966,8 +966,9 @@ static int check_decode(int Av, int F, int vd, int noff, int cd, const DecodeDim
     HGSR_REQUIRE(Av >= 0, "bad dims");
     HGSR_REQUIRE(F == kDecF, "decode: feat_dim must be %d (got %d)", kDecF, F);
     HGSR_REQUIRE(vd == 0 || vd == 3, "decode: view_dim must be 0 or 3 (got %d)", vd);
-    // 16 anchors x n_offsets slots per wave tile, 3 per lane (every reference config: 5 or 10)
-    HGSR_REQUIRE(noff >= 1 && noff <= 12, "decode: n_offsets must be 1..12 (got %d)", noff);
+    // 16 anchors x n_offsets slots per wave tile, 3 per lane; the cov head (7 x n_offsets rows) fits
+    // 5 output tiles: n_offsets <= 11 (every reference config: 5 or 10)
+    HGSR_REQUIRE(noff >= 1 && noff <= 11, "decode: n_offsets must be 1..11 (got %d)", noff);
     HGSR_REQUIRE(cd >= 1 && cd % 3 == 0, "decode: color_dim must be a positive multiple of 3 (got %d)", cd);
     HGSR_REQUIRE(d.rows <= kDecMaxRows, "decode: %d second-layer rows exceed the LDS plan (%d)", d.rows, kDecMaxRows);
     HGSR_REQUIRE(d.T[1] <= 5, "decode: n_offsets too large for the cov head plan");

@@ -281,7 +281,7 @@ int hgsr_lod_mask(int A, const float* anchor, const int32_t* level, const float*
                   const float* cam_center, float res_scale, float standard_dist, float log2_fork,
                   int max_level, uint8_t* mask, hgsr_stream_t stream);
 /* Decode of Av visible anchors (vis_idx [Av] int32 anchor ids, NULL = 0..Av-1):
- * feat_dim F = 32, view_dim 0 or 3, n_offsets <= 12, color_dim = 3 (RGB) or
+ * feat_dim F = 32, view_dim 0 or 3, n_offsets <= 11, color_dim = 3 (RGB) or
  * 3 (deg+1)^2 (SH); mlp is a HOST array of 12 device pointers: for the opacity,
  * cov and colour heads in that order {w1 [F, F+vd], b1 [F], w2 [O, F], b2 [O]}
  * (nn.Linear layout).  Two passes: hgsr_decode_count writes the number of kept

@@ -77,11 +77,14 @@ def _random_model(n_anchor, view_dim, color_dim, seed, n_off=10):
     return inputs, mlps
 
 
-@pytest.mark.parametrize("view_dim,color_dim,n_anchor", [(3, 3, 1000), (0, 27, 700), (3, 3, 20011)])
-def test_decode_backward(view_dim, color_dim, n_anchor):
-    """All input and weight gradients vs fp64 / fp32 autograd of the oracle restatement."""
+@pytest.mark.parametrize("view_dim,color_dim,n_anchor,n_off", [(3, 3, 1000, 10), (0, 27, 700, 10), (3, 3, 20011, 10),
+                                                              (3, 3, 1500, 5), (3, 3, 333, 11)])
+def test_decode_backward(view_dim, color_dim, n_anchor, n_off):
+    """All input and weight gradients vs fp64 / fp32 autograd of the oracle restatement.
+    n_offsets 5 is the Block_A chunk setting (config/ours/large_scene/block_A/config.yaml:11),
+    11 the largest the kernels take."""
     from horizongs_amd import decode as HD
-    inputs, mlps = _random_model(n_anchor, view_dim, color_dim, seed=5 + n_anchor)
+    inputs, mlps = _random_model(n_anchor, view_dim, color_dim, seed=5 + n_anchor, n_off=n_off)
     gen = torch.Generator().manual_seed(77)
     vis = torch.rand(n_anchor, generator=gen) < 0.8
 
@@ -90,7 +93,7 @@ def test_decode_backward(view_dim, color_dim, n_anchor):
         ws = {k: v.to(dtype).clone().requires_grad_(True) for k, v in mlps.items()}
         sub = {k: (v[vis] if k != "cam_center" else v) for k, v in ins.items()}
         outs = D.decode_torch(sub["anchor"], sub["feat"], sub["offset"], sub["scaling_raw"], sub["cam_center"], ws,
-                              view_dim, 10, color_dim)
+                              view_dim, n_off, color_dim)
         return ins, ws, outs
 
     ins32, ws32, outs32 = run_ref(torch.float32)
@@ -105,7 +108,7 @@ def test_decode_backward(view_dim, color_dim, n_anchor):
     dev_in = {k: v.to(DEV).clone().requires_grad_(k != "cam_center") for k, v in inputs.items()}
     dev_w = {k: v.to(DEV).clone().requires_grad_(True) for k, v in mlps.items()}
     outs = HD.decode(dev_in["anchor"], dev_in["feat"], dev_in["offset"], dev_in["scaling_raw"], dev_in["cam_center"],
-                     dev_w, vis.to(DEV), view_dim, 10, color_dim)
+                     dev_w, vis.to(DEV), view_dim, n_off, color_dim)
     np.testing.assert_array_equal(outs[6].cpu().numpy(), mask_ref.numpy())
     for o, r32, r64, name in zip(outs[:6], outs32[:6], outs64[:6], ("xyz", "offsets", "color", "opacity", "scaling",
                                                                    "rot")):
