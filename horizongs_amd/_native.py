@@ -80,6 +80,7 @@ _SIGS = {
     "hgsr_adam_step": (I, [I, P, ct.c_double, ct.c_double, ct.c_double, P]),
     "hgsr_timing_enable": (I, [I]),
     "hgsr_timing_reset": (I, []),
+    "hgsr_timing_only": (I, [ct.c_char_p]),
     "hgsr_timing_query": (I, [ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(I64)]),
 }
 

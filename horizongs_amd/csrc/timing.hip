@@ -20,6 +20,7 @@ std::vector<hipEvent_t> g_pool;
 std::vector<Rec> g_recs;
 size_t g_next = 0;
 constexpr size_t kMaxRecs = 1 << 16;
+std::string g_only;  // record only this kernel (empty = all)
 }  // namespace
 
 bool timing_on() { return g_on; }
@@ -27,6 +28,7 @@ bool timing_on() { return g_on; }
 int timing_begin(const char* name, hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_on || g_recs.size() >= kMaxRecs) return -1;
+    if (!g_only.empty() && g_only != name) return -1;
     while (g_pool.size() < g_next + 2) {
         hipEvent_t e;
         if (hipEventCreate(&e) != hipSuccess) return -1;
@@ -52,6 +54,12 @@ using namespace hgsr;
 extern "C" int hgsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_on = on != 0;
+    return HGSR_OK;
+}
+
+extern "C" int hgsr_timing_only(const char* kernel) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_only = kernel ? kernel : "";
     return HGSR_OK;
 }
 

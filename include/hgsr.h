@@ -437,6 +437,10 @@ int hgsr_adam_step(int n_tensors, const hgsr_adam_tensor* tensors, double beta1,
  * (events are pooled; at most 1<<16 records between resets). */
 int hgsr_timing_enable(int on);
 int hgsr_timing_reset(void);
+/* restrict the recording to one kernel name (NULL = every kernel): bench.py times only
+ * the dominant kernel inside its timed region, so the events add no per-launch overhead
+ * to the other kernels of the step. */
+int hgsr_timing_only(const char* kernel);
 /* total milliseconds and launch count recorded for `kernel` (synchronises the
  * recorded events); kernel names: project3d_fwd, project3d_bwd, project2d_fwd,
  * project2d_bwd, sh_fwd, sh_bwd, isect_count, isect_emit, tile_sort,
