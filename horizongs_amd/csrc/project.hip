@@ -203,7 +203,8 @@ __global__ __launch_bounds__(256) void project3d_fwd_kernel(
 
 // ---------------------------------------------------------------- 3DGS bwd
 // One lane per Gaussian, looping over cameras: deterministic accumulation.
-__global__ __launch_bounds__(256) void project3d_bwd_kernel(
+// 3 waves per SIMD (<= 168 VGPRs, a few spills): 0.079 -> 0.071 ms at 2M Gaussians; 4 spills heavily
+__global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
     int C, int N, const float* __restrict__ means, const float4* __restrict__ quats,
     const float* __restrict__ scales, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int W, int H, const int32_t* __restrict__ radii,
