@@ -187,37 +187,52 @@ __global__ __launch_bounds__(256) void isect_chunkscan_kernel(int n_chunks, int 
 __global__ __launch_bounds__(1024) void isect_binscan_kernel(int n_bins, const int32_t* __restrict__ totals,
                                                              int32_t* __restrict__ offsets,
                                                              int64_t* __restrict__ info) {
-    __shared__ int64_t s_sum[1024];
-    __shared__ int s_max[1024];
-    const int tid = threadIdx.x;
+    // thread t owns bins [t*per, t*per + per): its sum and max, then an in-wave shuffle scan
+    // and one cross-wave step through LDS (two barriers instead of a 10-level LDS scan)
+    __shared__ int64_t s_wsum[16];
+    __shared__ int s_wmax[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int per = (n_bins + 1023) / 1024;
-    const int b0 = tid * per, b1 = min(b0 + per, n_bins);
+    const int b0 = min(tid * per, n_bins), b1 = min(b0 + per, n_bins);
     int64_t local = 0;
     int mx = 0;
+#pragma unroll 8
     for (int i = b0; i < b1; ++i) {
-        local += totals[i];
-        mx = max(mx, totals[i]);
+        const int v = totals[i];
+        local += v;
+        mx = max(mx, v);
     }
-    s_sum[tid] = local;
-    s_max[tid] = mx;
+    int64_t inc = local;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t o = __shfl_up(inc, d);
+        if (lane >= d) inc += o;
+    }
+    int wm = mx;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) wm = max(wm, __shfl_xor(wm, d));
+    if (lane == 63) {
+        s_wsum[wave] = inc;
+        s_wmax[wave] = wm;
+    }
     __syncthreads();
-    // Hillis-Steele inclusive scan of 1024 partial sums
-    for (int d = 1; d < 1024; d <<= 1) {
-        int64_t v = tid >= d ? s_sum[tid - d] : 0;
-        int m2 = tid >= d ? s_max[tid - d] : 0;
-        __syncthreads();
-        s_sum[tid] += v;
-        s_max[tid] = max(s_max[tid], m2);
-        __syncthreads();
+    int64_t wpre = 0, total = 0;
+    int gmax = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+        const int64_t ws = s_wsum[w];
+        wpre += w < wave ? ws : 0;
+        total += ws;
+        gmax = max(gmax, s_wmax[w]);
     }
-    int64_t run = s_sum[tid] - local;
+    int64_t run = wpre + inc - local;
     for (int i = b0; i < b1; ++i) {
         offsets[i] = (int32_t)run;
         run += totals[i];
     }
-    if (tid == 1023) {
-        info[0] = s_sum[1023];
-        info[1] = s_max[1023];
+    if (tid == 0) {
+        info[0] = total;
+        info[1] = gmax;
     }
 }
 
