@@ -12,7 +12,8 @@
 // CDNA4 mapping: HBM-bound (28 B per element: p, g, m, v read; p, m, v written).
 // Every tensor of the step is described in the kernel arguments; a workgroup takes a
 // 4096-element chunk of one tensor (scalar lookup over the chunk prefix), each lane
-// four independent float4 rows (all loads issued before the first use).  Tensors whose
+// four independent float4 rows (all loads issued before the first use), streamed with
+// non-temporal loads / stores (every byte is touched once per step).  Tensors whose
 // four pointers are not 16-B aligned, and ragged tails, take a scalar path.
 #include "common.h"
 
@@ -21,6 +22,14 @@ namespace hgsr {
 constexpr int kAdamMaxT = 16;            // tensors per launch (more: several launches)
 constexpr int kAdamChunk = 4096;         // elements per workgroup
 constexpr int kAdamVec = kAdamChunk / 4 / 256;  // float4 rows per lane
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_nt(const float* p, int64_t i) {
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p) + i);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt(float* p, int64_t i, float4 v) {
+    __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p) + i);
+}
 
 struct AdamArgs {
     float* p[kAdamMaxT];
@@ -65,10 +74,10 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
 #pragma unroll
         for (int r = 0; r < kAdamVec; ++r) {
             const int64_t i = base / 4 + r * 256 + threadIdx.x;
-            p[r] = reinterpret_cast<const float4*>(P)[i];
-            g[r] = reinterpret_cast<const float4*>(G)[i];
-            m[r] = reinterpret_cast<const float4*>(M)[i];
-            v[r] = reinterpret_cast<const float4*>(V)[i];
+            p[r] = ld_nt(P, i);
+            g[r] = ld_nt(G, i);
+            m[r] = ld_nt(M, i);
+            v[r] = ld_nt(V, i);
         }
 #pragma unroll
         for (int r = 0; r < kAdamVec; ++r) {
@@ -77,9 +86,9 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
             adam_elem(p[r].z, g[r].z, m[r].z, v[r].z, a.w1, a.beta2, a.w2, a.eps, ss, bc);
             adam_elem(p[r].w, g[r].w, m[r].w, v[r].w, a.w1, a.beta2, a.w2, a.eps, ss, bc);
             const int64_t i = base / 4 + r * 256 + threadIdx.x;
-            reinterpret_cast<float4*>(P)[i] = p[r];
-            reinterpret_cast<float4*>(M)[i] = m[r];
-            reinterpret_cast<float4*>(V)[i] = v[r];
+            st_nt(P, i, p[r]);
+            st_nt(M, i, m[r]);
+            st_nt(V, i, v[r]);
         }
         return;
     }
