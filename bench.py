@@ -182,6 +182,27 @@ class Workload:
         return loss
 
 
+def hbm_kernels(wl, kernels, n_isects):
+    """Algorithmic-bytes rate of the HBM-bound kernels of the step (DESIGN.md §4 per-unit
+    bytes; unit counts of the last step) against the 8 TB/s HBM3E peak."""
+    if not kernels or n_isects is None:
+        return None
+    N = int(wl.last_colors.shape[0])
+    P = wl.args.width * wl.args.height
+    n_par = sum(p.numel() for p in wl.params)
+    per = {
+        "project3d_fwd": 68 * N, "project3d_bwd": 120 * N, "project2d_fwd": 104 * N, "project2d_bwd": 180 * N,
+        "tile_sort": 20 * n_isects, "isect_emit": 8 * n_isects + 16 * N,
+        "loss_fwd": 60 * 3 * P, "loss_bwd": 72 * 3 * P, "adam": 28 * n_par,
+    }
+    out = {}
+    for k, nbytes in per.items():
+        if k in kernels:
+            gbs = nbytes / (kernels[k]["avg_ms"] * 1e-3) / 1e9
+            out[k] = {"bytes": nbytes, "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 3)}
+    return out
+
+
 def raster_pairs(wl):
     """Evaluated (pixel, Gaussian) pairs of the last step: per tile, every Gaussian up to
     the tile's latest contributor, times the 256 pixels of the tile."""
@@ -416,6 +437,7 @@ def main():
                                        else "DDP over views, RCCL all-reduce of Gaussian grads")},
             "roofline": roof, "cpu_baseline": cpu, "quality": psnr_parity(args), "kernels": kernels,
             "kernels_source": "HIP events of every kernel over a separate pass after the timed region",
+            "hbm_kernels": hbm_kernels(wl, kernels, isects_after) if rank == 0 else None,
         }
         print(json.dumps(line))
     if world > 1:
