@@ -47,7 +47,7 @@ HBM_PEAK_GBS = 8000.0      # HBM3E spec
 FLOP_PER_PAIR = {"raster3d_fwd": 20.0, "raster3d_bwd": 60.0, "raster2d_fwd": 40.0, "raster2d_bwd": 120.0}
 KERNELS = ["project3d_fwd", "isect_count", "isect_emit", "tile_sort", "raster3d_fwd", "raster3d_bwd",
            "project3d_bwd", "project2d_fwd", "raster2d_fwd", "raster2d_bwd", "project2d_bwd", "sh_fwd", "sh_bwd",
-           "decode_count", "decode_fwd", "decode_bwd", "loss_fwd", "loss_bwd", "adam", "training_statis"]
+           "decode_count", "decode_fwd", "decode_bwd", "loss_fwd", "loss_bwd", "adam", "training_statis", "depth_normal_fwd", "depth_normal_bwd"]
 
 
 def parse():

@@ -19,6 +19,7 @@ RuntimeError, as gsplat's TORCH_CHECKs do.
 """
 from __future__ import annotations
 
+import ctypes as ct
 import math
 import threading
 from typing import Optional, Tuple
@@ -724,28 +725,65 @@ def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, 
     return render_colors, render_alphas, meta
 
 
-def _depth_to_points(depths, camtoworlds, Ks, z_depth=True):
-    height, width = depths.shape[-3:-1]
-    dev = depths.device
-    x, y = torch.meshgrid(torch.arange(width, device=dev), torch.arange(height, device=dev), indexing="xy")
-    fx, fy, cx, cy = Ks[..., 0, 0], Ks[..., 1, 1], Ks[..., 0, 2], Ks[..., 1, 2]
-    camera_dirs = F.pad(torch.stack([(x - cx[..., None, None] + 0.5) / fx[..., None, None],
-                                     (y - cy[..., None, None] + 0.5) / fy[..., None, None]], dim=-1),
-                        (0, 1), value=1.0)
-    directions = torch.einsum("...ij,...hwj->...hwi", camtoworlds[..., :3, :3], camera_dirs)
-    origins = camtoworlds[..., :3, -1]
-    if not z_depth:
-        directions = F.normalize(directions, dim=-1)
-    return origins[..., None, None, :] + depths * directions
+class _DepthToNormal(torch.autograd.Function):
+    """K13 on the device (hgsr_depth_normal_{fwd,bwd}); gradient to the depth map only."""
+
+    @staticmethod
+    def forward(ctx, depths, camtoworlds, Ks, z_depth):
+        C, H, W = depths.shape[0], depths.shape[-3], depths.shape[-2]
+        d = depths.reshape(C, H, W, -1)[..., 0] if depths.dim() == 4 else depths
+        if d.dtype != torch.float32:
+            d = d.float()
+        st = (ct.c_int64 * 3)(*d.stride())
+        c2w, K = _f32(camtoworlds), _f32(Ks)
+        out = torch.empty((C, H, W, 3), dtype=torch.float32, device=d.device)
+        N.call("hgsr_depth_normal_fwd", C, H, W, d.data_ptr(), ct.cast(st, ct.c_void_p), ptr(c2w), ptr(K),
+               int(z_depth), ptr(out), N.stream(d.device))
+        ctx.save_for_backward(d, c2w, K)
+        ctx.cfg = (z_depth, depths.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, v_normals):
+        d, c2w, K = ctx.saved_tensors
+        z_depth, shape = ctx.cfg
+        C, H, W = d.shape
+        st = (ct.c_int64 * 3)(*d.stride())
+        v_depth = torch.empty((C, H, W), dtype=torch.float32, device=d.device)
+        N.call("hgsr_depth_normal_bwd", C, H, W, d.data_ptr(), ct.cast(st, ct.c_void_p), ptr(c2w), ptr(K),
+               int(z_depth), ptr(_f32(v_normals)), ptr(v_depth), N.stream(d.device))
+        return v_depth.reshape(shape), None, None, None
 
 
 def depth_to_normal(depths, camtoworlds, Ks, z_depth=True):
-    """K13: central-difference normals of the unprojected depth map [C,H,W,1] -> [C,H,W,3]."""
-    points = _depth_to_points(depths, camtoworlds, Ks, z_depth=z_depth)
-    dx = points[..., 2:, 1:-1, :] - points[..., :-2, 1:-1, :]
-    dy = points[..., 1:-1, 2:, :] - points[..., 1:-1, :-2, :]
-    normals = F.normalize(torch.cross(dx, dy, dim=-1), dim=-1)
-    return F.pad(normals, (0, 0, 1, 1, 1, 1), value=0.0)
+    """K13: central-difference normals of the unprojected depth map [C,H,W,1] -> [C,H,W,3]
+    (the gsplat fork's depth_to_normal; HIP kernels, gradient to the depth map)."""
+    _check_cuda(depths, camtoworlds, Ks)
+    _unsupported(camtoworlds.requires_grad or Ks.requires_grad, "depth_to_normal gradients w.r.t. the cameras")
+    return _DepthToNormal.apply(depths, camtoworlds.detach(), Ks.detach(), bool(z_depth))
+
+
+class _Rotate3(torch.autograd.Function):
+    """vectors [C,...,3] -> R_c v (hgsr_rotate3); the vjp applies R_c^T.  R carries no gradient."""
+
+    @staticmethod
+    def forward(ctx, R, v):
+        C = v.shape[0]
+        vc = _f32(v)
+        out = torch.empty_like(vc)
+        R9 = _f32(R.reshape(C, 9))
+        N.call("hgsr_rotate3", C, vc.numel() // (3 * C), ptr(R9), 0, ptr(vc), ptr(out), N.stream(v.device))
+        ctx.save_for_backward(R9)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (R9,) = ctx.saved_tensors
+        C = g.shape[0]
+        gc = _f32(g)
+        out = torch.empty_like(gc)
+        N.call("hgsr_rotate3", C, gc.numel() // (3 * C), ptr(R9), 1, ptr(gc), ptr(out), N.stream(g.device))
+        return None, out
 
 
 def _camtoworlds(viewmats):
@@ -812,7 +850,7 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
     if render_mode in ("RGB+ED", "RGB+D"):
         dmap = render_median if depth_mode == "median" else render_colors[..., -1:]
         render_normals_from_depth = depth_to_normal(dmap, c2w, Ks)
-    render_normals = torch.einsum("cij,chwj->chwi", c2w[:, :3, :3], render_normals)
+    render_normals = _Rotate3.apply(c2w[:, :3, :3].contiguous(), render_normals)  # camera -> world frame
     meta = {
         "camera_ids": None, "gaussian_ids": None, "radii": radii, "means2d": means2d, "depths": depths,
         "ray_transforms": ray_transforms, "normals": normals, "opacities": opac, "tile_width": tw,

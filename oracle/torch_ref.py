@@ -184,3 +184,27 @@ def raster2d(means2d, rt, colors, opacities, normals, depths, radius, W, H, bg=N
     order = torch.argsort(depths.detach().float(), stable=True)
     (img, nrm), T = _composite(alpha, valid, [colors, normals], [bg, None], order)
     return img.reshape(H, W, -1), (1 - T).reshape(H, W, 1), nrm.reshape(H, W, 3)
+
+
+def depth_to_normal(depths, camtoworlds, Ks, z_depth=True):
+    """The gsplat fork's depth_to_normal restated in torch (any device / dtype; autograd):
+    unproject the depth map [C,H,W,1] through the pinhole rays, central differences along
+    y (dx) and x (dy), normalize(cross(dx, dy)), zero one-pixel border -> [C,H,W,3]."""
+    import torch.nn.functional as F
+    height, width = depths.shape[-3:-1]
+    dev, dt = depths.device, depths.dtype
+    x, y = torch.meshgrid(torch.arange(width, device=dev, dtype=dt), torch.arange(height, device=dev, dtype=dt),
+                          indexing="xy")
+    fx, fy, cx, cy = Ks[..., 0, 0], Ks[..., 1, 1], Ks[..., 0, 2], Ks[..., 1, 2]
+    camera_dirs = F.pad(torch.stack([(x - cx[..., None, None] + 0.5) / fx[..., None, None],
+                                     (y - cy[..., None, None] + 0.5) / fy[..., None, None]], dim=-1),
+                        (0, 1), value=1.0)
+    directions = torch.einsum("...ij,...hwj->...hwi", camtoworlds[..., :3, :3], camera_dirs)
+    origins = camtoworlds[..., :3, -1]
+    if not z_depth:
+        directions = F.normalize(directions, dim=-1)
+    points = origins[..., None, None, :] + depths * directions
+    dx = points[..., 2:, 1:-1, :] - points[..., :-2, 1:-1, :]
+    dy = points[..., 1:-1, 2:, :] - points[..., 1:-1, :-2, :]
+    normals = F.normalize(torch.cross(dx, dy, dim=-1), dim=-1)
+    return F.pad(normals, (0, 0, 1, 1, 1, 1), value=0.0)
