@@ -50,32 +50,45 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        # one launch per distinct (betas, eps); the reference has a single setting
+        # one launch per distinct (betas, eps); the reference has a single setting.  The host
+        # side is kept lean (it runs while the GPU drains the backward): the per-parameter
+        # step tensors are bumped with one foreach call.
         batches: dict = {}
         keep = []
+        work = []
         for group in self.param_groups:
             b1, b2 = group["betas"]
-            descs = batches.setdefault((float(b1), float(b2), float(group["eps"])), [])
+            key = (float(b1), float(b2), float(group["eps"]))
+            lr = float(group["lr"])
             for p in group["params"]:
-                if p.grad is None:
+                g = p.grad
+                if g is None:
                     continue
-                if p.grad.is_sparse:
+                if g.is_sparse:
                     raise RuntimeError("hgsr Adam does not support sparse gradients")
-                if p.dtype != torch.float32 or p.grad.dtype != torch.float32:
+                if p.dtype != torch.float32 or g.dtype != torch.float32:
                     raise RuntimeError("hgsr Adam: float32 parameters only")
+                if not (p.is_cuda and g.is_cuda):
+                    raise RuntimeError("hgsr Adam: tensors must live on the HIP device (no CPU path)")
                 st = self.state[p]
                 if len(st) == 0:
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                for t in (p, st["exp_avg"], st["exp_avg_sq"]):
-                    if not t.is_contiguous():
-                        raise RuntimeError("hgsr Adam: parameters and state must be contiguous")
-                st["step"] += 1
+                if not g.is_contiguous():
+                    g = g.contiguous()
+                m, v = st["exp_avg"], st["exp_avg_sq"]
+                if not (p.is_contiguous() and m.is_contiguous() and v.is_contiguous()):
+                    raise RuntimeError("hgsr Adam: parameters and state must be contiguous")
                 keep.append(g)
-                descs.append(_AdamTensor(NAT.ptr(p), NAT.ptr(g), NAT.ptr(st["exp_avg"]), NAT.ptr(st["exp_avg_sq"]),
-                                         p.numel(), float(group["lr"]), int(st["step"].item())))
+                work.append((key, p, g, m, v, lr, st["step"]))
+        if not work:
+            return loss
+        steps = [w[6] for w in work]
+        torch._foreach_add_(steps, 1.0)
+        for (key, p, g, m, v, lr, step), n in zip(work, torch.stack(steps).tolist()):
+            batches.setdefault(key, []).append(
+                _AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), lr, int(n)))
         for (b1, b2, eps), descs in batches.items():
             if not descs:
                 continue
