@@ -13,7 +13,8 @@
 // or 12-neighbour (backward) depth reads hit L1/L2; the origin cancels in a and b and is
 // never added (fewer roundings than o + d dir followed by the difference).  The backward
 // gathers instead of scattering: d depth(p) = dir(p) . (A(p - y) - A(p + y) + B(p - x) -
-// B(p + x)) with A = b x g_raw, B = g_raw x a the cross-product vjps of the neighbours.
+// B(p + x)) with A = b x g_raw, B = g_raw x a the cross-product vjps of the neighbours,
+// points and vjps staged once per 16 x 16 tile in LDS.
 #include "common.h"
 
 namespace hgsr {
@@ -101,57 +102,74 @@ __global__ __launch_bounds__(256) void depth_normal_fwd_kernel(NrmDims g, const 
     o[2] = n.z;
 }
 
-// the cross-product vjps at interior pixel (y, x): A = dL/da, B = dL/db
-__device__ __forceinline__ void nrm_vjp(const NrmDims& g, const NrmCam& k, int c, int y, int x,
-                                        const float* __restrict__ gn, float3& A, float3& B) {
-    const float3 a = sub3(nrm_point(g, k, c, y + 1, x), nrm_point(g, k, c, y - 1, x));
-    const float3 b = sub3(nrm_point(g, k, c, y, x + 1), nrm_point(g, k, c, y, x - 1));
-    const float3 n = cross3(a, b);
-    const float nr = sqrtf(n.x * n.x + n.y * n.y + n.z * n.z);
-    const float* gp = gn + (((int64_t)c * g.H + y) * g.W + x) * 3;
-    const float3 gv = make_float3(gp[0], gp[1], gp[2]);
-    float3 gr;
-    if (nr > 1e-12f) {
-        // d/dn (n / |n|) = (I - u u^T) / |n|
-        const float inv = 1.0f / nr;
-        const float3 u = make_float3(n.x * inv, n.y * inv, n.z * inv);
-        const float ug = u.x * gv.x + u.y * gv.y + u.z * gv.z;
-        gr = make_float3((gv.x - u.x * ug) * inv, (gv.y - u.y * ug) * inv, (gv.z - u.z * ug) * inv);
-    } else {
-        gr = make_float3(gv.x * 1e12f, gv.y * 1e12f, gv.z * 1e12f);  // n / eps
-    }
-    A = cross3(b, gr);
-    B = cross3(gr, a);
-}
-
+// LDS-tiled backward: the 20 x 20 points of the tile (+2 halo) are unprojected once, the
+// cross-product vjps of the 18 x 18 (+1 halo) normals once, then every pixel gathers its
+// four neighbours' terms (each point / vjp evaluated once instead of 4x / 4x recomputed).
+constexpr int kNT = 16, kNP = kNT + 4, kNV = kNT + 2;
 __global__ __launch_bounds__(256) void depth_normal_bwd_kernel(NrmDims g, const float* __restrict__ c2w,
                                                                const float* __restrict__ Ks,
                                                                const float* __restrict__ g_normals,
                                                                float* __restrict__ g_depth) {
-    int c, y, x;
-    if (!nrm_pixel(g, c, y, x)) return;
+    __shared__ float s_p[3][kNP * kNP];
+    __shared__ float s_a[3][kNV * kNV], s_b[3][kNV * kNV];
+    const int tw = (g.W + kNT - 1) / kNT, th = (g.H + kNT - 1) / kNT;
+    const int c = blockIdx.x / (tw * th);
+    const int t = blockIdx.x - c * tw * th;
+    const int ty0 = (t / tw) * kNT, tx0 = (t % tw) * kNT;
     const NrmCam k = nrm_cam(c2w, Ks, c);
-    // dL/dP(y, x): this pixel is the +y end of a at (y-1, x), the -y end at (y+1, x), the
-    // +x end of b at (y, x-1) and the -x end at (y, x+1)
-    float3 G = make_float3(0.f, 0.f, 0.f), A, B;
-    if (interior(g, y - 1, x)) {
-        nrm_vjp(g, k, c, y - 1, x, g_normals, A, B);
-        G = make_float3(G.x + A.x, G.y + A.y, G.z + A.z);
+    for (int e = threadIdx.x; e < kNP * kNP; e += 256) {
+        const int y = ty0 - 2 + e / kNP, x = tx0 - 2 + e % kNP;
+        float3 p = make_float3(0.f, 0.f, 0.f);
+        if (y >= 0 && y < g.H && x >= 0 && x < g.W) p = nrm_point(g, k, c, y, x);
+        s_p[0][e] = p.x;
+        s_p[1][e] = p.y;
+        s_p[2][e] = p.z;
     }
-    if (interior(g, y + 1, x)) {
-        nrm_vjp(g, k, c, y + 1, x, g_normals, A, B);
-        G = make_float3(G.x - A.x, G.y - A.y, G.z - A.z);
+    __syncthreads();
+    auto P = [&](int ly, int lx) {  // local point coordinates relative to (ty0 - 2, tx0 - 2)
+        const int e = ly * kNP + lx;
+        return make_float3(s_p[0][e], s_p[1][e], s_p[2][e]);
+    };
+    for (int e = threadIdx.x; e < kNV * kNV; e += 256) {
+        const int vy = e / kNV, vx = e % kNV;          // vjp pixel (ty0 - 1 + vy, tx0 - 1 + vx)
+        const int y = ty0 - 1 + vy, x = tx0 - 1 + vx;
+        float3 A = make_float3(0.f, 0.f, 0.f), B = A;
+        if (interior(g, y, x)) {
+            const int ly = vy + 1, lx = vx + 1;
+            const float3 a = sub3(P(ly + 1, lx), P(ly - 1, lx));
+            const float3 b = sub3(P(ly, lx + 1), P(ly, lx - 1));
+            const float3 n = cross3(a, b);
+            const float nr = sqrtf(n.x * n.x + n.y * n.y + n.z * n.z);
+            const float* gp = g_normals + (((int64_t)c * g.H + y) * g.W + x) * 3;
+            const float3 gv = make_float3(gp[0], gp[1], gp[2]);
+            float3 gr;
+            if (nr > 1e-12f) {
+                // d/dn (n / |n|) = (I - u u^T) / |n|
+                const float inv = 1.0f / nr;
+                const float3 u = make_float3(n.x * inv, n.y * inv, n.z * inv);
+                const float ug = u.x * gv.x + u.y * gv.y + u.z * gv.z;
+                gr = make_float3((gv.x - u.x * ug) * inv, (gv.y - u.y * ug) * inv, (gv.z - u.z * ug) * inv);
+            } else {
+                gr = make_float3(gv.x * 1e12f, gv.y * 1e12f, gv.z * 1e12f);  // n / eps
+            }
+            A = cross3(b, gr);
+            B = cross3(gr, a);
+        }
+        s_a[0][e] = A.x; s_a[1][e] = A.y; s_a[2][e] = A.z;
+        s_b[0][e] = B.x; s_b[1][e] = B.y; s_b[2][e] = B.z;
     }
-    if (interior(g, y, x - 1)) {
-        nrm_vjp(g, k, c, y, x - 1, g_normals, A, B);
-        G = make_float3(G.x + B.x, G.y + B.y, G.z + B.z);
-    }
-    if (interior(g, y, x + 1)) {
-        nrm_vjp(g, k, c, y, x + 1, g_normals, A, B);
-        G = make_float3(G.x - B.x, G.y - B.y, G.z - B.z);
-    }
+    __syncthreads();
+    const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
+    const int y = ty0 + ly, x = tx0 + lx;
+    if (y >= g.H || x >= g.W) return;
+    // this pixel is the +y end of a at (y-1, x), the -y end at (y+1, x), the +x end of b at
+    // (y, x-1) and the -x end at (y, x+1); vjp array index of pixel (y', x') = (y'-ty0+1, x'-tx0+1)
+    const int vc = (ly + 1) * kNV + (lx + 1);
+    float G[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) G[q] = s_a[q][vc - kNV] - s_a[q][vc + kNV] + s_b[q][vc - 1] - s_b[q][vc + 1];
     const float3 d = nrm_dir(k, y, x, g.z_depth);
-    g_depth[((int64_t)c * g.H + y) * g.W + x] = d.x * G.x + d.y * G.y + d.z * G.z;
+    g_depth[((int64_t)c * g.H + y) * g.W + x] = d.x * G[0] + d.y * G[1] + d.z * G[2];
 }
 
 }  // namespace hgsr
