@@ -20,6 +20,7 @@ oracle on a bounded sample, rank 0 at N=1 only).
 from __future__ import annotations
 
 import argparse
+import ctypes as ct
 import json
 import os
 import sys
@@ -203,52 +204,6 @@ def hbm_kernels(wl, kernels, n_isects):
     return out
 
 
-def raster_pairs(wl):
-    """Evaluated (pixel, Gaussian) pairs of the last step: per tile, every Gaussian up to
-    the tile's latest contributor, times the 256 pixels of the tile."""
-    meta = wl.meta
-    offs = meta["isect_offsets"].reshape(-1).to(torch.int64)
-    n_isects = meta["flatten_ids"].numel()
-    C, H, W = 1, wl.args.height, wl.args.width
-    dev = wl.dev
-    m2 = meta["means2d"].detach().contiguous()
-    fl = meta["flatten_ids"]
-    th, tw = meta["tile_height"], meta["tile_width"]
-    rc = torch.empty((C, H, W, 4), device=dev)
-    ra = torch.empty((C, H, W, 1), device=dev)
-    last = torch.empty((C, H, W), dtype=torch.int32, device=dev)
-    opac = meta["opacities"].detach().contiguous()
-    cols = torch.cat([wl.last_colors.detach()[None], meta["depths"].detach()[..., None]], -1).contiguous()
-    n_g = cols.shape[1]
-    if wl.args.gs == "3d":
-        ws_b = NAT.size_query("hgsr_raster3d_fwd_ws_bytes", C, n_g, 4)
-        ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
-        NAT.call("hgsr_raster3d_fwd", C, n_g, 4, NAT.ptr(m2), NAT.ptr(meta["conics"].detach().contiguous()),
-                 NAT.ptr(cols), NAT.ptr(opac), None, W, H, 16, tw, th, NAT.ptr(meta["isect_offsets"]), n_isects,
-                 NAT.ptr(fl), NAT.ptr(rc), NAT.ptr(ra), NAT.ptr(last), NAT.ptr(ws), ws_b, NAT.stream(dev))
-    else:
-        rn = torch.empty((C, H, W, 3), device=dev)
-        r1 = torch.empty((C, H, W, 1), device=dev)
-        r2 = torch.empty((C, H, W, 1), device=dev)
-        med = torch.empty((C, H, W), dtype=torch.int32, device=dev)
-        ws_b = NAT.size_query("hgsr_raster2d_fwd_ws_bytes", C, n_g, 4)
-        ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
-        NAT.call("hgsr_raster2d_fwd", C, n_g, 4, NAT.ptr(m2),
-                 NAT.ptr(meta["ray_transforms"].detach().reshape(C, -1, 9).contiguous()), NAT.ptr(cols),
-                 NAT.ptr(opac), NAT.ptr(meta["normals"].detach().contiguous()), None, W, H, 16, tw, th,
-                 NAT.ptr(meta["isect_offsets"]), n_isects, NAT.ptr(fl), NAT.ptr(rc), NAT.ptr(ra), NAT.ptr(rn),
-                 NAT.ptr(r1), NAT.ptr(r2), NAT.ptr(last), NAT.ptr(med), NAT.ptr(ws), ws_b, NAT.stream(dev))
-    # per-tile max last id (tile-major reduction on the host side of torch ops)
-    hp, wp = th * 16, tw * 16
-    lp = torch.full((C, hp, wp), -1, dtype=torch.int64, device=dev)
-    lp[:, :H, :W] = last.to(torch.int64)
-    contributed = (ra[..., 0] > 0)
-    lp[:, :H, :W] = torch.where(contributed, lp[:, :H, :W], torch.full_like(lp[:, :H, :W], -1))
-    tile_last = lp.reshape(C, th, 16, tw, 16).amax(dim=(2, 4)).reshape(-1)
-    visited = torch.clamp(tile_last - offs + 1, min=0)
-    return int(visited.sum().item()) * 256, n_isects
-
-
 def pmc_traffic(args):
     """HBM bytes per launch of each kernel from the newest committed PMC summary
     (profiles/rNN_pmc_traffic.json, written by scripts/profile_summary.py from separate
@@ -343,9 +298,6 @@ def main():
     torch.cuda.synchronize(dev)
     # the optimizer moves the scene: intersections before / after the timed steps show the drift
     isects_before = wl.meta["flatten_ids"].numel() if args.warmup else None
-    # pairs visited by the dominant kernel before and after the timed steps (the scene drifts
-    # under the optimizer; the roofline uses their mean over the same steps the events time)
-    pairs_before = raster_pairs(wl)[0] if (args.warmup and not args.no_timing and rank == 0) else None
     timing = not args.no_timing
     # live HIP events inside the timed region on the dominant kernel only (the roofline);
     # the per-kernel breakdown comes from a separate pass after it
@@ -354,6 +306,7 @@ def main():
         NAT.call("hgsr_timing_reset")
         NAT.call("hgsr_timing_only", dominant.encode())
         NAT.call("hgsr_timing_enable", 1)
+        NAT.call("hgsr_timing_pairs", None, 1)  # the backward counts its visited pairs on the device
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -372,8 +325,12 @@ def main():
         dt = float(tt.item())
     kernels = {}
     live = None
-    pairs_after, isects_after = raster_pairs(wl) if (timing and rank == 0) else (None, None)
+    isects_after = wl.meta["flatten_ids"].numel()
+    pairs_timed = None
     if timing:
+        pc = ct.c_ulonglong(0)
+        NAT.call("hgsr_timing_pairs", ct.byref(pc), 1)
+        pairs_timed = pc.value
         tot, cnt = NAT.kernel_time(dominant)
         live = {"avg_ms": round(tot / cnt, 4), "launches": cnt} if cnt else None
         # breakdown pass (outside the timed region): every kernel's events
@@ -394,7 +351,7 @@ def main():
     if live and rank == 0:
         dom = dominant
         n_isects = isects_after
-        pairs = (pairs_after + pairs_before) // 2 if pairs_before is not None else pairs_after
+        pairs = pairs_timed // args.steps  # mean over exactly the launches the events time
         avg_s = live["avg_ms"] * 1e-3
         if dom in FLOP_PER_PAIR:
             flops = pairs * FLOP_PER_PAIR[dom]
@@ -403,8 +360,8 @@ def main():
                     "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": traffic.get(dom), "kernel": dom,
                     "note": (f"fp32 VALU-bound compositing: peak = fp32 vector rate (= f32 MFMA rate); "
                              f"{pairs} (pixel,Gaussian) pairs visited x {FLOP_PER_PAIR[dom]:.0f} FLOP/pair "
-                             f"(SURVEY 8(d)), mean of {pairs_before} before and {pairs_after} after the timed "
-                             f"steps; {n_isects} intersections")}
+                             f"(SURVEY 8(d)), counted on the device over the timed launches; {n_isects} "
+                             f"intersections")}
         else:
             roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                     "traffic": None, "kernel": dom}
@@ -417,7 +374,8 @@ def main():
         roof["n_isects"] = n_isects
         roof["n_isects_before_timed"] = isects_before
         roof["kernel_avg_ms"] = live["avg_ms"]
-        roof["timing"] = "HIP events on the kernel's stream, recorded inside the timed region for this kernel only"
+        roof["timing"] = ("HIP events (no system fence) on the kernel's stream, recorded inside the timed region "
+                          "for this kernel only")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.gs == "3d" and not args.anchors:
         cpu = cpu_baseline(args, wl)

@@ -14,6 +14,9 @@ void set_error(const char* fmt, ...);
 bool timing_on();
 int timing_begin(const char* name, hipStream_t s);
 void timing_end(int id, hipStream_t s);
+// measurement only: device counter the raster backward adds its visited (pixel, Gaussian)
+// pairs to while `kernel` is being timed (nullptr otherwise)
+unsigned long long* timing_pair_counter(const char* kernel);
 struct KernelTimer {
     int id;
     hipStream_t s;

@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     int64_t n_isects, const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
     const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
     const float* __restrict__ v_render_alphas, const float* __restrict__ v_render_normals,
-    float* __restrict__ acc_rows) {
+    float* __restrict__ acc_rows, unsigned long long* __restrict__ pair_counter) {
     // row layout: 0-1 xy, 2-4 sum (p-m)_x v_c, 5-7 sum (p-m)_y v_c, 8-10 sum v_c (v_c = dL/d(h_u x h_v)),
     // 11 opac, 12-14 normal, 15.. colour, then abs xy; split2 maps v_c sums to u, v, w and densify
     constexpr int KV = 15 + D + (ABS ? 2 : 0);
@@ -420,6 +420,8 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
     const int32_t end = min(tc.end, blk_final + 1);
     const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
+    if (pair_counter && threadIdx.x == 0 && end > tc.start)  // measurement only (bench roofline)
+        atomicAdd(pair_counter, (unsigned long long)(end - tc.start) * kTilePixels);
     // records are staged with LDS-DMA (global_load_lds_dwordx4: per-lane source, LDS
     // destination base + 16 B x lane), one batch ahead, so they cost no VGPRs (89 -> 59);
     // the 64 loader lanes are exactly wave 0
@@ -825,13 +827,14 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         rec = own;
     }
     const dim3 grid(C * tile_w * tile_h);
+    unsigned long long* const pairs = timing_pair_counter("raster2d_bwd");
 #define LAUNCH_B2(DD)                                                                                             \
     {                                                                                                             \
         KernelTimer kt("raster2d_bwd", s);                                                                        \
         hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
                            tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,        \
                            flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,                \
-                           v_render_normals, rows);                                                               \
+                           v_render_normals, rows, pairs);                                                        \
     }                                                                                                             \
     hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s,   \
                        C, N, rows, rt, m2, reinterpret_cast<float2*>(v_means2d), v_rt, cd, v_normals,             \

@@ -285,7 +285,8 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     int bg_ch, int ed_ch, const float* __restrict__ render_colors, const int32_t* __restrict__ offsets,
     int64_t n_isects, const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
     const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
-    const float* __restrict__ v_render_alphas, float* __restrict__ acc_rows) {
+    const float* __restrict__ v_render_alphas, float* __restrict__ acc_rows,
+    unsigned long long* __restrict__ pair_counter) {
     constexpr int KV = 6 + D + (ABS ? 2 : 0);
     constexpr int NB = kBwdBatch;
     // double-buffered staging: batch b+1 is staged while batch b's partials are
@@ -338,6 +339,8 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     // Gaussians after the block's last contributor are never reached
     const int32_t end = min(tc.end, blk_final + 1);
     const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
+    if (pair_counter && threadIdx.x == 0 && end > tc.start)  // measurement only (bench roofline)
+        atomicAdd(pair_counter, (unsigned long long)(end - tc.start) * kTilePixels);
     // two-deep software pipeline (ids two batches ahead, records one), clamped
     // unconditional loads; lanes < NB load one Gaussian each
     float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
@@ -701,13 +704,14 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         rec = own;
     }
     const dim3 grid(C * tile_w * tile_h);
+    unsigned long long* const pairs = timing_pair_counter("raster3d_bwd");
     const bool abs = v_means2d_abs != nullptr;
 #define LAUNCH_B(DD, AA)                                                                                       \
     {                                                                                                          \
         KernelTimer kt("raster3d_bwd", s);                                                                     \
         hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
                            tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,       \
-                           flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows);        \
+                           flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, pairs); \
     }                                                                                                          \
     hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, \
                        N, rows, conics, reinterpret_cast<float2*>(v_means2d), v_conics, cd,                     \

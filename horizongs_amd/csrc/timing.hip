@@ -21,6 +21,7 @@ std::vector<Rec> g_recs;
 size_t g_next = 0;
 constexpr size_t kMaxRecs = 1 << 16;
 std::string g_only;  // record only this kernel (empty = all)
+unsigned long long* g_pairs = nullptr;  // device counter of (pixel, Gaussian) pairs the raster bwd visits
 }  // namespace
 
 bool timing_on() { return g_on; }
@@ -31,7 +32,9 @@ int timing_begin(const char* name, hipStream_t s) {
     if (!g_only.empty() && g_only != name) return -1;
     while (g_pool.size() < g_next + 2) {
         hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return -1;
+        // device-scope release only: a system-scope fence per record would stall the
+        // stream (~25 us per event pair on MI355X) and distort the timed region
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return -1;
         g_pool.push_back(e);
     }
     Rec r{name, g_pool[g_next], g_pool[g_next + 1]};
@@ -39,6 +42,16 @@ int timing_begin(const char* name, hipStream_t s) {
     if (hipEventRecord(r.a, s) != hipSuccess) return -1;
     g_recs.push_back(r);
     return (int)g_recs.size() - 1;
+}
+
+unsigned long long* timing_pair_counter(const char* kernel) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_on || (!g_only.empty() && g_only != kernel)) return nullptr;
+    if (!g_pairs) {
+        if (hipMalloc(&g_pairs, sizeof(unsigned long long)) != hipSuccess) return nullptr;
+        if (hipMemset(g_pairs, 0, sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    }
+    return g_pairs;
 }
 
 void timing_end(int id, hipStream_t s) {
@@ -60,6 +73,21 @@ extern "C" int hgsr_timing_enable(int on) {
 extern "C" int hgsr_timing_only(const char* kernel) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_only = kernel ? kernel : "";
+    return HGSR_OK;
+}
+
+extern "C" int hgsr_timing_pairs(unsigned long long* out, int reset) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    unsigned long long v = 0;
+    if (g_pairs) {
+        if (hipDeviceSynchronize() != hipSuccess ||
+            hipMemcpy(&v, g_pairs, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) {
+            set_error("timing: pair counter read failed");
+            return HGSR_ELAUNCH;
+        }
+        if (reset && hipMemset(g_pairs, 0, sizeof(v)) != hipSuccess) return HGSR_ELAUNCH;
+    }
+    if (out) *out = v;
     return HGSR_OK;
 }
 

@@ -461,6 +461,10 @@ int hgsr_timing_reset(void);
  * the dominant kernel inside its timed region, so the events add no per-launch overhead
  * to the other kernels of the step. */
 int hgsr_timing_only(const char* kernel);
+/* (pixel, Gaussian) pairs the timed raster backward visited (every Gaussian up to each tile's
+ * latest contributor x 256 pixels), counted on the device while raster3d_bwd / raster2d_bwd
+ * is being timed; synchronises the device; reset = 1 zeroes the counter. */
+int hgsr_timing_pairs(unsigned long long* out, int reset);
 /* total milliseconds and launch count recorded for `kernel` (synchronises the
  * recorded events); kernel names: project3d_fwd, project3d_bwd, project2d_fwd,
  * project2d_bwd, sh_fwd, sh_bwd, isect_count, isect_emit, tile_sort,

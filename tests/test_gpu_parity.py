@@ -399,3 +399,39 @@ def test_fullsize_c2_render_properties():
     out2, alpha2, _ = G.rasterization(means.detach(), quats, scales, opac.detach(), cols, vm, K, sc.width,
                                       sc.height, packed=False, render_mode="RGB+ED")
     assert torch.equal(out2, out.detach())
+
+
+def test_bench_pair_counter_matches_oracle():
+    """bench.py's roofline counts the backward's visited (pixel, Gaussian) pairs on the device
+    (hgsr_timing_pairs): every Gaussian up to each tile's latest contributor x 256 pixels.
+    Checked against the oracle's last contributors for the same scene."""
+    import ctypes as ct
+    from horizongs_amd import _native as NAT
+    sc = scene(n=400, seed=41)
+    ref = OP.Raster3D(sc.means, sc.quats, sc.scales, sc.opacities, sc.colors, sc.viewmats, sc.Ks, sc.width,
+                      sc.height, render_mode="RGB+ED")
+    ref.forward()
+    th, tw = ref.offsets.shape[1:]
+    offs = ref.offsets.reshape(-1).astype(np.int64)
+    ends = np.append(offs[1:], len(ref.flatten_ids))
+    last = np.full((th * 16, tw * 16), -1, np.int64)
+    last[:sc.height, :sc.width] = ref.last.reshape(sc.height, sc.width)
+    tile_last = last.reshape(th, 16, tw, 16).max(axis=(1, 3)).reshape(-1)
+    expect = int(np.clip(np.minimum(ends, tile_last + 1) - offs, 0, None).sum()) * 256
+    means, quats, scales, opac, cols, vm, K = to_dev(sc.means, sc.quats, sc.scales, sc.opacities, sc.colors,
+                                                     sc.viewmats, sc.Ks)
+    means.requires_grad_(True)
+    NAT.call("hgsr_timing_reset")
+    NAT.call("hgsr_timing_only", b"raster3d_bwd")
+    NAT.call("hgsr_timing_enable", 1)
+    NAT.call("hgsr_timing_pairs", None, 1)
+    try:
+        out, alpha, _ = G.rasterization(means, quats, scales, opac, cols, vm, K, sc.width, sc.height,
+                                        packed=False, render_mode="RGB+ED")
+        (out.sum() + alpha.sum()).backward()
+        pc = ct.c_ulonglong(0)
+        NAT.call("hgsr_timing_pairs", ct.byref(pc), 1)
+    finally:
+        NAT.call("hgsr_timing_enable", 0)
+        NAT.call("hgsr_timing_only", None)
+    assert expect > 0 and pc.value == expect
