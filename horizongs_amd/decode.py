@@ -56,6 +56,20 @@ def lod_mask(anchor, level, extra_level, cam_center, res_scale, standard_dist, f
     return mask.bool()
 
 
+_VIS_CACHE: list = []  # [(mask, its version counter, int32 index)]: one entry
+
+
+def visible_index(visible):
+    """int32 indices of a bool anchor mask (torch.nonzero: a host sync).  The last result is
+    kept so that training_statis, which receives the same render_pkg["visible_mask"] after
+    the backward (train.py:258-262), reuses it instead of syncing again."""
+    if _VIS_CACHE and _VIS_CACHE[0][0] is visible and _VIS_CACHE[0][1] == visible._version:
+        return _VIS_CACHE[0][2]
+    idx = torch.nonzero(visible, as_tuple=False).reshape(-1).to(torch.int32)
+    _VIS_CACHE[:] = [(visible, visible._version, idx)]
+    return idx
+
+
 class _Decode(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, feat, offset, scaling_raw, cam_center, vis_idx, cfg, *weights):
@@ -136,7 +150,7 @@ def decode(anchor, feat, offset, scaling_raw, cam_center, mlps, visible=None, vi
     if visible is None:
         vis_idx = torch.arange(A, dtype=torch.int32, device=anchor.device)
     elif visible.dtype == torch.bool:
-        vis_idx = torch.nonzero(visible, as_tuple=False).reshape(-1).to(torch.int32)
+        vis_idx = visible_index(visible)
     else:
         vis_idx = visible.to(torch.int32).contiguous()
     xyz, offs, color, opac, scaling, rot, mask = _Decode.apply(

@@ -18,6 +18,8 @@ from __future__ import annotations
 
 import torch
 
+from .decode import visible_index
+
 from . import _native as N
 from ._native import ptr
 
@@ -53,7 +55,10 @@ def training_statis(model, opt, render_pkg, width, height):
     if opt.growing_type not in ("mean", "max"):
         raise ValueError(f"Unknown growing_type: {opt.growing_type}")
     noff = model.n_offsets
-    vis_idx = torch.nonzero(vis, as_tuple=False).reshape(-1).to(torch.int32)
+    vm = render_pkg["visible_mask"]
+    # the decode's index of the same mask object is reused (no second host sync)
+    vis_idx = visible_index(vm if vm.dim() == 1 else vis) if vis.dtype == torch.bool else \
+        torch.nonzero(vis, as_tuple=False).reshape(-1).to(torch.int32)
     Av = vis_idx.numel()
     if sel.numel() != Av * noff:
         raise ValueError(f"hgsr training_statis: selection_mask has {sel.numel()} slots, expected {Av * noff}")
