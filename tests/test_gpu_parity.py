@@ -325,6 +325,13 @@ def test_rasterization_2dgs_fwd_bwd(seed, mode):
     close(distort.detach().cpu().numpy(), ref.rd, atol=1e-4, rtol=1e-3, name="2dgs distort")
     close(median.detach().cpu().numpy(), ref.rm, frac_ok=1e-3, name="2dgs median")
     assert nfd.shape == (1, sc.height, sc.width, 3)
+    if mode == "RGB+ED":  # K13 on the rendered expected depth vs the torch restatement of the fork
+        from oracle import torch_ref as TR
+        c2w = torch.linalg.inv(sc.viewmats.double())
+        dep = out.detach().cpu()[..., -1:]
+        n32 = TR.depth_to_normal(dep, c2w.float(), sc.Ks).numpy()
+        n64 = TR.depth_to_normal(dep.double(), c2w, sc.Ks.double()).numpy()
+        cond_close(nfd.detach().cpu().numpy(), n32, n64, "2dgs normals_from_depth")
     g = torch.Generator().manual_seed(seed)
     vrc = torch.randn(rc.shape, generator=g)
     vra = torch.randn(ra.shape, generator=g)
