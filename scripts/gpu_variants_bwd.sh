@@ -6,5 +6,5 @@ for v in base ${VARIANTS}; do
   timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 --warmup 5 ${BENCH_ARGS} > gpurun_out/var_$v.json 2>/dev/null || exit 1
   python -c "
 import json; d=json.load(open('gpurun_out/var_$v.json')); k=d['kernels']
-print('$v', d['value'], {n: k[n]['avg_ms'] for n in k if ('raster' in n or 'project' in n or 'adam' in n)})"
+print('$v', d['value'], {n: k[n]['avg_ms'] for n in k if ('raster' in n or 'project' in n or 'adam' in n or 'isect' in n or 'sort' in n)})"
 done
