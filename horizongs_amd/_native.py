@@ -77,9 +77,9 @@ _SIGS = {
     "hgsr_weed_out": (I, [I64, P, P, I, P, F, F, I, I, F, P, P]),
     "hgsr_loss_fwd": (I, [I, I, I, P, P, P, P, P, P, P, I64, I, P, P, P, SZ, P]),
     "hgsr_loss_bwd": (I, [I, I, I, P, P, P, P, P, P, P, I64, I, P, P, P, I, P, P, P, P, SZ, P]),
-    "hgsr_depth_normal_fwd": (I, [I, I, I, P, P, P, P, I, P, P]),
-    "hgsr_depth_normal_bwd": (I, [I, I, I, P, P, P, P, I, P, P, P]),
-    "hgsr_rotate3": (I, [I, I64, P, I, P, P, P]),
+    "hgsr_depth_normal_fwd": (I, [I, I, I, P, P, P, P, I, I, P, P]),
+    "hgsr_depth_normal_bwd": (I, [I, I, I, P, P, P, P, I, I, P, P, P]),
+    "hgsr_rotate3": (I, [I, I64, P, I, I, I, P, P, P]),
     "hgsr_adam_step": (I, [I, P, ct.c_double, ct.c_double, ct.c_double, P]),
     "hgsr_timing_enable": (I, [I]),
     "hgsr_timing_reset": (I, []),

@@ -27,16 +27,18 @@ struct NrmCam {
 struct NrmDims {
     int C, H, W;
     int z_depth;
+    int from_viewmat;  // the camera matrices are world -> camera viewmats: R_c2w = R^T
     const float* depth;  // [C,H,W] with strides
     int64_t ds[3];
 };
 
-__device__ __forceinline__ NrmCam nrm_cam(const float* __restrict__ c2w, const float* __restrict__ Ks, int c) {
+__device__ __forceinline__ NrmCam nrm_cam(const float* __restrict__ c2w, const float* __restrict__ Ks, int c,
+                                          int from_viewmat) {
     NrmCam k;
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) k.r[i * 3 + j] = c2w[c * 16 + i * 4 + j];
+        for (int j = 0; j < 3; ++j) k.r[i * 3 + j] = from_viewmat ? c2w[c * 16 + j * 4 + i] : c2w[c * 16 + i * 4 + j];
     k.fx = Ks[c * 9 + 0];
     k.fy = Ks[c * 9 + 4];
     k.cx = Ks[c * 9 + 2];
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(256) void depth_normal_fwd_kernel(NrmDims g, const 
     if (!nrm_pixel(g, c, y, x)) return;
     float3 n = make_float3(0.f, 0.f, 0.f);
     if (interior(g, y, x)) {
-        const NrmCam k = nrm_cam(c2w, Ks, c);
+        const NrmCam k = nrm_cam(c2w, Ks, c, g.from_viewmat);
         const float3 a = sub3(nrm_point(g, k, c, y + 1, x), nrm_point(g, k, c, y - 1, x));
         const float3 b = sub3(nrm_point(g, k, c, y, x + 1), nrm_point(g, k, c, y, x - 1));
         n = cross3(a, b);
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(256) void depth_normal_bwd_kernel(NrmDims g, const 
     const int c = blockIdx.x / (tw * th);
     const int t = blockIdx.x - c * tw * th;
     const int ty0 = (t / tw) * kNT, tx0 = (t % tw) * kNT;
-    const NrmCam k = nrm_cam(c2w, Ks, c);
+    const NrmCam k = nrm_cam(c2w, Ks, c, g.from_viewmat);
     for (int e = threadIdx.x; e < kNP * kNP; e += 256) {
         const int y = ty0 - 2 + e / kNP, x = tx0 - 2 + e % kNP;
         float3 p = make_float3(0.f, 0.f, 0.f);
@@ -184,11 +186,11 @@ static int nrm_check(int C, int H, int W, const float* depth, const float* c2w, 
 }
 
 extern "C" int hgsr_depth_normal_fwd(int C, int H, int W, const float* depth, const int64_t* depth_strides,
-                                     const float* camtoworlds, const float* Ks, int z_depth, float* normals,
-                                     hgsr_stream_t stream) {
+                                     const float* camtoworlds, const float* Ks, int z_depth, int from_viewmat,
+                                     float* normals, hgsr_stream_t stream) {
     if (int st = nrm_check(C, H, W, depth, camtoworlds, Ks)) return st;
     HGSR_REQUIRE(depth_strides && normals, "depth_normal: null pointer");
-    const NrmDims g{C, H, W, z_depth, depth, {depth_strides[0], depth_strides[1], depth_strides[2]}};
+    const NrmDims g{C, H, W, z_depth, from_viewmat, depth, {depth_strides[0], depth_strides[1], depth_strides[2]}};
     const unsigned grid = (unsigned)(C * ((H + 15) / 16) * ((W + 15) / 16));
     KernelTimer kt("depth_normal_fwd", as_stream(stream));
     hipLaunchKernelGGL(depth_normal_fwd_kernel, dim3(grid), dim3(256), 0, as_stream(stream), g, camtoworlds, Ks,
@@ -197,11 +199,11 @@ extern "C" int hgsr_depth_normal_fwd(int C, int H, int W, const float* depth, co
 }
 
 extern "C" int hgsr_depth_normal_bwd(int C, int H, int W, const float* depth, const int64_t* depth_strides,
-                                     const float* camtoworlds, const float* Ks, int z_depth, const float* v_normals,
-                                     float* v_depth, hgsr_stream_t stream) {
+                                     const float* camtoworlds, const float* Ks, int z_depth, int from_viewmat,
+                                     const float* v_normals, float* v_depth, hgsr_stream_t stream) {
     if (int st = nrm_check(C, H, W, depth, camtoworlds, Ks)) return st;
     HGSR_REQUIRE(depth_strides && v_normals && v_depth, "depth_normal: null pointer");
-    const NrmDims g{C, H, W, z_depth, depth, {depth_strides[0], depth_strides[1], depth_strides[2]}};
+    const NrmDims g{C, H, W, z_depth, from_viewmat, depth, {depth_strides[0], depth_strides[1], depth_strides[2]}};
     const unsigned grid = (unsigned)(C * ((H + 15) / 16) * ((W + 15) / 16));
     KernelTimer kt("depth_normal_bwd", as_stream(stream));
     hipLaunchKernelGGL(depth_normal_bwd_kernel, dim3(grid), dim3(256), 0, as_stream(stream), g, camtoworlds, Ks,
@@ -211,14 +213,16 @@ extern "C" int hgsr_depth_normal_bwd(int C, int H, int W, const float* depth, co
 
 namespace hgsr {
 // out[c, m] = R_c v (transpose = 0) or R_c^T v (transpose = 1) for vectors in[c, m] (3 floats)
-__global__ __launch_bounds__(256) void rotate3_kernel(int C, int64_t M, const float* __restrict__ R, int transpose,
-                                                      const float* __restrict__ in, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void rotate3_kernel(int C, int64_t M, const float* __restrict__ R, int cam_stride,
+                                                      int row_stride, int transpose, const float* __restrict__ in,
+                                                      float* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (int64_t)C * M) return;
     const int c = (int)(i / M);
     float r[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) r[k] = transpose ? R[c * 9 + (k % 3) * 3 + k / 3] : R[c * 9 + k];
+    for (int k = 0; k < 9; ++k)
+        r[k] = transpose ? R[c * cam_stride + (k % 3) * row_stride + k / 3] : R[c * cam_stride + (k / 3) * row_stride + k % 3];
     const float x = in[i * 3], y = in[i * 3 + 1], z = in[i * 3 + 2];
     out[i * 3] = r[0] * x + r[1] * y + r[2] * z;
     out[i * 3 + 1] = r[3] * x + r[4] * y + r[5] * z;
@@ -226,13 +230,13 @@ __global__ __launch_bounds__(256) void rotate3_kernel(int C, int64_t M, const fl
 }
 }  // namespace hgsr
 
-extern "C" int hgsr_rotate3(int C, int64_t M, const float* R, int transpose, const float* in, float* out,
-                            hgsr_stream_t stream) {
-    HGSR_REQUIRE(C >= 1 && M >= 0, "rotate3: bad dims");
+extern "C" int hgsr_rotate3(int C, int64_t M, const float* R, int cam_stride, int row_stride, int transpose,
+                            const float* in, float* out, hgsr_stream_t stream) {
+    HGSR_REQUIRE(C >= 1 && M >= 0 && cam_stride >= 0 && row_stride >= 3, "rotate3: bad dims");
     if (M == 0) return HGSR_OK;
     HGSR_REQUIRE(R && in && out, "rotate3: null pointer");
     const int64_t n = (int64_t)C * M;
     hipLaunchKernelGGL(rotate3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), C, M, R,
-                       transpose, in, out);
+                       cam_stride, row_stride, transpose, in, out);
     return check_launch("rotate3");
 }

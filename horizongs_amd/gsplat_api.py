@@ -729,7 +729,7 @@ class _DepthToNormal(torch.autograd.Function):
     """K13 on the device (hgsr_depth_normal_{fwd,bwd}); gradient to the depth map only."""
 
     @staticmethod
-    def forward(ctx, depths, camtoworlds, Ks, z_depth):
+    def forward(ctx, depths, camtoworlds, Ks, z_depth, from_viewmat=False):
         C, H, W = depths.shape[0], depths.shape[-3], depths.shape[-2]
         d = depths.reshape(C, H, W, -1)[..., 0] if depths.dim() == 4 else depths
         if d.dtype != torch.float32:
@@ -738,21 +738,21 @@ class _DepthToNormal(torch.autograd.Function):
         c2w, K = _f32(camtoworlds), _f32(Ks)
         out = torch.empty((C, H, W, 3), dtype=torch.float32, device=d.device)
         N.call("hgsr_depth_normal_fwd", C, H, W, d.data_ptr(), ct.cast(st, ct.c_void_p), ptr(c2w), ptr(K),
-               int(z_depth), ptr(out), N.stream(d.device))
+               int(z_depth), int(from_viewmat), ptr(out), N.stream(d.device))
         ctx.save_for_backward(d, c2w, K)
-        ctx.cfg = (z_depth, depths.shape)
+        ctx.cfg = (z_depth, depths.shape, from_viewmat)
         return out
 
     @staticmethod
     def backward(ctx, v_normals):
         d, c2w, K = ctx.saved_tensors
-        z_depth, shape = ctx.cfg
+        z_depth, shape, from_viewmat = ctx.cfg
         C, H, W = d.shape
         st = (ct.c_int64 * 3)(*d.stride())
         v_depth = torch.empty((C, H, W), dtype=torch.float32, device=d.device)
         N.call("hgsr_depth_normal_bwd", C, H, W, d.data_ptr(), ct.cast(st, ct.c_void_p), ptr(c2w), ptr(K),
-               int(z_depth), ptr(_f32(v_normals)), ptr(v_depth), N.stream(d.device))
-        return v_depth.reshape(shape), None, None, None
+               int(z_depth), int(from_viewmat), ptr(_f32(v_normals)), ptr(v_depth), N.stream(d.device))
+        return v_depth.reshape(shape), None, None, None, None
 
 
 def depth_to_normal(depths, camtoworlds, Ks, z_depth=True):
@@ -764,36 +764,33 @@ def depth_to_normal(depths, camtoworlds, Ks, z_depth=True):
 
 
 class _Rotate3(torch.autograd.Function):
-    """vectors [C,...,3] -> R_c v (hgsr_rotate3); the vjp applies R_c^T.  R carries no gradient."""
+    """vectors [C,...,3] -> R_c v (hgsr_rotate3); the vjp applies R_c^T.  R ([C,3,3], or [C,4,4]
+    whose rotation block is used) carries no gradient; transpose=True applies R_c^T forward
+    (camera -> world from world -> camera viewmats)."""
 
     @staticmethod
-    def forward(ctx, R, v):
+    def forward(ctx, R, v, transpose=False):
         C = v.shape[0]
         vc = _f32(v)
         out = torch.empty_like(vc)
-        R9 = _f32(R.reshape(C, 9))
-        N.call("hgsr_rotate3", C, vc.numel() // (3 * C), ptr(R9), 0, ptr(vc), ptr(out), N.stream(v.device))
-        ctx.save_for_backward(R9)
+        Rc = _f32(R)
+        cs, rs = (16, 4) if Rc.shape[-1] == 4 else (9, 3)
+        N.call("hgsr_rotate3", C, vc.numel() // (3 * C), ptr(Rc), cs, rs, int(transpose), ptr(vc), ptr(out),
+               N.stream(v.device))
+        ctx.save_for_backward(Rc)
+        ctx.cfg = (cs, rs, transpose)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        (R9,) = ctx.saved_tensors
+        (Rc,) = ctx.saved_tensors
+        cs, rs, transpose = ctx.cfg
         C = g.shape[0]
         gc = _f32(g)
         out = torch.empty_like(gc)
-        N.call("hgsr_rotate3", C, gc.numel() // (3 * C), ptr(R9), 1, ptr(gc), ptr(out), N.stream(g.device))
-        return None, out
-
-
-def _camtoworlds(viewmats):
-    R = viewmats[:, :3, :3]
-    t = viewmats[:, :3, 3]
-    c2w = torch.zeros_like(viewmats)
-    c2w[:, :3, :3] = R.transpose(1, 2)
-    c2w[:, :3, 3] = -(R.transpose(1, 2) @ t[..., None])[..., 0]
-    c2w[:, 3, 3] = 1.0
-    return c2w
+        N.call("hgsr_rotate3", C, gc.numel() // (3 * C), ptr(Rc), cs, rs, int(not transpose), ptr(gc), ptr(out),
+               N.stream(g.device))
+        return None, out, None
 
 
 def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, width, height, near_plane=0.01,
@@ -845,12 +842,15 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
         if render_mode in ("ED", "RGB+ED"):
             render_colors = torch.cat([render_colors[..., :-1],
                                        render_colors[..., -1:] / render_alphas.clamp(min=1e-10)], dim=-1)
-    c2w = _camtoworlds(viewmats)
+    # camera -> world rotations straight from the viewmats (R_c2w = R^T), no c2w tensor built
+    _unsupported(viewmats.requires_grad or Ks.requires_grad, "rasterization_2dgs gradients w.r.t. the cameras")
+    vm = _f32(viewmats.detach())
     render_normals_from_depth = None
     if render_mode in ("RGB+ED", "RGB+D"):
         dmap = render_median if depth_mode == "median" else render_colors[..., -1:]
-        render_normals_from_depth = depth_to_normal(dmap, c2w, Ks)
-    render_normals = _Rotate3.apply(c2w[:, :3, :3].contiguous(), render_normals)  # camera -> world frame
+        _check_cuda(dmap, vm, Ks)
+        render_normals_from_depth = _DepthToNormal.apply(dmap, vm, Ks.detach(), True, True)
+    render_normals = _Rotate3.apply(vm, render_normals, True)  # camera -> world frame
     meta = {
         "camera_ids": None, "gaussian_ids": None, "radii": radii, "means2d": means2d, "depths": depths,
         "ray_transforms": ray_transforms, "normals": normals, "opacities": opac, "tile_width": tw,

@@ -328,18 +328,20 @@ int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
  * strides depth_strides (elements; e.g. the expected-depth channel of render_colors),
  * camtoworlds [C,4,4], Ks [C,3,3]; z_depth = 0 normalises the ray directions.  normals
  * [C,H,W,3] (written; 0 on the one-pixel border).  The backward writes v_depth [C,H,W]
- * (contiguous) from v_normals [C,H,W,3]; no gradient to the cameras. */
+ * (contiguous) from v_normals [C,H,W,3]; no gradient to the cameras.  from_viewmat = 1: the
+ * [C,4,4] matrices are world -> camera viewmats (the rotation is transposed in place). */
 int hgsr_depth_normal_fwd(int C, int H, int W, const float* depth, const int64_t* depth_strides,
-                          const float* camtoworlds, const float* Ks, int z_depth, float* normals,
-                          hgsr_stream_t stream);
+                          const float* camtoworlds, const float* Ks, int z_depth, int from_viewmat,
+                          float* normals, hgsr_stream_t stream);
 int hgsr_depth_normal_bwd(int C, int H, int W, const float* depth, const int64_t* depth_strides,
-                          const float* camtoworlds, const float* Ks, int z_depth, const float* v_normals,
-                          float* v_depth, hgsr_stream_t stream);
-/* out[c,m] = R_c in[c,m] (transpose = 0) or R_c^T in[c,m] (transpose = 1), 3-vectors, R [C,3,3]
- * row-major: rasterization_2dgs's camera -> world rotation of render_normals (an einsum the
- * fork runs as a 3 x 3 x HW GEMM) and its vjp. */
-int hgsr_rotate3(int C, int64_t M, const float* R, int transpose, const float* in, float* out,
-                 hgsr_stream_t stream);
+                          const float* camtoworlds, const float* Ks, int z_depth, int from_viewmat,
+                          const float* v_normals, float* v_depth, hgsr_stream_t stream);
+/* out[c,m] = R_c in[c,m] (transpose = 0) or R_c^T in[c,m] (transpose = 1), 3-vectors; R_c is
+ * the 3x3 block at R + c*cam_stride with rows row_stride floats apart (9/3 for [C,3,3], 16/4
+ * for the rotation block of [C,4,4] viewmats): rasterization_2dgs's camera -> world rotation of
+ * render_normals (an einsum the fork runs as a 3 x 3 x HW GEMM) and its vjp. */
+int hgsr_rotate3(int C, int64_t M, const float* R, int cam_stride, int row_stride, int transpose,
+                 const float* in, float* out, hgsr_stream_t stream);
 
 /* ---- K15: fused training loss ---------------------------
  * replaces the loss head of reference train.py:153-202 with utils/loss_utils.py:17-60:

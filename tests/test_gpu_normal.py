@@ -101,3 +101,24 @@ def test_rotate3_matches_einsum():
     (ref * g.double()).sum().backward()
     np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(vd.grad.cpu().numpy(), vr.grad.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_rotate3_viewmat_transpose_and_depth_normal_from_viewmat():
+    """rasterization_2dgs passes world -> camera viewmats [C,4,4]: R^T applied in place."""
+    from horizongs_amd import gsplat_api as G
+    C, H, W = 2, 19, 29
+    c2w, Ks = _cams(C, W, H, seed=13)
+    vm = torch.linalg.inv(c2w.double()).float()
+    v = torch.randn(C, H, W, 3)
+    vd = v.to(DEV).requires_grad_(True)
+    out = G._Rotate3.apply(vm.to(DEV), vd, True)
+    g = torch.randn(C, H, W, 3)
+    (out * g.to(DEV)).sum().backward()
+    ref = torch.einsum("cij,chwj->chwi", c2w[:, :3, :3].double(), v.double())
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+    gref = torch.einsum("cji,chwj->chwi", c2w[:, :3, :3].double(), g.double())
+    np.testing.assert_allclose(vd.grad.cpu().numpy(), gref.numpy(), rtol=1e-5, atol=1e-5)
+    depth = _depth(C, H, W, seed=5).to(DEV)
+    n_c2w = G.depth_to_normal(depth, c2w.to(DEV), Ks.to(DEV))
+    n_vm = G._DepthToNormal.apply(depth, vm.to(DEV), Ks.to(DEV), True, True)
+    np.testing.assert_allclose(n_vm.cpu().numpy(), n_c2w.cpu().numpy(), rtol=1e-4, atol=2e-5)
