@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--mode", choices=["chunk", "ddp"], default="chunk")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events (rocprof runs)")
+    ap.add_argument("--sh-degree", type=int, default=None, choices=[0, 1, 2, 3],
+                    help="SH colours [N,(d+1)^2,3] ~ N(0, 0.3) through the SH kernel (c4 per-chunk config: 2)")
     ap.add_argument("--anchors", type=int, default=0,
                     help="decode-inclusive variant (SURVEY 8(d) c2): A anchors -> fused decode -> raster")
     return ap.parse_args()
@@ -73,7 +75,7 @@ class Workload:
         self.args = args
         self.dev = dev
         seed = rank if args.mode == "chunk" else 0
-        sc = make_scene(args.n, args.width, args.height, seed=seed)
+        sc = make_scene(args.n, args.width, args.height, seed=seed, sh_degree=args.sh_degree)
         self.sc = sc
         # trained in the 3DGS parametrisation: log scales and opacity logits, activated each step
         self.means = sc.means.to(dev).requires_grad_(True)
@@ -154,12 +156,14 @@ class Workload:
         self.last_colors = cols
         if self.args.gs == "3d":
             out, alpha, meta = G.rasterization(xyz, quats, scales, opac, cols, self.viewmats, self.Ks, W, H,
-                                               packed=False, backgrounds=self.bg, render_mode="RGB+ED")
+                                               packed=False, backgrounds=self.bg, render_mode="RGB+ED",
+                                               sh_degree=None if self.args.anchors else self.args.sh_degree)
             meta["means2d"].retain_grad()
         else:
             (out, alpha, normals, nfd, distort, median), meta = G.rasterization_2dgs(
                 xyz, quats, scales, opac, cols, self.viewmats, self.Ks, W, H,
-                packed=False, backgrounds=self.bg, render_mode="RGB+ED")
+                packed=False, backgrounds=self.bg, render_mode="RGB+ED",
+                sh_degree=None if self.args.anchors else self.args.sh_degree)
         # the reference fine-stage loss head (train.py:153-178, config/base/small_scene/fine.yaml:50-57):
         # 0.8 L1 + 0.2 D-SSIM + 0.01 scale reg + 0.05 sky opacity + 0.05 opacity entropy, all in the fused HIP loss
         # C == 1: reshape/permute are views, so the loss reads the channels-last render in place and
@@ -377,7 +381,8 @@ def main():
         roof["timing"] = ("HIP events (no system fence) on the kernel's stream, recorded inside the timed region "
                           "for this kernel only")
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.gs == "3d" and not args.anchors:
+    if (rank == 0 and world == 1 and not args.no_cpu_baseline and args.gs == "3d" and not args.anchors
+            and args.sh_degree is None):
         cpu = cpu_baseline(args, wl)
     if rank == 0:
         ms = dt / args.steps * 1e3
@@ -387,6 +392,8 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (seeded c2 scene, SURVEY 8(d); no dataset in the environment)",
             "config": {"workload": (f"c2 {'3DGS' if args.gs == '3d' else '2DGS'} train step: "
+                                    + (f"SH{args.sh_degree} colours + " if args.sh_degree is not None
+                                       and not args.anchors else "")
                                     + (f"anchor prefilter + fused anchor decode ({args.anchors} anchors) + " if args.anchors else "")
                                     + "rasterization fwd + reference loss (L1 + D-SSIM + alpha/scale regs) + bwd"
                                     + (" + training_statis" if args.anchors else "") + " + Adam step, RGB+ED"),
