@@ -192,20 +192,23 @@ def isect_offsets(isect_ids, C, tw, th):
 # rasterization
 # --------------------------------------------------------------------------
 def raster3d_fwd(means2d, conics, colors, opacities, backgrounds, W, H, tile_size, offsets,
-                 flatten_ids, dtype=np.float32):
+                 flatten_ids, dtype=np.float32, return_stopped=False):
     C, N = means2d.shape[:2]
     D = colors.shape[-1]
     th, tw = offsets.shape[1:]
     rc = np.zeros((C, H, W, D), dtype)
     ra = np.zeros((C, H, W, 1), dtype)
     last = np.zeros((C, H, W), np.int32)
+    stopped = np.zeros((C, H, W), np.uint8)  # 1 where the list ended at the T <= 1e-4 stop
+    margin = np.zeros((C, H, W), dtype)       # smallest relative distance of a value decision to its threshold
+    gmargin = np.zeros((C, H, W), dtype)      # ... of any decision, incl. gradient-path switches
     bg = None if backgrounds is None else _c(backgrounds, dtype)
     _fn(dtype, "raster3d_fwd")(I32(C), I32(N), I32(D), _p(_c(means2d, dtype)), _p(_c(conics, dtype)),
                                _p(_c(colors, dtype)), _p(_c(opacities, dtype)), _p(bg), I32(W), I32(H),
                                I32(tile_size), I32(tw), I32(th), _p(_c(offsets, np.int32)),
                                I64(flatten_ids.shape[0]), _p(_c(flatten_ids, np.int32)), _p(rc),
-                               _p(ra), _p(last))
-    return rc, ra, last
+                               _p(ra), _p(last), _p(stopped), _p(margin), _p(gmargin))
+    return (rc, ra, last, stopped, margin, gmargin) if return_stopped else (rc, ra, last)
 
 
 def raster3d_bwd(means2d, conics, colors, opacities, backgrounds, W, H, tile_size, offsets,
@@ -230,7 +233,7 @@ def raster3d_bwd(means2d, conics, colors, opacities, backgrounds, W, H, tile_siz
 
 
 def raster2d_fwd(means2d, ray_transforms, colors, opacities, normals, backgrounds, W, H,
-                 tile_size, offsets, flatten_ids, dtype=np.float32):
+                 tile_size, offsets, flatten_ids, dtype=np.float32, return_stopped=False):
     C, N = means2d.shape[:2]
     D = colors.shape[-1]
     th, tw = offsets.shape[1:]
@@ -241,14 +244,19 @@ def raster2d_fwd(means2d, ray_transforms, colors, opacities, normals, background
     rm = np.zeros((C, H, W, 1), dtype)
     last = np.zeros((C, H, W), np.int32)
     med = np.zeros((C, H, W), np.int32)
+    stopped = np.zeros((C, H, W), np.uint8)
+    margin = np.zeros((C, H, W), dtype)
+    gmargin = np.zeros((C, H, W), dtype)
     bg = None if backgrounds is None else _c(backgrounds, dtype)
     _fn(dtype, "raster2d_fwd")(I32(C), I32(N), I32(D), _p(_c(means2d, dtype)),
                                _p(_c(ray_transforms, dtype)), _p(_c(colors, dtype)),
                                _p(_c(opacities, dtype)), _p(_c(normals, dtype)), _p(bg), I32(W), I32(H),
                                I32(tile_size), I32(tw), I32(th), _p(_c(offsets, np.int32)),
                                I64(flatten_ids.shape[0]), _p(_c(flatten_ids, np.int32)), _p(rc),
-                               _p(ra), _p(rn), _p(rd), _p(rm), _p(last), _p(med))
-    return rc, ra, rn, rd, rm, last, med
+                               _p(ra), _p(rn), _p(rd), _p(rm), _p(last), _p(med), _p(stopped),
+                               _p(margin), _p(gmargin))
+    out = (rc, ra, rn, rd, rm, last, med)
+    return out + (stopped, margin, gmargin) if return_stopped else out
 
 
 def raster2d_bwd(means2d, ray_transforms, colors, opacities, normals, backgrounds, W, H,
@@ -274,3 +282,13 @@ def raster2d_bwd(means2d, ray_transforms, colors, opacities, normals, background
                                _p(_c(v_render_normals, dtype)), _p(v_means2d), _p(v_rt),
                                _p(v_colors), _p(v_opac), _p(v_normals), _p(v_dens))
     return v_means2d, v_rt, v_colors, v_opac, v_normals, v_dens
+
+
+def set_envelope(on, dtype=np.float64):
+    """Switch the raster backwards of one build into envelope mode (see hgsr_oracle.c)."""
+    _fn(dtype, "set_envelope")(I32(int(bool(on))))
+
+
+def set_hitform(form, dtype=np.float32):
+    """2DGS hit evaluation of one build: 0 gsplat's per-pixel cross product, 1 the plane form."""
+    _fn(dtype, "set_hitform")(I32(int(form)))

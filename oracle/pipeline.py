@@ -21,13 +21,20 @@ def _campos(viewmats):
     return -np.einsum("cji,cj->ci", R, t)
 
 
-class Raster3D:
+class _Band:
+    @property
+    def Hr(self):
+        return self.H if self.rows is None else min(self.rows, self.H)
+
+
+class Raster3D(_Band):
     """3DGS forward + backward through the C oracle (float32 by default)."""
 
     def __init__(self, means, quats, scales, opacities, colors, viewmats, Ks, W, H, sh_degree=None,
                  backgrounds=None, render_mode="RGB+ED", eps2d=0.3, near=0.01, far=1e10, tile_size=16,
-                 dtype=np.float32):
+                 dtype=np.float32, rows=None):
         self.dt = dtype
+        self.rows = rows  # rasterise only image rows [0, rows) (banded checks); None = all
         c = lambda a: None if a is None else np.ascontiguousarray(a, dtype=dtype)  # noqa: E731
         self.means, self.quats, self.scales = c(means), c(quats), c(scales)
         self.opacities, self.colors = c(opacities), c(colors)
@@ -68,9 +75,9 @@ class Raster3D:
                                                                    self.tw, self.th, dtype=dt)
         self.offsets = O.isect_offsets(self.isect_ids, C, self.tw, self.th)
         self.opac_c = np.ascontiguousarray(np.broadcast_to(self.opacities, (C, Nn)), dt)
-        self.rc_raw, self.ra, self.last = O.raster3d_fwd(self.means2d, self.conics, self.cols, self.opac_c,
-                                                         self.bg_r, self.W, self.H, self.ts, self.offsets,
-                                                         self.flatten_ids, dtype=dt)
+        self.rc_raw, self.ra, self.last, self.stopped, self.margin, self.gmargin = O.raster3d_fwd(
+            self.means2d, self.conics, self.cols, self.opac_c, self.bg_r, self.W, self.Hr, self.ts, self.offsets,
+            self.flatten_ids, dtype=dt, return_stopped=True)
         out = self.rc_raw.copy()
         if self.mode in ("ED", "RGB+ED"):
             out[..., -1:] = self.rc_raw[..., -1:] / np.maximum(self.ra, dt(1e-10))
@@ -90,7 +97,7 @@ class Raster3D:
             v_rc = v_rc.copy()
             v_rc[..., -1:] = g / den
         vm2, vcon, vcol, vop = O.raster3d_bwd(self.means2d, self.conics, self.cols, self.opac_c, self.bg_r, self.W,
-                                              self.H, self.ts, self.offsets, self.flatten_ids, self.ra, self.last,
+                                              self.Hr, self.ts, self.offsets, self.flatten_ids, self.ra, self.last,
                                               v_rc, v_ra, dtype=dt)
         v_depths = np.zeros((C, Nn), dt)
         if self.mode in ("RGB+D", "RGB+ED", "D", "ED"):
@@ -118,13 +125,87 @@ class Raster3D:
         grads["scales"] = vs
         return grads
 
+    def envelope(self, v_render_colors, v_render_alphas):
+        """Per-element magnitude envelopes E of every gradient of backward() (same keys):
+        the raster backward in envelope mode (sum of |term| per output, hgsr_oracle.c) on
+        |upstream|, then propagated through the projection / SH backward as |J|^T E, one
+        input component at a time.  Any f32 evaluation of gradient i is within a small
+        multiple of u * E_i of the exact value.  Use on the float64 instance after forward()."""
+        dt = self.dt
+        C, Nn = self.viewmats.shape[0], self.means.shape[0]
+        v_rc = np.abs(np.array(v_render_colors, dt))
+        v_ra = np.abs(np.array(v_render_alphas, dt))
+        if self.mode in ("ED", "RGB+ED"):
+            den = np.maximum(self.ra, dt(1e-10))
+            g = v_rc[..., -1:]
+            # alpha = 1 - T carries an absolute rounding error ~u, so the ED divide amplifies the
+            # relative error of every term it feeds by ~(1 + 1 / alpha)
+            k = 1 + 1 / den
+            v_ra = v_ra + np.where(self.ra >= dt(1e-10), k * g * np.abs(self.rc_raw[..., -1:]) / (den * den),
+                                   0).astype(dt)
+            v_rc = v_rc.copy()
+            v_rc[..., -1:] = k * g / den
+        O.set_envelope(True, dt)
+        try:
+            vm2, vcon, vcol, vop = O.raster3d_bwd(self.means2d, self.conics, self.cols, self.opac_c, self.bg_r,
+                                                  self.W, self.Hr, self.ts, self.offsets, self.flatten_ids, self.ra,
+                                                  self.last, v_rc, v_ra, dtype=dt)
+        finally:
+            O.set_envelope(False, dt)
+        v_depths = np.zeros((C, Nn), dt)
+        if self.mode in ("RGB+D", "RGB+ED", "D", "ED"):
+            v_depths += vcol[..., -1]
+            vcol_rgb = vcol[..., :-1]
+        else:
+            vcol_rgb = vcol
+        env = {"means2d": vm2, "conics": vcon, "opacities": vop.sum(0)}
+        v_means_extra = np.zeros((Nn, 3), dt)
+        if self.mode not in ("D", "ED"):
+            if self.sh_degree is None:
+                env["colors"] = vcol_rgb.sum(0)
+            else:
+                K = self.colors.shape[-2]
+                shs = np.broadcast_to(self.colors, (C, Nn, K, 3))
+                ec = np.zeros((C * Nn, K, 3), dt)
+                for ch in range(3):  # |J|^T E one colour channel at a time
+                    e1 = np.zeros((C * Nn, 3), dt)
+                    e1[:, ch] = np.where(self.sh_pre >= 0, vcol_rgb, 0).reshape(-1, 3)[:, ch]
+                    vc, vd = O.sh_bwd(self.sh_degree, self.dirs.reshape(-1, 3), shs.reshape(-1, K, 3), e1,
+                                      (self.radii > 0).reshape(-1), dtype=dt)
+                    ec += np.abs(vc)
+                    v_means_extra += np.abs(vd).reshape(C, Nn, 3).sum(0)
+                env["colors"] = ec.reshape(C, Nn, K, 3).sum(0)
+        ups = {"m2x": None, "m2y": None, "d": None, "c0": None, "c1": None, "c2": None}
+        acc = [np.zeros((Nn, 3), dt), np.zeros((Nn, 4), dt), np.zeros((Nn, 3), dt)]
+        for key in ups:
+            a2, ad, ac = np.zeros_like(vm2), np.zeros_like(v_depths), np.zeros_like(vcon)
+            if key == "m2x":
+                a2[..., 0] = vm2[..., 0]
+            elif key == "m2y":
+                a2[..., 1] = vm2[..., 1]
+            elif key == "d":
+                ad[...] = v_depths
+            else:
+                ac[..., int(key[1])] = vcon[..., int(key[1])]
+            out = O.proj3d_bwd(self.means, self.quats, self.scales, self.viewmats, self.Ks, self.W, self.H,
+                               self.radii, self.conics, a2, ad, ac, self.eps2d, dtype=dt)
+            for t, o in zip(acc, out):
+                t += np.abs(o)
+        env["means"] = acc[0] + v_means_extra
+        env["quats"] = acc[1]
+        env["scales"] = acc[2]
+        return env
 
-class Raster2D:
+
+class Raster2D(_Band):
     """2DGS forward (+ backward of colors/alphas/normals outputs) through the C oracle."""
 
     def __init__(self, means, quats, scales, opacities, colors, viewmats, Ks, W, H, backgrounds=None,
-                 render_mode="RGB+ED", near=0.01, far=1e10, tile_size=16, dtype=np.float32):
+                 render_mode="RGB+ED", near=0.01, far=1e10, tile_size=16, dtype=np.float32, rows=None,
+                 hitform=0):
         self.dt = dtype
+        self.hitform = hitform  # 2DGS hit evaluation form (hgsr_oracle.c eval_splat2d)
+        self.rows = rows  # rasterise only image rows [0, rows) (banded checks); None = all
         c = lambda a: None if a is None else np.ascontiguousarray(a, dtype=dtype)  # noqa: E731
         self.means, self.quats, self.scales = c(means), c(quats), c(scales)
         self.opacities, self.colors = c(opacities), c(colors)
@@ -150,9 +231,12 @@ class Raster2D:
                                                                    self.tw, self.th, dtype=dt)
         self.offsets = O.isect_offsets(self.isect_ids, C, self.tw, self.th)
         self.opac_c = np.ascontiguousarray(np.broadcast_to(self.opacities, (C, Nn)), dt)
+        O.set_hitform(self.hitform, dt)
         (self.rc_raw, self.ra, self.rn, self.rd, self.rm, self.last,
-         self.med) = O.raster2d_fwd(self.means2d, self.rt, self.cols, self.opac_c, self.normals, self.bg_r, self.W,
-                                    self.H, self.ts, self.offsets, self.flatten_ids, dtype=dt)
+         self.med, self.stopped, self.margin, self.gmargin) = O.raster2d_fwd(self.means2d, self.rt, self.cols, self.opac_c, self.normals,
+                                                  self.bg_r, self.W, self.Hr, self.ts, self.offsets, self.flatten_ids,
+                                                  dtype=dt, return_stopped=True)
+        O.set_hitform(0, dt)
         out = self.rc_raw.copy()
         if self.mode == "RGB+ED":
             out[..., -1:] = self.rc_raw[..., -1:] / np.maximum(self.ra, dt(1e-10))
@@ -171,12 +255,62 @@ class Raster2D:
             v_ra = v_ra + np.where(self.ra >= dt(1e-10), -g * self.rc_raw[..., -1:] / (den * den), 0).astype(dt)
             v_rc = v_rc.copy()
             v_rc[..., -1:] = g / den
-        vm2, vrt, vcol, vop, vn, vdens = O.raster2d_bwd(
-            self.means2d, self.rt, self.cols, self.opac_c, self.normals, self.bg_r, self.W, self.H, self.ts,
-            self.offsets, self.flatten_ids, self.ra, self.last, v_rc, v_ra, np.asarray(v_render_normals_cam, dt),
-            dtype=dt)
+        O.set_hitform(self.hitform, dt)
+        try:
+            vm2, vrt, vcol, vop, vn, vdens = O.raster2d_bwd(
+                self.means2d, self.rt, self.cols, self.opac_c, self.normals, self.bg_r, self.W, self.Hr, self.ts,
+                self.offsets, self.flatten_ids, self.ra, self.last, v_rc, v_ra, np.asarray(v_render_normals_cam, dt),
+                dtype=dt)
+        finally:
+            O.set_hitform(0, dt)
         v_depths = vcol[..., -1].copy()
         vm, vq, vs = O.proj2d_bwd(self.means, self.quats, self.scales, self.viewmats, self.Ks, self.W, self.H,
                                   self.radii, self.rt, vm2, v_depths, vrt, vn, dtype=dt)
         return {"means": vm, "quats": vq, "scales": vs, "opacities": vop.sum(0), "colors": vcol[..., :-1].sum(0),
                 "means2d": vm2, "densify": vdens}
+
+    def envelope(self, v_render_colors, v_render_alphas, v_render_normals_cam):
+        """Per-element magnitude envelopes of every gradient of backward(); see
+        Raster3D.envelope.  Use on the float64 instance after forward()."""
+        dt = self.dt
+        C, Nn = self.viewmats.shape[0], self.means.shape[0]
+        v_rc = np.abs(np.array(v_render_colors, dt))
+        v_ra = np.abs(np.array(v_render_alphas, dt))
+        if self.mode == "RGB+ED":
+            den = np.maximum(self.ra, dt(1e-10))
+            g = v_rc[..., -1:]
+            # alpha = 1 - T carries an absolute rounding error ~u, so the ED divide amplifies the
+            # relative error of every term it feeds by ~(1 + 1 / alpha)
+            k = 1 + 1 / den
+            v_ra = v_ra + np.where(self.ra >= dt(1e-10), k * g * np.abs(self.rc_raw[..., -1:]) / (den * den),
+                                   0).astype(dt)
+            v_rc = v_rc.copy()
+            v_rc[..., -1:] = k * g / den
+        O.set_envelope(True, dt)
+        try:
+            vm2, vrt, vcol, vop, vn, vdens = O.raster2d_bwd(
+                self.means2d, self.rt, self.cols, self.opac_c, self.normals, self.bg_r, self.W, self.Hr, self.ts,
+                self.offsets, self.flatten_ids, self.ra, self.last, v_rc, v_ra,
+                np.abs(np.asarray(v_render_normals_cam, dt)), dtype=dt)
+        finally:
+            O.set_envelope(False, dt)
+        v_depths = vcol[..., -1].copy()
+        acc = [np.zeros((Nn, 3), dt), np.zeros((Nn, 4), dt), np.zeros((Nn, 3), dt)]
+        comps = [("m2", k) for k in range(2)] + [("d", 0)] + [("rt", k) for k in range(9)] + [("n", k) for k in range(3)]
+        for kind, k in comps:
+            a2, ad = np.zeros_like(vm2), np.zeros_like(v_depths)
+            art, an = np.zeros(vrt.shape[:2] + (9,), dt), np.zeros_like(vn)
+            if kind == "m2":
+                a2[..., k] = vm2[..., k]
+            elif kind == "d":
+                ad[...] = v_depths
+            elif kind == "rt":
+                art[..., k] = vrt.reshape(art.shape)[..., k]
+            else:
+                an[..., k] = vn[..., k]
+            out = O.proj2d_bwd(self.means, self.quats, self.scales, self.viewmats, self.Ks, self.W, self.H,
+                               self.radii, self.rt, a2, ad, art.reshape(vrt.shape), an, dtype=dt)
+            for t, o in zip(acc, out):
+                t += np.abs(o)
+        return {"means": acc[0], "quats": acc[1], "scales": acc[2], "opacities": vop.sum(0),
+                "colors": vcol[..., :-1].sum(0), "means2d": vm2, "densify": vdens}

@@ -1,0 +1,166 @@
+"""Shared GPU-vs-oracle raster parity drivers (used by test_gpu_parity.py and
+test_gpu_parity_dense.py).  TEST INFRASTRUCTURE.
+
+run_3dgs / run_2dgs: gsplat.rasterization[_2dgs] fwd + bwd on the GPU against the C oracle
+(f32 checker + f64 truth) on the same seeded scene: integer outputs bit-exact, images per
+pixel with per-element conditioning (oracle/checks.py), pixels whose discrete decisions sit
+within a few ulps of a threshold excluded from the value bar and from the upstream gradient,
+every gradient per element.  Reference call site: gaussian_renderer/render.py:40-76.
+"""
+import numpy as np
+import torch
+
+from horizongs_amd import gsplat_api as G
+from oracle import pipeline as OP
+from oracle.checks import DELTA_2D, DELTA_3D, MAX_GRAD_AMBIGUOUS, ambiguous, cond_close, image_close
+
+DEV = "cuda:0"
+# bare 1e-5 abs / 1e-4 rel pass rate the RGB image must keep against the f32 oracle
+RGB_MIN_STRICT = 0.999
+
+
+def to_dev(*ts):
+    return [t.to(DEV).contiguous() for t in ts]
+
+
+def depth_stats(ref):
+    """(max Gaussians per tile, max backward replay depth of a tile, stopped-pixel fraction).
+
+    Replay depth = the tile's latest contributor over its rasterised rows - tile start + 1,
+    i.e. how far back the backward walks.  Stopped = the pixel's list ended at the exclusive
+    T <= 1e-4 stop (flag from the oracle forward)."""
+    C, th, tw = ref.offsets.shape
+    offs = ref.offsets.reshape(-1).astype(np.int64)
+    ends = np.append(offs[1:], len(ref.flatten_ids))
+    counts = ends - offs
+    rows = ref.Hr
+    last = np.full((C, th * 16, tw * 16), -1, np.int64)
+    last[:, :rows, :ref.W] = ref.last.reshape(C, rows, ref.W)
+    tile_last = last.reshape(C, th, 16, tw, 16).max(axis=(2, 4)).reshape(-1)
+    replay = np.where(tile_last >= 0, tile_last + 1 - offs, 0)
+    return int(counts.max()), int(replay.max()), float(ref.stopped.mean())
+
+
+def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None, train=None):
+    """rasterization() fwd + bwd on the GPU vs Raster3D f32 / f64; upstream gradients N(0,1)
+    on the rasterised rows, zero elsewhere."""
+    kw = dict(backgrounds=bg, render_mode=mode, rows=rows, sh_degree=sh)
+    args = (sc.means, sc.quats, sc.scales, sc.opacities, sc.colors, sc.viewmats, sc.Ks, sc.width, sc.height)
+    r32 = OP.Raster3D(*args, **kw)
+    rc, ra = r32.forward()
+    r64 = OP.Raster3D(*args, dtype=np.float64, **kw)
+    r64.forward()
+    stats = depth_stats(r32)
+    rr = r32.Hr
+    means, quats, scales, opac, cols, vm, K = to_dev(sc.means, sc.quats, sc.scales, sc.opacities, sc.colors,
+                                                     sc.viewmats, sc.Ks)
+    gbg = None if bg is None else bg.to(DEV)
+    leaves = dict(means=means, quats=quats, scales=scales, opacities=opac, colors=cols)
+    train = tuple(leaves) if train is None else train
+    for k in train:
+        leaves[k].requires_grad_(True)
+    out, alpha, meta = G.rasterization(means, quats, scales, opac, cols, vm, K, sc.width, sc.height, packed=False,
+                                       backgrounds=gbg, render_mode=mode, sh_degree=sh)
+    meta["means2d"].retain_grad()
+    np.testing.assert_array_equal(meta["isect_ids"].cpu().numpy(), r32.isect_ids)
+    np.testing.assert_array_equal(meta["flatten_ids"].cpu().numpy(), r32.flatten_ids)
+    np.testing.assert_array_equal(meta["isect_offsets"].cpu().numpy(), r32.offsets)
+    o = out.detach()[:, :rr].cpu().numpy()
+    amb = ambiguous(r32, DELTA_3D)                 # value decisions: excluded from the image bar
+    gamb = ambiguous(r32, DELTA_3D, gradient=True)  # + gradient-path switches: no upstream gradient
+    rates = {}
+    Dc = 3 if mode in ("RGB", "RGB+D", "RGB+ED") else 0
+    if Dc:
+        rates["rgb"], n_amb = image_close(o[..., :Dc], rc[..., :Dc], r64.render_colors[..., :Dc], amb, "render rgb",
+                                          min_strict=min_strict)
+    if o.shape[-1] > Dc:
+        rates["depth"], n_amb = image_close(o[..., Dc:], rc[..., Dc:], r64.render_colors[..., Dc:], amb,
+                                            "render depth")
+    rates["alpha"], _ = image_close(alpha.detach()[:, :rr].cpu().numpy(), ra, r64.ra, amb, "render alphas")
+    rates["ambiguous_px"] = n_amb
+    rates["grad_ambiguous_px"] = int(gamb.sum())
+    assert gamb.mean() <= MAX_GRAD_AMBIGUOUS, gamb.mean()
+    g = torch.Generator().manual_seed(seed)
+    keep = torch.from_numpy(~gamb)[..., None].float()  # no gradient flows from ambiguous pixels
+    vrc = torch.randn(rc.shape, generator=g) * keep
+    vra = torch.randn(ra.shape, generator=g) * keep
+    vrc_full = torch.zeros(out.shape)
+    vra_full = torch.zeros(alpha.shape)
+    vrc_full[:, :rr] = vrc
+    vra_full[:, :rr] = vra
+    ((out * vrc_full.to(DEV)).sum() + (alpha * vra_full.to(DEV)).sum()).backward()
+    gr32 = r32.backward(vrc.numpy(), vra.numpy())
+    gr64 = r64.backward(vrc.numpy(), vra.numpy())
+    genv = r64.envelope(vrc.numpy(), vra.numpy())
+    got = {"means2d": meta["means2d"].grad, **{k: leaves[k].grad for k in train}}
+    for k, v in got.items():
+        if k == "colors" and not Dc:
+            continue
+        rates["v_" + k] = cond_close(v.cpu().numpy(), gr32[k], gr64[k], "v_" + k, rel_floor=0, env=genv[k])
+    print("strict 1e-5/1e-4 pass rates:", {k: round(float(v), 6) for k, v in rates.items()}, "stats", stats)
+    return stats, rates, dict(out=out, alpha=alpha, meta=meta, r32=r32, r64=r64)
+
+
+def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
+    kw = dict(backgrounds=bg, render_mode=mode, rows=rows)
+    args = (sc.means, sc.quats, sc.scales, sc.opacities, sc.colors, sc.viewmats, sc.Ks, sc.width, sc.height)
+    r32 = OP.Raster2D(*args, **kw)
+    rc, ra, rn = r32.forward()
+    r64 = OP.Raster2D(*args, dtype=np.float64, **kw)
+    r64.forward()
+    # the plane-form hit (what the kernels evaluate) is a second correct f32 evaluation:
+    # near edge-on surfels the two forms differ far beyond an ulp (the hit's z cancels)
+    r32b = OP.Raster2D(*args, hitform=1, **kw)
+    r32b.forward()
+    stats = depth_stats(r32)
+    rr = r32.Hr
+    means, quats, scales, opac, cols, vm, K = to_dev(sc.means, sc.quats, sc.scales, sc.opacities, sc.colors,
+                                                     sc.viewmats, sc.Ks)
+    gbg = None if bg is None else bg.to(DEV)
+    for t in (means, quats, scales, opac, cols):
+        t.requires_grad_(True)
+    (out, alpha, normals, nfd, distort, median), meta = G.rasterization_2dgs(
+        means, quats, scales, opac, cols, vm, K, sc.width, sc.height, packed=False, backgrounds=gbg,
+        render_mode=mode)
+    np.testing.assert_array_equal(meta["isect_ids"].cpu().numpy(), r32.isect_ids)
+    np.testing.assert_array_equal(meta["flatten_ids"].cpu().numpy(), r32.flatten_ids)
+    o = out.detach()[:, :rr].cpu().numpy()
+    # either form's decisions near a threshold, or the two forms ending a pixel differently
+    split = (r32.last != r32b.last) | (r32.stopped != r32b.stopped)
+    amb = ambiguous(r32, DELTA_2D) | ambiguous(r32b, DELTA_2D) | split
+    gamb = ambiguous(r32, DELTA_2D, gradient=True) | ambiguous(r32b, DELTA_2D, gradient=True) | split
+    rates = {}
+    rb = r32b.render_colors
+    rates["rgb"], n_amb = image_close(o[..., :3], rc[..., :3], r64.render_colors[..., :3], amb, "2dgs rgb",
+                                      min_strict=min_strict, margin=r32.margin, alt32=rb[..., :3])
+    rates["depth"], _ = image_close(o[..., 3:], rc[..., 3:], r64.render_colors[..., 3:], amb, "2dgs depth",
+                                    alt32=rb[..., 3:])
+    rates["alpha"], _ = image_close(alpha.detach()[:, :rr].cpu().numpy(), ra, r64.ra, amb, "2dgs alphas",
+                                    alt32=r32b.ra)
+    # viewmat = I: the world-frame normals are the camera-frame ones
+    rates["normals"], _ = image_close(normals.detach()[:, :rr].cpu().numpy(), rn, r64.rn, amb, "2dgs normals",
+                                      alt32=r32b.rn)
+    rates["ambiguous_px"] = n_amb
+    rates["grad_ambiguous_px"] = int(gamb.sum())
+    assert gamb.mean() <= MAX_GRAD_AMBIGUOUS, gamb.mean()
+    g = torch.Generator().manual_seed(seed)
+    keep = torch.from_numpy(~gamb)[..., None].float()  # no gradient flows from ambiguous pixels
+    vrc = torch.randn(rc.shape, generator=g) * keep
+    vra = torch.randn(ra.shape, generator=g) * keep
+    vrn = torch.randn(rn.shape, generator=g) * keep
+    full = [torch.zeros(t.shape) for t in (out, alpha, normals)]
+    for f, v in zip(full, (vrc, vra, vrn)):
+        f[:, :rr] = v
+    ((out * full[0].to(DEV)).sum() + (alpha * full[1].to(DEV)).sum() + (normals * full[2].to(DEV)).sum()).backward()
+    gr32 = r32.backward(vrc.numpy(), vra.numpy(), vrn.numpy())
+    gr32b = r32b.backward(vrc.numpy(), vra.numpy(), vrn.numpy())
+    gr64 = r64.backward(vrc.numpy(), vra.numpy(), vrn.numpy())
+    genv = r64.envelope(vrc.numpy(), vra.numpy(), vrn.numpy())
+    got = {"densify": meta["gradient_2dgs"].grad, "opacities": opac.grad, "colors": cols.grad,
+           "means": means.grad, "quats": quats.grad, "scales": scales.grad}
+    for k, v in got.items():
+        rates["v_" + k] = cond_close(v.cpu().numpy(), gr32[k], gr64[k], "v_" + k, rel_floor=0, env=genv[k],
+                                     alt32=gr32b[k])
+    print("strict 1e-5/1e-4 pass rates:", {k: round(float(v), 6) for k, v in rates.items()}, "stats", stats)
+    return stats, rates, dict(out=out, alpha=alpha, normals=normals, nfd=nfd, distort=distort, median=median,
+                              meta=meta, r32=r32, r64=r64)
