@@ -7,15 +7,19 @@ head (fused HIP loss), loss.backward() (raster backward -> projection backward)
 and the optimizer step (Adam, eps=1e-15, one fused HIP launch), on a synthetic c2 scene: 2,000,000 Gaussians at
 1920x1080, fp32, inputs resident in HBM.
 
-Multi-GPU: one process per GPU (torchrun); the path shards per chunk (reference
-preprocess/generate_chunks_config.py: one chunk per GPU, no collectives), so each
-rank renders its own seeded scene ("scaling": "weak"); with --mode ddp the ranks
-render different views of ONE scene and all-reduce the Gaussian gradients over
-RCCL after backward (the c5 data-parallel mode).
+Multi-GPU: one process per GPU.  `--gpus N` with no WORLD_SIZE in the environment starts
+N ranks itself (a torch.distributed.run child process, before this process touches the
+GPU); under torchrun it is one rank.  The path shards per chunk (reference
+preprocess/generate_chunks_config.py: one chunk per GPU, no collectives), so each rank
+renders its own seeded scene ("scaling": "weak"); with --mode ddp the ranks render
+different views of ONE scene and average the Gaussian gradients with bucketed RCCL
+all-reduces launched from gradient hooks while the backward runs (the c5 data-parallel
+mode, multigpu.GradientAllReduce).
 
 Prints ONE JSON line (rank 0) with the metric, a roofline object for the dominant
-kernel (HIP-event timed live over the timed region) and a CPU baseline (the C
-oracle on a bounded sample, rank 0 at N=1 only).
+kernel (HIP-event timed live over the timed region), a CPU baseline (the C oracle on all
+host threads, rank 0 at N=1 only) and, at N=1, `secondary`: the same train step measured
+on BASELINE configs[1] (decode-inclusive, 500k anchors) and configs[2] (2DGS).
 """
 from __future__ import annotations
 
@@ -26,11 +30,40 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _launch_ranks() -> None:
+    """--gpus N without WORLD_SIZE: run N ranks under torch.distributed.run in a child process
+    (this process has not touched the GPU, and never execs) and exit with its status."""
+    import subprocess
+    argv = sys.argv[1:]
+    n = 1
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            n = int(argv[i + 1])
+        elif a.startswith("--gpus="):
+            n = int(a.split("=", 1)[1])
+    if n <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + argv
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+if __name__ == "__main__":
+    _launch_ranks()
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
 sys.path.insert(0, ROOT)
 
 from horizongs_amd import _native as NAT  # noqa: E402
@@ -62,6 +95,8 @@ def parse():
     ap.add_argument("--gs", choices=["3d", "2d"], default="3d")
     ap.add_argument("--mode", choices=["chunk", "ddp"], default="chunk")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the configs[1] (500k anchors) and configs[2] (2DGS) lines measured at N = 1")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events (rocprof runs)")
     ap.add_argument("--sh-degree", type=int, default=None, choices=[0, 1, 2, 3],
                     help="SH colours [N,(d+1)^2,3] ~ N(0, 0.3) through the SH kernel (c4 per-chunk config: 2)")
@@ -102,7 +137,8 @@ class Workload:
         # the reference optimizer (scene/lod_model.py:320): Adam(eps=1e-15), one group per tensor,
         # stepped every iteration (train.py:274-277) -- one fused HIP launch here
         self.optimizer = Adam([{"params": [p], "lr": lr} for p, lr in groups], lr=0.0, eps=1e-15)
-        self.allreduce = GradientAllReduce(self.params, bucket_mb=64.0)
+        # DDP over views: buckets follow the optimizer's current groups (densify surgery safe)
+        self.allreduce = GradientAllReduce(self.optimizer, bucket_mb=64.0)
 
     def _init_anchors(self, args, seed, dev):
         """SURVEY 8(d) decode-inclusive c2: anchors placed like the c2 Gaussians, feat ~ N(0, 0.1),
@@ -174,9 +210,12 @@ class Workload:
                                                  normals_from_depth=nfd.reshape(H, W, 3).permute(2, 0, 1),
                                                  lambda_normal=0.05)
         loss = fused_loss(img, self.target, None, 0.2, alpha.reshape(H, W), 0.05, 0.05, scales, 0.01, **aux)[0]
+        ddp = self.args.mode == "ddp"
+        if ddp:
+            self.allreduce.begin()  # gradient hooks launch the bucket all-reduces during the backward
         loss.backward()
-        if self.args.mode == "ddp":
-            self.allreduce()
+        if ddp:
+            self.allreduce.finish()
         if self.args.anchors:  # densification statistics of this view (train.py:258-262)
             HDn.training_statis(self.stats_model, self.stats_opt,
                                 dict(selection_mask=sel, visible_mask=visible, viewspace_points=meta["means2d"],
@@ -244,12 +283,25 @@ def psnr_parity(args):
             " (tests/test_gpu_training_parity.py)"}
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, wl):
-    """The C oracle (scalar, 1 thread) on a bounded sample of the same workload."""
+    """The C oracle (OpenMP over pixel rows / Gaussians, oracle/hgsr_oracle.c) on one whole
+    view of the same workload: projection, tile intersection + sort, raster fwd + bwd over
+    every pixel, projection backward.  Threads: the OpenMP default (OMP_NUM_THREADS, else
+    every host core)."""
     from oracle import oracle as O
     sc = wl.sc
     W, H = args.width, args.height
-    band = 160  # rasterise 160 of 1080 rows (10 of 68 tile rows), scale raster time by H / band
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
     t = {}
     t0 = time.perf_counter()
     r, m2, d, con = O.proj3d_fwd(sc.means.numpy(), sc.quats.numpy(), sc.scales.numpy(), sc.viewmats.numpy(),
@@ -263,39 +315,33 @@ def cpu_baseline(args, wl):
     cols = np.concatenate([sc.colors.numpy()[None], d[..., None]], -1).astype(np.float32)
     op = sc.opacities.numpy()[None].astype(np.float32)
     t0 = time.perf_counter()
-    rc, ra, last = O.raster3d_fwd(m2, con, cols, op, None, W, band, 16, offs, fl)
-    t["raster_fwd_band"] = time.perf_counter() - t0
+    rc, ra, last = O.raster3d_fwd(m2, con, cols, op, None, W, H, 16, offs, fl)
+    t["raster_fwd"] = time.perf_counter() - t0
     g = np.random.default_rng(0)
     vrc = (g.standard_normal(rc.shape) * 1e-6).astype(np.float32)
     vra = np.full(ra.shape, 1e-8, np.float32)
     t0 = time.perf_counter()
-    vm2, vcon, vcol, vop = O.raster3d_bwd(m2, con, cols, op, None, W, band, 16, offs, fl, ra, last, vrc, vra)
-    t["raster_bwd_band"] = time.perf_counter() - t0
+    vm2, vcon, vcol, vop = O.raster3d_bwd(m2, con, cols, op, None, W, H, 16, offs, fl, ra, last, vrc, vra)
+    t["raster_bwd"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     O.proj3d_bwd(sc.means.numpy(), sc.quats.numpy(), sc.scales.numpy(), sc.viewmats.numpy(), sc.Ks.numpy(), W, H,
                  r, con, vm2, vcol[..., -1].copy(), vcon)
     t["proj_bwd"] = time.perf_counter() - t0
-    scale = H / band
-    per_view = (t["proj_fwd"] + t["isect_sort"] + t["proj_bwd"]
-                + scale * (t["raster_fwd_band"] + t["raster_bwd_band"]))
+    per_view = sum(t.values())
     return {
-        "value": 1.0 / per_view, "unit": "views/s", "cores": 1, "kind": "port",
-        "sample": (f"C oracle (oracle/hgsr_oracle.c, 1 thread): projection fwd/bwd and tile intersection+sort on "
-                   f"all {args.n} Gaussians; raster fwd+bwd on a {band}x{W} band (rows 0-{band - 1}), raster time "
-                   f"scaled by {H}/{band}; measured {sum(t.values()):.1f}s"),
+        "value": 1.0 / per_view, "unit": "views/s", "cores": threads, "kind": "port",
+        "cpu_model": _cpu_model(), "host_cpu_count": os.cpu_count(),
+        "sample": (f"one full view of the same workload through the C oracle (oracle/hgsr_oracle.c, OpenMP, "
+                   f"{threads} threads): projection, tile intersection + sort (serial qsort), raster fwd + bwd "
+                   f"over all {W}x{H} pixels, projection backward, on all {args.n} Gaussians; measured "
+                   f"{per_view:.1f}s (no loss head / optimizer: the rasterizer path only)"),
         "breakdown_s": {k: round(v, 3) for k, v in t.items()},
     }
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+def measure(args, rank, world, dev):
+    """Warm up, time exactly args.steps steps (barrier + synchronize on both sides, max over
+    ranks), then a per-kernel breakdown pass.  Returns the measurements of this workload."""
     wl = Workload(args, rank, dev)
     for _ in range(args.warmup):
         wl.step()
@@ -310,7 +356,7 @@ def main():
         NAT.call("hgsr_timing_reset")
         NAT.call("hgsr_timing_only", dominant.encode())
         NAT.call("hgsr_timing_enable", 1)
-        NAT.call("hgsr_timing_pairs", None, 1)  # the backward counts its visited pairs on the device
+        NAT.call("hgsr_timing_pairs", None, 1)  # the backward counts its visited / stepped pairs on the device
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -327,63 +373,123 @@ def main():
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    kernels = {}
-    live = None
-    isects_after = wl.meta["flatten_ids"].numel()
-    pairs_timed = None
+    res = {"wl": wl, "dt": dt, "kernels": {}, "live": None, "isects_before": isects_before,
+           "isects_after": wl.meta["flatten_ids"].numel(), "dominant": dominant}
     if timing:
-        pc = ct.c_ulonglong(0)
+        pc, ec = ct.c_ulonglong(0), ct.c_ulonglong(0)
+        NAT.call("hgsr_timing_exec_pairs", ct.byref(ec))
         NAT.call("hgsr_timing_pairs", ct.byref(pc), 1)
-        pairs_timed = pc.value
+        res["pairs_timed"], res["exec_pairs_timed"] = pc.value, ec.value
         tot, cnt = NAT.kernel_time(dominant)
-        live = {"avg_ms": round(tot / cnt, 4), "launches": cnt} if cnt else None
+        res["live"] = {"avg_ms": round(tot / cnt, 4), "launches": cnt} if cnt else None
         # breakdown pass (outside the timed region): every kernel's events
-        n_bd = min(args.steps, 10)
         NAT.call("hgsr_timing_reset")
         NAT.call("hgsr_timing_only", None)
         NAT.call("hgsr_timing_enable", 1)
-        for _ in range(n_bd):
+        for _ in range(min(args.steps, 10)):
             wl.step()
         torch.cuda.synchronize(dev)
         NAT.call("hgsr_timing_enable", 0)
         for k in KERNELS:
             tot, cnt = NAT.kernel_time(k)
             if cnt:
-                kernels[k] = {"avg_ms": round(tot / cnt, 4), "launches": cnt}
-    roof = None
+                res["kernels"][k] = {"avg_ms": round(tot / cnt, 4), "launches": cnt}
+    return res
+
+
+def roofline(args, res):
+    """Dominant-kernel roofline: the raster backward is fp32-VALU bound (no MFMA, no HBM
+    limit), so achieved = algorithmic FLOP / kernel time against the fp32 vector peak.
+    Algorithmic FLOP = gsplat's visit count (every Gaussian up to each tile's latest
+    contributor x 256 pixels, counted on the device over the timed launches) x FLOP per
+    pair; frac_executed prices the lane-pairs the kernel actually stepped
+    (compacted per-quadrant lists x 64 lanes) the same way."""
+    live = res["live"]
+    if not live:
+        return None
+    dom, wl = res["dominant"], res["wl"]
     traffic, traffic_src = pmc_traffic(args)
-    if live and rank == 0:
-        dom = dominant
-        n_isects = isects_after
-        pairs = pairs_timed // args.steps  # mean over exactly the launches the events time
-        avg_s = live["avg_ms"] * 1e-3
-        if dom in FLOP_PER_PAIR:
-            flops = pairs * FLOP_PER_PAIR[dom]
-            ach = flops / avg_s / 1e12
-            roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": traffic.get(dom), "kernel": dom,
-                    "note": (f"fp32 VALU-bound compositing: peak = fp32 vector rate (= f32 MFMA rate); "
-                             f"{pairs} (pixel,Gaussian) pairs visited x {FLOP_PER_PAIR[dom]:.0f} FLOP/pair "
-                             f"(SURVEY 8(d)), counted on the device over the timed launches; {n_isects} "
-                             f"intersections")}
-        else:
-            roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                    "traffic": None, "kernel": dom}
-        # aggregate compulsory-bytes figure of SURVEY 8(d): B_step = 384 N + 132 I + 52 P
-        b_step = 384 * wl.last_colors.shape[0] + 132 * n_isects + 52 * args.width * args.height
-        if roof.get("traffic") is not None:
-            roof["traffic_unit"] = "bytes/launch"
-            roof["traffic_source"] = traffic_src
-        roof["aggregate_hbm_frac"] = round(b_step / (dt / args.steps) / (HBM_PEAK_GBS * 1e9), 4)
-        roof["n_isects"] = n_isects
-        roof["n_isects_before_timed"] = isects_before
-        roof["kernel_avg_ms"] = live["avg_ms"]
-        roof["timing"] = ("HIP events (no system fence) on the kernel's stream, recorded inside the timed region "
-                          "for this kernel only")
+    n_isects = res["isects_after"]
+    pairs = res["pairs_timed"] // args.steps  # mean over exactly the launches the events time
+    epairs = res["exec_pairs_timed"] // args.steps
+    avg_s = live["avg_ms"] * 1e-3
+    fpp = FLOP_PER_PAIR[dom]
+    ach = pairs * fpp / avg_s / 1e12
+    ach_x = epairs * fpp / avg_s / 1e12
+    roof = {"bound": "valu", "achieved": round(ach, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": traffic.get(dom), "kernel": dom,
+            "pairs_per_launch": pairs, "executed_pairs_per_launch": epairs,
+            "achieved_executed": round(ach_x, 3), "frac_executed": round(ach_x / FP32_PEAK_TFLOPS, 4),
+            "note": (f"fp32 VALU-bound compositing (no MFMA, far below the HBM roof): peak = fp32 vector rate; "
+                     f"frac = {pairs} gsplat (pixel, Gaussian) pairs x {fpp:.0f} FLOP/pair (SURVEY 8(d)) / "
+                     f"kernel time; frac_executed = {epairs} lane-pairs actually stepped after the per-quadrant "
+                     f"compaction x the same FLOP/pair; both counted on the device over the timed launches; "
+                     f"{n_isects} intersections; VALU counters in profiles/r02_pmc_valu_mfma.txt")}
+    # aggregate compulsory-bytes figure of SURVEY 8(d): B_step = 384 N + 132 I + 52 P
+    b_step = 384 * wl.last_colors.shape[0] + 132 * n_isects + 52 * args.width * args.height
+    if roof.get("traffic") is not None:
+        roof["traffic_unit"] = "bytes/launch"
+        roof["traffic_source"] = traffic_src
+    roof["aggregate_hbm_frac"] = round(b_step / (res["dt"] / args.steps) / (HBM_PEAK_GBS * 1e9), 4)
+    roof["n_isects"] = n_isects
+    roof["n_isects_before_timed"] = res["isects_before"]
+    roof["kernel_avg_ms"] = live["avg_ms"]
+    roof["timing"] = ("HIP events (no system fence) on the kernel's stream, recorded inside the timed region "
+                      "for this kernel only")
+    return roof
+
+
+def workload_name(args):
+    return (f"c2 {'3DGS' if args.gs == '3d' else '2DGS'} train step: "
+            + (f"SH{args.sh_degree} colours + " if args.sh_degree is not None and not args.anchors else "")
+            + (f"LoD mask + anchor prefilter + fused anchor decode ({args.anchors} anchors) + " if args.anchors
+               else "")
+            + "rasterization fwd + reference loss (L1 + D-SSIM + alpha/scale regs"
+            + (" + normal consistency" if args.gs == "2d" else "") + ") + bwd"
+            + (" + training_statis" if args.anchors else "") + " + Adam step, RGB+ED")
+
+
+def secondary(args, dev):
+    """BASELINE configs[1] (decode-inclusive, 500k anchors) and configs[2] (2DGS) through the
+    same step, measured after the headline workload is freed (N = 1 only)."""
+    out = []
+    for name, kw in (("configs[1] Block_small coarse: 500k anchors, 1080p, 3DGS", dict(anchors=500_000)),
+                     ("configs[2] Block_small fine: 2DGS surfels, depth + normal outputs, 1080p", dict(gs="2d"))):
+        a = argparse.Namespace(**vars(args))
+        a.steps, a.warmup = min(args.steps, 10), min(args.warmup, 3)
+        for k, v in kw.items():
+            setattr(a, k, v)
+        r = measure(a, 0, 1, dev)
+        roof = roofline(a, r)
+        out.append({"config": name, "workload": workload_name(a), "value": round(a.steps / r["dt"], 3),
+                    "unit": "views/s", "ms_per_step": round(r["dt"] / a.steps * 1e3, 3), "steps": a.steps,
+                    "warmup": a.warmup, "gaussians": int(r["wl"].last_colors.shape[0]),
+                    "n_isects": r["isects_after"],
+                    "roofline": None if roof is None else {k: roof[k] for k in (
+                        "bound", "kernel", "achieved", "frac", "frac_executed", "kernel_avg_ms")},
+                    "kernels": r["kernels"]})
+        del r
+        torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    res = measure(args, rank, world, dev)
+    wl, dt = res["wl"], res["dt"]
+    roof = roofline(args, res) if rank == 0 else None
     cpu = None
     if (rank == 0 and world == 1 and not args.no_cpu_baseline and args.gs == "3d" and not args.anchors
             and args.sh_degree is None):
         cpu = cpu_baseline(args, wl)
+    line = None
     if rank == 0:
         ms = dt / args.steps * 1e3
         line = {
@@ -391,19 +497,20 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (seeded c2 scene, SURVEY 8(d); no dataset in the environment)",
-            "config": {"workload": (f"c2 {'3DGS' if args.gs == '3d' else '2DGS'} train step: "
-                                    + (f"SH{args.sh_degree} colours + " if args.sh_degree is not None
-                                       and not args.anchors else "")
-                                    + (f"anchor prefilter + fused anchor decode ({args.anchors} anchors) + " if args.anchors else "")
-                                    + "rasterization fwd + reference loss (L1 + D-SSIM + alpha/scale regs) + bwd"
-                                    + (" + training_statis" if args.anchors else "") + " + Adam step, RGB+ED"),
+            "config": {"workload": workload_name(args),
                        "gaussians": int(wl.last_colors.shape[0]), "width": args.width, "height": args.height,
-                       "parallelism": ("per-chunk, one scene per GPU, no collectives" if args.mode == "chunk"
-                                       else "DDP over views, RCCL all-reduce of Gaussian grads")},
-            "roofline": roof, "cpu_baseline": cpu, "quality": psnr_parity(args), "kernels": kernels,
+                       "parallelism": (f"per-chunk, one scene per GPU, no collectives (x{world})"
+                                       if args.mode == "chunk" else
+                                       f"DDP over views (x{world}), RCCL all-reduce of the gradients from hooks")},
+            "roofline": roof, "cpu_baseline": cpu, "quality": psnr_parity(args), "kernels": res["kernels"],
             "kernels_source": "HIP events of every kernel over a separate pass after the timed region",
-            "hbm_kernels": hbm_kernels(wl, kernels, isects_after) if rank == 0 else None,
+            "hbm_kernels": hbm_kernels(wl, res["kernels"], res["isects_after"]),
         }
+    if rank == 0 and world == 1 and not args.no_secondary and not args.anchors and args.gs == "3d":
+        del res, wl
+        torch.cuda.empty_cache()
+        line["secondary"] = secondary(args, dev)
+    if rank == 0:
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

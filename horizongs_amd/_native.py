@@ -85,6 +85,7 @@ _SIGS = {
     "hgsr_timing_reset": (I, []),
     "hgsr_timing_only": (I, [ct.c_char_p]),
     "hgsr_timing_pairs": (I, [ct.POINTER(ct.c_ulonglong), I]),
+    "hgsr_timing_exec_pairs": (I, [ct.POINTER(ct.c_ulonglong)]),
     "hgsr_timing_query": (I, [ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(I64)]),
 }
 

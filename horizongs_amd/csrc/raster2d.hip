@@ -447,6 +447,7 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     const int slot0 = row == 0 ? 0 : row == 1 ? 1 : row == 2 ? TR::H : TR::H + 1;
     uint8_t* my_list = s_list[wave];
     int prev_bsz = 0;
+    uint32_t stepped = 0;  // compacted list entries this wave stepped (bench roofline only)
     for (int b = 0; b <= nb; ++b) {
         const int cur = b & 1, prv = cur ^ 1;
         const int32_t batch_end = end - 1 - b * NB;
@@ -478,6 +479,7 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
         const uint64_t m = __ballot(rel);
         if (rel) my_list[lanes_below2(m)] = (uint8_t)t;
         const int n_mine = __popcll(m);
+        stepped += (uint32_t)n_mine;
         if (n_mine > 0) {
             const int lst = my_list[lane];
             for (int i = 0; i < n_mine; ++i) {
@@ -538,6 +540,8 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
         prev_bsz = bsz;
         lds_barrier();
     }
+    if (pair_counter && lane == 0 && stepped)  // measurement only: lane-pairs stepped
+        atomicAdd(pair_counter + 1, (unsigned long long)stepped * 64ull);
 }
 
 // Per surfel: fold the accumulated sums into gsplat's gradient tensors (overwrite), in f64.

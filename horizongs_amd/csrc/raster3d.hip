@@ -358,6 +358,7 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     const int slot0 = row == 0 ? 0 : row == 1 ? 1 : row == 2 ? TR::H : TR::H + 1;
     uint8_t* my_list = s_list[wave];
     int prev_bsz = 0;
+    uint32_t stepped = 0;  // compacted list entries this wave stepped (bench roofline only)
     for (int b = 0; b <= nb; ++b) {
         const int cur = b & 1, prv = cur ^ 1;
         const int32_t batch_end = end - 1 - b * NB;
@@ -402,6 +403,7 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
             if (rel) my_list[n_mine + lanes_below(m)] = (uint8_t)t;
             n_mine += __popcll(m);
         }
+        stepped += (uint32_t)n_mine;
         if (n_mine > 0) {
             // the list comes back into registers once per batch; the loop reads
             // entries with readlane so no LDS index read sits on the critical path
@@ -465,6 +467,8 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
         prev_bsz = bsz;
         lds_barrier();
     }
+    if (pair_counter && lane == 0 && stepped)  // measurement only: lane-pairs stepped
+        atomicAdd(pair_counter + 1, (unsigned long long)stepped * 64ull);
 }
 
 // scatter accumulator rows into gsplat's separate gradient tensors (overwrite);

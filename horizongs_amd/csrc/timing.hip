@@ -21,7 +21,9 @@ std::vector<Rec> g_recs;
 size_t g_next = 0;
 constexpr size_t kMaxRecs = 1 << 16;
 std::string g_only;  // record only this kernel (empty = all)
-unsigned long long* g_pairs = nullptr;  // device counter of (pixel, Gaussian) pairs the raster bwd visits
+// device counters of the timed raster bwd: [0] (pixel, Gaussian) pairs visited (gsplat's span),
+// [1] lane-pairs stepped (compacted list entries x 64)
+unsigned long long* g_pairs = nullptr;
 }  // namespace
 
 bool timing_on() { return g_on; }
@@ -48,8 +50,8 @@ unsigned long long* timing_pair_counter(const char* kernel) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_on || (!g_only.empty() && g_only != kernel)) return nullptr;
     if (!g_pairs) {
-        if (hipMalloc(&g_pairs, sizeof(unsigned long long)) != hipSuccess) return nullptr;
-        if (hipMemset(g_pairs, 0, sizeof(unsigned long long)) != hipSuccess) return nullptr;
+        if (hipMalloc(&g_pairs, 2 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+        if (hipMemset(g_pairs, 0, 2 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
     }
     return g_pairs;
 }
@@ -85,7 +87,21 @@ extern "C" int hgsr_timing_pairs(unsigned long long* out, int reset) {
             set_error("timing: pair counter read failed");
             return HGSR_ELAUNCH;
         }
-        if (reset && hipMemset(g_pairs, 0, sizeof(v)) != hipSuccess) return HGSR_ELAUNCH;
+        if (reset && hipMemset(g_pairs, 0, 2 * sizeof(v)) != hipSuccess) return HGSR_ELAUNCH;
+    }
+    if (out) *out = v;
+    return HGSR_OK;
+}
+
+extern "C" int hgsr_timing_exec_pairs(unsigned long long* out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    unsigned long long v = 0;
+    if (g_pairs) {
+        if (hipDeviceSynchronize() != hipSuccess ||
+            hipMemcpy(&v, g_pairs + 1, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) {
+            set_error("timing: pair counter read failed");
+            return HGSR_ELAUNCH;
+        }
     }
     if (out) *out = v;
     return HGSR_OK;

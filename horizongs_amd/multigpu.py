@@ -29,52 +29,155 @@ def chunks_for_rank(chunks: Sequence[str], rank: int, world: int) -> List[str]:
 
 
 class GradientAllReduce:
-    """Bucketed gradient averaging across ranks.
+    """Bucketed gradient averaging across ranks, overlapped with the backward.
 
-    Gradients are packed into flat fp32 buckets of ~`bucket_mb` MiB (few, large
-    collectives: xGMI rings are per-link bound, so fewer calls of larger
-    messages amortise the latency), all-reduced asynchronously, then unpacked.
-    Parameters without a gradient contribute zeros (a Gaussian may be invisible
-    from a rank's view)."""
+    * Buckets (~`bucket_mb` MiB of fp32: few, large collectives -- xGMI rings are per-link
+      bound, so fewer calls of larger messages amortise the latency) are built from the
+      optimizer's CURRENT param_groups and rebuilt whenever the parameter set changes, so
+      densification surgery (cat_tensors_to_optimizer / prune, reference
+      scene/lod_model.py:487-596) that replaces the Parameter objects is picked up.
+    * A post-accumulate-grad hook copies each gradient, pre-scaled by 1 / world, into its
+      bucket slice and makes that slice the parameter's .grad (no copy back after the
+      collective).  A bucket's async all-reduce is launched as soon as all its parameters
+      have a gradient -- i.e. while the backward is still running -- and buckets are always
+      launched in bucket order, so every rank issues the same collectives in the same order.
+    * Each bucket carries one presence slot per parameter: after the reduction a parameter
+      no rank produced a gradient for keeps grad = None (torch.optim.Adam then skips it, as
+      single-GPU training would), while one that some ranks did not reach averages their
+      zeros in (the reference's mean over the views of a batch).
 
-    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, group=None):
-        self.params = [p for p in params if p.requires_grad]
+    Usage per step: ``red.begin()`` before backward, ``loss.backward()``, ``red.finish()``
+    before the optimizer step.  ``red()`` = begin-less synchronous form for grads already
+    computed."""
+
+    def __init__(self, params_or_optimizer, bucket_mb: float = 64.0, group=None):
+        self.source = params_or_optimizer
         self.group = group
-        cap = int(bucket_mb * (1 << 20) // 4)
-        self.buckets: List[List[torch.nn.Parameter]] = []
+        self.cap = max(1, int(bucket_mb * (1 << 20) // 4))
+        self._key = None
+        self._hooks = []
+        self.buckets: List[dict] = []
+
+    # ---------------------------------------------------------------- setup
+    def _params(self) -> List[torch.Tensor]:
+        src = self.source
+        if hasattr(src, "param_groups"):
+            ps = [p for g in src.param_groups for p in g["params"]]
+        else:
+            ps = list(src)
+        return [p for p in ps if p.requires_grad]
+
+    def _active(self) -> bool:
+        return dist.is_initialized() and dist.get_world_size(self.group) > 1
+
+    def _bind(self) -> None:
+        """(Re)build the buckets when the parameter objects changed.  Buckets follow the
+        reverse parameter order, the order a backward usually produces the gradients."""
+        params = self._params()
+        key = tuple(id(p) for p in params) + tuple(p.numel() for p in params)
+        if key == self._key:
+            return
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self.buckets = []
         cur, size = [], 0
-        for p in self.params:
+        for p in reversed(params):
             n = p.numel()
-            if cur and size + n > cap:
+            if cur and size + n > self.cap:
                 self.buckets.append(cur)
                 cur, size = [], 0
             cur.append(p)
             size += n
         if cur:
             self.buckets.append(cur)
+        self.buckets = [self._make_bucket(b) for b in self.buckets]
+        self._where = {}
+        for bi, b in enumerate(self.buckets):
+            for k, p in enumerate(b["params"]):
+                self._where[id(p)] = (bi, k)
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self._key = key
+
+    @staticmethod
+    def _make_bucket(params):
+        offs, o = [], 0
+        for p in params:
+            offs.append(o)
+            o += p.numel()
+        dev = params[0].device
+        # flat = [grads of every parameter | one presence slot per parameter]
+        flat = torch.empty(o + len(params), dtype=torch.float32, device=dev)
+        return {"params": params, "offs": offs, "n": o, "flat": flat, "ready": [False] * len(params),
+                "work": None, "launched": False}
+
+    # ---------------------------------------------------------------- per step
+    def begin(self) -> None:
+        if not self._active():
+            return
+        self._bind()
+        self.world = dist.get_world_size(self.group)
+        self._next = 0
+        for b in self.buckets:
+            b["ready"] = [False] * len(b["params"])
+            b["work"], b["launched"] = None, False
+
+    def _on_grad(self, p) -> None:
+        if not self._active() or p.grad is None:
+            return
+        bi, k = self._where[id(p)]
+        b = self.buckets[bi]
+        if b["launched"]:
+            return
+        n = p.numel()
+        dst = b["flat"][b["offs"][k]:b["offs"][k] + n].view_as(p)
+        torch.mul(p.grad, 1.0 / self.world, out=dst)
+        b["flat"][b["n"] + k] = 1.0
+        p.grad = dst  # the bucket slice is the gradient: no copy back after the collective
+        b["ready"][k] = True
+        self._launch_ready()
+
+    def _launch(self, b) -> None:
+        for k, p in enumerate(b["params"]):  # parameters this rank never reached: zeros, absent
+            if not b["ready"][k]:
+                n = p.numel()
+                b["flat"][b["offs"][k]:b["offs"][k] + n].zero_()
+                b["flat"][b["n"] + k] = 0.0
+        b["work"] = dist.all_reduce(b["flat"], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        b["launched"] = True
+
+    def _launch_ready(self) -> None:
+        while self._next < len(self.buckets) and all(self.buckets[self._next]["ready"]):
+            self._launch(self.buckets[self._next])
+            self._next += 1
+
+    def finish(self) -> None:
+        """Launch what the backward left (in bucket order), wait, set the averaged grads."""
+        if not self._active():
+            return
+        while self._next < len(self.buckets):
+            self._launch(self.buckets[self._next])
+            self._next += 1
+        for b in self.buckets:
+            b["work"].wait()
+            pres = b["flat"][b["n"]:].tolist() if not all(b["ready"]) else None
+            for k, p in enumerate(b["params"]):
+                n = p.numel()
+                if pres is not None and pres[k] == 0.0:
+                    p.grad = None  # no rank produced a gradient
+                elif not b["ready"][k]:
+                    p.grad = b["flat"][b["offs"][k]:b["offs"][k] + n].view_as(p)
 
     def __call__(self) -> None:
-        if not dist.is_initialized() or dist.get_world_size() == 1:
+        """Synchronous form: average gradients that are already in place (no overlap)."""
+        if not self._active():
             return
-        world = dist.get_world_size(self.group)
-        work = []
-        for bucket in self.buckets:
-            flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
-                              for p in bucket])
-            h = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            work.append((h, flat, bucket))
-        for h, flat, bucket in work:
-            h.wait()
-            flat.div_(world)
-            off = 0
-            for p in bucket:
-                n = p.numel()
-                g = flat[off:off + n].view_as(p)
-                if p.grad is None:
-                    p.grad = g.clone()
-                else:
-                    p.grad.copy_(g)
-                off += n
+        self.begin()
+        for b in self.buckets:
+            for p in b["params"]:
+                if p.grad is not None:
+                    self._on_grad(p)
+        self.finish()
 
 
 MAX_FIELDS = ("max_radii2D",)

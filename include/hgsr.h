@@ -11,7 +11,10 @@
  *   - every pointer is a DEVICE pointer to row-major contiguous memory, allocated
  *     by the caller (the library never allocates); fp32 data, int32 ids/radii,
  *     int64 intersection keys;
- *   - gradient outputs are zero-initialised by the caller and ACCUMULATED into;
+ *   - gradient outputs are OVERWRITTEN unless the entry's comment says otherwise
+ *     (the raster / projection / SH-coefficient backwards write every element; v_dirs of
+ *     hgsr_sh_bwd and the decode backward's input / weight gradients accumulate (+=) into
+ *     caller-zeroed buffers, as noted at each entry);
  *   - work is enqueued on `stream` (a hipStream_t; NULL = default stream) and the
  *     call returns without synchronising;
  *   - return 0 (HGSR_OK) or a negative status; hgsr_last_error() then holds a
@@ -467,6 +470,10 @@ int hgsr_timing_only(const char* kernel);
  * latest contributor x 256 pixels), counted on the device while raster3d_bwd / raster2d_bwd
  * is being timed; synchronises the device; reset = 1 zeroes the counter. */
 int hgsr_timing_pairs(unsigned long long* out, int reset);
+/* lane-pairs the timed raster backward actually stepped: every entry of each wave's
+ * compacted per-batch list (Gaussians whose footprint reaches the wave's 8x8 quadrant)
+ * x 64 lanes, counted with the pairs above (read before a resetting hgsr_timing_pairs). */
+int hgsr_timing_exec_pairs(unsigned long long* out);
 /* total milliseconds and launch count recorded for `kernel` (synchronises the
  * recorded events); kernel names: project3d_fwd, project3d_bwd, project2d_fwd,
  * project2d_bwd, sh_fwd, sh_bwd, isect_count, isect_emit, tile_sort,

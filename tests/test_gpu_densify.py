@@ -138,14 +138,17 @@ class _LoDShim:
 
 
 def test_anchor_growing_matches_reference():
-    """End to end against the reference's own anchor_growing (fine stage, weed-out on):
-    the same new anchors in the same order, with the same scatter-max features."""
+    """End to end against the reference's own anchor_growing (fine stage, weed-out on, golden
+    from scripts/make_golden.py): the same new anchors in the same order, with the same
+    scatter-max features, with the duplicate removal / weed-out / scatter-max on the GPU."""
     from horizongs_amd import densify as HD
     g = np.load(os.path.join(GOLD, "anchor_growing.npz"))
     m = _LoDShim(g)
     opt = SimpleNamespace(update_ratio=0.5, densify_grad_threshold=0.0002, extra_ratio=0.25, extra_up=0.01,
                           overlap=False)
-    HD.anchor_growing(m, torch.from_numpy(g["grads"]).to(DEV), opt, torch.from_numpy(g["offset_mask"]).to(DEV), 1000)
+    # the reference's control flow (oracle restatement) on the HIP primitives, as densify.bind wires
+    # them into the reference's own GaussianLoDModel.anchor_growing
+    Dn.anchor_growing(m, torch.from_numpy(g["grads"]).to(DEV), opt, torch.from_numpy(g["offset_mask"]).to(DEV), HD)
     for n in ("_anchor", "_offset", "_anchor_feat", "_scaling", "_rotation", "_level", "_extra_level",
               "anchor_demon", "anchor_opacity_accum"):
         got = getattr(m, n).cpu().numpy()

@@ -68,3 +68,115 @@ def test_chunks_dealt_once():
         dealt = [c for r in range(world) for c in chunks_for_rank(chunks, r, world)]
         assert sorted(dealt) == sorted(chunks)
     assert chunks_for_rank(chunks, 3, 8) == ["1_1"]
+
+
+# ---------------------------------------------------------------------------------------
+# DDP over views: 2 ranks x 1 view == 1 rank x 2 views (averaged), across densification
+# ---------------------------------------------------------------------------------------
+def _make_params():
+    g = torch.Generator().manual_seed(0)
+    a = torch.nn.Parameter(torch.randn(300, 3, generator=g))   # every view
+    b = torch.nn.Parameter(torch.randn(50, generator=g))        # every view
+    c = torch.nn.Parameter(torch.randn(7, 2, generator=g))      # view 0 only
+    d = torch.nn.Parameter(torch.randn(5, generator=g))         # no view: grad stays None
+    return [a, b, c, d]
+
+
+def _view_loss(params, view):
+    """CPU stand-in for render + loss of one camera view (reference train.py:150-206)."""
+    a, b, c, _ = params
+    w = torch.linspace(0.5, 1.5, a.numel()).reshape(a.shape) * (view + 1)
+    loss = (torch.sin(a * w) ** 2).sum() + ((b * (view + 1)) ** 2).sum()
+    if view == 0:
+        loss = loss + (c ** 3).sum()
+    return loss
+
+
+def _optimizer(params):
+    return torch.optim.Adam([{"params": [p], "lr": 0.01, "name": str(i)} for i, p in enumerate(params)], eps=1e-15)
+
+
+def _grow(opt, params):
+    """cat_tensors_to_optimizer (reference scene/basic_model.py): every group's Parameter is
+    replaced by a longer one with zero-extended Adam state -- the reducer must follow."""
+    new = []
+    for gidx, (group, p) in enumerate(zip(opt.param_groups, params)):
+        ext = torch.full((2,) + tuple(p.shape[1:]), 0.25 * (gidx + 1))
+        q = torch.nn.Parameter(torch.cat([p.detach(), ext], 0))
+        st = opt.state.pop(p, None)
+        if st:
+            st["exp_avg"] = torch.cat([st["exp_avg"], torch.zeros_like(ext)], 0)
+            st["exp_avg_sq"] = torch.cat([st["exp_avg_sq"], torch.zeros_like(ext)], 0)
+            opt.state[q] = st
+        group["params"][0] = q
+        new.append(q)
+    return new
+
+
+def _train(n_steps, views_per_step, reduce_fn=None, reducer=None):
+    params = _make_params()
+    opt = _optimizer(params)
+    grads = []
+    for step in range(n_steps):
+        if step == 1:
+            params = _grow(opt, params)
+        opt.zero_grad(set_to_none=True)
+        if reducer is not None:
+            reducer.begin()
+        loss = sum(_view_loss(params, v) for v in views_per_step) / len(views_per_step)
+        loss.backward()
+        if reducer is not None:
+            reducer.finish()
+        grads.append([None if p.grad is None else p.grad.clone() for p in params])
+        opt.step()
+    return grads, [p.detach().clone() for p in params]
+
+
+def _ddp_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        params = _make_params()
+        opt = _optimizer(params)
+        red = GradientAllReduce(opt, bucket_mb=0.0012)  # ~300 floats: several buckets
+        grads = []
+        for step in range(3):
+            if step == 1:
+                params = _grow(opt, params)
+            opt.zero_grad(set_to_none=True)
+            red.begin()
+            _view_loss(params, rank).backward()  # one view per rank, gradients averaged by the hooks
+            red.finish()
+            grads.append([None if p.grad is None else p.grad.clone() for p in params])
+            opt.step()
+        npy = lambda t: None if t is None else t.detach().numpy().copy()  # noqa: E731
+        q.put((rank, [[npy(g) for g in gs] for gs in grads], [npy(p) for p in params], len(red.buckets)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_two_ranks_match_one_rank_two_views():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref_grads, ref_params = _train(3, [0, 1])
+    for rank, grads, params, n_buckets in res:
+        assert n_buckets >= 2
+        for step, (gs, rs) in enumerate(zip(grads, ref_grads)):
+            for k, (g, r) in enumerate(zip(gs, rs)):
+                if r is None:
+                    assert g is None, (rank, step, k)  # no rank produced one: stays None (Adam skips it)
+                else:
+                    torch.testing.assert_close(torch.from_numpy(g), r, rtol=1e-6, atol=1e-7,
+                                               msg=f"rank {rank} step {step} p{k}")
+        for p, r in zip(params, ref_params):
+            torch.testing.assert_close(torch.from_numpy(p), r, rtol=1e-6, atol=1e-7)
