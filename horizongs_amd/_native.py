@@ -81,6 +81,10 @@ _SIGS = {
     "hgsr_depth_normal_bwd": (I, [I, I, I, P, P, P, P, I, I, P, P, P]),
     "hgsr_rotate3": (I, [I, I64, P, I, I, I, P, P, P]),
     "hgsr_adam_step": (I, [I, P, ct.c_double, ct.c_double, ct.c_double, P]),
+    "hgsr_explicit_ws_bytes": (SZ, [I64]),
+    "hgsr_explicit_count": (I, [I64, P, P, P, P, F, F, F, I, P, P, P, SZ, P, P]),
+    "hgsr_explicit_gather": (I, [I64, I, P, P, P, P, P, P, P, P, SZ, P, P, P, P, P, P, P]),
+    "hgsr_explicit_scatter": (I, [I64, I, P, P, SZ, P, P, P, P, P, P, P, P, P, P, P, P]),
     "hgsr_timing_enable": (I, [I]),
     "hgsr_timing_reset": (I, []),
     "hgsr_timing_only": (I, [ct.c_char_p]),

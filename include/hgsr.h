@@ -455,6 +455,33 @@ typedef struct {
 int hgsr_adam_step(int n_tensors, const hgsr_adam_tensor* tensors, double beta1, double beta2, double eps,
                    hgsr_stream_t stream);
 
+/* ---- explicit (merged-scene) Gaussians: the c5 render path -------------------
+ * Reference render() with pc.explicit_gs (gaussian_renderer/render.py:22-25):
+ * set_gs_mask (scene/lod_model.py:292-296) + generate_explicit_gaussians
+ * (scene/basic_model.py:373-383) as one ordered stream compaction.
+ * hgsr_explicit_count: with visible == NULL, the LoD mask of the N centres (same test as
+ * hgsr_lod_mask) is written to mask[N] (bytes); otherwise `visible` [N] bytes is used as the
+ * mask.  Writes the kept count to *total (device int64) and the block bases to ws
+ * (hgsr_explicit_ws_bytes(N)), which hgsr_explicit_gather / _scatter read. */
+size_t hgsr_explicit_ws_bytes(int64_t N);
+int hgsr_explicit_count(int64_t N, const float* xyz, const int32_t* level, const float* extra_level,
+                        const float* cam_center, float res_scale, float standard_dist, float log2_fork,
+                        int max_level, const uint8_t* visible, uint8_t* mask, void* ws, size_t ws_bytes,
+                        int64_t* total, hgsr_stream_t stream);
+/* kept rows in source order: out_xyz [M,3], out_color [M,K,3] = cat(f_dc [N,1,3],
+ * f_rest [N,K-1,3]) rows, out_opacity [M,1], out_scaling [M,3], out_rotation [M,4],
+ * out_index [M] (source row).  M = the count of hgsr_explicit_count. */
+int hgsr_explicit_gather(int64_t N, int K, const uint8_t* mask, const float* xyz, const float* f_dc,
+                         const float* f_rest, const float* opacity, const float* scaling, const float* rotation,
+                         const void* ws, size_t ws_bytes, float* out_xyz, float* out_color, float* out_opacity,
+                         float* out_scaling, float* out_rotation, int32_t* out_index, hgsr_stream_t stream);
+/* vjp of the gather: every source row's gradient (OVERWRITTEN) is its output row's gradient,
+ * or 0 where the mask dropped it; any g_* / v_* may be NULL (g NULL = zero). */
+int hgsr_explicit_scatter(int64_t N, int K, const uint8_t* mask, const void* ws, size_t ws_bytes,
+                          const float* g_xyz, const float* g_color, const float* g_opacity, const float* g_scaling,
+                          const float* g_rotation, float* v_xyz, float* v_f_dc, float* v_f_rest, float* v_opacity,
+                          float* v_scaling, float* v_rotation, hgsr_stream_t stream);
+
 /* ---- measurement ----------------------------------------------------------
  * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):
  * when enabled, the main kernel of every entry point is bracketed by
