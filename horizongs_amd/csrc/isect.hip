@@ -19,6 +19,8 @@
 // Keys inside a bin are unique ((depth, id) pairs), so ANY correct sort yields
 // exactly the order of gsplat's stable radix sort: depth ascending, ties in
 // Gaussian-major emission order.  Integer outputs are bit-identical.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace hgsr {
@@ -241,7 +243,8 @@ __global__ __launch_bounds__(256) void isect_emit_lds_kernel(
     int64_t CN, int N, int per_block, const float2* __restrict__ means2d,
     const int32_t* __restrict__ radii, const float* __restrict__ depths, int tile_size, int tw,
     int th, int n_tiles, int n_bins, const int32_t* __restrict__ offsets,
-    const int32_t* __restrict__ blockhist, const int32_t* __restrict__ chunk_pre, uint64_t* __restrict__ keys) {
+    const int32_t* __restrict__ blockhist, const int32_t* __restrict__ chunk_pre, uint64_t* __restrict__ keys,
+    int phases) {
     extern __shared__ __attribute__((aligned(16))) int s_cur[];
     // Logical block = XCD-contiguous remap of the dispatch index: the blocks resident on one
     // XCD hold consecutive slices of every bin, so their scattered 8-B key writes to a bin
@@ -264,20 +267,36 @@ __global__ __launch_bounds__(256) void isect_emit_lds_kernel(
             m[k] = o < g1 ? means2d[o] : make_float2(0.f, 0.f);
             d[k] = o < g1 ? depths[o] : 0.f;
         }
+        // Phases over bands of tile rows: every block of an XCD emits into the same band at
+        // the same time, so the partially written key lines the XCD's L2 must hold until
+        // their 16 keys (from 16 neighbouring blocks) arrive are 1 / phases of all bins --
+        // they merge in L2 instead of leaving as partial-line writes.
+        // rectangles once (an empty one for culled / out-of-range Gaussians), clipped per phase
+        int rx0[kIsectBatch], ry0[kIsectBatch], rx1[kIsectBatch], ry1[kIsectBatch];
 #pragma unroll
         for (int k = 0; k < kIsectBatch; ++k) {
             const int64_t o = ob + 256 * k;
-            if (o >= g1) break;
-            if (r[k] <= 0) continue;
-            int x0, y0, x1, y1;
-            tile_rect(m[k].x, m[k].y, r[k], tile_size, tw, th, x0, y0, x1, y1);
-            const uint64_t key = ((uint64_t)__float_as_uint(d[k]) << 32) | (uint32_t)o;
-            const int base = (int)(o / N) * n_tiles;
-            for (int y = y0; y < y1; ++y)
-                for (int x = x0; x < x1; ++x) {
-                    const int pos = atomicAdd(&s_cur[base + y * tw + x], 1);
-                    keys[pos] = key;
-                }
+            if (o < g1 && r[k] > 0) {
+                tile_rect(m[k].x, m[k].y, r[k], tile_size, tw, th, rx0[k], ry0[k], rx1[k], ry1[k]);
+            } else {
+                rx0[k] = ry0[k] = rx1[k] = ry1[k] = 0;
+            }
+        }
+        for (int ph = 0; ph < phases; ++ph) {
+            const int ylo = (int)((int64_t)ph * th / phases), yhi = (int)((int64_t)(ph + 1) * th / phases);
+#pragma unroll
+            for (int k = 0; k < kIsectBatch; ++k) {
+                const int y0 = max(ry0[k], ylo), y1 = min(ry1[k], yhi);
+                if (y0 >= y1) continue;
+                const int64_t o = ob + 256 * k;
+                const uint64_t key = ((uint64_t)__float_as_uint(d[k]) << 32) | (uint32_t)o;
+                const int base = (int)(o / N) * n_tiles;
+                for (int y = y0; y < y1; ++y)
+                    for (int x = rx0[k]; x < rx1[k]; ++x) {
+                        const int pos = atomicAdd(&s_cur[base + y * tw + x], 1);
+                        keys[pos] = key;
+                    }
+            }
         }
     }
 }
@@ -669,6 +688,15 @@ extern "C" int hgsr_isect_count(int C, int N, const float* means2d, const int32_
     return check_launch("isect_binscan");
 }
 
+static int emit_phases(int tile_h) {
+    static const int env = [] {
+        const char* e = getenv("HGSR_EMIT_PHASES");
+        return e ? atoi(e) : 0;
+    }();
+    int p = env > 0 ? env : 4;
+    return p < tile_h ? p : (tile_h > 0 ? tile_h : 1);
+}
+
 extern "C" int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const int32_t* radii,
                                       const float* depths, int tile_size, int tile_w, int tile_h,
                                       const int32_t* isect_offsets, int64_t n_isects, int64_t max_bin,
@@ -689,7 +717,8 @@ extern "C" int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const 
         KernelTimer kt("isect_emit", s);
         hipLaunchKernelGGL(isect_emit_lds_kernel, dim3(g.n_blocks), dim3(256), g.n_bins * 4, s, g.CN, N,
                            g.per_block, reinterpret_cast<const float2*>(means2d), radii, depths, tile_size,
-                           tile_w, tile_h, g.n_tiles, g.n_bins, isect_offsets, w.blockhist, w.chunk_pre, keys);
+                           tile_w, tile_h, g.n_tiles, g.n_bins, isect_offsets, w.blockhist, w.chunk_pre, keys,
+                           emit_phases(tile_h));
     } else {
         hipLaunchKernelGGL(copy_i32_kernel, dim3((g.n_bins + 255) / 256), dim3(256), 0, s, g.n_bins,
                            isect_offsets, w.cursor);
