@@ -81,7 +81,8 @@ HBM_PEAK_GBS = 8000.0      # HBM3E spec
 FLOP_PER_PAIR = {"raster3d_fwd": 20.0, "raster3d_bwd": 60.0, "raster2d_fwd": 40.0, "raster2d_bwd": 120.0}
 KERNELS = ["project3d_fwd", "isect_count", "isect_emit", "tile_sort", "raster3d_fwd", "raster3d_bwd",
            "project3d_bwd", "project2d_fwd", "raster2d_fwd", "raster2d_bwd", "project2d_bwd", "sh_fwd", "sh_bwd",
-           "decode_count", "decode_fwd", "decode_bwd", "loss_fwd", "loss_bwd", "adam", "training_statis", "depth_normal_fwd", "depth_normal_bwd"]
+           "decode_count", "decode_fwd", "decode_bwd", "loss_fwd", "loss_bwd", "adam", "training_statis", "depth_normal_fwd",
+           "depth_normal_bwd", "anchor_prefilter", "explicit_gather"]
 
 
 def parse():
@@ -159,6 +160,10 @@ class Workload:
             p for m in self.mlps for p in m.parameters()]
         self.anchor_quats = torch.zeros(A, 4, device=dev)
         self.anchor_quats[:, 0] = 1.0  # get_rotation at init (_rotation is not trained)
+        # LoD inputs of set_anchor_mask (every synthetic anchor on level 0: the test runs, all pass)
+        self.lod = dict(level=torch.zeros(A, dtype=torch.int32, device=dev),
+                        extra_level=torch.zeros(A, device=dev), cam_center=self.cam_center, res_scale=1.0,
+                        standard_dist=4.0, fork=2, street_levels=4)
         # densification statistics updated every step by training_statis (train.py:258-262)
         k = 10
         self.stats = dict(anchor_opacity_accum=torch.zeros(A, 1, device=dev), anchor_demon=torch.zeros(A, 1, device=dev),
@@ -176,15 +181,14 @@ class Workload:
             p.grad = None
         W, H = self.args.width, self.args.height
         if self.args.anchors:
-            # prefilter_voxel (gaussian_renderer/render.py:120-197): project the anchors with their
-            # offset scale, keep radii > 0
+            # set_anchor_mask + prefilter_voxel (scene/lod_model.py:286-290, gaussian_renderer/render.py
+            # :120-197) fused: LoD test AND radius > 0 of the anchors projected with their first three
+            # scales, compacted on the device into the visible-anchor index the decode consumes
             with torch.no_grad():
-                radii_a = G.fully_fused_projection(self.anchor.detach(), None, self.anchor_quats,
-                                                   torch.exp(self.scaling_raw.detach()[:, :3]), self.viewmats, self.Ks,
-                                                   W, H, eps2d=0.3, packed=False)[0]
-                visible = radii_a[0] > 0
+                visible, vis_idx = HD.prefilter(self.anchor.detach(), torch.exp(self.scaling_raw.detach()),
+                                                self.anchor_quats, self.viewmats[0], self.Ks[0], W, H, lod=self.lod)
             xyz, _, cols, opac, scales, quats, sel = HD.decode(self.anchor, self.feat, self.offset, self.scaling_raw,
-                                                               self.cam_center, self.mlps, visible, 3, 10, 3)
+                                                               self.cam_center, self.mlps, vis_idx, 3, 10, 3)
             opac = opac.reshape(-1)
         else:
             xyz, quats, cols = self.means, self.quats, self.colors

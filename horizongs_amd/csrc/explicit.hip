@@ -233,6 +233,17 @@ __global__ __launch_bounds__(256) void explicit_scatter_kernel(int64_t N, int K,
     }
 }
 
+// kept indices of a mask, in order (the compaction of explicit_gather without the rows)
+__global__ __launch_bounds__(256) void mask_index_kernel(int64_t N, const uint8_t* __restrict__ mask,
+                                                         const int64_t* __restrict__ block_base,
+                                                         int32_t* __restrict__ index) {
+    __shared__ int32_t s_rows[kExBlock];
+    const int64_t b0 = (int64_t)blockIdx.x * kExBlock;
+    const int n = ex_block_rows(N, mask, b0, s_rows);
+    const int64_t o0 = block_base[blockIdx.x];
+    for (int e = threadIdx.x; e < n; e += 256) index[o0 + e] = (int32_t)(b0 + s_rows[e]);
+}
+
 }  // namespace hgsr
 
 using namespace hgsr;
@@ -301,4 +312,16 @@ extern "C" int hgsr_explicit_scatter(int64_t N, int K, const uint8_t* mask, cons
     hipLaunchKernelGGL(explicit_scatter_kernel, dim3((unsigned)nb), dim3(256), 0, as_stream(stream), N, K, mask,
                        base, g, v);
     return check_launch("explicit_scatter");
+}
+
+extern "C" int hgsr_mask_index(int64_t N, const uint8_t* mask, const void* ws, size_t ws_bytes, int32_t* index,
+                               hgsr_stream_t stream) {
+    HGSR_REQUIRE(N >= 0, "bad dims");
+    HGSR_REQUIRE(ws_bytes >= hgsr_explicit_ws_bytes(N), "mask_index: workspace too small");
+    if (N == 0) return HGSR_OK;
+    HGSR_REQUIRE(mask && ws && index, "null pointer");
+    const int64_t nb = ex_blocks(N);
+    const int64_t* base = (const int64_t*)((const char*)ws + (nb * (int64_t)sizeof(int32_t) + 255) / 256 * 256);
+    hipLaunchKernelGGL(mask_index_kernel, dim3((unsigned)nb), dim3(256), 0, as_stream(stream), N, mask, base, index);
+    return check_launch("mask_index");
 }

@@ -134,27 +134,23 @@ __device__ __forceinline__ Mat3 covar_from_qs(float4 q, float3 s, Mat3& Rq) {
 }
 
 // ---------------------------------------------------------------- 3DGS fwd
-__global__ __launch_bounds__(256) void project3d_fwd_kernel(
-    int N, const float* __restrict__ means, const float4* __restrict__ quats,
-    const float* __restrict__ scales, const float* __restrict__ viewmats,
-    const float* __restrict__ Ks, int W, int H, float eps2d, float near_plane, float far_plane,
-    float radius_clip, int32_t* __restrict__ radii, float2* __restrict__ means2d,
-    float* __restrict__ depths, float* __restrict__ conics) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    const int c = blockIdx.y;
-    if (g >= N) return;
-    const int64_t o = (int64_t)c * N + g;
-    const View v = load_view(viewmats + c * 16, Ks + c * 9);
-    const Lims L = make_lims(v, W, H);
-    const float m[3] = {means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2]};
+struct Proj3 {
+    int32_t rad;
+    float2 m2;
+    float dep, ca, cb, cc;
+};
+
+// gsplat fully_fused_projection (pinhole, non-packed) of one Gaussian; shared by the
+// projection and the anchor prefilter so both decide radius > 0 with the same bits
+__device__ __forceinline__ Proj3 project3d_one(const View& v, const Lims& L, const float m[3], float4 q, float3 s,
+                                               int W, int H, float eps2d, float near_plane, float far_plane,
+                                               float radius_clip) {
+    Proj3 r{0, make_float2(0.f, 0.f), 0.f, 0.f, 0.f, 0.f};
     float mc[3];
     to_camera(v, m, mc);
-    int32_t rad = 0;
-    float2 m2 = make_float2(0.f, 0.f);
-    float dep = 0.f, ca = 0.f, cb = 0.f, cc = 0.f;
     if (!(mc[2] < near_plane || mc[2] > far_plane)) {
         Mat3 Rq;
-        const Mat3 cov = covar_from_qs(quats[g], ld3(scales + (int64_t)g * 3), Rq);
+        const Mat3 cov = covar_from_qs(q, s, Rq);
         const Mat3 covc = mm3_bt(mm3(v.R, cov), v.R);
         const float x = mc[0], y = mc[1], z = mc[2];
         const float rz = 1.0f / z;
@@ -184,21 +180,72 @@ __global__ __launch_bounds__(256) void project3d_fwd_kernel(
             const float radius = ceilf(3.0f * sqrtf(v1));
             if (radius > radius_clip && !(mx + radius <= 0.f || mx - radius >= (float)W ||
                                           my + radius <= 0.f || my - radius >= (float)H)) {
-                rad = (int32_t)radius;
-                m2 = make_float2(mx, my);
-                dep = z;
-                ca = c2[1][1] * idet;
-                cb = -c2[0][1] * idet;
-                cc = c2[0][0] * idet;
+                r.rad = (int32_t)radius;
+                r.m2 = make_float2(mx, my);
+                r.dep = z;
+                r.ca = c2[1][1] * idet;
+                r.cb = -c2[0][1] * idet;
+                r.cc = c2[0][0] * idet;
             }
         }
     }
-    radii[o] = rad;
-    means2d[o] = m2;
-    depths[o] = dep;
-    conics[o * 3 + 0] = ca;
-    conics[o * 3 + 1] = cb;
-    conics[o * 3 + 2] = cc;
+    return r;
+}
+
+__global__ __launch_bounds__(256) void project3d_fwd_kernel(
+    int N, const float* __restrict__ means, const float4* __restrict__ quats,
+    const float* __restrict__ scales, const float* __restrict__ viewmats,
+    const float* __restrict__ Ks, int W, int H, float eps2d, float near_plane, float far_plane,
+    float radius_clip, int32_t* __restrict__ radii, float2* __restrict__ means2d,
+    float* __restrict__ depths, float* __restrict__ conics) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y;
+    if (g >= N) return;
+    const int64_t o = (int64_t)c * N + g;
+    const View v = load_view(viewmats + c * 16, Ks + c * 9);
+    const Lims L = make_lims(v, W, H);
+    const float m[3] = {means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2]};
+    const Proj3 r = project3d_one(v, L, m, quats[g], ld3(scales + (int64_t)g * 3), W, H, eps2d, near_plane,
+                                  far_plane, radius_clip);
+    radii[o] = r.rad;
+    means2d[o] = r.m2;
+    depths[o] = r.dep;
+    conics[o * 3 + 0] = r.ca;
+    conics[o * 3 + 1] = r.cb;
+    conics[o * 3 + 2] = r.cc;
+}
+
+// Anchor prefilter (reference gaussian_renderer/render.py:120-197 prefilter_voxel after
+// set_anchor_mask, scene/lod_model.py:286-290): visible[a] = LoD level test (when `level`
+// is given; the test of hgsr_lod_mask) AND radius > 0 of the anchor projected with its
+// first three scales (gsplat projection, camera 0).  One byte per anchor; no projection
+// outputs are written (the reference keeps only radii > 0).
+__global__ __launch_bounds__(256) void anchor_prefilter_kernel(
+    int A, const float* __restrict__ anchor, const float4* __restrict__ quats, const float* __restrict__ scales,
+    int scale_stride, const float* __restrict__ viewmat, const float* __restrict__ K, int W, int H, float eps2d,
+    float near_plane, float far_plane, const int32_t* __restrict__ level, const float* __restrict__ extra_level,
+    const float* __restrict__ cam, float res_scale, float standard_dist, float log2_fork, int max_level,
+    uint8_t* __restrict__ visible) {
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    if (a >= A) return;
+    const float m[3] = {anchor[(int64_t)a * 3], anchor[(int64_t)a * 3 + 1], anchor[(int64_t)a * 3 + 2]};
+    bool vis = true;
+    if (level) {
+        const float dx = m[0] - cam[0], dy = m[1] - cam[1], dz = m[2] - cam[2];
+        const float dist = sqrtf(dx * dx + dy * dy + dz * dz) * res_scale;
+        const float pred = log2f(standard_dist / dist) / log2_fork + extra_level[a];
+        const float fl = floorf(pred);
+        const int il = fl <= 0.f ? 0 : (fl >= (float)max_level ? max_level : (int)fl);
+        vis = level[a] <= il;
+    }
+    if (vis) {
+        const View v = load_view(viewmat, K);
+        const Lims L = make_lims(v, W, H);
+        const Proj3 r = project3d_one(v, L, m, quats[a], ld3(scales + (int64_t)a * scale_stride), W, H, eps2d,
+                                      near_plane, far_plane, 0.0f);
+        vis = r.rad > 0;
+    }
+    visible[a] = vis ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- 3DGS bwd
@@ -582,4 +629,22 @@ extern "C" int hgsr_project2d_bwd(int C, int N, const float* means, const float*
                        ray_transforms, reinterpret_cast<const float2*>(v_means2d), v_depths,
                        v_ray_transforms, v_normals, v_means, reinterpret_cast<float4*>(v_quats), v_scales);
     return check_launch("project2d_bwd");
+}
+
+extern "C" int hgsr_anchor_prefilter(int A, const float* anchor, const float* quats, const float* scales,
+                                     int scale_stride, const float* viewmat, const float* K, int width, int height,
+                                     float eps2d, float near_plane, float far_plane, const int32_t* level,
+                                     const float* extra_level, const float* cam_center, float res_scale,
+                                     float standard_dist, float log2_fork, int max_level, uint8_t* visible,
+                                     hgsr_stream_t stream) {
+    HGSR_REQUIRE(A >= 0 && width > 0 && height > 0 && scale_stride >= 3, "bad dims");
+    if (A == 0) return HGSR_OK;
+    HGSR_REQUIRE(anchor && quats && scales && viewmat && K && visible, "null pointer");
+    HGSR_REQUIRE(!level || (extra_level && cam_center && max_level >= 0), "LoD inputs incomplete");
+    KernelTimer kt("anchor_prefilter", as_stream(stream));
+    hipLaunchKernelGGL(anchor_prefilter_kernel, dim3((A + 255) / 256), dim3(256), 0, as_stream(stream), A, anchor,
+                       reinterpret_cast<const float4*>(quats), scales, scale_stride, viewmat, K, width, height, eps2d,
+                       near_plane, far_plane, level, extra_level, cam_center, res_scale, standard_dist, log2_fork,
+                       max_level, visible);
+    return check_launch("anchor_prefilter");
 }

@@ -5,6 +5,9 @@ anchors to the fused HIP kernels instead of the ~10 torch launches of
 `generate_neural_gaussians`:
 
 * `lod_mask`       <- scene/lod_model.py:286-290 set_anchor_mask (dist2level 'floor')
+* `prefilter`      <- set_anchor_mask + gaussian_renderer/render.py:120-197 prefilter_voxel fused:
+                      one kernel (LoD test AND gsplat radius > 0) + an ordered compaction to the
+                      visible-anchor index the decode consumes (`prefilter_voxel` is the drop-in)
 * `decode`         <- scene/basic_model.py:297-371 generate_neural_gaussians on the
                       visible anchors, MLPs of scene/lod_model.py:67-84
 * `generate_neural_gaussians(model, camera, visible_mask)` takes the reference model
@@ -54,6 +57,68 @@ def lod_mask(anchor, level, extra_level, cam_center, res_scale, standard_dist, f
            float(standard_dist), float(math.log2(fork)), int(street_levels) - 1, ptr(mask),
            N.stream(anchor.device))
     return mask.bool()
+
+
+@torch.no_grad()
+def prefilter(anchor, scales, quats, viewmat, K, width, height, lod=None, eps2d=0.3, near_plane=0.01,
+              far_plane=1e10):
+    """Fused set_anchor_mask + prefilter_voxel (scene/lod_model.py:286-290,
+    gaussian_renderer/render.py:120-197): visible[a] = LoD test (lod = dict(level, extra_level,
+    cam_center, res_scale, standard_dist, fork, street_levels), or None for all anchors) AND
+    gsplat radius > 0 of the anchor projected with `scales` (activated, [A,3] or [A,6] of which
+    the first three are used) and `quats`.  One kernel for the mask, then an ordered
+    compaction: returns (visible bool [A], vis_idx int32 [Av]); one host read (Av)."""
+    _check_dev(anchor, scales, quats, viewmat, K)
+    A = anchor.shape[0]
+    dev = anchor.device
+    vis = torch.empty(A, dtype=torch.uint8, device=dev)
+    sc = scales if scales.dtype == torch.float32 and scales.stride(-1) == 1 and scales.stride(0) >= 3 else \
+        scales.float().contiguous()
+    stride = sc.stride(0)
+    s = N.stream(dev)
+    args = [None, None, None, 1.0, 1.0, 1.0, 0]
+    keep = []
+    if lod is not None:
+        lv = lod["level"].reshape(-1).to(torch.int32).contiguous()
+        el = _f32(lod["extra_level"].reshape(-1))
+        cc = _f32(lod["cam_center"].reshape(3))
+        keep = [lv, el, cc]
+        args = [ptr(lv), ptr(el), ptr(cc), float(lod.get("res_scale", 1.0)), float(lod["standard_dist"]),
+                float(math.log2(lod["fork"])), int(lod["street_levels"]) - 1]
+    N.call("hgsr_anchor_prefilter", A, ptr(_f32(anchor)), ptr(_f32(quats)), sc.data_ptr(), stride,
+           ptr(_f32(viewmat.reshape(4, 4))), ptr(_f32(K.reshape(3, 3))), int(width), int(height), float(eps2d),
+           float(near_plane), float(far_plane), *args, ptr(vis), s)
+    ws_b = N.size_query("hgsr_explicit_ws_bytes", A)
+    ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+    total = torch.empty(1, dtype=torch.int64, device=dev)
+    N.call("hgsr_explicit_count", A, None, None, None, None, 1.0, 1.0, 1.0, 0, ptr(vis), None, ptr(ws), ws_b,
+           ptr(total), s)
+    Av = int(total.item())  # the one host read (the reference's boolean mask indexing syncs too)
+    vis_idx = torch.empty(Av, dtype=torch.int32, device=dev)
+    if Av:
+        N.call("hgsr_mask_index", A, ptr(vis), ptr(ws), ws_b, ptr(vis_idx), s)
+    del keep
+    visible = vis.view(torch.bool)
+    _VIS_CACHE[:] = [(visible, visible._version, vis_idx)]
+    return visible, vis_idx
+
+
+def prefilter_voxel(viewpoint_camera, pc):
+    """Drop-in for reference prefilter_voxel (gaussian_renderer/render.py:120-197) for the 3DGS
+    branch, with set_anchor_mask fused in (pc._anchor_mask is set as the reference does)."""
+    if getattr(pc, "gs_attr", "3D") != "3D":
+        raise NotImplementedError("hgsr prefilter: 3DGS branch only (2DGS uses fully_fused_projection_2dgs)")
+    K = torch.tensor([[viewpoint_camera.fx, 0, viewpoint_camera.cx], [0, viewpoint_camera.fy, viewpoint_camera.cy],
+                      [0, 0, 1]], dtype=torch.float32, device=pc.get_anchor.device)
+    viewmat = viewpoint_camera.world_view_transform.transpose(0, 1)
+    lod = dict(level=pc._level, extra_level=pc._extra_level, cam_center=viewpoint_camera.camera_center,
+               res_scale=viewpoint_camera.resolution_scale, standard_dist=pc.standard_dist, fork=pc.fork,
+               street_levels=pc.street_levels)
+    pc._anchor_mask = lod_mask(pc.get_anchor, pc._level, pc._extra_level, viewpoint_camera.camera_center,
+                               viewpoint_camera.resolution_scale, pc.standard_dist, pc.fork, pc.street_levels)
+    visible, _ = prefilter(pc.get_anchor, pc.get_scaling, pc.get_rotation, viewmat, K,
+                           int(viewpoint_camera.image_width), int(viewpoint_camera.image_height), lod=lod)
+    return visible
 
 
 _VIS_CACHE: list = []  # [(mask, its version counter, int32 index)]: one entry

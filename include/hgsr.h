@@ -482,6 +482,21 @@ int hgsr_explicit_scatter(int64_t N, int K, const uint8_t* mask, const void* ws,
                           const float* g_rotation, float* v_xyz, float* v_f_dc, float* v_f_rest, float* v_opacity,
                           float* v_scaling, float* v_rotation, hgsr_stream_t stream);
 
+/* Ordered indices of the set bytes of mask[N] into index[M] (M = the count written by
+ * hgsr_explicit_count(visible = mask) into the same ws). */
+int hgsr_mask_index(int64_t N, const uint8_t* mask, const void* ws, size_t ws_bytes, int32_t* index,
+                    hgsr_stream_t stream);
+/* Anchor prefilter (reference gaussian_renderer/render.py:120-197 prefilter_voxel, after
+ * set_anchor_mask scene/lod_model.py:286-290): visible[a] = 1 iff the LoD test passes (when
+ * level != NULL; the test of hgsr_lod_mask) and the anchor projected with scales[a*stride .. +3]
+ * (activated) and quats[a] by camera (viewmat [4,4], K [3,3]) has radius > 0, with the
+ * projection of hgsr_project3d_fwd (same bits).  Writes no projection outputs. */
+int hgsr_anchor_prefilter(int A, const float* anchor, const float* quats, const float* scales, int scale_stride,
+                          const float* viewmat, const float* K, int width, int height, float eps2d,
+                          float near_plane, float far_plane, const int32_t* level, const float* extra_level,
+                          const float* cam_center, float res_scale, float standard_dist, float log2_fork,
+                          int max_level, uint8_t* visible, hgsr_stream_t stream);
+
 /* ---- measurement ----------------------------------------------------------
  * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):
  * when enabled, the main kernel of every entry point is bracketed by

@@ -118,3 +118,35 @@ def test_decode_backward(view_dim, color_dim, n_anchor, n_off):
         cond_close(dev_in[k].grad.cpu().numpy(), ins32[k].grad.numpy(), ins64[k].grad.numpy(), "d_" + k)
     for k in mlps:
         cond_close(dev_w[k].grad.cpu().numpy(), ws32[k].grad.numpy(), ws64[k].grad.numpy(), "d_" + k)
+
+
+@pytest.mark.parametrize("with_lod", [False, True])
+def test_anchor_prefilter_matches_projection_and_lod(with_lod):
+    """decode.prefilter (fused set_anchor_mask + prefilter_voxel, render.py:120-197) vs the oracle
+    projection's radii > 0 and the LoD restatement: the visible mask and its ordered index
+    bit-exact (the same projection bits as hgsr_project3d_fwd)."""
+    from horizongs_amd import decode as HD
+    from horizongs_amd.synthetic import make_scene
+    from oracle import explicit_ref as XR
+    from oracle import oracle as O
+    A = 20000
+    sc = make_scene(A, 320, 240, seed=11, scale_range=(0.002, 0.4), depth_range=(0.005, 30.0))
+    g = torch.Generator().manual_seed(3)
+    scal6 = torch.exp(torch.randn(A, 6, generator=g) * 0.5 - 4.0)
+    quats = sc.quats / sc.quats.norm(dim=-1, keepdim=True)
+    r, _, _, _ = O.proj3d_fwd(sc.means.numpy(), quats.numpy(), scal6[:, :3].contiguous().numpy(),
+                              sc.viewmats.numpy(), sc.Ks.numpy(), 320, 240)
+    ref = torch.from_numpy(r[0] > 0)
+    lod = None
+    if with_lod:
+        level = torch.randint(0, 4, (A,), generator=g, dtype=torch.int32)
+        extra = torch.rand(A, generator=g) - 0.5
+        cam = torch.tensor([0.0, 0.0, 0.5])
+        ref &= XR.gs_mask(sc.means, level, extra, cam, 1.0, 8.0, 2, 4)
+        lod = dict(level=level.to(DEV), extra_level=extra.to(DEV), cam_center=cam.to(DEV), res_scale=1.0,
+                   standard_dist=8.0, fork=2, street_levels=4)
+    assert 0 < int(ref.sum()) < A
+    vis, idx = HD.prefilter(sc.means.to(DEV), scal6.to(DEV), quats.to(DEV), sc.viewmats[0].to(DEV),
+                            sc.Ks[0].to(DEV), 320, 240, lod=lod)
+    np.testing.assert_array_equal(vis.cpu().numpy(), ref.numpy())
+    np.testing.assert_array_equal(idx.cpu().numpy(), torch.nonzero(ref).reshape(-1).numpy())
