@@ -70,6 +70,7 @@ from horizongs_amd import _native as NAT  # noqa: E402
 from horizongs_amd import decode as HD  # noqa: E402
 from horizongs_amd import densify as HDn  # noqa: E402
 from horizongs_amd import gsplat_api as G  # noqa: E402
+from horizongs_amd.activations import activate  # noqa: E402
 from horizongs_amd.loss import fused_loss  # noqa: E402
 from horizongs_amd.multigpu import GradientAllReduce  # noqa: E402
 from horizongs_amd.optim import Adam  # noqa: E402
@@ -192,7 +193,8 @@ class Workload:
             opac = opac.reshape(-1)
         else:
             xyz, quats, cols = self.means, self.quats, self.colors
-            scales, opac = torch.exp(self.log_scales), torch.sigmoid(self.opac_logit)
+            # scaling_activation = exp, opacity_activation = sigmoid: one fused HIP pass each way
+            scales, opac = activate(self.log_scales, self.opac_logit)
         self.last_colors = cols
         if self.args.gs == "3d":
             out, alpha, meta = G.rasterization(xyz, quats, scales, opac, cols, self.viewmats, self.Ks, W, H,

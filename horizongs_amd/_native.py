@@ -87,6 +87,8 @@ _SIGS = {
     "hgsr_explicit_scatter": (I, [I64, I, P, P, SZ, P, P, P, P, P, P, P, P, P, P, P, P]),
     "hgsr_mask_index": (I, [I64, P, P, SZ, P, P]),
     "hgsr_anchor_prefilter": (I, [I, P, P, P, I, P, P, I, I, F, F, F, P, P, P, F, F, F, I, P, P]),
+    "hgsr_activate_fwd": (I, [I64, P, P, P, P, P]),
+    "hgsr_activate_bwd": (I, [I64, P, P, P, P, P, P, P]),
     "hgsr_timing_enable": (I, [I]),
     "hgsr_timing_reset": (I, []),
     "hgsr_timing_only": (I, [ct.c_char_p]),

@@ -497,6 +497,16 @@ int hgsr_anchor_prefilter(int A, const float* anchor, const float* quats, const 
                           const float* cam_center, float res_scale, float standard_dist, float log2_fork,
                           int max_level, uint8_t* visible, hgsr_stream_t stream);
 
+/* ---- 3DGS parametrisation activations of a train step (scaling_activation = exp,
+ * opacity_activation = sigmoid of the reference models): scales [N,3] = exp(log_scales),
+ * opacities [N] = sigmoid(logits) in one pass; the vjp writes (OVERWRITES) v_log_scales =
+ * v_scales * scales and v_logits = v_opacities * o (1 - o) (either output nullable; a NULL
+ * upstream gradient counts as zero). */
+int hgsr_activate_fwd(int64_t N, const float* log_scales, const float* logits, float* scales, float* opacities,
+                      hgsr_stream_t stream);
+int hgsr_activate_bwd(int64_t N, const float* scales, const float* opacities, const float* v_scales,
+                      const float* v_opacities, float* v_log_scales, float* v_logits, hgsr_stream_t stream);
+
 /* ---- measurement ----------------------------------------------------------
  * Optional per-kernel HIP-event timing used by bench.py (roofline numbers):
  * when enabled, the main kernel of every entry point is bracketed by
