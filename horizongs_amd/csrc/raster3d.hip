@@ -279,8 +279,36 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
     return v;
 }
 
+// Backward "input transpose".  Per step a wave composites one Gaussian over its 8x8
+// quadrant (pass 1) and keeps only two numbers per pixel: fac = alpha T (the colour
+// weight) and v_sigma.  Every 4 steps the 4 x 2 registers are transposed across the
+// wave (v_permlane32_swap, v_permlane16_swap) so that lane L = 16 s + r holds step s's
+// values for the 4 pixels r + 16 m (m = 0..3) -- one pixel column, rows y0, y0+2, y0+4,
+// y0+6 -- and accumulates the 10 gradient values of that Gaussian over them in
+// registers (pass 2).  With dx constant down a column the sigma moments factor:
+//   Sx = dx S0, Sxx = dx^2 S0, Sxy = dx Sy,  S0 = sum v_sigma, Sy = sum v_sigma dy,
+//   Syy = sum v_sigma dy^2,
+// and the opacity gradient sum vis va = -S0 / opacity is formed once per Gaussian in
+// split3.  A 16-lane DPP tree finishes the sums (colours pre-permuted per lane class so
+// that the first two levels transpose instead of add).  Two transposed inputs replace
+// the ten reduced outputs of a per-step wave reduction.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {  // lane-shuffled copy of x (bound_ctrl: 0 for invalid)
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
+#ifdef HGSR_BWD_WAVES_N
+#define HGSR_BWD_WAVES __attribute__((amdgpu_waves_per_eu(HGSR_BWD_WAVES_N, 8)))
+#else
+#define HGSR_BWD_WAVES
+#endif
+struct Pass2Lane {
+    float pxc, py0c;         // pixel-centre x of this lane's column, y of its first row
+    float vo[4][4];          // [m][slot]: upstream colour gradient of pixel m, lane-permuted channels
+};
+
 template <int D, bool ABS>
-__global__ __launch_bounds__(256) void raster3d_bwd_kernel(
+__global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
     int bg_ch, int ed_ch, const float* __restrict__ render_colors, const int32_t* __restrict__ offsets,
     int64_t n_isects, const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
@@ -288,52 +316,85 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
     const float* __restrict__ v_render_alphas, float* __restrict__ acc_rows,
     unsigned long long* __restrict__ pair_counter) {
     constexpr int KV = 6 + D + (ABS ? 2 : 0);
+    constexpr int KVS = KV > 10 ? KV : 10;  // colour slots 6..9 always exist (unused ones add exact 0)
+    constexpr int KVP = KVS | 1;
     constexpr int NB = kBwdBatch;
     // double-buffered staging: batch b+1 is staged while batch b's partials are
-    // combined, so each batch costs two barriers
-    __shared__ float4 s_rec[2][NB][3];  // interleaved {g0, g1, col}: one address per record
+    // combined, so each batch costs two barriers; slot NB is a zero-opacity dummy
+    __shared__ float4 s_rec[2][NB + 1][3];  // interleaved {g0, g1, col}: one address per record
     __shared__ int32_t s_id[2][NB];
-    // row j of a lane row r lands in slot slot0(r) + 2j (TransposeReduce's pattern); the
-    // pattern's positions past KV are never read, and a padding position inside [0, KV) only
-    // ever receives an exact 0 (the padded values), so one base address serves every j
-    constexpr int KVP = (KV + 1) > (2 * TransposeReduce<KV>::G + TransposeReduce<KV>::H)
-                            ? (KV + 1) : (2 * TransposeReduce<KV>::G + TransposeReduce<KV>::H);
-    __shared__ float s_part[NB * KVP];  // the four waves' partials merged with LDS float atomics
+    __shared__ float s_part[(NB + 1) * KVP];  // the four waves' partials merged with LDS float atomics
     __shared__ uint8_t s_list[4][NB];
     __shared__ int32_t s_last[4];
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
-    const float T_final = tc.inside ? 1.0f - render_alphas[tc.pix] : 1.0f;
+    // per-pixel upstream terms of pixel (i, j); the ED channel is divided by max(alpha, 1e-10)
+    auto pixel_terms = [&](int i, int j, float (&v)[4], float& vterm) {
+        const bool in = i < H && j < W;
+        const int64_t pix = ((int64_t)tc.cam * H + i) * W + j;
+        const float Tf = in ? 1.0f - render_alphas[pix] : 1.0f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = (in && k < D) ? v_render_colors[pix * D + k] : 0.f;
+        float va = in ? v_render_alphas[pix] : 0.f;
+        if (ed_ch >= 0 && in) {
+            // ED = raw / max(alpha, 1e-10): d/d raw = 1/ac, d/d alpha = -ED/ac (alpha >= 1e-10)
+            const float alpha = 1.0f - Tf, ac = fmaxf(alpha, 1e-10f);
+            float v_ed = 0.f;
+#pragma unroll
+            for (int k = 0; k < D; ++k)
+                if (k == ed_ch) {
+                    v_ed = v[k];
+                    v[k] = v_ed / ac;
+                }
+            if (alpha >= 1e-10f) va -= v_ed * render_colors[pix * D + ed_ch] / ac;
+        }
+        float bg_dot = 0.f;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+            if (backgrounds && k < bg_ch) bg_dot += backgrounds[tc.cam * bg_ch + k] * v[k];
+        vterm = Tf * (va - bg_dot);  // multiplied by ra per Gaussian
+        return Tf;
+    };
+    float vo[4], va_term;
+    const float T_final = pixel_terms(tc.i, tc.j, vo, va_term);
     float T = T_final;
     // B = sum_k buf_k * vo_k, the upstream-weighted colour composited behind the
     // current Gaussian: v_alpha only ever needs this dot product, never buf_k itself
-    float B = 0.f, vo[4] = {0.f, 0.f, 0.f, 0.f};
+    float B = 0.f;
+    // pass-2 role of this lane: column cx = r & 7, rows y0 + 2m of the quadrant
+    const int r16 = lane & 15, cx = r16 & 7, y0 = r16 >> 3;
+    const int qi0 = tc.i - (lane >> 3), qj0 = tc.j - (lane & 7);  // quadrant origin
+    Pass2Lane p2;
+    p2.pxc = (float)(qj0 + cx) + 0.5f;
+    p2.py0c = (float)(qi0 + y0) + 0.5f;
+    {
+        // colour slots permuted by lane class (bit 3, bit 2 of r) so the first two DPP
+        // levels of the 16-lane tree transpose (see the reduction below):
+        // class (b3,b2) = (0,0): 0 1 2 3, (1,0): 1 0 3 2, (0,1): 2 3 0 1, (1,1): 3 2 1 0
+        const int perm = ((r16 >> 3) & 1) | (((r16 >> 2) & 1) << 1);
 #pragma unroll
-    for (int k = 0; k < D; ++k) vo[k] = tc.inside ? v_render_colors[tc.pix * D + k] : 0.f;
-    float va = tc.inside ? v_render_alphas[tc.pix] : 0.f;
-    if (ed_ch >= 0 && tc.inside) {
-        // ED = raw / max(alpha, 1e-10): d/d raw = 1/ac, d/d alpha = -ED/ac (alpha >= 1e-10)
-        const float alpha = 1.0f - T_final, ac = fmaxf(alpha, 1e-10f);
-        float v_ed = 0.f;
+        for (int m = 0; m < 4; ++m) {
+            float v[4], vt;
+            pixel_terms(qi0 + y0 + 2 * m, qj0 + cx, v, vt);
 #pragma unroll
-        for (int k = 0; k < D; ++k)
-            if (k == ed_ch) {
-                v_ed = vo[k];
-                vo[k] = v_ed / ac;
+            for (int q = 0; q < 4; ++q) {
+                const int k = q ^ perm;
+                p2.vo[m][q] = k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3];
             }
-        if (alpha >= 1e-10f) va -= v_ed * render_colors[tc.pix * D + ed_ch] / ac;
+        }
     }
-    float bg_dot = 0.f;
-#pragma unroll
-    for (int k = 0; k < D; ++k)
-        if (backgrounds && k < bg_ch) bg_dot += backgrounds[tc.cam * bg_ch + k] * vo[k];
-    const float va_term = T_final * (va - bg_dot);  // multiplied by ra per Gaussian
     const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
     const int32_t wave_final = wave_max_i32(bin_final);
     if (lane == 0) s_last[wave] = wave_final;
-    for (int e = tid; e < NB * KVP; e += 256) s_part[e] = 0.f;
+    for (int e = tid; e < (NB + 1) * KVP; e += 256) s_part[e] = 0.f;
+    if (tid < 6) {
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_rec[tid >> 1][NB][0] = z;  // both buffers' dummy records: opacity 0, never composited
+        s_rec[tid >> 1][NB][1] = z;
+        s_rec[tid >> 1][NB][2] = z;
+    }
     lds_barrier();
     const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
     // Gaussians after the block's last contributor are never reached
@@ -352,13 +413,10 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
         n0 = r[0]; n1 = r[1]; n2 = r[2];
         nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
     }
-    using TR = TransposeReduce<KV>;
-    const int row = lane >> 4;
-    // first accumulator slot of this lane row's reduced values (slot0 + 2j for value j)
-    const int slot0 = row == 0 ? 0 : row == 1 ? 1 : row == 2 ? TR::H : TR::H + 1;
     uint8_t* my_list = s_list[wave];
     int prev_bsz = 0;
     uint32_t stepped = 0;  // compacted list entries this wave stepped (bench roofline only)
+    const int slot = lane >> 4;  // pass-2 Gaussian slot of this lane
     for (int b = 0; b <= nb; ++b) {
         const int cur = b & 1, prv = cur ^ 1;
         const int32_t batch_end = end - 1 - b * NB;
@@ -391,7 +449,8 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
         lds_barrier();
         // phase 2: composite batch b
         // order-preserving compaction to the Gaussians that reach this quadrant and
-        // are not behind every pixel's last contributor
+        // are not behind every pixel's last contributor; padded with the dummy to a
+        // multiple of 4
         const int t0 = max(0, batch_end - wave_final);
         int n_mine = 0;
 #pragma unroll
@@ -403,14 +462,17 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
             if (rel) my_list[n_mine + lanes_below(m)] = (uint8_t)t;
             n_mine += __popcll(m);
         }
+        if (lane < 4 && n_mine + lane < NB) my_list[n_mine + lane] = (uint8_t)NB;
         stepped += (uint32_t)n_mine;
         if (n_mine > 0) {
             // the list comes back into registers once per batch; the loop reads
             // entries with readlane so no LDS index read sits on the critical path
             const int lst0 = my_list[lane], lst1 = my_list[64 + lane];
-            auto step = [&](const int t) {
+            // pass 1: composite record t for this lane's pixel (branch-free: a padding entry
+            // is the zero-opacity dummy and composites nothing); returns fac and v_sigma
+            auto step = [&](const int t, float& F, float& V) {
                 const float4* rp = s_rec[cur][t];
-                const float4 g0 = rp[0], g1 = rp[1];
+                const float4 g0 = rp[0], g1 = rp[1], c = rp[2];
                 const float dx = g0.x - tc.px, dy = g0.y - tc.py;
                 float xx, yy, xy;
                 const float sigma = sigma2(g0, g1, dx, dy, xx, yy, xy);
@@ -418,51 +480,130 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
                 const float araw = g1.y * vis;
                 const float alpha = fminf(0.999f, araw);
                 const bool valid = (batch_end - t <= bin_final) & (sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
-                if (!__any(valid)) return;
-                const float4 c = rp[2];
                 const float ck[4] = {c.x, c.y, c.z, c.w};
                 // an invalid lane composites alpha = 0: T, fac and B come out unchanged
                 const float al = valid ? alpha : 0.f;
                 const float ra = __builtin_amdgcn_rcpf(1.0f - al);
                 const float Tn = T * ra;
                 const float fac = al * Tn;
-                float gv[KV];
                 float cv = ck[0] * vo[0];
 #pragma unroll
                 for (int k = 1; k < D; ++k) cv += ck[k] * vo[k];
-#pragma unroll
-                for (int k = 0; k < D; ++k) gv[6 + k] = fac * vo[k];
                 const float v_alpha = Tn * cv + ra * (va_term - B);
                 B += fac * cv;
                 // alpha clamped at 0.999 (or not composited): no gradient through it
                 const float va2 = (valid & (araw <= 0.999f)) ? v_alpha : 0.f;
-                const float v_sigma = -araw * va2;  // dL/dsigma (unscaled sigma)
-                // sigma moments; split3 turns them into v_means2d = Q (Sx, Sy) and
-                // v_conic = (Sxx / 2, Sxy, Syy / 2), Q the conic
-                gv[0] = v_sigma * dx;
-                gv[1] = v_sigma * dy;
-                gv[2] = v_sigma * xx;
-                gv[3] = v_sigma * xy;
-                gv[4] = v_sigma * yy;
-                gv[5] = vis * va2;
-                if (ABS) {  // |per-pixel v_means2d|: Q d = (2 a' dx + b' dy, b' dx + 2 c' dy) / log2(e)
-                    constexpr float kLn2 = 0.6931471805599453f;
-                    gv[6 + D] = fabsf(v_sigma * kLn2 * (2.f * g0.z * dx + g0.w * dy));
-                    gv[7 + D] = fabsf(v_sigma * kLn2 * (g0.w * dx + 2.f * g1.x * dy));
-                }
                 T = Tn;
-                float u[TR::G];
-                TR::run(gv, u);
-                if ((lane & 15) == 0) {
-                    float* dst = s_part + t * KVP;
+                F = fac;
+                V = -araw * va2;  // dL/dsigma (unscaled sigma)
+            };
+            // pass 2 over 4 composited steps (records ts[0..3], values F/V in pass-1 layout)
+            auto pass2 = [&](const int li, float (&F)[4], float (&V)[4]) {
+                // transpose: lane bit 5 <-> register bit 1, lane bit 4 <-> register bit 0
 #pragma unroll
-                    for (int j = 0; j < TR::G; ++j) atomicAdd(dst + slot0 + 2 * j, u[j]);  // ds_add_f32
+                for (int q = 0; q < 2; ++q) {
+                    auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(F[q]), __float_as_uint(F[q + 2]), false, false);
+                    F[q] = __uint_as_float(a[0]); F[q + 2] = __uint_as_float(a[1]);
+                    auto v = __builtin_amdgcn_permlane32_swap(__float_as_uint(V[q]), __float_as_uint(V[q + 2]), false, false);
+                    V[q] = __uint_as_float(v[0]); V[q + 2] = __uint_as_float(v[1]);
                 }
+#pragma unroll
+                for (int q = 0; q < 4; q += 2) {
+                    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(F[q]), __float_as_uint(F[q + 1]), false, false);
+                    F[q] = __uint_as_float(a[0]); F[q + 1] = __uint_as_float(a[1]);
+                    auto v = __builtin_amdgcn_permlane16_swap(__float_as_uint(V[q]), __float_as_uint(V[q + 1]), false, false);
+                    V[q] = __uint_as_float(v[0]); V[q + 1] = __uint_as_float(v[1]);
+                }
+                // now F[m], V[m]: step `slot`, pixel (column cx, row y0 + 2m)
+                const int t = my_list[li + slot];  // this lane's Gaussian (list entry li + slot)
+                const float4 g0 = s_rec[cur][t][0];
+                const float dx = g0.x - p2.pxc, dy0 = g0.y - p2.py0c;
+                float S0 = 0.f, Sy = 0.f, Syy = 0.f, P[4] = {0.f, 0.f, 0.f, 0.f}, A0 = 0.f, A1 = 0.f;
+                float ax = 0.f, ay = 0.f, bx = 0.f, c2 = 0.f;
+                if (ABS) {
+                    const float4 g1 = s_rec[cur][t][1];
+                    ax = 2.f * g0.z * dx;
+                    bx = g0.w * dx;
+                    ay = g0.w;
+                    c2 = 2.f * g1.x;
+                }
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const float dy = dy0 - (float)(2 * m);
+                    const float vdy = V[m] * dy;
+                    S0 += V[m];
+                    Sy += vdy;
+                    Syy = __builtin_fmaf(vdy, dy, Syy);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) P[q] = __builtin_fmaf(F[m], p2.vo[m][q], P[q]);
+                    if (ABS) {  // |per-pixel v_means2d| up to ln 2: |v_sigma (2a'dx + b'dy)|, |v_sigma (b'dx + 2c'dy)|
+                        A0 += fabsf(V[m] * __builtin_fmaf(ay, dy, ax));
+                        A1 += fabsf(V[m] * __builtin_fmaf(c2, dy, bx));
+                    }
+                }
+                // level 1 (xor 8: the two lanes of a column): plain sums before the dx
+                // products; colours transposed (slot q of class b3 = 1 holds slot q^1's channel)
+                // row_ror:8 = 0x128, row_half_mirror = 0x141, quad_perm [1,0,3,2] = 0xB1, [2,3,0,1] = 0x4E
+                S0 += dpp<0x128>(S0);
+                Sy += dpp<0x128>(Sy);
+                Syy += dpp<0x128>(Syy);
+                if (ABS) {
+                    A0 += dpp<0x128>(A0);
+                    A1 += dpp<0x128>(A1);
+                }
+                const float C01 = P[0] + dpp<0x128>(P[1]), C23 = P[2] + dpp<0x128>(P[3]);
+                float g[7];
+                g[0] = dx * S0;       // Sx
+                g[1] = Sy;            // Sy
+                g[2] = dx * dx * S0;  // Sxx
+                g[3] = dx * Sy;       // Sxy
+                g[4] = Syy;           // Syy
+                g[5] = S0;            // sum v_sigma (split3: opacity gradient = -S0 / opacity)
+                // level 2 (half mirror, partner r ^ 7): colours transposed again
+                g[6] = C01 + dpp<0x141>(C23);
+#pragma unroll
+                for (int k = 0; k < 6; ++k) g[k] += dpp<0x141>(g[k]);
+                if (ABS) {
+                    A0 += dpp<0x141>(A0);
+                    A1 += dpp<0x141>(A1);
+                }
+#pragma unroll
+                for (int k = 0; k < 7; ++k) g[k] += dpp<0xB1>(g[k]);
+                if (ABS) {
+                    A0 += dpp<0xB1>(A0);
+                    A1 += dpp<0xB1>(A1);
+                }
+#pragma unroll
+                for (int k = 0; k < 7; ++k) g[k] += dpp<0x4E>(g[k]);
+                if (ABS) {
+                    A0 += dpp<0x4E>(A0);
+                    A1 += dpp<0x4E>(A1);
+                }
+#pragma unroll
+                for (int k = 0; k < 7; ++k) asm volatile("" : "+v"(g[k]));
+                float* dst = s_part + t * KVP;
+                if (r16 == 0) {
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) atomicAdd(dst + k, g[k]);  // ds_add_f32
+                    if (ABS) {
+                        constexpr float kLn2 = 0.6931471805599453f;
+                        atomicAdd(dst + 6 + D, kLn2 * A0);
+                        atomicAdd(dst + 7 + D, kLn2 * A1);
+                    }
+                }
+                // colour channel of lane class (b3, b2): 0 (0,0), 1 (1,0), 2 (0,1), 3 (1,1)
+                if ((r16 & 3) == 0) atomicAdd(dst + 6 + ((r16 >> 3) | ((r16 >> 1) & 2)), g[6]);
+            };
+            auto group = [&](const int lst, const int i0, const int li) {
+                float F[4], V[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) step(__builtin_amdgcn_readlane(lst, i0 + q), F[q], V[q]);
+                pass2(li, F, V);
             };
             // two loops instead of a per-step select between the list halves
             const int n0 = min(n_mine, 64);
-            for (int i = 0; i < n0; ++i) step(__builtin_amdgcn_readlane(lst0, i));
-            for (int i = 64; i < n_mine; ++i) step(__builtin_amdgcn_readlane(lst1, i - 64));
+            for (int i = 0; i < n0; i += 4) group(lst0, i, i);
+            for (int i = 64; i < n_mine; i += 4) group(lst1, i - 64, i);
         }
         prev_bsz = bsz;
         lds_barrier();
@@ -474,10 +615,11 @@ __global__ __launch_bounds__(256) void raster3d_bwd_kernel(
 // scatter accumulator rows into gsplat's separate gradient tensors (overwrite);
 // one lane per Gaussian, looping cameras in order (deterministic sums).  The rows
 // hold sigma moments (Sx, Sy, Sxx, Sxy, Syy) = sum_p v_sigma (dx, dy, dx^2, dx dy, dy^2):
-// v_means2d = Q (Sx, Sy) with Q the conic, v_conic = (Sxx / 2, Sxy, Syy / 2).
+// v_means2d = Q (Sx, Sy) with Q the conic, v_conic = (Sxx / 2, Sxy, Syy / 2); slot 5
+// holds S0 = sum_p v_sigma, and v_opacity = sum_p vis v_alpha = -S0 / opacity.
 template <int D, bool ABS>
 __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* __restrict__ rows,
-                                                     const float* __restrict__ conics,
+                                                     const Rec3* __restrict__ rec, const float* __restrict__ conics,
                                                      float2* __restrict__ v_means2d, float* __restrict__ v_conics,
                                                      ChanDst cd, float2* __restrict__ v_abs) {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -497,8 +639,10 @@ __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* 
         v_conics[i * 3] = 0.5f * r[2];
         v_conics[i * 3 + 1] = r[3];
         v_conics[i * 3 + 2] = 0.5f * r[4];
-        if (cd.op_shared) op_sum += r[5];
-        else cd.opac[i] = r[5];
+        // S0 != 0 only if the Gaussian composited somewhere, i.e. opacity >= 1/255
+        const float v_op = r[5] != 0.f ? -r[5] / rec[i].g1.y : 0.f;
+        if (cd.op_shared) op_sum += v_op;
+        else cd.opac[i] = v_op;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             if (k < cd.dc) {
@@ -718,7 +862,7 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                            flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, pairs); \
     }                                                                                                          \
     hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, \
-                       N, rows, conics, reinterpret_cast<float2*>(v_means2d), v_conics, cd,                     \
+                       N, rows, rec, conics, reinterpret_cast<float2*>(v_means2d), v_conics, cd,                     \
                        reinterpret_cast<float2*>(v_means2d_abs))
     switch (D * 2 + (abs ? 1 : 0)) {
         case 2: LAUNCH_B(1, false); break;
