@@ -297,7 +297,12 @@ __device__ __forceinline__ float dpp(float x) {  // lane-shuffled copy of x (bou
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
 }
 
-#ifdef HGSR_BWD_WAVES_N
+// 8 waves / SIMD (64 VGPRs; the register budget costs two spilled values outside the
+// step loop): 0.789 -> 0.776 ms at c2
+#ifndef HGSR_BWD_WAVES_N
+#define HGSR_BWD_WAVES_N 8
+#endif
+#if HGSR_BWD_WAVES_N > 0
 #define HGSR_BWD_WAVES __attribute__((amdgpu_waves_per_eu(HGSR_BWD_WAVES_N, 8)))
 #else
 #define HGSR_BWD_WAVES
@@ -319,9 +324,14 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     constexpr int KVS = KV > 10 ? KV : 10;  // colour slots 6..9 always exist (unused ones add exact 0)
     constexpr int KVP = KVS | 1;
     constexpr int NB = kBwdBatch;
-    // double-buffered staging: batch b+1 is staged while batch b's partials are
-    // combined, so each batch costs two barriers; slot NB is a zero-opacity dummy
-    __shared__ float4 s_rec[2][NB + 1][3];  // interleaved {g0, g1, col}: one address per record
+    // double-buffered staging: batch b+1 is loaded while batch b is composited and
+    // batch b-1's partials are combined (two barriers per batch); slot NB is a
+    // zero-opacity dummy
+    // one LDS object, so every component of record t sits at a compile-time offset from one
+    // address; filled by LDS-DMA (no staging VGPRs)
+    __shared__ struct {
+        float4 g0[2][NB + 1], g1[2][NB + 1], col[2][NB + 1];
+    } sr;
     __shared__ int32_t s_id[2][NB];
     __shared__ float s_part[(NB + 1) * KVP];  // the four waves' partials merged with LDS float atomics
     __shared__ uint8_t s_list[4][NB];
@@ -391,9 +401,9 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     for (int e = tid; e < (NB + 1) * KVP; e += 256) s_part[e] = 0.f;
     if (tid < 6) {
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        s_rec[tid >> 1][NB][0] = z;  // both buffers' dummy records: opacity 0, never composited
-        s_rec[tid >> 1][NB][1] = z;
-        s_rec[tid >> 1][NB][2] = z;
+        sr.g0[tid >> 1][NB] = z;  // both buffers' dummy records: opacity 0, never composited
+        sr.g1[tid >> 1][NB] = z;
+        sr.col[tid >> 1][NB] = z;
     }
     lds_barrier();
     const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
@@ -402,15 +412,24 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
     if (pair_counter && threadIdx.x == 0 && end > tc.start)  // measurement only (bench roofline)
         atomicAdd(pair_counter, (unsigned long long)(end - tc.start) * kTilePixels);
-    // two-deep software pipeline (ids two batches ahead, records one), clamped
-    // unconditional loads; lanes < NB load one Gaussian each
-    float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
+    // records are staged with LDS-DMA (global_load_lds_dwordx4: per-lane source, LDS
+    // destination wave base + 16 B x lane) one batch ahead; ids two batches ahead in a
+    // register; lanes < NB (waves 0, 1) load one Gaussian each, clamped indices
     int32_t cid = 0, nid = 0;
     const bool loader = tid < NB;
+    auto dma_batch = [&](int buf, int32_t id) {
+        const float4* r = reinterpret_cast<const float4*>(rec + id);
+        const int w0 = tid & ~63;
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r),
+                                         (void __attribute__((address_space(3)))*)(&sr.g0[buf][w0]), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + 1),
+                                         (void __attribute__((address_space(3)))*)(&sr.g1[buf][w0]), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + 2),
+                                         (void __attribute__((address_space(3)))*)(&sr.col[buf][w0]), 16, 0, 0);
+    };
     if (nb > 0 && loader) {
         cid = flatten_ids[max(end - 1 - tid, tc.start)];
-        const float4* r = reinterpret_cast<const float4*>(rec + cid);
-        n0 = r[0]; n1 = r[1]; n2 = r[2];
+        dma_batch(0, cid);
         nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
     }
     uint8_t* my_list = s_list[wave];
@@ -421,20 +440,14 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         const int cur = b & 1, prv = cur ^ 1;
         const int32_t batch_end = end - 1 - b * NB;
         const int bsz = b < nb ? min(NB, batch_end + 1 - tc.start) : 0;
-        // phase 1 (after the previous barrier): stage batch b, issue the loads of
-        // batch b+1, then combine batch b-1.  The atomics go last so that the next
-        // wait on prefetched loads (they share the vector-memory counter) finds
-        // them a whole batch old.
-        if (tid < bsz) {
-            s_id[cur][tid] = cid;
-            s_rec[cur][tid][0] = n0;
-            s_rec[cur][tid][1] = n1;
-            s_rec[cur][tid][2] = n2;
-        }
-        if (b < nb && loader) {
+        // batch b's DMA (issued one iteration ago, together with one batch-old atomics) lands
+        // before the barrier below publishes it; then DMA batch b+1 into the other buffer
+        // (its previous records were last read before the previous barrier) and combine b-1
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+        if (tid < bsz) s_id[cur][tid] = cid;
+        if (b + 1 < nb && loader) {
             cid = nid;
-            const float4* r = reinterpret_cast<const float4*>(rec + cid);
-            n0 = r[0]; n1 = r[1]; n2 = r[2];
+            dma_batch(prv, cid);
             nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
         if (b > 0) {
@@ -456,8 +469,8 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
 #pragma unroll
         for (int k = 0; k < NB / 64; ++k) {
             const int t = k * 64 + lane;
-            const bool rel = t < bsz && t >= t0 && reaches(s_rec[cur][t][0], s_rec[cur][t][1], qx, qy) &&
-                             ellipse_reaches(s_rec[cur][t][0], s_rec[cur][t][1], qx, qy);
+            const bool rel = t < bsz && t >= t0 && reaches(sr.g0[cur][t], sr.g1[cur][t], qx, qy) &&
+                             ellipse_reaches(sr.g0[cur][t], sr.g1[cur][t], qx, qy);
             const uint64_t m = __ballot(rel);
             if (rel) my_list[n_mine + lanes_below(m)] = (uint8_t)t;
             n_mine += __popcll(m);
@@ -471,8 +484,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
             // pass 1: composite record t for this lane's pixel (branch-free: a padding entry
             // is the zero-opacity dummy and composites nothing); returns fac and v_sigma
             auto step = [&](const int t, float& F, float& V) {
-                const float4* rp = s_rec[cur][t];
-                const float4 g0 = rp[0], g1 = rp[1], c = rp[2];
+                const float4 g0 = sr.g0[cur][t], g1 = sr.g1[cur][t], c = sr.col[cur][t];
                 const float dx = g0.x - tc.px, dy = g0.y - tc.py;
                 float xx, yy, xy;
                 const float sigma = sigma2(g0, g1, dx, dy, xx, yy, xy);
@@ -516,12 +528,12 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                 }
                 // now F[m], V[m]: step `slot`, pixel (column cx, row y0 + 2m)
                 const int t = my_list[li + slot];  // this lane's Gaussian (list entry li + slot)
-                const float4 g0 = s_rec[cur][t][0];
+                const float4 g0 = sr.g0[cur][t];
                 const float dx = g0.x - p2.pxc, dy0 = g0.y - p2.py0c;
                 float S0 = 0.f, Sy = 0.f, Syy = 0.f, P[4] = {0.f, 0.f, 0.f, 0.f}, A0 = 0.f, A1 = 0.f;
                 float ax = 0.f, ay = 0.f, bx = 0.f, c2 = 0.f;
                 if (ABS) {
-                    const float4 g1 = s_rec[cur][t][1];
+                    const float4 g1 = sr.g1[cur][t];
                     ax = 2.f * g0.z * dx;
                     bx = g0.w * dx;
                     ay = g0.w;
