@@ -139,6 +139,19 @@ __device__ __forceinline__ bool ellipse_reaches(const float4 g0, const float4 g1
     return m <= lim + 1e-3f * fabsf(lim) + 1e-3f;
 }
 
+// Quadrant masks (forward -> backward): bit r of array w says whether record r of a tile's
+// list (r = isect index - tile start) passed wave w's quadrant culling in the forward
+// (reaches() && ellipse_reaches(), the same test the backward would repeat).  A tile's bits
+// start at word qmask_word0(start, bin) = ceil(start / 64) + bin + 2 and it writes only the
+// ceil(n / 64) words holding its n records, so no two tiles share a word; the backward may
+// read up to two words before a tile's first.  One array of qstride words per quadrant.
+__host__ __device__ __forceinline__ int64_t qmask_word0(int64_t start, int64_t bin) {
+    return (start + 63) / 64 + bin + 2;
+}
+__host__ __device__ __forceinline__ int64_t qmask_stride(int64_t n_isects, int64_t n_bins) {
+    return (n_isects + 63) / 64 + n_bins + 4;
+}
+
 __device__ __forceinline__ int lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
@@ -171,7 +184,7 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
     int bg_ch, int ed_ch, const int32_t* __restrict__ offsets, int64_t n_isects,
     const int32_t* __restrict__ flatten_ids, float* __restrict__ render_colors, float* __restrict__ render_alphas,
-    int32_t* __restrict__ last_ids) {
+    int32_t* __restrict__ last_ids, uint64_t* __restrict__ qmask, int64_t qstride) {
     // slot kFwdBatch is a zero-opacity dummy used to pad the per-wave lists
     __shared__ float4 s_g0[kFwdBatch + 1];
     __shared__ float4 s_g1[kFwdBatch + 1];
@@ -235,6 +248,10 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
         // order-preserving compaction of the batch to the Gaussians that can reach
         // this wave's quadrant (each lane tests 4 of them)
         int n_mine = 0;
+        // quadrant mask words of this batch (read by the backward), one per 64 records
+        uint64_t* const qw = qmask ? qmask + wave * qstride + qmask_word0(tc.start, (int64_t)tc.cam * (tw * th) + tc.tile) +
+                                         (int64_t)b * (kFwdBatch / 64)
+                                   : nullptr;
 #pragma unroll
         for (int k = 0; k < kFwdBatch / 64; ++k) {
             const int t = k * 64 + lane;
@@ -242,6 +259,7 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
             const uint64_t m = __ballot(rel);
             if (rel) my_list[n_mine + lanes_below(m)] = (uint32_t)t * 16u;
             n_mine += __popcll(m);
+            if (qw && lane == k && k * 64 < cnt) qw[k] = m;  // only words holding records of this tile
         }
         if (lane < 4) my_list[n_mine + lane] = (uint32_t)kFwdBatch * 16u;  // pad to a multiple of 4
         uint32_t cur_off = 0xffffffffu;  // byte offset of this batch's latest contributor, if any
@@ -319,7 +337,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     int64_t n_isects, const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
     const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
     const float* __restrict__ v_render_alphas, float* __restrict__ acc_rows,
-    unsigned long long* __restrict__ pair_counter) {
+    unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask, int64_t qstride) {
     constexpr int KV = 6 + D + (ABS ? 2 : 0);
     constexpr int KVS = KV > 10 ? KV : 10;  // colour slots 6..9 always exist (unused ones add exact 0)
     constexpr int KVP = KVS | 1;
@@ -436,6 +454,19 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     int prev_bsz = 0;
     uint32_t stepped = 0;  // compacted list entries this wave stepped (bench roofline only)
     const int slot = lane >> 4;  // pass-2 Gaussian slot of this lane
+    // quadrant-mask words of batch bb: wave-uniform index, so they are scalar loads
+    uint64_t qw[3] = {0, 0, 0};
+    auto qfetch = [&](int bb) {
+        const int64_t lo = (end - 1 - (int64_t)bb * NB - tc.start) - (NB - 1);
+        const int64_t bin = (int64_t)tc.cam * (tw * th) + tc.tile;
+        const int idx = __builtin_amdgcn_readfirstlane(
+            (int)(__builtin_amdgcn_readfirstlane(wave) * qstride + qmask_word0(tc.start, bin) + (lo >> 6)));
+        const uint64_t* qp = qmask + idx;
+        qw[0] = qp[0];
+        qw[1] = qp[1];
+        qw[2] = qp[2];
+    };
+    if (qmask && nb > 0) qfetch(0);
     for (int b = 0; b <= nb; ++b) {
         const int cur = b & 1, prv = cur ^ 1;
         const int32_t batch_end = end - 1 - b * NB;
@@ -460,21 +491,47 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         }
         if (b == nb) break;
         lds_barrier();
-        // phase 2: composite batch b
-        // order-preserving compaction to the Gaussians that reach this quadrant and
-        // are not behind every pixel's last contributor; padded with the dummy to a
-        // multiple of 4
+        // phase 2: composite batch b, first the per-wave list of its records that reach this
+        // quadrant and are not behind every pixel's last contributor (order-preserving)
         const int t0 = max(0, batch_end - wave_final);
         int n_mine = 0;
+        if (qmask) {
+            // the forward's culling bits: record t <-> tile-relative bit R - t, R = batch_end -
+            // start; the 128-bit window [R - 127, R] (3 words, prefetched one batch ahead) is
+            // realigned and bit-reversed
+            const int64_t R = batch_end - tc.start, lo = R - (NB - 1);
+            const uint64_t w0 = qw[0], w1 = qw[1], w2 = qw[2];
+            if (b + 1 < nb) qfetch(b + 1);  // scalar loads, done long before the next batch
+            const int sh = (int)(lo & 63);
+            const uint64_t wlo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+            const uint64_t whi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+            uint64_t mk[2] = {__builtin_bitreverse64(whi), __builtin_bitreverse64(wlo)};
 #pragma unroll
-        for (int k = 0; k < NB / 64; ++k) {
-            const int t = k * 64 + lane;
-            const bool rel = t < bsz && t >= t0 && reaches(sr.g0[cur][t], sr.g1[cur][t], qx, qy) &&
-                             ellipse_reaches(sr.g0[cur][t], sr.g1[cur][t], qx, qy);
-            const uint64_t m = __ballot(rel);
-            if (rel) my_list[n_mine + lanes_below(m)] = (uint8_t)t;
-            n_mine += __popcll(m);
+            for (int k = 0; k < 2; ++k) {  // keep t in [t0, bsz)
+                const int a = min(max(t0 - 64 * k, 0), 64), z = min(max(bsz - 64 * k, 0), 64);
+                const uint64_t below_z = z >= 64 ? ~0ull : ((1ull << z) - 1);
+                const uint64_t below_a = a >= 64 ? ~0ull : ((1ull << a) - 1);
+                mk[k] &= below_z & ~below_a;
+                // (uint32_t casts: readfirstlane returns int, which would sign-extend)
+                const uint64_t m = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mk[k]) |
+                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mk[k] >> 32)) << 32);
+                if ((m >> lane) & 1) my_list[n_mine + lanes_below(m)] = (uint8_t)(k * 64 + lane);
+                n_mine += __popcll(m);
+            }
+        } else {
+            // order-preserving compaction to the Gaussians that reach this quadrant and
+            // are not behind every pixel's last contributor
+#pragma unroll
+            for (int k = 0; k < NB / 64; ++k) {
+                const int t = k * 64 + lane;
+                const bool rel = t < bsz && t >= t0 && reaches(sr.g0[cur][t], sr.g1[cur][t], qx, qy) &&
+                                 ellipse_reaches(sr.g0[cur][t], sr.g1[cur][t], qx, qy);
+                const uint64_t m = __ballot(rel);
+                if (rel) my_list[n_mine + lanes_below(m)] = (uint8_t)t;
+                n_mine += __popcll(m);
+            }
         }
+        // padded with the dummy to a multiple of 4
         if (lane < 4 && n_mine + lane < NB) my_list[n_mine + lane] = (uint8_t)NB;
         stepped += (uint32_t)n_mine;
         if (n_mine > 0) {
@@ -705,6 +762,10 @@ static int pack3(int C, int N, int D, const float* means2d, const float* conics,
     return check_launch("raster3d_pack");
 }
 
+extern "C" size_t hgsr_raster3d_qmask_bytes(int C, int tile_w, int tile_h, int64_t n_isects) {
+    return (size_t)(4 * qmask_stride(n_isects, (int64_t)C * tile_w * tile_h)) * sizeof(uint64_t);
+}
+
 extern "C" size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D) {
     (void)D;
     return rec_bytes(C, N);
@@ -713,7 +774,7 @@ extern "C" size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D) {
 static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backgrounds, int bg_ch, int ed_ch,
                                int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
-                               float* render_alphas, int32_t* last_ids, hipStream_t s);
+                               float* render_alphas, int32_t* last_ids, hipStream_t s, uint64_t* qmask = nullptr);
 
 static int raster3d_fwd_impl(int C, int N, int D, const float* means2d, const float* conics, const ChanSrc& cs,
                              const float* backgrounds, int bg_ch, int ed_ch, int width, int height, int tile_size,
@@ -736,13 +797,14 @@ static int raster3d_fwd_impl(int C, int N, int D, const float* means2d, const fl
 static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backgrounds, int bg_ch, int ed_ch,
                                int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
-                               float* render_alphas, int32_t* last_ids, hipStream_t s) {
+                               float* render_alphas, int32_t* last_ids, hipStream_t s, uint64_t* qmask) {
     const dim3 grid(C * tile_w * tile_h);
+    const int64_t qstride = qmask_stride(n_isects, (int64_t)C * tile_w * tile_h);
     KernelTimer kt("raster3d_fwd", s);
 #define LAUNCH_F(DD)                                                                                           \
     hipLaunchKernelGGL(raster3d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,    \
                        backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,          \
-                       render_alphas, last_ids)
+                       render_alphas, last_ids, qmask, qstride)
     switch (D) {
         case 1: LAUNCH_F(1); break;
         case 2: LAUNCH_F(2); break;
@@ -802,7 +864,7 @@ extern "C" int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, in
                                         int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
                                         const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                                         int32_t* last_ids, const void* records, size_t records_bytes,
-                                        hgsr_stream_t stream) {
+                                        void* qmask, size_t qmask_bytes, hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || with_depth), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !with_depth), "expected_depth needs depths");
     const int D = Dc + (with_depth ? 1 : 0);
@@ -810,9 +872,11 @@ extern "C" int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, in
     HGSR_REQUIRE(records_bytes >= hgsr_raster3d_fwd_ws_bytes(C, N, D), "raster3d_fwd_packed: records too small");
     HGSR_REQUIRE(isect_offsets && render_colors && render_alphas && last_ids, "null pointer");
     HGSR_REQUIRE(n_isects == 0 || (flatten_ids && records), "null pointer");
+    HGSR_REQUIRE(!qmask || qmask_bytes >= hgsr_raster3d_qmask_bytes(C, tile_w, tile_h, n_isects),
+                 "raster3d_fwd_packed: quadrant-mask buffer too small");
     return raster3d_fwd_launch(C, D, (const Rec3*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
                                tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
-                               last_ids, as_stream(stream));
+                               last_ids, as_stream(stream), (uint64_t*)qmask);
 }
 
 extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
@@ -828,7 +892,7 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* render_alphas, const int32_t* last_ids, const float* v_render_colors,
                              const float* v_render_alphas, float* v_means2d, float* v_conics, const ChanDst& cd,
                              float* v_means2d_abs, const void* fwd_ws, void* ws, size_t ws_bytes,
-                             hgsr_stream_t stream) {
+                             hgsr_stream_t stream, const uint64_t* qmask = nullptr) {
     if (int st = check_raster(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
                  "raster3d_bwd workspace too small");
@@ -865,13 +929,15 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     }
     const dim3 grid(C * tile_w * tile_h);
     unsigned long long* const pairs = timing_pair_counter("raster3d_bwd");
+    const int64_t qstride = qmask_stride(n_isects, (int64_t)C * tile_w * tile_h);
     const bool abs = v_means2d_abs != nullptr;
 #define LAUNCH_B(DD, AA)                                                                                       \
     {                                                                                                          \
         KernelTimer kt("raster3d_bwd", s);                                                                     \
         hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
                            tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,       \
-                           flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, pairs); \
+                           flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, pairs,  \
+                           qmask, qstride);                                                                    \
     }                                                                                                          \
     hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, \
                        N, rows, rec, conics, reinterpret_cast<float2*>(v_means2d), v_conics, cd,                     \
@@ -916,8 +982,11 @@ extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2
                                        const float* v_render_colors, const float* v_render_alphas,
                                        float* v_means2d, float* v_conics, float* v_colors, float* v_depths,
                                        float* v_opacities, float* v_means2d_abs, const void* fwd_ws, void* ws,
-                                       size_t ws_bytes, hgsr_stream_t stream) {
+                                       size_t ws_bytes, const void* qmask, size_t qmask_bytes,
+                                       hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
+    HGSR_REQUIRE(!qmask || qmask_bytes >= hgsr_raster3d_qmask_bytes(C, tile_w, tile_h, n_isects),
+                 "raster3d_bwd_fused: quadrant-mask buffer too small");
     HGSR_REQUIRE(!(expected_depth && !depths), "expected_depth needs depths");
     HGSR_REQUIRE(!depths || v_depths, "null pointer");
     const int D = Dc + (depths ? 1 : 0);
@@ -928,5 +997,5 @@ extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2
     return raster3d_bwd_impl(C, N, D, means2d, conics, cs, backgrounds, Dc, expected_depth ? Dc : -1,
                              render_colors, width, height, tile_size, tile_w, tile_h, isect_offsets, n_isects,
                              flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, v_means2d,
-                             v_conics, cd, v_means2d_abs, fwd_ws, ws, ws_bytes, stream);
+                             v_conics, cd, v_means2d_abs, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask);
 }

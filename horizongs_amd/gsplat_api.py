@@ -386,12 +386,16 @@ class _Raster3DFused(torch.autograd.Function):
         rc = torch.empty((C, height, width, D), dtype=torch.float32, device=dev)
         ra = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
         last = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        qmask = None
         if records is not None:
             ws = records
+            # the forward's per-quadrant culling bits, read back by the backward
+            q_b = N.size_query("hgsr_raster3d_qmask_bytes", C, tw, th, flatten_ids.numel())
+            qmask = torch.empty(q_b, dtype=torch.uint8, device=dev)
             N.call("hgsr_raster3d_fwd_packed", C, Ng, Dc, int(depths is not None), int(expected_depth),
                    ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
                    ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(ws),
-                   ws.numel(), N.stream(dev))
+                   ws.numel(), ptr(qmask), q_b, N.stream(dev))
         else:
             ws_b = N.size_query("hgsr_raster3d_fwd_ws_bytes", C, Ng, D)
             ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
@@ -404,6 +408,7 @@ class _Raster3DFused(torch.autograd.Function):
                               rc, ra, last)
         ctx.cfg = (width, height, tile_size, expected_depth, absgrad, Dc, col_shared, op_shared)
         ctx.fwd_ws = ws  # packed raster records, reused by the backward
+        ctx.qmask = qmask
         return rc, ra
 
     @staticmethod
@@ -429,7 +434,7 @@ class _Raster3DFused(torch.autograd.Function):
                tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
                ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_means2d), ptr(v_conics), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_abs), ptr(fwd_ws),
-               ptr(ws), ws_b, N.stream(dev))
+               ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(), N.stream(dev))
         if absgrad:
             means2d.absgrad = v_abs
         v_bg = None

@@ -179,7 +179,11 @@ int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * per-Gaussian raster records of the fused channel layout into ws (size as above; it
  * needs no intersection data), hgsr_raster3d_fwd_packed composites from them (with_depth:
  * the records carry the depth channel after the Dc colours).  The records stay valid for
- * hgsr_raster3d_bwd_fused's fwd_ws. */
+ * hgsr_raster3d_bwd_fused's fwd_ws.  qmask (nullable, hgsr_raster3d_qmask_bytes) receives
+ * the forward's per-quadrant culling bits of every tile list, which hgsr_raster3d_bwd_fused
+ * (given the same buffer) reads instead of repeating the culling tests; caller-allocated,
+ * OVERWRITTEN where the forward visits a tile (the backward reads only those bits). */
+size_t hgsr_raster3d_qmask_bytes(int C, int tile_w, int tile_h, int64_t n_isects);
 int hgsr_raster3d_pack_fused(int C, int N, int Dc, const float* means2d, const float* conics,
                              const float* colors, int colors_shared, const float* depths,
                              const float* opacities, int opacities_shared, void* ws, size_t ws_bytes,
@@ -189,10 +193,11 @@ int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_
                              int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
                              const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                              int32_t* last_ids, const void* records, size_t records_bytes,
-                             hgsr_stream_t stream);
+                             void* qmask, size_t qmask_bytes, hgsr_stream_t stream);
 /* vjp of hgsr_raster3d_fwd_fused: v_colors in the colours' layout (shared colours
  * summed over cameras in camera order), v_depths [C,N] (when depths), v_opacities
- * in the opacities' layout; render_colors is the forward output (needed for ED). */
+ * in the opacities' layout; render_colors is the forward output (needed for ED);
+ * qmask (nullable): the buffer hgsr_raster3d_fwd_packed filled for the same lists. */
 int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* conics,
                             const float* colors, int colors_shared, const float* depths,
                             int expected_depth, const float* opacities, int opacities_shared,
@@ -203,7 +208,8 @@ int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             const float* v_render_colors, const float* v_render_alphas,
                             float* v_means2d, float* v_conics, float* v_colors, float* v_depths,
                             float* v_opacities, float* v_means2d_abs, const void* fwd_ws, void* ws,
-                            size_t ws_bytes, hgsr_stream_t stream);
+                            size_t ws_bytes, const void* qmask, size_t qmask_bytes,
+                            hgsr_stream_t stream);
 
 /* ---- K11/K12: 2DGS surfel rasterization -----------------------------------
  * replaces gsplat rasterize_to_pixels_2dgs.  The LAST colour channel is the
