@@ -85,6 +85,19 @@ __device__ __forceinline__ float wave_sum_to_lane63(float v) {
 // issued -- which dominated the raster backward (SQ_WAIT_ANY ~47 % of wave cycles).
 // Valid only where no global-memory value written by one wave is read by another
 // wave of the workgroup across the barrier.
+// Quadrant masks (raster forward -> backward, 3DGS and 2DGS): bit r of array w says whether
+// record r of a tile's list (r = isect index - tile start) passed wave w's quadrant culling
+// in the forward (the same test the backward would repeat).  A tile's bits
+// start at word qmask_word0(start, bin) = ceil(start / 64) + bin + 2 and it writes only the
+// ceil(n / 64) words holding its n records, so no two tiles share a word; the backward may
+// read up to two words before a tile's first.  One array of qstride words per quadrant.
+__host__ __device__ __forceinline__ int64_t qmask_word0(int64_t start, int64_t bin) {
+    return (start + 63) / 64 + bin + 2;
+}
+__host__ __device__ __forceinline__ int64_t qmask_stride(int64_t n_isects, int64_t n_bins) {
+    return (n_isects + 63) / 64 + n_bins + 4;
+}
+
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }

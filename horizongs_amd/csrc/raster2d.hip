@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     const int32_t* __restrict__ flatten_ids, float* __restrict__ render_colors, float* __restrict__ render_alphas,
     float* __restrict__ render_normals,
     float* __restrict__ render_distort, float* __restrict__ render_median, int32_t* __restrict__ last_ids,
-    int32_t* __restrict__ median_ids) {
+    int32_t* __restrict__ median_ids, uint64_t* __restrict__ qmask, int64_t qstride) {
     constexpr int NB = kFwd2Batch;
     // one LDS object: every component of record t sits at a compile-time offset from one address
     __shared__ struct {
@@ -280,6 +280,11 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
         }
         if (wave_done) continue;
         int n_mine = 0;
+        // quadrant mask words of this batch (read by the backward), one per 64 records
+        uint64_t* const qw = qmask ? qmask + wave * qstride +
+                                         qmask_word0(tc.start, (int64_t)tc.cam * (tw * th) + tc.tile) +
+                                         (int64_t)b * (NB / 64)
+                                   : nullptr;
 #pragma unroll
         for (int k = 0; k < NB / 64; ++k) {
             const int t = k * 64 + lane;
@@ -287,6 +292,7 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
             const uint64_t m = __ballot(rel);
             if (rel) my_list[n_mine + lanes_below2(m)] = (uint8_t)t;
             n_mine += __popcll(m);
+            if (qw && lane == k && k * 64 < cnt) qw[k] = m;  // only words holding records of this tile
         }
         if (n_mine == 0) continue;
         const int lst0 = my_list[lane], lst1 = my_list[64 + lane];
@@ -357,7 +363,8 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     int64_t n_isects, const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
     const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
     const float* __restrict__ v_render_alphas, const float* __restrict__ v_render_normals,
-    float* __restrict__ acc_rows, unsigned long long* __restrict__ pair_counter) {
+    float* __restrict__ acc_rows, unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask,
+    int64_t qstride) {
     // row layout: 0-1 xy, 2-4 sum (p-m)_x v_c, 5-7 sum (p-m)_y v_c, 8-10 sum v_c (v_c = dL/d(h_u x h_v)),
     // 11 opac, 12-14 normal, 15.. colour, then abs xy; split2 maps v_c sums to u, v, w and densify
     constexpr int KV = 15 + D + (ABS ? 2 : 0);
@@ -448,6 +455,19 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     uint8_t* my_list = s_list[wave];
     int prev_bsz = 0;
     uint32_t stepped = 0;  // compacted list entries this wave stepped (bench roofline only)
+    // quadrant-mask words of batch bb (the forward's culling bits): wave-uniform index, so
+    // they are scalar loads, issued one batch ahead
+    uint64_t qw[2] = {0, 0};
+    auto qfetch = [&](int bb) {
+        const int64_t lo = (end - 1 - (int64_t)bb * NB - tc.start) - (NB - 1);
+        const int64_t bin = (int64_t)tc.cam * (tw * th) + tc.tile;
+        const int idx = __builtin_amdgcn_readfirstlane(
+            (int)(__builtin_amdgcn_readfirstlane(wave) * qstride + qmask_word0(tc.start, bin) + (lo >> 6)));
+        const uint64_t* qp = qmask + idx;
+        qw[0] = qp[0];
+        qw[1] = qp[1];
+    };
+    if (qmask && nb > 0) qfetch(0);
     for (int b = 0; b <= nb; ++b) {
         const int cur = b & 1, prv = cur ^ 1;
         const int32_t batch_end = end - 1 - b * NB;
@@ -474,9 +494,28 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
         lds_barrier();
         const int t0 = max(0, batch_end - wave_final);
         const int t = lane;
-        const bool rel = t < bsz && t >= t0 &&
-                         reaches2_exact(s_r0[cur][t], s_r1[cur][t], s_r2[cur][t], s_r4[cur][t], s_box[cur][t], qx, qy);
-        const uint64_t m = __ballot(rel);
+        uint64_t m;
+        bool rel;
+        if (qmask) {
+            // record t <-> tile-relative bit R - t (R = batch_end - start): the 64-bit window
+            // [R - 63, R] realigned from two words and bit-reversed, then limited to [t0, bsz)
+            const int64_t R = batch_end - tc.start, lo = R - (NB - 1);
+            const uint64_t w0 = qw[0], w1 = qw[1];
+            if (b + 1 < nb) qfetch(b + 1);
+            const int sh = (int)(lo & 63);
+            const uint64_t win = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+            const uint64_t below_z = bsz >= 64 ? ~0ull : ((1ull << bsz) - 1);
+            const uint64_t below_a = t0 >= 64 ? ~0ull : ((1ull << t0) - 1);
+            const uint64_t mk = __builtin_bitreverse64(win) & below_z & ~below_a;
+            // (uint32_t casts: readfirstlane returns int, which would sign-extend)
+            m = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mk) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mk >> 32)) << 32);
+            rel = (m >> lane) & 1;
+        } else {
+            rel = t < bsz && t >= t0 &&
+                  reaches2_exact(s_r0[cur][t], s_r1[cur][t], s_r2[cur][t], s_r4[cur][t], s_box[cur][t], qx, qy);
+            m = __ballot(rel);
+        }
         if (rel) my_list[lanes_below2(m)] = (uint8_t)t;
         const int n_mine = __popcll(m);
         stepped += (uint32_t)n_mine;
@@ -661,7 +700,8 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
                                int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
                                float* render_alphas, float* render_normals, float* render_distort,
-                               float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s);
+                               float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s,
+                               uint64_t* qmask = nullptr);
 
 static int raster2d_fwd_impl(int C, int N, int D, const float* means2d, const float* rt, const ChanSrc& cs,
                              const float* normals, const float* backgrounds, int bg_ch, int ed_ch, int width,
@@ -691,13 +731,16 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
                                int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
                                float* render_alphas, float* render_normals, float* render_distort,
-                               float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s) {
+                               float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s,
+                               uint64_t* qmask) {
     const dim3 grid(C * tile_w * tile_h);
+    const int64_t qstride = qmask_stride(n_isects, (int64_t)C * tile_w * tile_h);
     KernelTimer kt("raster2d_fwd", s);
 #define LAUNCH_F2(DD)                                                                                            \
     hipLaunchKernelGGL(raster2d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,     \
                        backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,           \
-                       render_alphas, render_normals, render_distort, render_median, last_ids, median_ids)
+                       render_alphas, render_normals, render_distort, render_median, last_ids, median_ids, qmask,   \
+                       qstride)
     switch (D) {
         case 1: LAUNCH_F2(1); break;
         case 2: LAUNCH_F2(2); break;
@@ -765,7 +808,8 @@ extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, in
                                         const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                                         float* render_normals, float* render_distort, float* render_median,
                                         int32_t* last_ids, int32_t* median_ids, const void* records,
-                                        size_t records_bytes, hgsr_stream_t stream) {
+                                        size_t records_bytes, void* qmask, size_t qmask_bytes,
+                                        hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || with_depth), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !with_depth), "expected_depth needs depths");
     const int D = Dc + (with_depth ? 1 : 0);
@@ -775,10 +819,12 @@ extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, in
                      render_median && last_ids && median_ids,
                  "null pointer");
     HGSR_REQUIRE(n_isects == 0 || (flatten_ids && records), "null pointer");
+    HGSR_REQUIRE(!qmask || qmask_bytes >= (size_t)(4 * qmask_stride(n_isects, (int64_t)C * tile_w * tile_h)) * 8,
+                 "raster2d_fwd_packed: quadrant-mask buffer too small");
     return raster2d_fwd_launch(C, D, (const Rec2*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
                                tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
                                render_normals, render_distort, render_median, last_ids, median_ids,
-                               as_stream(stream));
+                               as_stream(stream), (uint64_t*)qmask);
 }
 
 extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
@@ -794,7 +840,7 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* render_alphas, const int32_t* last_ids, const float* v_render_colors,
                              const float* v_render_alphas, const float* v_render_normals, float* v_means2d,
                              float* v_rt, const ChanDst& cd, float* v_normals, float* v_densify,
-                             const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
+                             const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream, const uint64_t* qmask = nullptr) {
     if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
                  "raster2d_bwd workspace too small");
@@ -832,13 +878,14 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     }
     const dim3 grid(C * tile_w * tile_h);
     unsigned long long* const pairs = timing_pair_counter("raster2d_bwd");
+    const int64_t qstride = qmask_stride(n_isects, (int64_t)C * tile_w * tile_h);
 #define LAUNCH_B2(DD)                                                                                             \
     {                                                                                                             \
         KernelTimer kt("raster2d_bwd", s);                                                                        \
         hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
                            tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,        \
                            flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,                \
-                           v_render_normals, rows, pairs);                                                        \
+                           v_render_normals, rows, pairs, qmask, qstride);                                        \
     }                                                                                                             \
     hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s,   \
                        C, N, rows, rt, m2, reinterpret_cast<float2*>(v_means2d), v_rt, cd, v_normals,             \
@@ -881,10 +928,12 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                                        const float* v_render_normals, float* v_means2d, float* v_ray_transforms,
                                        float* v_colors, float* v_depths, float* v_opacities, float* v_normals,
                                        float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
-                                       hgsr_stream_t stream) {
+                                       const void* qmask, size_t qmask_bytes, hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !depths), "expected_depth needs depths");
     HGSR_REQUIRE(!depths || v_depths, "null pointer");
+    HGSR_REQUIRE(!qmask || qmask_bytes >= (size_t)(4 * qmask_stride(n_isects, (int64_t)C * tile_w * tile_h)) * 8,
+                 "raster2d_bwd_fused: quadrant-mask buffer too small");
     const int D = Dc + (depths ? 1 : 0);
     const ChanSrc cs{colors, colors_shared ? 0 : (int64_t)N * Dc, Dc, depths, opacities,
                      opacities_shared ? 0 : (int64_t)N};
@@ -894,5 +943,5 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                              expected_depth ? Dc : -1, render_colors, width, height, tile_size, tile_w, tile_h,
                              isect_offsets, n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
                              v_render_alphas, v_render_normals, v_means2d, v_ray_transforms, cd, v_normals,
-                             v_densify, fwd_ws, ws, ws_bytes, stream);
+                             v_densify, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask);
 }

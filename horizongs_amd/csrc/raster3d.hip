@@ -139,19 +139,6 @@ __device__ __forceinline__ bool ellipse_reaches(const float4 g0, const float4 g1
     return m <= lim + 1e-3f * fabsf(lim) + 1e-3f;
 }
 
-// Quadrant masks (forward -> backward): bit r of array w says whether record r of a tile's
-// list (r = isect index - tile start) passed wave w's quadrant culling in the forward
-// (reaches() && ellipse_reaches(), the same test the backward would repeat).  A tile's bits
-// start at word qmask_word0(start, bin) = ceil(start / 64) + bin + 2 and it writes only the
-// ceil(n / 64) words holding its n records, so no two tiles share a word; the backward may
-// read up to two words before a tile's first.  One array of qstride words per quadrant.
-__host__ __device__ __forceinline__ int64_t qmask_word0(int64_t start, int64_t bin) {
-    return (start + 63) / 64 + bin + 2;
-}
-__host__ __device__ __forceinline__ int64_t qmask_stride(int64_t n_isects, int64_t n_bins) {
-    return (n_isects + 63) / 64 + n_bins + 4;
-}
-
 __device__ __forceinline__ int lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }

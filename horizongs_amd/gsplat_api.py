@@ -497,6 +497,7 @@ class _Raster2D(torch.autograd.Function):
                               ra, last)
         ctx.cfg = (width, height, tile_size)
         ctx.fwd_ws = ws  # packed surfel records, reused by the backward
+        ctx.qmask = qmask  # the forward's quadrant culling bits, reused by the backward
         ctx.mark_non_differentiable(rd, rm)
         return rc, ra, rn, rd, rm
 
@@ -563,12 +564,16 @@ class _Raster2DFused(torch.autograd.Function):
         rm = torch.empty((C, height, width, 1), dtype=torch.float32, device=dev)
         last = torch.empty((C, height, width), dtype=torch.int32, device=dev)
         med = torch.empty((C, height, width), dtype=torch.int32, device=dev)
+        qmask = None
         if records is not None:
             ws = records
+            # the forward's per-quadrant culling bits, read back by the backward
+            q_b = N.size_query("hgsr_raster3d_qmask_bytes", C, tw, th, flatten_ids.numel())
+            qmask = torch.empty(q_b, dtype=torch.uint8, device=dev)
             N.call("hgsr_raster2d_fwd_packed", C, Ng, Dc, int(depths is not None), int(expected_depth),
                    ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
                    ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(rn), ptr(rd), ptr(rm),
-                   ptr(last), ptr(med), ptr(ws), ws.numel(), N.stream(dev))
+                   ptr(last), ptr(med), ptr(ws), ws.numel(), ptr(qmask), q_b, N.stream(dev))
         else:
             ws_b = N.size_query("hgsr_raster2d_fwd_ws_bytes", C, Ng, D)
             ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
@@ -581,6 +586,7 @@ class _Raster2DFused(torch.autograd.Function):
                               flatten_ids, rc, ra, last)
         ctx.cfg = (width, height, tile_size, expected_depth, Dc, col_shared, op_shared)
         ctx.fwd_ws = ws  # packed surfel records, reused by the backward
+        ctx.qmask = qmask  # the forward's quadrant culling bits, reused by the backward
         ctx.mark_non_differentiable(rd, rm)
         return rc, ra, rn, rd, rm
 
@@ -609,7 +615,8 @@ class _Raster2DFused(torch.autograd.Function):
                width, height, tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
                ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_rn), ptr(v_means2d), ptr(v_rt), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_normals),
-               ptr(v_dens), ptr(fwd_ws), ptr(ws), ws_b, N.stream(dev))
+               ptr(v_dens), ptr(fwd_ws), ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(),
+               N.stream(dev))
         v_bg = None
         if backgrounds is not None and ctx.needs_input_grad[7]:
             v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))

@@ -255,7 +255,9 @@ int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             size_t ws_bytes, hgsr_stream_t stream);
 /* hgsr_raster2d_fwd_fused split in two (as hgsr_raster3d_pack_fused / _fwd_packed): the
  * surfel records (ws, hgsr_raster2d_fwd_ws_bytes) are packed while the host reads the
- * intersection count, then composited; they stay valid as hgsr_raster2d_bwd_fused's fwd_ws. */
+ * intersection count, then composited; they stay valid as hgsr_raster2d_bwd_fused's fwd_ws.
+ * qmask (nullable; size hgsr_raster3d_qmask_bytes, the same layout): the forward's
+ * per-quadrant culling bits, read by hgsr_raster2d_bwd_fused instead of repeating the tests. */
 int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                              const float* colors, int colors_shared, const float* depths,
                              const float* opacities, int opacities_shared, const float* normals, void* ws,
@@ -266,7 +268,7 @@ int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_
                              const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                              float* render_normals, float* render_distort, float* render_median,
                              int32_t* last_ids, int32_t* median_ids, const void* records,
-                             size_t records_bytes, hgsr_stream_t stream);
+                             size_t records_bytes, void* qmask, size_t qmask_bytes, hgsr_stream_t stream);
 int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                             const float* colors, int colors_shared, const float* depths,
                             int expected_depth, const float* opacities, int opacities_shared,
@@ -278,6 +280,7 @@ int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             const float* v_render_normals, float* v_means2d, float* v_ray_transforms,
                             float* v_colors, float* v_depths, float* v_opacities, float* v_normals,
                             float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
+                            const void* qmask, size_t qmask_bytes,
                             hgsr_stream_t stream);
 
 /* ---- K14: anchor -> neural-Gaussian decode --------------
