@@ -24,6 +24,14 @@ struct KernelTimer {
     ~KernelTimer() { timing_end(id, s); }
 };
 
+// The pair counters are spread over kPairSlots 128-B lines (two counters per workgroup
+// slot) so the per-tile atomics of the timed kernel never queue on one L2 channel; the
+// readout sums the slots.
+constexpr int kPairSlots = 256;
+__device__ __forceinline__ unsigned long long* pair_slot(unsigned long long* base, int which) {
+    return base + ((int)(blockIdx.x & (kPairSlots - 1)) * 2 + which) * 16;
+}
+
 // Returns HGSR_ELAUNCH (and records the HIP error) if the last launch failed.
 int check_launch(const char* what);
 

@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     const int32_t end = min(tc.end, blk_final + 1);
     const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
     if (pair_counter && threadIdx.x == 0 && end > tc.start)  // measurement only (bench roofline)
-        atomicAdd(pair_counter, (unsigned long long)(end - tc.start) * kTilePixels);
+        atomicAdd(pair_slot(pair_counter, 0), (unsigned long long)(end - tc.start) * kTilePixels);
     // records are staged with LDS-DMA (global_load_lds_dwordx4: per-lane source, LDS
     // destination base + 16 B x lane), one batch ahead, so they cost no VGPRs (89 -> 59);
     // the 64 loader lanes are exactly wave 0
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
         lds_barrier();
     }
     if (pair_counter && lane == 0 && stepped)  // measurement only: lane-pairs stepped
-        atomicAdd(pair_counter + 1, (unsigned long long)stepped * 64ull);
+        atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
 }
 
 // Per surfel: fold the accumulated sums into gsplat's gradient tensors (overwrite), in f64.

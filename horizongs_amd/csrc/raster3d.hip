@@ -15,9 +15,9 @@
 //    early exit, so the scalar unit is not saturated by exec-mask bookkeeping;
 //  * backward: replay back-to-front bounded by the tile's latest contributor,
 //    wave-ballot skip of Gaussians no lane sees, all gradient components
-//    reduced across the wave together (step-major DPP, no hazard stalls), the
-//    four wave partials combined in LDS and ONE packed record of float atomics
-//    per (Gaussian, tile) into a 64-byte accumulator row (one memory request).
+//    reduced across the wave together (step-major DPP, no hazard stalls), and
+//    each wave's sums go straight to the Gaussian's 64-byte accumulator row as
+//    one float-atomic instruction per 4 steps (the waves' partials meet in L2).
 #include "common.h"
 
 namespace hgsr {
@@ -325,20 +325,15 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
     const float* __restrict__ v_render_alphas, float* __restrict__ acc_rows,
     unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask, int64_t qstride) {
-    constexpr int KV = 6 + D + (ABS ? 2 : 0);
-    constexpr int KVS = KV > 10 ? KV : 10;  // colour slots 6..9 always exist (unused ones add exact 0)
-    constexpr int KVP = KVS | 1;
     constexpr int NB = kBwdBatch;
-    // double-buffered staging: batch b+1 is loaded while batch b is composited and
-    // batch b-1's partials are combined (two barriers per batch); slot NB is a
-    // zero-opacity dummy
+    // double-buffered staging: batch b+1 is loaded while batch b is composited (two
+    // barriers per batch); slot NB is a zero-opacity dummy
     // one LDS object, so every component of record t sits at a compile-time offset from one
     // address; filled by LDS-DMA (no staging VGPRs)
     __shared__ struct {
         float4 g0[2][NB + 1], g1[2][NB + 1], col[2][NB + 1];
     } sr;
     __shared__ int32_t s_id[2][NB];
-    __shared__ float s_part[(NB + 1) * KVP];  // the four waves' partials merged with LDS float atomics
     __shared__ uint8_t s_list[4][NB];
     __shared__ int32_t s_last[4];
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
@@ -403,7 +398,6 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
     const int32_t wave_final = wave_max_i32(bin_final);
     if (lane == 0) s_last[wave] = wave_final;
-    for (int e = tid; e < (NB + 1) * KVP; e += 256) s_part[e] = 0.f;
     if (tid < 6) {
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
         sr.g0[tid >> 1][NB] = z;  // both buffers' dummy records: opacity 0, never composited
@@ -416,7 +410,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     const int32_t end = min(tc.end, blk_final + 1);
     const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
     if (pair_counter && threadIdx.x == 0 && end > tc.start)  // measurement only (bench roofline)
-        atomicAdd(pair_counter, (unsigned long long)(end - tc.start) * kTilePixels);
+        atomicAdd(pair_slot(pair_counter, 0), (unsigned long long)(end - tc.start) * kTilePixels);
     // records are staged with LDS-DMA (global_load_lds_dwordx4: per-lane source, LDS
     // destination wave base + 16 B x lane) one batch ahead; ids two batches ahead in a
     // register; lanes < NB (waves 0, 1) load one Gaussian each, clamped indices
@@ -438,9 +432,17 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
     }
     uint8_t* my_list = s_list[wave];
-    int prev_bsz = 0;
     uint32_t stepped = 0;  // compacted list entries this wave stepped (bench roofline only)
     const int slot = lane >> 4;  // pass-2 Gaussian slot of this lane
+    // pass-2 output lane roles: after the 16-lane tree every lane of a row holds the six
+    // sigma sums (and |v_xy|) and each quad one colour channel; lane r16 = 4 q + 3 adds its
+    // quad's channel, lanes 0-2 / 4-6 the sums 0-2 / 3-5, lanes 8 / 9 the |v_xy| pair (ABS)
+    const int qlo = r16 & 3;
+    const bool qb2 = (r16 >> 2) & 1;
+    const int koff = qlo == 3 ? 6 + ((r16 >> 3) | ((r16 >> 1) & 2))
+                   : r16 < 8  ? qlo + (qb2 ? 3 : 0)
+                   : (ABS && r16 == 8) ? 6 + D
+                   : (ABS && r16 == 9) ? 7 + D : -1;
     // quadrant-mask words of batch bb: wave-uniform index, so they are scalar loads
     uint64_t qw[3] = {0, 0, 0};
     auto qfetch = [&](int bb) {
@@ -454,13 +456,13 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         qw[2] = qp[2];
     };
     if (qmask && nb > 0) qfetch(0);
-    for (int b = 0; b <= nb; ++b) {
+    for (int b = 0; b < nb; ++b) {
         const int cur = b & 1, prv = cur ^ 1;
         const int32_t batch_end = end - 1 - b * NB;
-        const int bsz = b < nb ? min(NB, batch_end + 1 - tc.start) : 0;
-        // batch b's DMA (issued one iteration ago, together with one batch-old atomics) lands
+        const int bsz = min(NB, batch_end + 1 - tc.start);
+        // batch b's DMA (issued one iteration ago, before batch b-1's gradient atomics) lands
         // before the barrier below publishes it; then DMA batch b+1 into the other buffer
-        // (its previous records were last read before the previous barrier) and combine b-1
+        // (its previous records were last read before the previous barrier)
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
         if (tid < bsz) s_id[cur][tid] = cid;
         if (b + 1 < nb && loader) {
@@ -468,15 +470,6 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
             dma_batch(prv, cid);
             nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
-        if (b > 0) {
-            for (int e = tid; e < prev_bsz * KV; e += 256) {
-                const int t = e / KV, k = e - t * KV;
-                const float sv = s_part[t * KVP + k];
-                s_part[t * KVP + k] = 0.f;
-                if (sv != 0.f) atomicAdd(acc_rows + (int64_t)s_id[prv][t] * kRec3 + k, sv);
-            }
-        }
-        if (b == nb) break;
         lds_barrier();
         // phase 2: composite batch b, first the per-wave list of its records that reach this
         // quadrant and are not behind every pixel's last contributor (order-preserving)
@@ -637,18 +630,16 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                 }
 #pragma unroll
                 for (int k = 0; k < 7; ++k) asm volatile("" : "+v"(g[k]));
-                float* dst = s_part + t * KVP;
-                if (r16 == 0) {
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) atomicAdd(dst + k, g[k]);  // ds_add_f32
-                    if (ABS) {
-                        constexpr float kLn2 = 0.6931471805599453f;
-                        atomicAdd(dst + 6 + D, kLn2 * A0);
-                        atomicAdd(dst + 7 + D, kLn2 * A1);
-                    }
+                {
+                    // one float atomic per value straight into the Gaussian's accumulator row:
+                    // the four waves' partials meet in L2 (no LDS staging, no per-batch combine)
+                    constexpr float kLn2 = 0.6931471805599453f;
+                    float v = qlo == 0 ? (qb2 ? g[3] : g[0]) : qlo == 1 ? (qb2 ? g[4] : g[1]) : (qb2 ? g[5] : g[2]);
+                    v = qlo == 3 ? g[6] : v;
+                    if (ABS) v = r16 == 8 ? kLn2 * A0 : r16 == 9 ? kLn2 * A1 : v;
+                    if (koff >= 0 && t < NB && v != 0.f)
+                        atomicAdd(acc_rows + (int64_t)s_id[cur][t] * kRec3 + koff, v);
                 }
-                // colour channel of lane class (b3, b2): 0 (0,0), 1 (1,0), 2 (0,1), 3 (1,1)
-                if ((r16 & 3) == 0) atomicAdd(dst + 6 + ((r16 >> 3) | ((r16 >> 1) & 2)), g[6]);
             };
             auto group = [&](const int lst, const int i0, const int li) {
                 float F[4], V[4];
@@ -661,11 +652,10 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
             for (int i = 0; i < n0; i += 4) group(lst0, i, i);
             for (int i = 64; i < n_mine; i += 4) group(lst1, i - 64, i);
         }
-        prev_bsz = bsz;
         lds_barrier();
     }
     if (pair_counter && lane == 0 && stepped)  // measurement only: lane-pairs stepped
-        atomicAdd(pair_counter + 1, (unsigned long long)stepped * 64ull);
+        atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
 }
 
 // scatter accumulator rows into gsplat's separate gradient tensors (overwrite);

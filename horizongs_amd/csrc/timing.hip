@@ -24,6 +24,7 @@ std::string g_only;  // record only this kernel (empty = all)
 // device counters of the timed raster bwd: [0] (pixel, Gaussian) pairs visited (gsplat's span),
 // [1] lane-pairs stepped (compacted list entries x 64)
 unsigned long long* g_pairs = nullptr;
+constexpr size_t kPairBytes = (size_t)kPairSlots * 2 * 16 * sizeof(unsigned long long);
 }  // namespace
 
 bool timing_on() { return g_on; }
@@ -50,10 +51,24 @@ unsigned long long* timing_pair_counter(const char* kernel) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_on || (!g_only.empty() && g_only != kernel)) return nullptr;
     if (!g_pairs) {
-        if (hipMalloc(&g_pairs, 2 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
-        if (hipMemset(g_pairs, 0, 2 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+        if (hipMalloc(&g_pairs, kPairBytes) != hipSuccess) return nullptr;
+        if (hipMemset(g_pairs, 0, kPairBytes) != hipSuccess) return nullptr;
     }
     return g_pairs;
+}
+
+// counter `which` summed over the workgroup slots (pair_slot in common.h)
+static int read_pairs(int which, unsigned long long* out) {
+    std::vector<unsigned long long> h(kPairBytes / sizeof(unsigned long long));
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(h.data(), g_pairs, kPairBytes, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error("timing: pair counter read failed");
+        return HGSR_ELAUNCH;
+    }
+    unsigned long long v = 0;
+    for (int s = 0; s < kPairSlots; ++s) v += h[(s * 2 + which) * 16];
+    *out = v;
+    return HGSR_OK;
 }
 
 void timing_end(int id, hipStream_t s) {
@@ -82,12 +97,8 @@ extern "C" int hgsr_timing_pairs(unsigned long long* out, int reset) {
     std::lock_guard<std::mutex> lk(g_mu);
     unsigned long long v = 0;
     if (g_pairs) {
-        if (hipDeviceSynchronize() != hipSuccess ||
-            hipMemcpy(&v, g_pairs, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) {
-            set_error("timing: pair counter read failed");
-            return HGSR_ELAUNCH;
-        }
-        if (reset && hipMemset(g_pairs, 0, 2 * sizeof(v)) != hipSuccess) return HGSR_ELAUNCH;
+        if (int st = read_pairs(0, &v)) return st;
+        if (reset && hipMemset(g_pairs, 0, kPairBytes) != hipSuccess) return HGSR_ELAUNCH;
     }
     if (out) *out = v;
     return HGSR_OK;
@@ -96,13 +107,8 @@ extern "C" int hgsr_timing_pairs(unsigned long long* out, int reset) {
 extern "C" int hgsr_timing_exec_pairs(unsigned long long* out) {
     std::lock_guard<std::mutex> lk(g_mu);
     unsigned long long v = 0;
-    if (g_pairs) {
-        if (hipDeviceSynchronize() != hipSuccess ||
-            hipMemcpy(&v, g_pairs + 1, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) {
-            set_error("timing: pair counter read failed");
-            return HGSR_ELAUNCH;
-        }
-    }
+    if (g_pairs)
+        if (int st = read_pairs(1, &v)) return st;
     if (out) *out = v;
     return HGSR_OK;
 }
