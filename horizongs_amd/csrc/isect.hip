@@ -328,15 +328,16 @@ __global__ __launch_bounds__(256) void isect_emit_global_kernel(
 // a wave they arrive by DPP / ds_swizzle / v_permlane32_swap (no LDS memory); only
 // partners in another wave go through LDS (lane-contiguous, conflict-free layout).
 // The network is unrolled at compile time.
+// (mov_dpp, not update_dpp with an old value: no v_mov initialising the destination first)
 template <int M>
 __device__ __forceinline__ uint32_t lane_xor32(uint32_t x) {
-    if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-    else if constexpr (M == 3) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x1B, 0xF, 0xF, false);  // quad_perm [3,2,1,0]
+    if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+    else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+    else if constexpr (M == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x1B, 0xF, 0xF, true);  // quad_perm [3,2,1,0]
     else if constexpr (M == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (4 << 10));
-    else if constexpr (M == 7) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
-    else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
-    else if constexpr (M == 15) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);  // row_mirror
+    else if constexpr (M == 7) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, true);  // row_half_mirror
+    else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, true);  // row_ror:8
+    else if constexpr (M == 15) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true);  // row_mirror
     else if constexpr (M == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (16 << 10));
     else if constexpr (M == 31) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (31 << 10));
     else if constexpr (M == 32) {

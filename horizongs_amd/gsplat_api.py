@@ -51,6 +51,17 @@ def _unsupported(flag, what):
 # =========================================================================
 # projection
 # =========================================================================
+def _grads_or_zeros(grads, lead, tails, like):
+    """Output gradients of a projection (materialize_grads off): zeros for unused outputs."""
+    out = []
+    for g, t in zip(grads, tails):
+        if g is None:
+            shape = lead + (() if t is None else (t if isinstance(t, tuple) else (t,)))
+            g = torch.zeros(shape, dtype=torch.float32, device=like.device)
+        out.append(g)
+    return out
+
+
 class _Project3D(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means, quats, scales, viewmats, Ks, width, height, eps2d, near_plane, far_plane,
@@ -67,6 +78,7 @@ class _Project3D(torch.autograd.Function):
         ctx.save_for_backward(means, quats, scales, viewmats, Ks, radii, conics)
         ctx.cfg = (width, height, eps2d)
         ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)  # no zero-filled int grad for radii per step
         return radii, means2d, depths, conics
 
     @staticmethod
@@ -77,6 +89,7 @@ class _Project3D(torch.autograd.Function):
         v_means = torch.empty_like(means)
         v_quats = torch.empty_like(quats)
         v_scales = torch.empty_like(scales)
+        v_means2d, v_depths, v_conics = _grads_or_zeros((v_means2d, v_depths, v_conics), (C, Ng), (2, None, 3), means)
         N.call("hgsr_project3d_bwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks), width,
                height, eps2d, ptr(radii), ptr(conics), ptr(_f32(v_means2d)), ptr(_f32(v_depths)),
                ptr(_f32(v_conics)), ptr(v_means), ptr(v_quats), ptr(v_scales), N.stream(means.device))
@@ -120,6 +133,7 @@ class _Project2D(torch.autograd.Function):
         ctx.save_for_backward(means, quats, scales, viewmats, Ks, radii, rt)
         ctx.cfg = (width, height)
         ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)  # no zero-filled int grad for radii per step
         return radii, means2d, depths, rt, normals
 
     @staticmethod
@@ -130,6 +144,8 @@ class _Project2D(torch.autograd.Function):
         v_means = torch.empty_like(means)
         v_quats = torch.empty_like(quats)
         v_scales = torch.empty_like(scales)
+        v_means2d, v_depths, v_rt, v_normals = _grads_or_zeros((v_means2d, v_depths, v_rt, v_normals), (C, Ng),
+                                                               (2, None, (3, 3), 3), means)
         N.call("hgsr_project2d_bwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks), width,
                height, ptr(radii), ptr(rt), ptr(_f32(v_means2d)), ptr(_f32(v_depths)), ptr(_f32(v_rt)),
                ptr(_f32(v_normals)), ptr(v_means), ptr(v_quats), ptr(v_scales), N.stream(means.device))
