@@ -57,9 +57,9 @@ __device__ __forceinline__ TileCtx tile_ctx(int C, int W, int H, int tw, int th,
 
 // 48-B raster record of one (camera, Gaussian).  The conic is stored pre-scaled,
 // {a', b', c'} = log2(e) * {a/2, b, c/2}, so that
-//   sigma' = a' dx^2 + c' dy^2 + b' dx dy = log2(e) * sigma,  vis = exp2(-sigma')
+//   sigma' = dx (a' dx + b' dy) + c' dy^2 = log2(e) * sigma,  vis = exp2(-sigma')
 // costs three products and two FMAs and feeds v_exp_f32 directly (same value as
-// gsplat's exp(-sigma) up to the last ulp; forward and backward share sigma2()).
+// gsplat's exp(-sigma) up to the last ulps; forward and backward share sigma2()).
 constexpr float kLog2e = 1.4426950408889634f;
 struct Rec3 {
     float4 g0;  // x, y, a', b'
@@ -67,13 +67,10 @@ struct Rec3 {
     float4 col; // colour (D <= 4, zero padded)
 };
 
-// sigma' of a record at offset (dx, dy); xx, yy, xy are returned for the backward
-__device__ __forceinline__ float sigma2(const float4 g0, const float4 g1, float dx, float dy, float& xx, float& yy,
-                                        float& xy) {
-    xx = dx * dx;
-    yy = dy * dy;
-    xy = dx * dy;
-    return __builtin_fmaf(g0.w, xy, __builtin_fmaf(g1.x, yy, g0.z * xx));
+// sigma' of a record at offset (dx, dy), factored as dx (a' dx + b' dy) + (c' dy) dy
+__device__ __forceinline__ float sigma2(const float4 g0, const float4 g1, float dx, float dy) {
+    const float h = __builtin_fmaf(g0.w, dy, g0.z * dx);
+    return __builtin_fmaf(g1.x * dy, dy, dx * h);
 }
 
 // Exact screen-space half-extents of the region where alpha = o*exp(-sigma) can
@@ -151,8 +148,7 @@ template <int D>
 __device__ __forceinline__ void fwd_step(const float4 g0, const float4 g1, const float4 c, uint32_t idx, float px,
                                          float py, float& T, float (&acc)[4], uint32_t& cur) {
     const float dx = g0.x - px, dy = g0.y - py;
-    float xx, yy, xy;
-    const float sigma = sigma2(g0, g1, dx, dy, xx, yy, xy);
+    const float sigma = sigma2(g0, g1, dx, dy);
     const float alpha = fminf(0.999f, g1.y * __builtin_amdgcn_exp2f(-sigma));
     const float nT = T * (1.0f - alpha);
     const bool valid = (sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
@@ -523,8 +519,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
             auto step = [&](const int t, float& F, float& V) {
                 const float4 g0 = sr.g0[cur][t], g1 = sr.g1[cur][t], c = sr.col[cur][t];
                 const float dx = g0.x - tc.px, dy = g0.y - tc.py;
-                float xx, yy, xy;
-                const float sigma = sigma2(g0, g1, dx, dy, xx, yy, xy);
+                const float sigma = sigma2(g0, g1, dx, dy);
                 const float vis = __builtin_amdgcn_exp2f(-sigma);
                 const float araw = g1.y * vis;
                 const float alpha = fminf(0.999f, araw);
