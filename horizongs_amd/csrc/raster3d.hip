@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     // sigma sums (and |v_xy|) and each quad one colour channel; lane r16 = 4 q + 3 adds its
     // quad's channel, lanes 0-2 / 4-6 the sums 0-2 / 3-5, lanes 8 / 9 the |v_xy| pair (ABS)
     const int qlo = r16 & 3;
-    const bool qb2 = (r16 >> 2) & 1;
+    const bool qb2 = (r16 >> 2) & 1, qsel1 = qlo == 1, qsel2 = qlo == 2, qcol = qlo == 3;
     const int koff = qlo == 3 ? 6 + ((r16 >> 3) | ((r16 >> 1) & 2))
                    : r16 < 8  ? qlo + (qb2 ? 3 : 0)
                    : (ABS && r16 == 8) ? 6 + D
@@ -562,7 +562,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                 const int t = my_list[li + slot];  // this lane's Gaussian (list entry li + slot)
                 const float4 g0 = sr.g0[cur][t];
                 const float dx = g0.x - p2.pxc, dy0 = g0.y - p2.py0c;
-                float S0 = 0.f, Sy = 0.f, Syy = 0.f, P[4] = {0.f, 0.f, 0.f, 0.f}, A0 = 0.f, A1 = 0.f;
+                float S0, Sy, Syy, P[4], A0 = 0.f, A1 = 0.f;
                 float ax = 0.f, ay = 0.f, bx = 0.f, c2 = 0.f;
                 if (ABS) {
                     const float4 g1 = sr.g1[cur][t];
@@ -571,15 +571,16 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                     ay = g0.w;
                     c2 = 2.f * g1.x;
                 }
+                // the sums start from the first pixel's terms (an add to +0 is not foldable)
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
                     const float dy = dy0 - (float)(2 * m);
                     const float vdy = V[m] * dy;
-                    S0 += V[m];
-                    Sy += vdy;
-                    Syy = __builtin_fmaf(vdy, dy, Syy);
+                    S0 = m ? S0 + V[m] : V[m];
+                    Sy = m ? Sy + vdy : vdy;
+                    Syy = m ? __builtin_fmaf(vdy, dy, Syy) : vdy * dy;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) P[q] = __builtin_fmaf(F[m], p2.vo[m][q], P[q]);
+                    for (int q = 0; q < 4; ++q) P[q] = m ? __builtin_fmaf(F[m], p2.vo[m][q], P[q]) : F[m] * p2.vo[m][q];
                     if (ABS) {  // |per-pixel v_means2d| up to ln 2: |v_sigma (2a'dx + b'dy)|, |v_sigma (b'dx + 2c'dy)|
                         A0 += fabsf(V[m] * __builtin_fmaf(ay, dy, ax));
                         A1 += fabsf(V[m] * __builtin_fmaf(c2, dy, bx));
@@ -603,6 +604,11 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                 g[3] = dx * Sy;       // Sxy
                 g[4] = Syy;           // Syy
                 g[5] = S0;            // sum v_sigma (split3: opacity gradient = -S0 / opacity)
+                // opaque products: the next level's DPP add must not be contracted into an FMA
+                // (that recomputes the product and needs a separate DPP move)
+                asm volatile("" : "+v"(g[0]));
+                asm volatile("" : "+v"(g[2]));
+                asm volatile("" : "+v"(g[3]));
                 // level 2 (half mirror, partner r ^ 7): colours transposed again
                 g[6] = C01 + dpp<0x141>(C23);
 #pragma unroll
@@ -629,8 +635,10 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                     // one float atomic per value straight into the Gaussian's accumulator row:
                     // the four waves' partials meet in L2 (no LDS staging, no per-batch combine)
                     constexpr float kLn2 = 0.6931471805599453f;
-                    float v = qlo == 0 ? (qb2 ? g[3] : g[0]) : qlo == 1 ? (qb2 ? g[4] : g[1]) : (qb2 ? g[5] : g[2]);
-                    v = qlo == 3 ? g[6] : v;
+                    const float a = qb2 ? g[3] : g[0], b = qb2 ? g[4] : g[1], c = qb2 ? g[5] : g[2];
+                    float v = qsel1 ? b : a;
+                    v = qsel2 ? c : v;
+                    v = qcol ? g[6] : v;
                     if (ABS) v = r16 == 8 ? kLn2 * A0 : r16 == 9 ? kLn2 * A1 : v;
                     if (koff >= 0 && t < NB && v != 0.f)
                         atomicAdd(acc_rows + (int64_t)s_id[cur][t] * kRec3 + koff, v);
