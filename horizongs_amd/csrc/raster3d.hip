@@ -16,7 +16,7 @@
 //  * backward: replay back-to-front bounded by the tile's latest contributor,
 //    wave-ballot skip of Gaussians no lane sees, all gradient components
 //    reduced across the wave together (step-major DPP, no hazard stalls), and
-//    each wave's sums go straight to the Gaussian's 64-byte accumulator row as
+//    each wave's sums go straight to the Gaussian's 48-byte accumulator row as
 //    one float-atomic instruction per 4 steps (the waves' partials meet in L2).
 #include "common.h"
 
@@ -24,7 +24,7 @@ namespace hgsr {
 
 constexpr int kFwdBatch = 256;
 constexpr int kBwdBatch = 128;
-constexpr int kRec3 = 16;  // floats per accumulator row: sigma moments(5) opac(1) color(D<=4) absxy(2)
+constexpr int kRec3 = 12;  // floats per accumulator row (48 B): sigma moments(5) S0(1) color(D<=4) absxy(2)
 
 struct TileCtx {
     int cam, tile, i, j;
