@@ -18,7 +18,7 @@
 //    reduced across the wave together (step-major DPP, no hazard stalls), and
 //    each wave's sums go straight to the Gaussian's 48-byte accumulator row as
 //    one float-atomic instruction per 4 steps (the waves' partials meet in L2).
-#include "common.h"
+#include "rec3.h"
 
 namespace hgsr {
 
@@ -55,36 +55,10 @@ __device__ __forceinline__ TileCtx tile_ctx(int C, int W, int H, int tw, int th,
     return t;
 }
 
-// 48-B raster record of one (camera, Gaussian).  The conic is stored pre-scaled,
-// {a', b', c'} = log2(e) * {a/2, b, c/2}, so that
-//   sigma' = dx (a' dx + b' dy) + c' dy^2 = log2(e) * sigma,  vis = exp2(-sigma')
-// costs three products and two FMAs and feeds v_exp_f32 directly (same value as
-// gsplat's exp(-sigma) up to the last ulps; forward and backward share sigma2()).
-constexpr float kLog2e = 1.4426950408889634f;
-struct Rec3 {
-    float4 g0;  // x, y, a', b'
-    float4 g1;  // c', opacity, footprint half-extent x, half-extent y
-    float4 col; // colour (D <= 4, zero padded)
-};
-
 // sigma' of a record at offset (dx, dy), factored as dx (a' dx + b' dy) + (c' dy) dy
 __device__ __forceinline__ float sigma2(const float4 g0, const float4 g1, float dx, float dy) {
     const float h = __builtin_fmaf(g0.w, dy, g0.z * dx);
     return __builtin_fmaf(g1.x * dy, dy, dx * h);
-}
-
-// Exact screen-space half-extents of the region where alpha = o*exp(-sigma) can
-// reach 1/255: 0.5 d^T Conic d <= L, L = ln(255 o); the ellipse's bounding box
-// is |dx| <= sqrt(2L * Cov_xx), |dy| <= sqrt(2L * Cov_yy) with Cov = Conic^-1.
-// Padded by 1 % + 0.01 px (the kernels use the hardware exp).  Purely a skip
-// test: a Gaussian outside a wave's quadrant by this box has alpha < 1/255 at
-// every pixel of it, so skipping it changes no result.
-__device__ __forceinline__ float2 footprint(float a, float b, float c, float opac) {
-    const float L = __logf(255.0f * opac);
-    const float det = a * c - b * b;
-    if (!(L > 0.f) || !(det > 0.f)) return make_float2(-1e30f, -1e30f);
-    const float k = 2.0f * L / det;
-    return make_float2(sqrtf(k * c) * 1.01f + 0.01f, sqrtf(k * a) * 1.01f + 0.01f);
 }
 
 template <int D>
@@ -97,16 +71,11 @@ __global__ __launch_bounds__(256) void pack3_kernel(int64_t n, int N, const floa
     const float2 m = means2d[i];
     const float a = conics[i * 3], b = conics[i * 3 + 1], cc = conics[i * 3 + 2];
     const float o = cs.opac[c * cs.op_cstride + g];
-    const float2 ext = footprint(a, b, cc, o);
-    Rec3 r;
-    r.g0 = make_float4(m.x, m.y, (0.5f * kLog2e) * a, kLog2e * b);
-    r.g1 = make_float4((0.5f * kLog2e) * cc, o, ext.x, ext.y);
     float col[4] = {0.f, 0.f, 0.f, 0.f};
     const float* src = cs.colors + c * cs.col_cstride + g * cs.dc;
 #pragma unroll
     for (int k = 0; k < D; ++k) col[k] = k < cs.dc ? src[k] : cs.depths[i];
-    r.col = make_float4(col[0], col[1], col[2], col[3]);
-    rec[i] = r;
+    rec[i] = make_rec3(m, a, b, cc, o, col);
 }
 
 // does the footprint box of (g0, g1) reach the 8x8 quadrant centred at (qx, qy)?

@@ -11,5 +11,5 @@ libs = os.environ["LIBS"].split()
 for n in range(1, len(libs) + 1):
   for r in ('1','2'):
     d=json.loads(open(f'gpurun_out/libs/{n}.{r}.json').read().strip().splitlines()[-1]); k=d['kernels']
-    print(libs[n-1].split('/')[-1], r, d['value'], d['ms_per_step'], {x:k[x]['avg_ms'] for x in k if x in ('isect_emit','tile_sort','raster3d_fwd','raster3d_bwd','raster2d_fwd','raster2d_bwd')})
+    print(libs[n-1].split('/')[-1], r, d['value'], d['ms_per_step'], {x:k[x]['avg_ms'] for x in k if x in ('isect_emit','tile_sort','raster3d_fwd','raster3d_bwd','raster2d_fwd','raster2d_bwd','project3d_bwd','adam','loss_fwd','loss_bwd')})
 PY

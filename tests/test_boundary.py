@@ -58,8 +58,8 @@ def test_pure_host_entry_points(lib):
     assert _native.size_query("hgsr_isect_ws1_bytes", 1, 2_000_000, 120, 68) > 0
     assert _native.size_query("hgsr_isect_ws2_bytes", 1000, 10) >= 8000
     assert _native.size_query("hgsr_isect_ws2_bytes", 1000, 5000) >= 16000
-    assert _native.size_query("hgsr_raster3d_bwd_ws_bytes", 1, 100, 4, 0) >= 100 * 16 * 4 + 100 * 48
-    assert _native.size_query("hgsr_raster3d_bwd_ws_bytes", 1, 100, 4, 1) >= 100 * 16 * 4
+    assert _native.size_query("hgsr_raster3d_bwd_ws_bytes", 1, 100, 4, 0) >= 100 * 12 * 4 + 100 * 48
+    assert _native.size_query("hgsr_raster3d_bwd_ws_bytes", 1, 100, 4, 1) >= 100 * 12 * 4
     assert _native.size_query("hgsr_raster2d_bwd_ws_bytes", 1, 100, 4, 0) >= 100 * 32 * 4 + 100 * 96
 
 
