@@ -35,17 +35,34 @@ __host__ __device__ inline int nbits64(int64_t v) {
     return b;
 }
 
-// gsplat isect_tiles rectangle; identical float ops to oracle/hgsr_oracle.c tile_rect
+// gsplat isect_tiles rectangle; identical float ops to oracle/hgsr_oracle.c tile_rect.  For a
+// power-of-two tile size (gsplat's 16) x / tile_size is x times the exact reciprocal, bit for
+// bit, so the correctly rounded division sequence is only run for other sizes.
 __device__ __forceinline__ void tile_rect(float mx, float my, int32_t radius, int tile_size, int tw,
                                           int th, int& x0, int& y0, int& x1, int& y1) {
 #pragma clang fp contract(off)
-    const float tr = (float)radius / (float)tile_size;
-    const float tx = mx / (float)tile_size, ty = my / (float)tile_size;
+    const float ts = (float)tile_size;
+    float tr, tx, ty;
+    if ((tile_size & (tile_size - 1)) == 0) {
+        const float inv = __int_as_float(0x7F000000 - __float_as_int(ts));  // 2^-k exactly
+        tr = (float)radius * inv;
+        tx = mx * inv;
+        ty = my * inv;
+    } else {
+        tr = (float)radius / ts;
+        tx = mx / ts;
+        ty = my / ts;
+    }
     const float fx0 = floorf(tx - tr), fy0 = floorf(ty - tr), fx1 = ceilf(tx + tr), fy1 = ceilf(ty + tr);
     x0 = fx0 <= 0.f ? 0 : (fx0 >= (float)tw ? tw : (int)fx0);
     y0 = fy0 <= 0.f ? 0 : (fy0 >= (float)th ? th : (int)fy0);
     x1 = fx1 <= 0.f ? 0 : (fx1 >= (float)tw ? tw : (int)fx1);
     y1 = fy1 <= 0.f ? 0 : (fy1 >= (float)th ? th : (int)fy1);
+}
+
+// camera of flattened index o (< 2^31 by the entry checks): 32-bit division, none for o < N
+__device__ __forceinline__ int cam_of(int64_t o, int N) {
+    return o < N ? 0 : (int)((uint32_t)o / (uint32_t)N);
 }
 
 struct IsectGeom {
@@ -106,7 +123,7 @@ __global__ __launch_bounds__(256) void isect_count_lds_kernel(
             int x0, y0, x1, y1;
             tile_rect(m[k].x, m[k].y, r[k], tile_size, tw, th, x0, y0, x1, y1);
             tiles_per_gauss[o] = (y1 - y0) * (x1 - x0);
-            const int base = (int)(o / N) * n_tiles;
+            const int base = cam_of(o, N) * n_tiles;
             for (int y = y0; y < y1; ++y)
                 for (int x = x0; x < x1; ++x) atomicAdd(&s_hist[base + y * tw + x], 1);
         }
@@ -131,7 +148,7 @@ __global__ __launch_bounds__(256) void isect_count_global_kernel(
     int x0, y0, x1, y1;
     tile_rect(m.x, m.y, r, tile_size, tw, th, x0, y0, x1, y1);
     tiles_per_gauss[o] = (y1 - y0) * (x1 - x0);
-    const int base = (int)(o / N) * n_tiles;
+    const int base = cam_of(o, N) * n_tiles;
     for (int y = y0; y < y1; ++y)
         for (int x = x0; x < x1; ++x) atomicAdd(&totals[base + y * tw + x], 1);
 }
@@ -290,7 +307,7 @@ __global__ __launch_bounds__(256) void isect_emit_lds_kernel(
                 if (y0 >= y1) continue;
                 const int64_t o = ob + 256 * k;
                 const uint64_t key = ((uint64_t)__float_as_uint(d[k]) << 32) | (uint32_t)o;
-                const int base = (int)(o / N) * n_tiles;
+                const int base = cam_of(o, N) * n_tiles;
                 for (int y = y0; y < y1; ++y)
                     for (int x = rx0[k]; x < rx1[k]; ++x) {
                         const int pos = atomicAdd(&s_cur[base + y * tw + x], 1);
@@ -313,7 +330,7 @@ __global__ __launch_bounds__(256) void isect_emit_global_kernel(
     int x0, y0, x1, y1;
     tile_rect(m.x, m.y, r, tile_size, tw, th, x0, y0, x1, y1);
     const uint64_t key = ((uint64_t)__float_as_uint(depths[o]) << 32) | (uint32_t)o;
-    const int base = (int)(o / N) * n_tiles;
+    const int base = cam_of(o, N) * n_tiles;
     for (int y = y0; y < y1; ++y)
         for (int x = x0; x < x1; ++x) keys[atomicAdd(&cursor[base + y * tw + x], 1)] = key;
 }
