@@ -162,8 +162,12 @@ class _Decode(torch.autograd.Function):
         del arr
         ctx.save_for_backward(anchor, feat, offset, scaling_raw, cam_center, vis_idx, slot_row, *w)
         ctx.cfg = cfg
-        ctx.mark_non_differentiable(mask)
-        return t["xyz"], t["offsets"], t["color"], t["opacity"], t["scaling"], t["rot"], mask.bool()
+        sel = mask.view(torch.bool)  # 0/1 bytes: a view, no conversion kernel
+        # the output row of every selected slot IS the exclusive cumsum of the selection mask:
+        # training_statis takes it from here instead of recomputing it
+        sel._hgsr_slot_row = slot_row
+        ctx.mark_non_differentiable(sel)
+        return t["xyz"], t["offsets"], t["color"], t["opacity"], t["scaling"], t["rot"], sel
 
     @staticmethod
     def backward(ctx, g_xyz, g_offs, g_color, g_opac, g_scaling, g_rot, g_mask):

@@ -32,6 +32,13 @@ def _check_dev(*ts):
             raise RuntimeError("hgsr: inputs must be HIP device tensors (no CPU fallback)")
 
 
+def _as_u8(mask):
+    """A bool / 0-1 mask as contiguous uint8 (a view of a contiguous bool tensor: no copy)."""
+    if mask.dtype == torch.bool and mask.is_contiguous():
+        return mask.view(torch.uint8)
+    return mask.to(torch.uint8).contiguous()
+
+
 def _state(t, name):
     if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
         raise RuntimeError(f"hgsr training_statis: model.{name} must be a contiguous float32 HIP tensor")
@@ -43,7 +50,9 @@ def training_statis(model, opt, render_pkg, width, height):
     """BasicModel.training_statis: updates model.{anchor_opacity_accum, anchor_demon,
     offset_gradient_accum, offset_denom[, max_radii2D, offset_opacity_accum]} in place.
     Unlike the reference it leaves viewspace_points.grad unscaled."""
-    sel = render_pkg["selection_mask"].reshape(-1)
+    sel_t = render_pkg["selection_mask"]
+    slot_row = getattr(sel_t, "_hgsr_slot_row", None)  # set by the fused decode
+    sel = sel_t.reshape(-1)
     vis = render_pkg["visible_mask"].reshape(-1)
     grad = render_pkg["viewspace_points"].grad
     filt = render_pkg["visibility_filter"].reshape(-1)
@@ -62,11 +71,14 @@ def training_statis(model, opt, render_pkg, width, height):
     Av = vis_idx.numel()
     if sel.numel() != Av * noff:
         raise ValueError(f"hgsr training_statis: selection_mask has {sel.numel()} slots, expected {Av * noff}")
-    sel8 = sel.to(torch.uint8).contiguous()
-    rank = (torch.cumsum(sel8, 0, dtype=torch.int32) - sel8).contiguous()
+    sel8 = _as_u8(sel)
+    if slot_row is not None and slot_row.numel() == sel.numel():
+        rank = slot_row  # output row of each selected slot (the decode's compaction)
+    else:
+        rank = (torch.cumsum(sel8, 0, dtype=torch.int32) - sel8).contiguous()
     gmax = opt.growing_type == "max"
     N.call("hgsr_training_statis", Av, noff, int(width), int(height), int(opt.pruning_type == "max"), int(gmax),
-           ptr(vis_idx), ptr(sel8), ptr(rank), ptr(filt.to(torch.uint8).contiguous()),
+           ptr(vis_idx), ptr(sel8), ptr(rank), ptr(_as_u8(filt)),
            ptr(grad.reshape(-1, 2).float().contiguous()), ptr(opacity.float().contiguous()),
            ptr(radii.to(torch.int32).contiguous()) if gmax else None,
            ptr(_state(model.anchor_opacity_accum, "anchor_opacity_accum")),
