@@ -187,7 +187,8 @@ class Workload:
             # scales, compacted on the device into the visible-anchor index the decode consumes
             with torch.no_grad():
                 visible, vis_idx = HD.prefilter(self.anchor.detach(), torch.exp(self.scaling_raw.detach()),
-                                                self.anchor_quats, self.viewmats[0], self.Ks[0], W, H, lod=self.lod)
+                                                self.anchor_quats, self.viewmats[0], self.Ks[0], W, H, lod=self.lod,
+                                                lazy=True)  # Av stays on the device: one sync less
             xyz, _, cols, opac, scales, quats, sel = HD.decode(self.anchor, self.feat, self.offset, self.scaling_raw,
                                                                self.cam_center, self.mlps, vis_idx, 3, 10, 3)
             opac = opac.reshape(-1)

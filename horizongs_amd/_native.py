@@ -67,7 +67,7 @@ _SIGS = {
                                     P, P, P, P, P, P, P, P, P, P, P, SZ, P, SZ, P]),
     "hgsr_lod_mask": (I, [I, P, P, P, P, F, F, F, I, P, P]),
     "hgsr_decode_ws_bytes": (SZ, [I]),
-    "hgsr_decode_count": (I, [I, I, I, I, I, P, P, P, P, P, P, SZ, P, P]),
+    "hgsr_decode_count": (I, [I, I, I, I, I, P, P, P, P, P, P, SZ, P, P, P]),
     "hgsr_decode_fwd": (I, [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P]),
     "hgsr_decode_bwd_ws_bytes": (SZ, [I]),
     "hgsr_decode_bwd": (I, [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P]),

@@ -260,8 +260,10 @@ __global__ __launch_bounds__(256) void decode_count_kernel(DecodeDims d, MlpPtrs
                                                            const float* __restrict__ anchor,
                                                            const float* __restrict__ feat,
                                                            const float* __restrict__ cam,
-                                                           int32_t* __restrict__ tile_cnt) {
+                                                           int32_t* __restrict__ tile_cnt,
+                                                           const int64_t* __restrict__ av_dev) {
     __shared__ CountSmem sm;
+    if (av_dev) d.Av = (int)*av_dev;  // device-resident visible count (d.Av was the capacity)
     stage_weights(sm, mp, d, 32, 16);  // opacity head only
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
@@ -288,8 +290,10 @@ __global__ __launch_bounds__(256) void decode_count_kernel(DecodeDims d, MlpPtrs
 
 // exclusive scan of the tile counts -> tile offsets; total = number of kept Gaussians
 __global__ __launch_bounds__(1024) void decode_scan_kernel(int n, const int32_t* __restrict__ cnt,
-                                                           int32_t* __restrict__ off, int64_t* __restrict__ total) {
+                                                           int32_t* __restrict__ off, int64_t* __restrict__ total,
+                                                           const int64_t* __restrict__ av_dev) {
     __shared__ int64_t s_sum[1024];
+    if (av_dev) n = (int)((*av_dev + kDecTile - 1) / kDecTile);
     const int tid = threadIdx.x;
     const int per = (n + 1023) / 1024;
     const int b0 = min(tid * per, n), b1 = min(b0 + per, n);
@@ -999,7 +1003,7 @@ extern "C" size_t hgsr_decode_ws_bytes(int Av) {
 extern "C" int hgsr_decode_count(int Av, int F, int view_dim, int n_offsets, int color_dim,
                                  const int32_t* vis_idx, const float* anchor, const float* feat,
                                  const float* cam_center, const float* const* mlp, void* ws, size_t ws_bytes,
-                                 int64_t* total, hgsr_stream_t stream) {
+                                 int64_t* total, const int64_t* av_dev, hgsr_stream_t stream) {
     const DecodeDims d = decode_dims(Av, view_dim, n_offsets, color_dim);
     if (int st = check_decode(Av, F, view_dim, n_offsets, color_dim, d)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_decode_ws_bytes(Av), "decode workspace too small");
@@ -1010,17 +1014,19 @@ extern "C" int hgsr_decode_count(int Av, int F, int view_dim, int n_offsets, int
     for (int q = 0; q < 12; ++q) HGSR_REQUIRE(mlp[q], "null MLP pointer %d", q);
     const MlpPtrs mp = mlp_ptrs(mlp);
     const int n_tiles = (Av + kDecTile - 1) / kDecTile;
-    int32_t* cnt = (int32_t*)ws;
-    int32_t* off = (int32_t*)((char*)ws + (((size_t)(n_tiles + 1) * 4 + 255) & ~(size_t)255));
+    // tile offsets first (decode_fwd finds them at the workspace start whatever Av it is given),
+    // tile counts after them
+    int32_t* off = (int32_t*)ws;
+    int32_t* cnt = (int32_t*)((char*)ws + (((size_t)(n_tiles + 1) * 4 + 255) & ~(size_t)255));
     KernelTimer kt("decode_count", s);
     if (view_dim == 3)
         hipLaunchKernelGGL(decode_count_kernel<9>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
-                           feat, cam_center, cnt);
+                           feat, cam_center, cnt, av_dev);
     else
         hipLaunchKernelGGL(decode_count_kernel<8>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
-                           feat, cam_center, cnt);
+                           feat, cam_center, cnt, av_dev);
     if (int st = check_launch("decode_count")) return st;
-    hipLaunchKernelGGL(decode_scan_kernel, dim3(1), dim3(1024), 0, s, n_tiles, cnt, off, total);
+    hipLaunchKernelGGL(decode_scan_kernel, dim3(1), dim3(1024), 0, s, n_tiles, cnt, off, total, av_dev);
     return check_launch("decode_scan");
 }
 
@@ -1037,8 +1043,7 @@ extern "C" int hgsr_decode_fwd(int Av, int F, int view_dim, int n_offsets, int c
                  "null pointer");
     for (int q = 0; q < 12; ++q) HGSR_REQUIRE(mlp[q], "null MLP pointer %d", q);
     const MlpPtrs mp = mlp_ptrs(mlp);
-    const int n_tiles = (Av + kDecTile - 1) / kDecTile;
-    const int32_t* off = (const int32_t*)((char*)ws + (((size_t)(n_tiles + 1) * 4 + 255) & ~(size_t)255));
+    const int32_t* off = (const int32_t*)ws;  // written by hgsr_decode_count's scan
     DecodeOut out{xyz, offsets_out, color, opacity, scaling, rot, mask, slot_row};
     hipStream_t s = as_stream(stream);
     KernelTimer kt("decode_fwd", s);

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes as ct
 import math
+import threading
 
 import torch
 
@@ -59,15 +60,36 @@ def lod_mask(anchor, level, extra_level, cam_center, res_scale, standard_dist, f
     return mask.bool()
 
 
+class VisibleIndex:
+    """The visible-anchor index of prefilter(lazy=True) with its length still on the device:
+    `buf` int32 [A] holds the ordered visible ids in its first Av entries, `counts` (device
+    int64 [2]) holds Av in [1] and receives the decode's kept count in [0], so the decode reads
+    both with ONE host sync instead of one each."""
+
+    def __init__(self, buf, counts, visible):
+        self.buf, self.counts, self.visible = buf, counts, visible
+
+
+_pinned_dec = threading.local()
+
+
+def _pinned_pair():
+    buf = getattr(_pinned_dec, "buf", None)
+    if buf is None:
+        buf = _pinned_dec.buf = torch.empty(2, dtype=torch.int64, pin_memory=True)
+    return buf
+
+
 @torch.no_grad()
 def prefilter(anchor, scales, quats, viewmat, K, width, height, lod=None, eps2d=0.3, near_plane=0.01,
-              far_plane=1e10):
+              far_plane=1e10, lazy=False):
     """Fused set_anchor_mask + prefilter_voxel (scene/lod_model.py:286-290,
     gaussian_renderer/render.py:120-197): visible[a] = LoD test (lod = dict(level, extra_level,
     cam_center, res_scale, standard_dist, fork, street_levels), or None for all anchors) AND
     gsplat radius > 0 of the anchor projected with `scales` (activated, [A,3] or [A,6] of which
     the first three are used) and `quats`.  One kernel for the mask, then an ordered
-    compaction: returns (visible bool [A], vis_idx int32 [Av]); one host read (Av)."""
+    compaction: returns (visible bool [A], vis_idx int32 [Av]); one host read (Av).  With
+    lazy=True the index is a VisibleIndex for decode() and there is no host read here."""
     _check_dev(anchor, scales, quats, viewmat, K)
     A = anchor.shape[0]
     dev = anchor.device
@@ -90,9 +112,17 @@ def prefilter(anchor, scales, quats, viewmat, K, width, height, lod=None, eps2d=
            float(near_plane), float(far_plane), *args, ptr(vis), s)
     ws_b = N.size_query("hgsr_explicit_ws_bytes", A)
     ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
-    total = torch.empty(1, dtype=torch.int64, device=dev)
+    counts = torch.empty(2, dtype=torch.int64, device=dev)  # [decode's kept count, Av]
+    total = counts[1:]
     N.call("hgsr_explicit_count", A, None, None, None, None, 1.0, 1.0, 1.0, 0, ptr(vis), None, ptr(ws), ws_b,
            ptr(total), s)
+    if lazy:
+        buf = torch.empty(max(A, 1), dtype=torch.int32, device=dev)
+        if A:
+            N.call("hgsr_mask_index", A, ptr(vis), ptr(ws), ws_b, ptr(buf), s)
+        del keep
+        visible = vis.view(torch.bool)
+        return visible, VisibleIndex(buf, counts, visible)
     Av = int(total.item())  # the one host read (the reference's boolean mask indexing syncs too)
     vis_idx = torch.empty(Av, dtype=torch.int32, device=dev)
     if Av:
@@ -140,17 +170,35 @@ class _Decode(torch.autograd.Function):
     def forward(ctx, anchor, feat, offset, scaling_raw, cam_center, vis_idx, cfg, *weights):
         view_dim, n_off, color_dim = cfg
         dev = anchor.device
-        Av = vis_idx.numel()
         F = feat.shape[1]
         w = [_f32(t) for t in weights]
         arr, mlp = _ptr_array(w)
-        ws_b = N.size_query("hgsr_decode_ws_bytes", Av)
-        ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
-        total = torch.empty(1, dtype=torch.int64, device=dev)
         s = N.stream(dev)
-        N.call("hgsr_decode_count", Av, F, view_dim, n_off, color_dim, ptr(vis_idx), ptr(anchor), ptr(feat),
-               ptr(cam_center), mlp, ptr(ws), ws_b, ptr(total), s)
-        M = int(total.item())  # the one host sync (the reference's boolean masking has it too)
+        if isinstance(vis_idx, VisibleIndex):
+            # visible count still on the device: the count pass takes its upper bound A and
+            # reads Av there; Av and the kept count come back with one host read
+            vi = vis_idx
+            cap = vi.buf.numel()
+            ws_b = N.size_query("hgsr_decode_ws_bytes", cap)
+            ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
+            N.call("hgsr_decode_count", cap, F, view_dim, n_off, color_dim, ptr(vi.buf), ptr(anchor), ptr(feat),
+                   ptr(cam_center), mlp, ptr(ws), ws_b, ptr(vi.counts), vi.counts.data_ptr() + 8, s)
+            host = _pinned_pair()
+            host.copy_(vi.counts, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            ev.synchronize()
+            M, Av = int(host[0]), int(host[1])
+            vis_idx = vi.buf[:Av]
+            _VIS_CACHE[:] = [(vi.visible, vi.visible._version, vis_idx)]
+        else:
+            Av = vis_idx.numel()
+            ws_b = N.size_query("hgsr_decode_ws_bytes", Av)
+            ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
+            total = torch.empty(1, dtype=torch.int64, device=dev)
+            N.call("hgsr_decode_count", Av, F, view_dim, n_off, color_dim, ptr(vis_idx), ptr(anchor), ptr(feat),
+                   ptr(cam_center), mlp, ptr(ws), ws_b, ptr(total), None, s)
+            M = int(total.item())  # the one host sync (the reference's boolean masking has it too)
         out = dict(xyz=(M, 3), offsets=(M, 3), color=(M, color_dim), opacity=(M, 1), scaling=(M, 3), rot=(M, 4))
         t = {k: torch.empty(v, dtype=torch.float32, device=dev) for k, v in out.items()}
         mask = torch.empty(Av * n_off, dtype=torch.uint8, device=dev)
@@ -218,6 +266,8 @@ def decode(anchor, feat, offset, scaling_raw, cam_center, mlps, visible=None, vi
     A = anchor.shape[0]
     if visible is None:
         vis_idx = torch.arange(A, dtype=torch.int32, device=anchor.device)
+    elif isinstance(visible, VisibleIndex):
+        vis_idx = visible
     elif visible.dtype == torch.bool:
         vis_idx = visible_index(visible)
     else:

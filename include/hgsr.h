@@ -302,12 +302,15 @@ int hgsr_lod_mask(int A, const float* anchor, const int32_t* level, const float*
  * offset): xyz, offsets (scaled), color [M, cd], opacity [M], scaling [M,3],
  * rot [M,4]; mask [Av*n_offsets] (uint8) and slot_row [Av*n_offsets] (output row
  * or -1, consumed by the backward).  ws: hgsr_decode_ws_bytes(Av), kept between
- * the two calls. */
+ * the two calls.  av_dev (nullable, device int64): the visible count is read on the
+ * device (as hgsr_explicit_count wrote it) and the count pass's Av is only its upper
+ * bound (the workspace is sized for it) -- the prefilter then needs no host read; the
+ * caller reads *av_dev together with *total and passes the real Av to hgsr_decode_fwd. */
 size_t hgsr_decode_ws_bytes(int Av);
 int hgsr_decode_count(int Av, int F, int view_dim, int n_offsets, int color_dim,
                       const int32_t* vis_idx, const float* anchor, const float* feat,
                       const float* cam_center, const float* const* mlp, void* ws, size_t ws_bytes,
-                      int64_t* total, hgsr_stream_t stream);
+                      int64_t* total, const int64_t* av_dev, hgsr_stream_t stream);
 int hgsr_decode_fwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
                     const int32_t* vis_idx, const float* anchor, const float* feat,
                     const float* offset, const float* scaling_raw, const float* cam_center,

@@ -150,3 +150,39 @@ def test_anchor_prefilter_matches_projection_and_lod(with_lod):
                             sc.Ks[0].to(DEV), 320, 240, lod=lod)
     np.testing.assert_array_equal(vis.cpu().numpy(), ref.numpy())
     np.testing.assert_array_equal(idx.cpu().numpy(), torch.nonzero(ref).reshape(-1).numpy())
+
+
+def test_lazy_prefilter_decode_equals_eager():
+    """prefilter(lazy=True) keeps the visible count on the device (one host read less per
+    view): decode through it gives bit-identical outputs, selection mask, gradients and the
+    slot rows training_statis reuses, as through the eager index."""
+    from horizongs_amd import decode as HD
+    from horizongs_amd.synthetic import make_scene
+    A = 30000
+    sc = make_scene(A, 640, 480, seed=5)
+    g = torch.Generator().manual_seed(4)
+    anchor = sc.means.to(DEV)
+    feat = (torch.randn(A, 32, generator=g) * 0.3).to(DEV)
+    offset = (torch.randn(A, 10, 3, generator=g) * 0.1).to(DEV)
+    scaling = (np.log(0.02) + torch.randn(A, 6, generator=g) * 0.2).float().to(DEV)
+    quats = torch.zeros(A, 4, device=DEV)
+    quats[:, 0] = 1.0
+    torch.manual_seed(7)
+    mlps = [torch.nn.Sequential(torch.nn.Linear(35, 32), torch.nn.ReLU(True), torch.nn.Linear(32, o)).to(DEV)
+            for o in (10, 70, 30)]
+    cam = torch.zeros(3, device=DEV)
+    outs = []
+    for lazy in (False, True):
+        vis, idx = HD.prefilter(anchor, torch.exp(scaling), quats, sc.viewmats[0].to(DEV), sc.Ks[0].to(DEV), 640, 480,
+                                lazy=lazy)
+        ps = [t.clone().requires_grad_(True) for t in (feat, offset, scaling)]
+        xyz, offs, col, op, scl, rot, sel = HD.decode(anchor, ps[0], ps[1], ps[2], cam, mlps, idx, 3, 10, 3)
+        assert 1000 < xyz.shape[0]
+        loss = xyz.square().sum() + col.sum() + op.sum() + scl.sum() + rot.sum()
+        loss.backward()
+        vis_idx = HD.visible_index(vis)  # cached by the decode in both modes
+        outs.append([vis.cpu(), vis_idx.cpu(), xyz.detach().cpu(), col.detach().cpu(), op.detach().cpu(),
+                     sel.cpu(), sel._hgsr_slot_row.cpu()] + [p.grad.cpu() for p in ps])
+    assert torch.equal(outs[0][1], torch.nonzero(outs[0][0]).reshape(-1).to(torch.int32))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
