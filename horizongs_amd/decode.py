@@ -215,6 +215,7 @@ class _Decode(torch.autograd.Function):
         # training_statis takes it from here instead of recomputing it
         sel._hgsr_slot_row = slot_row
         ctx.mark_non_differentiable(sel)
+        ctx.set_materialize_grads(False)  # unused outputs (mask, offsets) get no zero-filled grads
         return t["xyz"], t["offsets"], t["color"], t["opacity"], t["scaling"], t["rot"], sel
 
     @staticmethod
