@@ -372,13 +372,21 @@ __device__ __forceinline__ uint64_t lane_xor64(uint64_t x) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+template <int M, typename K>
+__device__ __forceinline__ K lane_xor(K x) {
+    if constexpr (sizeof(K) == 8) return lane_xor64<M>(x);
+    else return lane_xor32<M>(x);
+}
+
+// The network is written for 64-bit (depth, id) keys and for 32-bit (truncated depth, local
+// index) keys (K); unique keys in both cases.
 // cross-thread stage: partner thread t ^ M, partner slot r (FLIP: E-1-r); the lower
-// thread of the pair (t & LOWBIT == 0) keeps the minimum.  Keys are unique.
-template <int E, int M, int LOWBIT, bool FLIP>
-__device__ __forceinline__ void thread_stage(uint64_t (&v)[E], uint64_t* __restrict__ s, bool active) {
+// thread of the pair (t & LOWBIT == 0) keeps the minimum.
+template <typename K, int E, int M, int LOWBIT, bool FLIP>
+__device__ __forceinline__ void thread_stage(K (&v)[E], K* __restrict__ s, bool active) {
     const int t = threadIdx.x;
     const bool keep_min = (t & LOWBIT) == 0;
-    uint64_t p[E];
+    K p[E];
     if constexpr (M >= 64) {
         lds_barrier();  // earlier reads of s are done
 #pragma unroll
@@ -390,59 +398,59 @@ __device__ __forceinline__ void thread_stage(uint64_t (&v)[E], uint64_t* __restr
     } else {
         if (!active) return;
 #pragma unroll
-        for (int r = 0; r < E; ++r) p[r] = lane_xor64<M>(v[FLIP ? E - 1 - r : r]);
+        for (int r = 0; r < E; ++r) p[r] = lane_xor<M>(v[FLIP ? E - 1 - r : r]);
     }
 #pragma unroll
     for (int r = 0; r < E; ++r) v[r] = ((v[r] < p[r]) == keep_min) ? v[r] : p[r];
 }
 
 // in-thread stage over aligned groups of G slots: FLIP pairs r <-> r ^ (G-1), else r <-> r + G/2
-template <int E, int G, bool FLIP>
-__device__ __forceinline__ void reg_stage(uint64_t (&v)[E], bool active) {
+template <typename K, int E, int G, bool FLIP>
+__device__ __forceinline__ void reg_stage(K (&v)[E], bool active) {
     if (!active) return;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
         if (r & (G / 2)) continue;
         const int q = FLIP ? (r ^ (G - 1)) : (r + G / 2);
-        const uint64_t a = v[r], b = v[q];
+        const K a = v[r], b = v[q];
         const bool keep = a < b;
         v[r] = keep ? a : b;
         v[q] = keep ? b : a;
     }
 }
 
-template <int E, int K, int J>
-__device__ __forceinline__ void half_stages(uint64_t (&v)[E], uint64_t* s, bool active) {
+template <typename K, int E, int L, int J>
+__device__ __forceinline__ void half_stages(K (&v)[E], K* s, bool active) {
     if constexpr (J >= 1) {
-        if constexpr (J >= E) thread_stage<E, J / E, J / E, false>(v, s, active);
-        else reg_stage<E, 2 * J, false>(v, active);
-        half_stages<E, K, J / 2>(v, s, active);
+        if constexpr (J >= E) thread_stage<K, E, J / E, J / E, false>(v, s, active);
+        else reg_stage<K, E, 2 * J, false>(v, active);
+        half_stages<K, E, L, J / 2>(v, s, active);
     }
 }
 
-template <int E, int K>
-__device__ __forceinline__ void merge_levels(uint64_t (&v)[E], uint64_t* s, bool active) {
-    if constexpr (K <= 256 * E) {
-        if constexpr (K <= E) reg_stage<E, K, true>(v, active);
-        else thread_stage<E, K / E - 1, K / (2 * E), true>(v, s, active);
-        half_stages<E, K, K / 4>(v, s, active);
-        merge_levels<E, 2 * K>(v, s, active);
+template <typename K, int E, int L>
+__device__ __forceinline__ void merge_levels(K (&v)[E], K* s, bool active) {
+    if constexpr (L <= 256 * E) {
+        if constexpr (L <= E) reg_stage<K, E, L, true>(v, active);
+        else thread_stage<K, E, L / E - 1, L / (2 * E), true>(v, s, active);
+        half_stages<K, E, L, L / 4>(v, s, active);
+        merge_levels<K, E, 2 * L>(v, s, active);
     }
 }
 
-template <int E>
-__device__ __forceinline__ void bitonic_regs(uint64_t (&v)[E], uint64_t* __restrict__ s, int n) {
+template <typename K, int E>
+__device__ __forceinline__ void bitonic_regs(K (&v)[E], K* __restrict__ s, int n) {
     // a wave holds elements [wave*64*E, (wave+1)*64*E)
     const bool active = (int)(threadIdx.x >> 6) * 64 * E < n;
-    merge_levels<E, 2>(v, s, active);
+    merge_levels<K, E, 2>(v, s, active);
     lds_barrier();
 }
 
 // back to lane-contiguous order through LDS so the global stores coalesce; the
 // row pitch of 260 keys keeps the transposed reads within two-way bank sharing
 constexpr int kSortPitch = 260;
-template <int E>
-__device__ __forceinline__ void untranspose(uint64_t (&v)[E], uint64_t* s) {
+template <typename K, int E>
+__device__ __forceinline__ void untranspose(K (&v)[E], K* s) {
     const int t = threadIdx.x;
 #pragma unroll
     for (int r = 0; r < E; ++r) s[r * kSortPitch + t] = v[r];
@@ -456,8 +464,8 @@ __device__ __forceinline__ void untranspose(uint64_t (&v)[E], uint64_t* s) {
 }
 
 // inverse of untranspose: lane-contiguous element i = r*256 + t -> thread i/E, slot i%E
-template <int E>
-__device__ __forceinline__ void to_blocked(uint64_t (&v)[E], uint64_t* s) {
+template <typename K, int E>
+__device__ __forceinline__ void to_blocked(K (&v)[E], K* s) {
     const int t = threadIdx.x;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
@@ -481,8 +489,8 @@ __device__ __forceinline__ void sort_chunk(const uint64_t* src, int n, uint64_t*
         v[r] = i < n ? src[i] : ~0ull;
     }
     // the network wants the padding in the suffix of the blocked order t*E + r
-    to_blocked<E>(v, s);
-    bitonic_regs<E>(v, s, n);
+    to_blocked<uint64_t, E>(v, s);
+    bitonic_regs<uint64_t, E>(v, s, n);
 }
 
 template <int E>
@@ -490,7 +498,7 @@ __device__ __forceinline__ void sort_and_emit(const uint64_t* keys, int n, uint6
                                               int64_t* __restrict__ isect_ids, int32_t* __restrict__ flatten_ids) {
     uint64_t v[E];
     sort_chunk<E>(keys, n, s, v);
-    untranspose<E>(v, s);
+    untranspose<uint64_t, E>(v, s);
     const int t = threadIdx.x;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
@@ -498,6 +506,87 @@ __device__ __forceinline__ void sort_and_emit(const uint64_t* keys, int n, uint6
         if (i < n) {
             isect_ids[i] = hi | (int64_t)(v[r] >> 32);
             flatten_ids[i] = (int32_t)(uint32_t)v[r];
+        }
+    }
+}
+
+// Bins of 257..2048 keys: sort 32-bit keys (depth bits >> 10 : 21 bits | local index : 11
+// bits) -- half the compare / select work of the 64-bit network -- gather the full keys in
+// that order and repair the runs of equal truncated depth with odd-even transposition
+// passes (the keys inside such a run are in emission order).  Two passes fix every bin of
+// the c2 scene (scripts/sim: at most 2 needed); a bin still unsorted after them (many equal
+// depths) is sorted again by the 64-bit network, so the result is always the exact order.
+constexpr int kFixPasses = 2;
+
+// pair (thread t's last, thread t+1's first): t keeps the smaller, t+1 the larger
+template <int E>
+__device__ __forceinline__ void oe_boundary(uint64_t (&w)[E], uint64_t* sb) {
+    const int t = threadIdx.x;
+    sb[t] = w[E - 1];
+    sb[256 + t] = w[0];
+    lds_barrier();
+    const uint64_t nf = t < 255 ? sb[256 + t + 1] : ~0ull;
+    const uint64_t pl = t > 0 ? sb[t - 1] : 0ull;
+    lds_barrier();
+    w[E - 1] = w[E - 1] < nf ? w[E - 1] : nf;
+    w[0] = w[0] > pl ? w[0] : pl;
+}
+
+template <int E>
+__device__ __forceinline__ void sort32_and_emit(const uint64_t* keys, int n, uint64_t* smem, int64_t hi,
+                                                int64_t* __restrict__ isect_ids, int32_t* __restrict__ flatten_ids) {
+    static_assert(E % 2 == 0, "blocked pairs");
+    uint64_t* full = smem;                                  // [2048] full keys by local index
+    uint32_t* s32 = reinterpret_cast<uint32_t*>(smem + 2048);  // 32-bit network scratch
+    const int t = threadIdx.x;
+    uint32_t v[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = r * 256 + t;
+        if (i < n) {
+            const uint64_t k = keys[i];
+            full[i] = k;
+            v[r] = ((uint32_t)(k >> 42) << 11) | (uint32_t)i;
+        } else {
+            v[r] = ~0u;
+        }
+    }
+    to_blocked<uint32_t, E>(v, s32);  // its barriers also publish full[]
+    bitonic_regs<uint32_t, E>(v, s32, n);
+    uint64_t w[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) w[r] = v[r] == ~0u ? ~0ull : full[v[r] & 2047u];
+    uint64_t* sb = reinterpret_cast<uint64_t*>(s32);  // boundary exchange (after the network)
+#pragma unroll
+    for (int pass = 0; pass < kFixPasses; ++pass) {
+#pragma unroll
+        for (int r = 0; r < E; r += 2) {
+            const uint64_t a = w[r], b = w[r + 1];
+            w[r] = a < b ? a : b;
+            w[r + 1] = a < b ? b : a;
+        }
+#pragma unroll
+        for (int r = 1; r + 1 < E; r += 2) {
+            const uint64_t a = w[r], b = w[r + 1];
+            w[r] = a < b ? a : b;
+            w[r + 1] = a < b ? b : a;
+        }
+        oe_boundary<E>(w, sb);
+    }
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r + 1 < E; ++r) ok &= w[r] <= w[r + 1];
+    sb[256 + t] = w[0];
+    lds_barrier();
+    ok &= t == 255 || w[E - 1] <= sb[256 + t + 1];
+    if (!__syncthreads_and(ok)) bitonic_regs<uint64_t, E>(w, smem, n);  // rare: many equal depths
+    untranspose<uint64_t, E>(w, smem);
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = r * 256 + t;
+        if (i < n) {
+            if (isect_ids) isect_ids[i] = hi | (int64_t)(w[r] >> 32);
+            flatten_ids[i] = (int32_t)(uint32_t)w[r];
         }
     }
 }
@@ -530,7 +619,8 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(int n_bins, int n_tiles,
                                                         uint64_t* __restrict__ tmp,
                                                         int64_t* __restrict__ isect_ids,
                                                         int32_t* __restrict__ flatten_ids) {
-    __shared__ uint64_t s_keys[8 * kSortPitch];
+    // 64-bit network scratch, or (32-bit path) 2048 full keys + the 32-bit network's scratch
+    __shared__ uint64_t s_keys[2048 + 4 * kSortPitch];
     const int bin = blockIdx.x;
     const int64_t start = offsets[bin];
     const int64_t end = bin + 1 < n_bins ? (int64_t)offsets[bin + 1] : n_isects;
@@ -540,9 +630,9 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(int n_bins, int n_tiles,
     const int64_t hi = ((int64_t)cam << (32 + tile_bits)) | ((int64_t)tile << 32);
     if (n <= kSortCap) {
         if (n <= 256) sort_and_emit<1>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
-        else if (n <= 512) sort_and_emit<2>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
-        else if (n <= 1024) sort_and_emit<4>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
-        else sort_and_emit<8>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
+        else if (n <= 512) sort32_and_emit<2>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
+        else if (n <= 1024) sort32_and_emit<4>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
+        else sort32_and_emit<8>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         return;
     }
     // large bin: LDS-sorted chunks, then merge passes ping-ponging keys <-> tmp
@@ -552,7 +642,7 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(int n_bins, int n_tiles,
         const int cn = min(kSortCap, n - c0);
         uint64_t v[8];
         sort_chunk<8>(a + c0, cn, s_keys, v);
-        untranspose<8>(v, s_keys);
+        untranspose<uint64_t, 8>(v, s_keys);
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const int i = r * 256 + threadIdx.x;
