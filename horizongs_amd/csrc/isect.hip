@@ -514,7 +514,7 @@ __device__ __forceinline__ void sort_and_emit(const uint64_t* keys, int n, uint6
 // bits) -- half the compare / select work of the 64-bit network -- gather the full keys in
 // that order and repair the runs of equal truncated depth with odd-even transposition
 // passes (the keys inside such a run are in emission order).  Two passes fix every bin of
-// the c2 scene (scripts/sim: at most 2 needed); a bin still unsorted after them (many equal
+// the c2 scene (scripts/sim_sort_fixup.py: at most 2 needed); a bin still unsorted after them (many equal
 // depths) is sorted again by the 64-bit network, so the result is always the exact order.
 constexpr int kFixPasses = 2;
 
