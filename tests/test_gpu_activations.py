@@ -34,3 +34,14 @@ def test_activate_fwd_bwd_vs_torch():
     s, o = activate(a, b)
     s.sum().backward()
     assert float(b.grad.abs().max()) == 0.0
+
+
+def test_activate_unaligned_views():
+    """Views starting off a 16-B boundary take the scalar path: same values as aligned ones."""
+    from horizongs_amd.activations import activate
+    g = torch.Generator().manual_seed(1)
+    ls = (torch.randn(1001, 3, generator=g) - 3).to(DEV)
+    lg = torch.randn(1001, generator=g).to(DEV)
+    s0, o0 = activate(ls[1:].clone(), lg[1:].clone())
+    s1, o1 = activate(ls[1:], lg[1:])  # 12-B / 4-B offset bases
+    assert torch.equal(s0, s1) and torch.equal(o0, o1)
