@@ -532,31 +532,12 @@ __device__ __forceinline__ void oe_boundary(uint64_t (&w)[E], uint64_t* sb) {
     w[0] = w[0] > pl ? w[0] : pl;
 }
 
+// the fix-up passes over the gathered full keys (thread t holds sorted slots t*E..t*E+E-1);
+// true when every thread's keys are then in exact order (one workgroup-wide vote)
 template <int E>
-__device__ __forceinline__ void sort32_and_emit(const uint64_t* keys, int n, uint64_t* smem, int64_t hi,
-                                                int64_t* __restrict__ isect_ids, int32_t* __restrict__ flatten_ids) {
+__device__ __forceinline__ bool fix_runs(uint64_t (&w)[E], uint64_t* sb) {
     static_assert(E % 2 == 0, "blocked pairs");
-    uint64_t* full = smem;                                  // [2048] full keys by local index
-    uint32_t* s32 = reinterpret_cast<uint32_t*>(smem + 2048);  // 32-bit network scratch
     const int t = threadIdx.x;
-    uint32_t v[E];
-#pragma unroll
-    for (int r = 0; r < E; ++r) {
-        const int i = r * 256 + t;
-        if (i < n) {
-            const uint64_t k = keys[i];
-            full[i] = k;
-            v[r] = ((uint32_t)(k >> 42) << 11) | (uint32_t)i;
-        } else {
-            v[r] = ~0u;
-        }
-    }
-    to_blocked<uint32_t, E>(v, s32);  // its barriers also publish full[]
-    bitonic_regs<uint32_t, E>(v, s32, n);
-    uint64_t w[E];
-#pragma unroll
-    for (int r = 0; r < E; ++r) w[r] = v[r] == ~0u ? ~0ull : full[v[r] & 2047u];
-    uint64_t* sb = reinterpret_cast<uint64_t*>(s32);  // boundary exchange (after the network)
 #pragma unroll
     for (int pass = 0; pass < kFixPasses; ++pass) {
 #pragma unroll
@@ -579,7 +560,13 @@ __device__ __forceinline__ void sort32_and_emit(const uint64_t* keys, int n, uin
     sb[256 + t] = w[0];
     lds_barrier();
     ok &= t == 255 || w[E - 1] <= sb[256 + t + 1];
-    if (!__syncthreads_and(ok)) bitonic_regs<uint64_t, E>(w, smem, n);  // rare: many equal depths
+    return __syncthreads_and(ok);
+}
+
+template <int E>
+__device__ __forceinline__ void emit_sorted(uint64_t (&w)[E], int n, uint64_t* smem, int64_t hi,
+                                            int64_t* __restrict__ isect_ids, int32_t* __restrict__ flatten_ids) {
+    const int t = threadIdx.x;
     untranspose<uint64_t, E>(w, smem);
 #pragma unroll
     for (int r = 0; r < E; ++r) {
@@ -589,6 +576,112 @@ __device__ __forceinline__ void sort32_and_emit(const uint64_t* keys, int n, uin
             flatten_ids[i] = (int32_t)(uint32_t)w[r];
         }
     }
+}
+
+__device__ __forceinline__ uint32_t key32(uint64_t k, int i) { return ((uint32_t)(k >> 42) << 11) | (uint32_t)i; }
+
+template <int E>
+__device__ __forceinline__ void sort32_and_emit(const uint64_t* keys, int n, uint64_t* smem, int64_t hi,
+                                                int64_t* __restrict__ isect_ids, int32_t* __restrict__ flatten_ids) {
+    uint64_t* full = smem;                                  // [2048] full keys by local index
+    uint32_t* s32 = reinterpret_cast<uint32_t*>(smem + 2048);  // 32-bit network scratch
+    const int t = threadIdx.x;
+    uint32_t v[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = r * 256 + t;
+        if (i < n) {
+            const uint64_t k = keys[i];
+            full[i] = k;
+            v[r] = key32(k, i);
+        } else {
+            v[r] = ~0u;
+        }
+    }
+    to_blocked<uint32_t, E>(v, s32);  // its barriers also publish full[]
+    bitonic_regs<uint32_t, E>(v, s32, n);
+    uint64_t w[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) w[r] = v[r] == ~0u ? ~0ull : full[v[r] & 2047u];
+    // boundary exchange in the network scratch (its last reads were before bitonic_regs' barrier)
+    if (!fix_runs<E>(w, reinterpret_cast<uint64_t*>(s32)))
+        bitonic_regs<uint64_t, E>(w, smem, n);  // rare: many equal depths
+    emit_sorted<E>(w, n, smem, hi, isect_ids, flatten_ids);
+}
+
+// Bins of 1025..1280 keys (90 % of the c2 bins hold 1025-1254): a 1024-key network (4 keys
+// per thread) and a 256-key one (1 per thread) instead of one padded 2048-key network (8 per
+// thread), then a merge by co-ranking -- each key's output slot is its index in its own run
+// plus its lower bound in the other run (binary search in LDS; the 32-bit keys are unique) --
+// and the same full-key gather and fix-up passes, 6 slots per thread.  The 32-bit order is
+// the E = 8 path's exactly; a bin the fix-up leaves unsorted takes the E = 8 path instead.
+__device__ __forceinline__ void sort32_split_and_emit(const uint64_t* keys, int n, uint64_t* smem, int64_t hi,
+                                                      int64_t* __restrict__ isect_ids,
+                                                      int32_t* __restrict__ flatten_ids) {
+    constexpr int E = 6;
+    uint64_t* full = smem;
+    uint32_t* s32 = reinterpret_cast<uint32_t*>(smem + 2048);
+    const int t = threadIdx.x;
+    const int nb = n - 1024;  // 1..256
+    uint32_t a[4], b[1];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = r * 256 + t;
+        const uint64_t k = keys[i];
+        full[i] = k;
+        a[r] = key32(k, i);
+    }
+    if (t < nb) {
+        const uint64_t k = keys[1024 + t];
+        full[1024 + t] = k;
+        b[0] = key32(k, 1024 + t);
+    } else {
+        b[0] = ~0u;
+    }
+    to_blocked<uint32_t, 4>(a, s32);
+    bitonic_regs<uint32_t, 4>(a, s32, 1024);
+    bitonic_regs<uint32_t, 1>(b, s32, nb);  // E = 1: blocked order is lane order
+    uint32_t* sA = s32;         // run A, sorted [1024]
+    uint32_t* sB = s32 + 1024;  // run B, sorted [256] (~0 padded)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sA[4 * t + r] = a[r];
+    sB[t] = b[0];
+    lds_barrier();
+    int pa[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        int lo = 0;
+#pragma unroll
+        for (int step = 128; step >= 1; step >>= 1) lo += sB[lo + step - 1] < a[r] ? step : 0;
+        lo += sB[lo] < a[r];  // lo reaches 256 only when every B key is smaller
+        pa[r] = 4 * t + r + lo;
+    }
+    int pb;
+    {
+        int lo = 0;
+#pragma unroll
+        for (int step = 512; step >= 1; step >>= 1) lo += sA[lo + step - 1] < b[0] ? step : 0;
+        lo += sA[lo] < b[0];
+        pb = t + lo;
+    }
+    lds_barrier();  // every search is done before the merged order overwrites the runs
+    uint32_t* sM = s32;  // merged [n]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sM[pa[r]] = a[r];
+    if (t < nb) sM[pb] = b[0];
+    lds_barrier();
+    uint64_t w[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = t * E + r;
+        w[r] = i < n ? full[sM[i] & 2047u] : ~0ull;
+    }
+    lds_barrier();  // the fix-up's boundary exchange reuses the merged array's space
+    if (!fix_runs<E>(w, reinterpret_cast<uint64_t*>(s32))) {
+        sort32_and_emit<8>(keys, n, smem, hi, isect_ids, flatten_ids);  // rare: many equal depths
+        return;
+    }
+    emit_sorted<E>(w, n, smem, hi, isect_ids, flatten_ids);
 }
 
 // merge sorted runs A=[0,la), B=[la,la+lb) of src into dst (unique keys)
@@ -632,6 +725,7 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(int n_bins, int n_tiles,
         if (n <= 256) sort_and_emit<1>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         else if (n <= 512) sort32_and_emit<2>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         else if (n <= 1024) sort32_and_emit<4>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
+        else if (n <= 1280) sort32_split_and_emit(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         else sort32_and_emit<8>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         return;
     }

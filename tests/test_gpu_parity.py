@@ -202,6 +202,38 @@ def test_isect_large_bins_and_ties():
     np.testing.assert_array_equal(goffs.cpu().numpy(), offs)
 
 
+def test_isect_split_sort_bins():
+    """Bins of 1025-1280 keys take the split sort (1024 + 256 networks, co-rank merge): exact
+    order at both size edges, with distinct depths, depths equal only in their truncated high
+    bits (fix-up passes) and heavily repeated depths (fallback to the 2048-key path)."""
+    rng = np.random.default_rng(11)
+    sizes = [1025, 1280, 1100, 1200, 1279, 700]
+    m2, d = [], []
+    for k, c in enumerate(sizes):
+        m2.append(np.tile([16.0 * k + 8.0, 8.0], (c, 1)))
+        if k == 2:
+            dk = rng.choice(rng.uniform(1, 50, 40), c)  # ~28 equal depths per value
+        elif k == 3:
+            dk = np.float32(7.0) + np.float32(1e-6) * rng.integers(0, 64, c)  # equal above bit 10
+        else:
+            dk = rng.uniform(0.5, 80.0, c)
+        d.append(dk)
+    perm = rng.permutation(sum(sizes))  # Gaussians of all tiles interleaved
+    m2 = np.concatenate(m2)[perm].astype(np.float32)[None]
+    d = np.concatenate(d)[perm].astype(np.float32)[None]
+    r = np.ones((1, m2.shape[1]), np.int32)
+    tw, th = len(sizes), 1
+    tpg, ids, fl = O.isect_tiles(m2, r, d, 16, tw, th)
+    offs = O.isect_offsets(ids, 1, tw, th)
+    counts = np.diff(np.concatenate([offs.reshape(-1), [len(ids)]]))
+    assert counts.tolist() == sizes
+    gr, gm2, gd = to_dev(torch.from_numpy(r), torch.from_numpy(m2), torch.from_numpy(d))
+    gtpg, gids, gfl, goffs = G._isect_binned(gm2, gr, 16, tw, th, gd)
+    np.testing.assert_array_equal(gids.cpu().numpy(), ids)
+    np.testing.assert_array_equal(gfl.cpu().numpy(), fl)
+    np.testing.assert_array_equal(goffs.cpu().numpy(), offs)
+
+
 def test_isect_empty():
     r = torch.zeros(1, 10, dtype=torch.int32, device=DEV)
     m2 = torch.zeros(1, 10, 2, device=DEV)
