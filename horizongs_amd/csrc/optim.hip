@@ -11,8 +11,8 @@
 //
 // CDNA4 mapping: HBM-bound (28 B per element: p, g, m, v read; p, m, v written).
 // Every tensor of the step is described in the kernel arguments; a workgroup takes a
-// 4096-element chunk of one tensor (scalar lookup over the chunk prefix), each lane
-// four independent float4 rows (all loads issued before the first use), streamed with
+// 2048-element chunk of one tensor (scalar lookup over the chunk prefix), each lane
+// two independent float4 rows (all loads issued before the first use), streamed with
 // non-temporal loads / stores (every byte is touched once per step).  Tensors whose
 // four pointers are not 16-B aligned, and ragged tails, take a scalar path.
 #include "common.h"
@@ -20,7 +20,7 @@
 namespace hgsr {
 
 constexpr int kAdamMaxT = 16;            // tensors per launch (more: several launches)
-constexpr int kAdamChunk = 4096;         // elements per workgroup
+constexpr int kAdamChunk = 2048;         // elements per workgroup (1024 / 4096 / 8192: slower)
 constexpr int kAdamVec = kAdamChunk / 4 / 256;  // float4 rows per lane
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld_nt(const float* p, int64_t i) {
