@@ -610,20 +610,23 @@ __device__ __forceinline__ void sort32_and_emit(const uint64_t* keys, int n, uin
 }
 
 // Bins of 1025..1280 keys (90 % of the c2 bins hold 1025-1254): a 1024-key network (4 keys
-// per thread) and a 256-key one (1 per thread) instead of one padded 2048-key network (8 per
-// thread), then a merge by co-ranking -- each key's output slot is its index in its own run
-// plus its lower bound in the other run (binary search in LDS; the 32-bit keys are unique) --
-// and the same full-key gather and fix-up passes, 6 slots per thread.  The 32-bit order is
-// the E = 8 path's exactly; a bin the fix-up leaves unsorted takes the E = 8 path instead.
+// per thread) and a 256 * EB-key one (EB per thread) instead of one padded 2048-key
+// network (8 per thread), then a merge by co-ranking -- each key's output slot is its index in
+// its own run plus its lower bound in the other run (binary search in LDS; the 32-bit keys are
+// unique) -- and the same full-key gather and fix-up passes, 6 slots per thread.  The 32-bit
+// order is the E = 8 path's exactly; a bin the fix-up leaves unsorted takes the E = 8 path.
+// (EB = 2 for 1281..1536 keys measured slower than the E = 8 path on the anchor scene's bins:
+// tile_sort 0.153 -> 0.184 ms; not dispatched.)
+template <int EB>
 __device__ __forceinline__ void sort32_split_and_emit(const uint64_t* keys, int n, uint64_t* smem, int64_t hi,
                                                       int64_t* __restrict__ isect_ids,
                                                       int32_t* __restrict__ flatten_ids) {
-    constexpr int E = 6;
+    constexpr int E = 6, NB = 256 * EB;
     uint64_t* full = smem;
     uint32_t* s32 = reinterpret_cast<uint32_t*>(smem + 2048);
     const int t = threadIdx.x;
-    const int nb = n - 1024;  // 1..256
-    uint32_t a[4], b[1];
+    const int nb = n - 1024;  // 1..NB
+    uint32_t a[4], b[EB];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = r * 256 + t;
@@ -631,44 +634,52 @@ __device__ __forceinline__ void sort32_split_and_emit(const uint64_t* keys, int 
         full[i] = k;
         a[r] = key32(k, i);
     }
-    if (t < nb) {
-        const uint64_t k = keys[1024 + t];
-        full[1024 + t] = k;
-        b[0] = key32(k, 1024 + t);
-    } else {
-        b[0] = ~0u;
+#pragma unroll
+    for (int r = 0; r < EB; ++r) {
+        const int j = r * 256 + t;
+        if (j < nb) {
+            const uint64_t k = keys[1024 + j];
+            full[1024 + j] = k;
+            b[r] = key32(k, 1024 + j);
+        } else {
+            b[r] = ~0u;
+        }
     }
     to_blocked<uint32_t, 4>(a, s32);
     bitonic_regs<uint32_t, 4>(a, s32, 1024);
-    bitonic_regs<uint32_t, 1>(b, s32, nb);  // E = 1: blocked order is lane order
+    if constexpr (EB > 1) to_blocked<uint32_t, EB>(b, s32);  // (E = 1: blocked order is lane order)
+    bitonic_regs<uint32_t, EB>(b, s32, nb);
     uint32_t* sA = s32;         // run A, sorted [1024]
-    uint32_t* sB = s32 + 1024;  // run B, sorted [256] (~0 padded)
+    uint32_t* sB = s32 + 1024;  // run B, sorted [NB] (~0 padded)
 #pragma unroll
     for (int r = 0; r < 4; ++r) sA[4 * t + r] = a[r];
-    sB[t] = b[0];
+#pragma unroll
+    for (int r = 0; r < EB; ++r) sB[EB * t + r] = b[r];
     lds_barrier();
-    int pa[4];
+    int pa[4], pb[EB];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         int lo = 0;
 #pragma unroll
-        for (int step = 128; step >= 1; step >>= 1) lo += sB[lo + step - 1] < a[r] ? step : 0;
-        lo += sB[lo] < a[r];  // lo reaches 256 only when every B key is smaller
+        for (int step = NB / 2; step >= 1; step >>= 1) lo += sB[lo + step - 1] < a[r] ? step : 0;
+        lo += sB[lo] < a[r];  // lo reaches NB only when every B key is smaller
         pa[r] = 4 * t + r + lo;
     }
-    int pb;
-    {
+#pragma unroll
+    for (int r = 0; r < EB; ++r) {
         int lo = 0;
 #pragma unroll
-        for (int step = 512; step >= 1; step >>= 1) lo += sA[lo + step - 1] < b[0] ? step : 0;
-        lo += sA[lo] < b[0];
-        pb = t + lo;
+        for (int step = 512; step >= 1; step >>= 1) lo += sA[lo + step - 1] < b[r] ? step : 0;
+        lo += sA[lo] < b[r];
+        pb[r] = EB * t + r + lo;
     }
     lds_barrier();  // every search is done before the merged order overwrites the runs
     uint32_t* sM = s32;  // merged [n]
 #pragma unroll
     for (int r = 0; r < 4; ++r) sM[pa[r]] = a[r];
-    if (t < nb) sM[pb] = b[0];
+#pragma unroll
+    for (int r = 0; r < EB; ++r)
+        if (EB * t + r < nb) sM[pb[r]] = b[r];
     lds_barrier();
     uint64_t w[E];
 #pragma unroll
@@ -725,7 +736,7 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(int n_bins, int n_tiles,
         if (n <= 256) sort_and_emit<1>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         else if (n <= 512) sort32_and_emit<2>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         else if (n <= 1024) sort32_and_emit<4>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
-        else if (n <= 1280) sort32_split_and_emit(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
+        else if (n <= 1280) sort32_split_and_emit<1>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         else sort32_and_emit<8>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         return;
     }
