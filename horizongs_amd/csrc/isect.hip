@@ -510,12 +510,13 @@ __device__ __forceinline__ void sort_and_emit(const uint64_t* keys, int n, uint6
     }
 }
 
-// Bins of 257..2048 keys: sort 32-bit keys (depth bits >> 10 : 21 bits | local index : 11
-// bits) -- half the compare / select work of the 64-bit network -- gather the full keys in
-// that order and repair the runs of equal truncated depth with odd-even transposition
-// passes (the keys inside such a run are in emission order).  Two passes fix every bin of
-// the c2 scene (scripts/sim_sort_fixup.py: at most 2 needed); a bin still unsorted after them (many equal
-// depths) is sorted again by the 64-bit network, so the result is always the exact order.
+// Bins of 257..2048 keys: sort 32-bit keys (quantised depth : 20 bits | local index : 11
+// bits, see depth_q) -- half the compare / select work of the 64-bit network -- gather the
+// full keys in that order and repair the runs of equal quantised depth with odd-even
+// transposition passes (the keys inside such a run are in emission order).  Two passes fixed
+// every bin of the c2 scene already with a fixed depth >> 10 (scripts/sim_sort_fixup.py); a bin
+// still unsorted after them (many equal depths) is sorted again by the 64-bit network, so the
+// result is always the exact order.
 constexpr int kFixPasses = 2;
 
 // pair (thread t's last, thread t+1's first): t keeps the smaller, t+1 the larger
@@ -578,7 +579,39 @@ __device__ __forceinline__ void emit_sorted(uint64_t (&w)[E], int n, uint64_t* s
     }
 }
 
-__device__ __forceinline__ uint32_t key32(uint64_t k, int i) { return ((uint32_t)(k >> 42) << 11) | (uint32_t)i; }
+// Per-bin depth quantiser of the 32-bit keys: (depth bits - the bin's minimum) >> shift, the
+// smallest shift that fits 20 bits, so two keys of a bin tie only where their depths agree to
+// within 2^shift ulps (the fixed depth bits >> 10 tied long runs in bins whose depths span a
+// narrow range).  20 bits keep every real key below the ~0 padding.
+struct DepthQ {
+    uint32_t lo;
+    int shift;
+};
+__device__ __forceinline__ DepthQ depth_q(uint32_t mn, uint32_t mx) {
+    __shared__ uint32_t s_red[8];
+    // wave min / max over the network's in-wave lane exchanges (DPP / swizzle / permlane)
+    mn = min(mn, lane_xor32<1>(mn)), mx = max(mx, lane_xor32<1>(mx));
+    mn = min(mn, lane_xor32<2>(mn)), mx = max(mx, lane_xor32<2>(mx));
+    mn = min(mn, lane_xor32<4>(mn)), mx = max(mx, lane_xor32<4>(mx));
+    mn = min(mn, lane_xor32<8>(mn)), mx = max(mx, lane_xor32<8>(mx));
+    mn = min(mn, lane_xor32<16>(mn)), mx = max(mx, lane_xor32<16>(mx));
+    mn = min(mn, lane_xor32<32>(mn)), mx = max(mx, lane_xor32<32>(mx));
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_red[w] = mn;
+        s_red[4 + w] = mx;
+    }
+    lds_barrier();
+    mn = min(min(s_red[0], s_red[1]), min(s_red[2], s_red[3]));
+    mx = max(max(s_red[4], s_red[5]), max(s_red[6], s_red[7]));
+    const uint32_t span = mx - mn;
+    const int bits = span ? 32 - __clz((int)span) : 0;
+    return {mn, bits > 20 ? bits - 20 : 0};
+}
+
+__device__ __forceinline__ uint32_t key32(uint64_t k, int i, DepthQ q) {
+    return ((((uint32_t)(k >> 32) - q.lo) >> q.shift) << 11) | (uint32_t)i;
+}
 
 template <int E>
 __device__ __forceinline__ void sort32_and_emit(const uint64_t* keys, int n, uint64_t* smem, int64_t hi,
@@ -586,17 +619,24 @@ __device__ __forceinline__ void sort32_and_emit(const uint64_t* keys, int n, uin
     uint64_t* full = smem;                                  // [2048] full keys by local index
     uint32_t* s32 = reinterpret_cast<uint32_t*>(smem + 2048);  // 32-bit network scratch
     const int t = threadIdx.x;
-    uint32_t v[E];
+    uint64_t kk[E];
+    uint32_t mn = ~0u, mx = 0u;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
         const int i = r * 256 + t;
         if (i < n) {
-            const uint64_t k = keys[i];
-            full[i] = k;
-            v[r] = key32(k, i);
-        } else {
-            v[r] = ~0u;
+            kk[r] = keys[i];
+            full[i] = kk[r];
+            mn = min(mn, (uint32_t)(kk[r] >> 32));
+            mx = max(mx, (uint32_t)(kk[r] >> 32));
         }
+    }
+    const DepthQ q = depth_q(mn, mx);
+    uint32_t v[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = r * 256 + t;
+        v[r] = i < n ? key32(kk[r], i, q) : ~0u;
     }
     to_blocked<uint32_t, E>(v, s32);  // its barriers also publish full[]
     bitonic_regs<uint32_t, E>(v, s32, n);
@@ -626,25 +666,32 @@ __device__ __forceinline__ void sort32_split_and_emit(const uint64_t* keys, int 
     uint32_t* s32 = reinterpret_cast<uint32_t*>(smem + 2048);
     const int t = threadIdx.x;
     const int nb = n - 1024;  // 1..NB
-    uint32_t a[4], b[EB];
+    uint64_t ka[4], kb[EB];
+    uint32_t mn = ~0u, mx = 0u;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = r * 256 + t;
-        const uint64_t k = keys[i];
-        full[i] = k;
-        a[r] = key32(k, i);
+        ka[r] = keys[i];
+        full[i] = ka[r];
+        mn = min(mn, (uint32_t)(ka[r] >> 32));
+        mx = max(mx, (uint32_t)(ka[r] >> 32));
     }
 #pragma unroll
     for (int r = 0; r < EB; ++r) {
         const int j = r * 256 + t;
         if (j < nb) {
-            const uint64_t k = keys[1024 + j];
-            full[1024 + j] = k;
-            b[r] = key32(k, 1024 + j);
-        } else {
-            b[r] = ~0u;
+            kb[r] = keys[1024 + j];
+            full[1024 + j] = kb[r];
+            mn = min(mn, (uint32_t)(kb[r] >> 32));
+            mx = max(mx, (uint32_t)(kb[r] >> 32));
         }
     }
+    const DepthQ q = depth_q(mn, mx);
+    uint32_t a[4], b[EB];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[r] = key32(ka[r], r * 256 + t, q);
+#pragma unroll
+    for (int r = 0; r < EB; ++r) b[r] = r * 256 + t < nb ? key32(kb[r], 1024 + r * 256 + t, q) : ~0u;
     to_blocked<uint32_t, 4>(a, s32);
     bitonic_regs<uint32_t, 4>(a, s32, 1024);
     if constexpr (EB > 1) to_blocked<uint32_t, EB>(b, s32);  // (E = 1: blocked order is lane order)
