@@ -655,8 +655,8 @@ __device__ __forceinline__ void sort32_and_emit(const uint64_t* keys, int n, uin
 // its own run plus its lower bound in the other run (binary search in LDS; the 32-bit keys are
 // unique) -- and the same full-key gather and fix-up passes, 6 slots per thread.  The 32-bit
 // order is the E = 8 path's exactly; a bin the fix-up leaves unsorted takes the E = 8 path.
-// (EB = 2 for 1281..1536 keys measured slower than the E = 8 path on the anchor scene's bins:
-// tile_sort 0.153 -> 0.184 ms; not dispatched.)
+// (EB = 2 for 1281..1536 keys: no gain over the E = 8 path on the anchor scene's bins, 0.083 ms
+// either way once the quantised keys stopped the fallbacks; not dispatched.)
 template <int EB>
 __device__ __forceinline__ void sort32_split_and_emit(const uint64_t* keys, int n, uint64_t* smem, int64_t hi,
                                                       int64_t* __restrict__ isect_ids,
