@@ -207,12 +207,14 @@ def test_isect_split_sort_bins():
     ones the 2048-key network: exact order at the size edges, with distinct depths, depths equal
     only in their truncated high bits (fix-up passes) and heavily repeated depths (fallbacks)."""
     rng = np.random.default_rng(11)
-    sizes = [1025, 1280, 1100, 1200, 1279, 700, 1281, 1536, 1400, 1537]
+    sizes = [1025, 1280, 1100, 1200, 1279, 700, 1281, 1536, 1400, 1537, 1200, 900]
     m2, d = [], []
     for k, c in enumerate(sizes):
         m2.append(np.tile([16.0 * k + 8.0, 8.0], (c, 1)))
         if k in (2, 8):
             dk = rng.choice(rng.uniform(1, 50, 40), c)  # ~28 equal depths per value
+        elif k in (10, 11):
+            dk = np.repeat(rng.uniform(1, 50, c // 2), 2)  # equal pairs: repaired by the fix-up passes
         elif k == 3:
             dk = np.float32(7.0) + np.float32(1e-6) * rng.integers(0, 64, c)  # equal above bit 10
         else:
