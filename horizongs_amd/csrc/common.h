@@ -106,6 +106,18 @@ __host__ __device__ __forceinline__ int64_t qmask_stride(int64_t n_isects, int64
     return (n_isects + 63) / 64 + n_bins + 4;
 }
 
+// count floats from src to LDS dst (16-B aligned) as float4 runs when src allows
+__device__ __forceinline__ void stage_floats(const float* __restrict__ src, int count, float* dst) {
+    int done = 0;
+    if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+        const int n4 = count >> 2;
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        for (int q = threadIdx.x; q < n4; q += 256) *reinterpret_cast<float4*>(dst + 4 * q) = s4[q];
+        done = n4 << 2;
+    }
+    for (int e = done + threadIdx.x; e < count; e += 256) dst[e] = src[e];
+}
+
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }

@@ -123,35 +123,55 @@ __device__ __forceinline__ void cross_abc(const float* M, float mx, float my, fl
     }
 }
 
+// One workgroup packs 256 consecutive (camera, surfel) records.  The ray transforms (36 B
+// each) and normals (12 B) come in as contiguous float4 runs through LDS and the 96-B
+// records leave the same way: lane-strided AoS loads / stores made every instruction touch
+// ~36 cache lines.
 template <int D>
 __global__ __launch_bounds__(256) void pack2_kernel(int64_t n, int N, const float2* __restrict__ means2d,
                                                     const float* __restrict__ rt, ChanSrc cs,
                                                     const float* __restrict__ normals, Rec2* __restrict__ rec) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const int64_t c = i / N, g = i - c * N;
-    float M[9];
+    constexpr int kOP = 25;  // record pitch in LDS (24 floats + 1: conflict-free lane stride)
+    __shared__ __attribute__((aligned(16))) float s_buf[256 * kOP];
+    const int64_t i0 = (int64_t)blockIdx.x * 256;
+    const int nloc = (int)min((int64_t)256, n - i0);
+    const int t = threadIdx.x;
+    const int64_t i = i0 + t;
+    stage_floats(rt + i0 * 9, nloc * 9, s_buf);
+    stage_floats(normals + i0 * 3, nloc * 3, s_buf + 256 * 9);
+    __syncthreads();
+    float M[9], nr[3];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) M[k] = rt[i * 9 + k];
-    const float2 m = means2d[i];
-    const float o = cs.opac[c * cs.op_cstride + g];
-    float4 box;
-    float disk;
-    surfel_footprint(M, M + 3, M + 6, o, box, disk);
-    float abc[9];
-    cross_abc(M, m.x, m.y, abc);
-    Rec2 r;
-    r.r0 = make_float4(abc[0], abc[1], abc[2], abc[3]);
-    r.r1 = make_float4(abc[4], abc[5], abc[6], abc[7]);
-    r.r2 = make_float4(abc[8], m.x, m.y, o);
-    float col[4] = {0.f, 0.f, 0.f, 0.f};
-    const float* src = cs.colors + c * cs.col_cstride + g * cs.dc;
+    for (int k = 0; k < 9; ++k) M[k] = s_buf[t * 9 + k];
 #pragma unroll
-    for (int k = 0; k < D; ++k) col[k] = k < cs.dc ? src[k] : cs.depths[i];
-    r.col = make_float4(col[0], col[1], col[2], col[3]);
-    r.r4 = make_float4(normals[i * 3], normals[i * 3 + 1], normals[i * 3 + 2], disk);
-    r.box = box;
-    rec[i] = r;
+    for (int k = 0; k < 3; ++k) nr[k] = s_buf[256 * 9 + t * 3 + k];
+    __syncthreads();  // s_buf now holds the records
+    if (t < nloc) {
+        const int64_t c = i / N, g = i - c * N;
+        const float2 m = means2d[i];
+        const float o = cs.opac[c * cs.op_cstride + g];
+        float4 box;
+        float disk;
+        surfel_footprint(M, M + 3, M + 6, o, box, disk);
+        float abc[9];
+        cross_abc(M, m.x, m.y, abc);
+        float col[4] = {0.f, 0.f, 0.f, 0.f};
+        const float* src = cs.colors + c * cs.col_cstride + g * cs.dc;
+#pragma unroll
+        for (int k = 0; k < D; ++k) col[k] = k < cs.dc ? src[k] : cs.depths[i];
+        const float r[24] = {abc[0], abc[1], abc[2], abc[3], abc[4], abc[5], abc[6], abc[7],
+                             abc[8], m.x,    m.y,    o,      col[0], col[1], col[2], col[3],
+                             nr[0],  nr[1],  nr[2],  disk,   box.x,  box.y,  box.z,  box.w};
+#pragma unroll
+        for (int k = 0; k < 24; ++k) s_buf[t * kOP + k] = r[k];
+    }
+    __syncthreads();
+    float4* dst = reinterpret_cast<float4*>(rec + i0);
+    for (int q = t; q < nloc * 6; q += 256) {
+        const int e = q / 6, f = q - e * 6;
+        const float* p = s_buf + e * kOP + 4 * f;
+        dst[q] = make_float4(p[0], p[1], p[2], p[3]);
+    }
 }
 
 // Does the surfel reach the 8x8 quadrant centred at (qx, qy)?  Both passes use this test, so
