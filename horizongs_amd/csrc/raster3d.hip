@@ -61,21 +61,44 @@ __device__ __forceinline__ float sigma2(const float4 g0, const float4 g1, float 
     return __builtin_fmaf(g1.x * dy, dy, dx * h);
 }
 
+// One workgroup packs 256 consecutive (camera, Gaussian) records; the conics (12 B each)
+// come in and the 48-B records leave as contiguous float4 runs through LDS (lane-strided
+// AoS loads / stores touch ~12-48 cache lines per instruction): 37.6 -> 29.3 us at c2.
 template <int D>
 __global__ __launch_bounds__(256) void pack3_kernel(int64_t n, int N, const float2* __restrict__ means2d,
                                                     const float* __restrict__ conics, ChanSrc cs,
                                                     Rec3* __restrict__ rec) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const int64_t c = i / N, g = i - c * N;
-    const float2 m = means2d[i];
-    const float a = conics[i * 3], b = conics[i * 3 + 1], cc = conics[i * 3 + 2];
-    const float o = cs.opac[c * cs.op_cstride + g];
-    float col[4] = {0.f, 0.f, 0.f, 0.f};
-    const float* src = cs.colors + c * cs.col_cstride + g * cs.dc;
+    constexpr int kOP = 13;  // record pitch in LDS (12 floats + 1: conflict-free lane stride)
+    __shared__ __attribute__((aligned(16))) float s_buf[256 * kOP];
+    const int64_t i0 = (int64_t)blockIdx.x * 256;
+    const int nloc = (int)min((int64_t)256, n - i0);
+    const int t = threadIdx.x;
+    const int64_t i = i0 + t;
+    stage_floats(conics + i0 * 3, nloc * 3, s_buf);
+    __syncthreads();
+    const float a = s_buf[t * 3], b = s_buf[t * 3 + 1], cc = s_buf[t * 3 + 2];
+    __syncthreads();  // s_buf now holds the records
+    if (t < nloc) {
+        const int64_t c = i / N, g = i - c * N;
+        const float2 m = means2d[i];
+        const float o = cs.opac[c * cs.op_cstride + g];
+        float col[4] = {0.f, 0.f, 0.f, 0.f};
+        const float* src = cs.colors + c * cs.col_cstride + g * cs.dc;
 #pragma unroll
-    for (int k = 0; k < D; ++k) col[k] = k < cs.dc ? src[k] : cs.depths[i];
-    rec[i] = make_rec3(m, a, b, cc, o, col);
+        for (int k = 0; k < D; ++k) col[k] = k < cs.dc ? src[k] : cs.depths[i];
+        const Rec3 r = make_rec3(m, a, b, cc, o, col);
+        const float v[12] = {r.g0.x, r.g0.y, r.g0.z, r.g0.w, r.g1.x, r.g1.y,
+                             r.g1.z, r.g1.w, r.col.x, r.col.y, r.col.z, r.col.w};
+#pragma unroll
+        for (int k = 0; k < 12; ++k) s_buf[t * kOP + k] = v[k];
+    }
+    __syncthreads();
+    float4* dst = reinterpret_cast<float4*>(rec + i0);
+    for (int q = t; q < nloc * 3; q += 256) {
+        const int e = q / 3, f = q - e * 3;
+        const float* p = s_buf + e * kOP + 4 * f;
+        dst[q] = make_float4(p[0], p[1], p[2], p[3]);
+    }
 }
 
 // does the footprint box of (g0, g1) reach the 8x8 quadrant centred at (qx, qy)?
