@@ -14,7 +14,7 @@ namespace hgsr {
 
 constexpr int kFwd2Batch = 128;
 constexpr int kBwd2Batch = 64;
-constexpr int kRec2 = 32;  // floats per accumulator row: xy(2) rt(9) opac(1) normal(3) densify(2) color(D<=4) absxy(2)
+constexpr int kRec2 = 24;  // floats per accumulator row (96 B): 15 + D colour + 2 abs xy <= 21 used
 
 struct Tile2 {
     int cam, tile, i, j;

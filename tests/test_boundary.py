@@ -60,7 +60,7 @@ def test_pure_host_entry_points(lib):
     assert _native.size_query("hgsr_isect_ws2_bytes", 1000, 5000) >= 16000
     assert _native.size_query("hgsr_raster3d_bwd_ws_bytes", 1, 100, 4, 0) >= 100 * 12 * 4 + 100 * 48
     assert _native.size_query("hgsr_raster3d_bwd_ws_bytes", 1, 100, 4, 1) >= 100 * 12 * 4
-    assert _native.size_query("hgsr_raster2d_bwd_ws_bytes", 1, 100, 4, 0) >= 100 * 32 * 4 + 100 * 96
+    assert _native.size_query("hgsr_raster2d_bwd_ws_bytes", 1, 100, 4, 0) >= 100 * 24 * 4 + 100 * 96
 
 
 def test_invalid_args_return_status(lib):
