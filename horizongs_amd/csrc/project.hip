@@ -400,19 +400,28 @@ __global__ __launch_bounds__(256) void project2d_fwd_kernel(
     const float* __restrict__ Ks, int W, int H, float near_plane, float far_plane,
     float radius_clip, int32_t* __restrict__ radii, float2* __restrict__ means2d,
     float* __restrict__ depths, float* __restrict__ ray_transforms, float* __restrict__ normals) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    // the 12-B rows (means, scales) come in and the 36-B ray transforms / 12-B normals go out
+    // as contiguous runs through LDS
+    __shared__ __attribute__((aligned(16))) float s_io[256 * 12];
+    const int g0 = blockIdx.x * blockDim.x, t = threadIdx.x, g = g0 + t;
     const int c = blockIdx.y;
-    if (g >= N) return;
-    const int64_t o = (int64_t)c * N + g;
+    const int nloc = min(256, N - g0);
+    const bool live = t < nloc;
+    const int64_t o = (int64_t)c * N + g, o0 = (int64_t)c * N + g0;
+    stage_floats(means + (int64_t)g0 * 3, nloc * 3, s_io);
+    stage_floats(scales + (int64_t)g0 * 3, nloc * 3, s_io + 768);
+    __syncthreads();
+    const float m[3] = {s_io[t * 3], s_io[t * 3 + 1], s_io[t * 3 + 2]};
+    const float3 s3 = make_float3(s_io[768 + t * 3], s_io[768 + t * 3 + 1], s_io[768 + t * 3 + 2]);
+    __syncthreads();  // s_io now collects the outputs
     const View v = load_view(viewmats + c * 16, Ks + c * 9);
-    const float m[3] = {means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2]};
-    const Surfel f = surfel_frame(v, m, quats[g], ld3(scales + (int64_t)g * 3));
+    const Surfel f = surfel_frame(v, m, live ? quats[g] : make_float4(1.f, 0.f, 0.f, 0.f), s3);
     float M[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
     float nrm[3] = {0.f, 0.f, 0.f};
     int32_t rad = 0;
     float2 m2 = make_float2(0.f, 0.f);
     float dep = 0.f;
-    if (!(f.mc[2] < near_plane || f.mc[2] > far_plane)) {
+    if (live && !(f.mc[2] < near_plane || f.mc[2] > far_plane)) {
         float WH[3][3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
@@ -454,15 +463,20 @@ __global__ __launch_bounds__(256) void project2d_fwd_kernel(
             }
         }
     }
-    radii[o] = rad;
-    means2d[o] = m2;
-    depths[o] = dep;
+    if (live) {
+        radii[o] = rad;
+        means2d[o] = m2;
+        depths[o] = dep;
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) ray_transforms[o * 9 + i * 3 + j] = M[i][j];
+        for (int j = 0; j < 3; ++j) s_io[t * 9 + i * 3 + j] = M[i][j];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) normals[o * 3 + i] = nrm[i];
+    for (int i = 0; i < 3; ++i) s_io[256 * 9 + t * 3 + i] = nrm[i];
+    __syncthreads();
+    for (int e = t; e < nloc * 9; e += 256) ray_transforms[o0 * 9 + e] = s_io[e];
+    for (int e = t; e < nloc * 3; e += 256) normals[o0 * 3 + e] = s_io[256 * 9 + e];
 }
 
 // ---------------------------------------------------------------- 2DGS bwd
