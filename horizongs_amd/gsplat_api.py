@@ -513,7 +513,6 @@ class _Raster2D(torch.autograd.Function):
                               ra, last)
         ctx.cfg = (width, height, tile_size)
         ctx.fwd_ws = ws  # packed surfel records, reused by the backward
-        ctx.qmask = qmask  # the forward's quadrant culling bits, reused by the backward
         ctx.mark_non_differentiable(rd, rm)
         return rc, ra, rn, rd, rm
 
