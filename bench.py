@@ -4,22 +4,31 @@ One "step" = one training view through the rasterizer path Horizon-GS runs at
 train.py:150-206: gsplat.rasterization(..., packed=False, render_mode="RGB+ED")
 (projection -> tile binning + depth sort -> raster forward), the reference loss
 head (fused HIP loss), loss.backward() (raster backward -> projection backward)
-and the optimizer step (Adam, eps=1e-15, one fused HIP launch), on a synthetic c2 scene: 2,000,000 Gaussians at
-1920x1080, fp32, inputs resident in HBM.
+and the optimizer step (Adam, eps=1e-15, one fused HIP launch), on a synthetic c2 scene
+(SURVEY.md §8(d)): 2,000,000 Gaussians at 1920x1080, fp32, inputs resident in HBM.
+
+`--config` selects the workload of the headline line (default c2); the other BASELINE
+configs are measured as `secondary` lines of the same JSON object:
+  c2          2M explicit Gaussians (the metric's own size), 3DGS
+  c2-anchors  configs[1] Block_small coarse: 500k anchors -> LoD + prefilter + fused decode -> 3DGS
+  c3          configs[2] Block_small fine: the c2 scene through rasterization_2dgs (+ normal loss)
+  c4          configs[3] Block_A per-chunk fine: a 500k-anchor SH2 chunk (color_attr SH2, view_dim 0,
+              10 offsets, colour head [32, 270]; config/ours/large_scene/block_A/chunk_fine/*.yaml),
+              one chunk per GPU, no collectives
+  c5          configs[4] UCGS: 1M anchors (RGB, view_dim 3; config/ours/ucgs/sf/fine.yaml), DDP over views
 
 Multi-GPU: one process per GPU.  `--gpus N` with no WORLD_SIZE in the environment starts
 N ranks itself (a torch.distributed.run child process, before this process touches the
-GPU); under torchrun it is one rank.  The path shards per chunk (reference
-preprocess/generate_chunks_config.py: one chunk per GPU, no collectives), so each rank
-renders its own seeded scene ("scaling": "weak"); with --mode ddp the ranks render
-different views of ONE scene and average the Gaussian gradients with bucketed RCCL
-all-reduces launched from gradient hooks while the backward runs (the c5 data-parallel
-mode, multigpu.GradientAllReduce).
+GPU); under torchrun it is one rank.  At N > 1 the headline c2 line trains ONE scene
+data-parallel over views (each rank renders its own camera; the Gaussian gradients are
+averaged with bucketed RCCL all-reduces launched from gradient hooks while the backward
+runs, multigpu.GradientAllReduce), and the secondary lines are c4 (per chunk: each rank
+trains its own chunk, no collectives -- reference preprocess/generate_chunks_config.py,
+merge.py) and c5 (DDP over views).  At N = 1 the DDP modes are the single-GPU step.
 
 Prints ONE JSON line (rank 0) with the metric, a roofline object for the dominant
 kernel (HIP-event timed live over the timed region), a CPU baseline (the C oracle on all
-host threads, rank 0 at N=1 only) and, at N=1, `secondary`: the same train step measured
-on BASELINE configs[1] (decode-inclusive, 500k anchors) and configs[2] (2DGS).
+host threads, rank 0 at N=1 only) and the secondary lines.
 """
 from __future__ import annotations
 
@@ -86,25 +95,60 @@ KERNELS = ["project3d_fwd", "isect_count", "isect_emit", "tile_sort", "raster3d_
            "depth_normal_bwd", "anchor_prefilter", "explicit_gather"]
 
 
-def parse():
+CONFIGS = {
+    "c2": dict(label="headline: 2M explicit Gaussians (the metric's own size), 1080p, 3DGS", gs="3d", anchors=0,
+               sh_degree=None, mode=None),
+    "c2-anchors": dict(label="configs[1] Block_small coarse: 500k anchors (RGB, view_dim 3), 1080p, 3DGS", gs="3d",
+                       anchors=500_000, sh_degree=None, view_dim=3, mode=None),
+    "c3": dict(label="configs[2] Block_small fine: 2DGS surfels, depth + normal outputs, 1080p", gs="2d", anchors=0,
+               sh_degree=None, mode=None),
+    "c4": dict(label=("configs[3] MatrixCity Block_A per-chunk fine: 500k-anchor SH2 chunk (view_dim 0, 10 offsets, "
+                      "colour head [32,270]), one chunk per GPU, no collectives"), gs="3d", anchors=500_000,
+               sh_degree=2, view_dim=0, mode="chunk"),
+    "c5": dict(label=("configs[4] UCGS: 1M anchors (RGB, view_dim 3; ~10M neural Gaussians before the opacity "
+                      "mask), DDP over views with RCCL all-reduce"), gs="3d", anchors=1_000_000, sh_degree=None,
+               view_dim=3, mode="ddp"),
+}
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="workload of the headline line (default c2; the flags below override it)")
     ap.add_argument("--n", type=int, default=2_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--gs", choices=["3d", "2d"], default="3d")
-    ap.add_argument("--mode", choices=["chunk", "ddp"], default="chunk")
+    ap.add_argument("--gs", choices=["3d", "2d"], default=None)
+    ap.add_argument("--mode", choices=["auto", "chunk", "ddp"], default="auto",
+                    help="auto: the config's own mapping (c4 per chunk, c5 DDP; c2 / c3 DDP over views at N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the configs[1] (500k anchors) and configs[2] (2DGS) lines measured at N = 1")
+                    help="skip the secondary config lines (N = 1: c2-anchors, c3, c4, c5; N > 1: c4, c5)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events (rocprof runs)")
     ap.add_argument("--sh-degree", type=int, default=None, choices=[0, 1, 2, 3],
-                    help="SH colours [N,(d+1)^2,3] ~ N(0, 0.3) through the SH kernel (c4 per-chunk config: 2)")
-    ap.add_argument("--anchors", type=int, default=0,
+                    help="SH colours: [N,(d+1)^2,3] ~ N(0, 0.3) (explicit), or an SH colour head (anchors)")
+    ap.add_argument("--anchors", type=int, default=None,
                     help="decode-inclusive variant (SURVEY 8(d) c2): A anchors -> fused decode -> raster")
-    return ap.parse_args()
+    ap.add_argument("--view-dim", type=int, default=None, choices=[0, 3])
+    return ap.parse_args(argv)
+
+
+def resolve(args, world):
+    """Fill gs / anchors / sh_degree / view_dim / mode from --config, explicit flags winning."""
+    name = args.config or ("c2-anchors" if args.anchors else ("c3" if args.gs == "2d" else "c2"))
+    c = CONFIGS[name]
+    args.config = name
+    args.gs = args.gs or c["gs"]
+    args.anchors = c["anchors"] if args.anchors is None else args.anchors
+    if args.sh_degree is None:
+        args.sh_degree = c["sh_degree"]
+    args.view_dim = c.get("view_dim", 3) if args.view_dim is None else args.view_dim
+    if args.mode == "auto":
+        args.mode = c["mode"] or ("ddp" if world > 1 else "chunk")
+    return args
 
 
 class Workload:
@@ -112,14 +156,9 @@ class Workload:
         self.args = args
         self.dev = dev
         seed = rank if args.mode == "chunk" else 0
-        sc = make_scene(args.n, args.width, args.height, seed=seed, sh_degree=args.sh_degree)
+        # anchor workloads build their anchors in _init_anchors; the explicit scene needs only a camera
+        sc = make_scene(2 if args.anchors else args.n, args.width, args.height, seed=seed, sh_degree=args.sh_degree)
         self.sc = sc
-        # trained in the 3DGS parametrisation: log scales and opacity logits, activated each step
-        self.means = sc.means.to(dev).requires_grad_(True)
-        self.quats = sc.quats.to(dev).requires_grad_(True)
-        self.log_scales = torch.log(sc.scales).to(dev).requires_grad_(True)
-        self.opac_logit = torch.logit(sc.opacities).to(dev).requires_grad_(True)
-        self.colors = sc.colors.to(dev).requires_grad_(True)
         vm = sc.viewmats.clone()
         if args.mode == "ddp" and rank > 0:  # a different view of the same scene per rank
             th = 0.02 * rank
@@ -130,12 +169,19 @@ class Workload:
         self.bg = torch.zeros(1, 3, device=dev)
         g = torch.Generator().manual_seed(1000 + rank)
         self.target = torch.rand(3, args.height, args.width, generator=g).to(dev)
-        self.params = [self.means, self.quats, self.log_scales, self.opac_logit, self.colors]
-        # 3DGS per-attribute learning rates for the explicit Gaussians
-        groups = [(self.means, 1.6e-4), (self.quats, 1e-3), (self.log_scales, 5e-3), (self.opac_logit, 5e-2),
-                  (self.colors, 2.5e-3)]
         if args.anchors:
             groups = self._init_anchors(args, seed, dev)
+        else:
+            # trained in the 3DGS parametrisation: log scales and opacity logits, activated each step
+            self.means = sc.means.to(dev).requires_grad_(True)
+            self.quats = sc.quats.to(dev).requires_grad_(True)
+            self.log_scales = torch.log(sc.scales).to(dev).requires_grad_(True)
+            self.opac_logit = torch.logit(sc.opacities).to(dev).requires_grad_(True)
+            self.colors = sc.colors.to(dev).requires_grad_(True)
+            self.params = [self.means, self.quats, self.log_scales, self.opac_logit, self.colors]
+            # 3DGS per-attribute learning rates for the explicit Gaussians
+            groups = [(self.means, 1.6e-4), (self.quats, 1e-3), (self.log_scales, 5e-3), (self.opac_logit, 5e-2),
+                      (self.colors, 2.5e-3)]
         # the reference optimizer (scene/lod_model.py:320): Adam(eps=1e-15), one group per tensor,
         # stepped every iteration (train.py:274-277) -- one fused HIP launch here
         self.optimizer = Adam([{"params": [p], "lr": lr} for p, lr in groups], lr=0.0, eps=1e-15)
@@ -145,17 +191,22 @@ class Workload:
     def _init_anchors(self, args, seed, dev):
         """SURVEY 8(d) decode-inclusive c2: anchors placed like the c2 Gaussians, feat ~ N(0, 0.1),
         offsets ~ N(0, 0.1), _scaling = ln 0.01 + N(0, 0.1), default-initialised MLPs (seed 2),
-        feat_dim 32, view_dim 3, 10 offsets, RGB (scene/lod_model.py:67-84)."""
+        feat_dim 32, 10 offsets; view_dim 3 + RGB (Block_small, UCGS) or view_dim 0 + an SH colour
+        head of 3 (d+1)^2 outputs per offset (Block_A chunks: SH2, [32, 270]) (scene/lod_model.py:67-84)."""
         A = args.anchors
+        k = 10
+        self.view_dim = args.view_dim
+        self.color_dim = 3 if args.sh_degree is None else 3 * (args.sh_degree + 1) ** 2
         sc = make_scene(A, args.width, args.height, seed=seed)
         g = torch.Generator().manual_seed(2)
         self.anchor = sc.means.to(dev).requires_grad_(True)
         self.feat = (torch.randn(A, 32, generator=g) * 0.1).to(dev).requires_grad_(True)
-        self.offset = (torch.randn(A, 10, 3, generator=g) * 0.1).to(dev).requires_grad_(True)
+        self.offset = (torch.randn(A, k, 3, generator=g) * 0.1).to(dev).requires_grad_(True)
         self.scaling_raw = (np.log(0.01) + torch.randn(A, 6, generator=g) * 0.1).float().to(dev).requires_grad_(True)
         torch.manual_seed(2)
         nn = torch.nn
-        self.mlps = [nn.Sequential(nn.Linear(35, 32), nn.ReLU(True), nn.Linear(32, o)).to(dev) for o in (10, 70, 30)]
+        self.mlps = [nn.Sequential(nn.Linear(32 + self.view_dim, 32), nn.ReLU(True), nn.Linear(32, o)).to(dev)
+                     for o in (k, 7 * k, self.color_dim * k)]
         self.cam_center = torch.zeros(3, device=dev)
         self.params = [self.anchor, self.feat, self.offset, self.scaling_raw] + [
             p for m in self.mlps for p in m.parameters()]
@@ -166,7 +217,6 @@ class Workload:
                         extra_level=torch.zeros(A, device=dev), cam_center=self.cam_center, res_scale=1.0,
                         standard_dist=4.0, fork=2, street_levels=4)
         # densification statistics updated every step by training_statis (train.py:258-262)
-        k = 10
         self.stats = dict(anchor_opacity_accum=torch.zeros(A, 1, device=dev), anchor_demon=torch.zeros(A, 1, device=dev),
                           offset_gradient_accum=torch.zeros(A * k, 1, device=dev),
                           offset_denom=torch.zeros(A * k, 1, device=dev))
@@ -190,7 +240,8 @@ class Workload:
                                                 self.anchor_quats, self.viewmats[0], self.Ks[0], W, H, lod=self.lod,
                                                 lazy=True)  # Av stays on the device: one sync less
             xyz, _, cols, opac, scales, quats, sel = HD.decode(self.anchor, self.feat, self.offset, self.scaling_raw,
-                                                               self.cam_center, self.mlps, vis_idx, 3, 10, 3)
+                                                               self.cam_center, self.mlps, vis_idx, self.view_dim, 10,
+                                                               self.color_dim)
             opac = opac.reshape(-1)
         else:
             xyz, quats, cols = self.means, self.quats, self.colors
@@ -200,13 +251,12 @@ class Workload:
         if self.args.gs == "3d":
             out, alpha, meta = G.rasterization(xyz, quats, scales, opac, cols, self.viewmats, self.Ks, W, H,
                                                packed=False, backgrounds=self.bg, render_mode="RGB+ED",
-                                               sh_degree=None if self.args.anchors else self.args.sh_degree)
+                                               sh_degree=self.args.sh_degree)
             meta["means2d"].retain_grad()
         else:
             (out, alpha, normals, nfd, distort, median), meta = G.rasterization_2dgs(
                 xyz, quats, scales, opac, cols, self.viewmats, self.Ks, W, H,
-                packed=False, backgrounds=self.bg, render_mode="RGB+ED",
-                sh_degree=None if self.args.anchors else self.args.sh_degree)
+                packed=False, backgrounds=self.bg, render_mode="RGB+ED", sh_degree=self.args.sh_degree)
         # the reference fine-stage loss head (train.py:153-178, config/base/small_scene/fine.yaml:50-57):
         # 0.8 L1 + 0.2 D-SSIM + 0.01 scale reg + 0.05 sky opacity + 0.05 opacity entropy, all in the fused HIP loss
         # C == 1: reshape/permute are views, so the loss reads the channels-last render in place and
@@ -274,20 +324,25 @@ def pmc_traffic(args):
 
 
 def psnr_parity(args):
-    """The "PSNR delta vs ref" half of the metric: equal-iteration training parity measured
-    by tests/test_gpu_training_parity.py (HIP path vs the autograd torch restatement of
-    gsplat, same init / target / Adam steps) and committed as profiles/rNN_psnr_parity_*.json.
-    Training to convergence cannot run inside a timed bench step, so the newest recorded
-    figure for this path is quoted."""
+    """The "PSNR delta vs ref" half of the metric: equal-iteration training parity measured by
+    tests/test_gpu_training_parity.py -- 200 Adam iterations of the whole train step on an
+    anchor model (prefilter -> fused decode -> rasterization -> fused loss -> HIP Adam) against
+    the CPU chain whose decode and loss stages are pinned to the reference's goldens.  Training
+    to convergence cannot run inside a timed bench step, so the newest figure is quoted: the
+    one the GPU suite wrote in this tree (gpurun_out/, the same box) if present, else the
+    newest committed profiles/rNN_psnr_pipeline_*.json."""
     import glob
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                          f"r*_psnr_parity_{args.gs}gs.json")))
+    root = os.path.dirname(os.path.abspath(__file__))
+    name = f"psnr_pipeline_{args.gs}gs.json"
+    files = [os.path.join(root, "gpurun_out", name)]
+    files = [f for f in files if os.path.exists(f)] or sorted(glob.glob(os.path.join(root, "profiles", "r*_" + name)))
     if not files:
         return None
     d = json.load(open(files[-1]))
+    src = os.path.relpath(files[-1], root)
     return {"psnr_delta_db": d["psnr_delta_db"], "psnr_hip_db": d["psnr_hip_db"], "psnr_ref_db": d["psnr_ref_db"],
-            "iterations": d["iterations"], "source": os.path.basename(files[-1]) +
-            " (tests/test_gpu_training_parity.py)"}
+            "iterations": d["iterations"], "anchors": d.get("anchors"),
+            "source": src + " (tests/test_gpu_training_parity.py::test_psnr_parity_pipeline_*)"}
 
 
 def _cpu_model():
@@ -339,7 +394,7 @@ def cpu_baseline(args, wl):
         "value": 1.0 / per_view, "unit": "views/s", "cores": threads, "kind": "port",
         "cpu_model": _cpu_model(), "host_cpu_count": os.cpu_count(),
         "sample": (f"one full view of the same workload through the C oracle (oracle/hgsr_oracle.c, OpenMP, "
-                   f"{threads} threads): projection, tile intersection + sort (serial qsort), raster fwd + bwd "
+                   f"{threads} threads): projection, tile intersection + sort (a counting pass over the tile bits, then per-tile sorts spread over the threads), raster fwd + bwd "
                    f"over all {W}x{H} pixels, projection backward, on all {args.n} Gaussians; measured "
                    f"{per_view:.1f}s (no loss head / optimizer: the rasterizer path only)"),
         "breakdown_s": {k: round(v, 3) for k, v in t.items()},
@@ -447,44 +502,59 @@ def roofline(args, res):
 
 
 def workload_name(args):
-    return (f"c2 {'3DGS' if args.gs == '3d' else '2DGS'} train step: "
+    anchors = (f"LoD mask + anchor prefilter + fused anchor decode ({args.anchors} anchors, view_dim {args.view_dim}, "
+               + ("RGB" if args.sh_degree is None else f"SH{args.sh_degree} colour head") + ") + ")
+    return (f"{args.config} {'3DGS' if args.gs == '3d' else '2DGS'} train step: "
             + (f"SH{args.sh_degree} colours + " if args.sh_degree is not None and not args.anchors else "")
-            + (f"LoD mask + anchor prefilter + fused anchor decode ({args.anchors} anchors) + " if args.anchors
-               else "")
-            + "rasterization fwd + reference loss (L1 + D-SSIM + alpha/scale regs"
+            + (anchors if args.anchors else "")
+            + "rasterization fwd" + (f" (SH degree {args.sh_degree})" if args.sh_degree is not None else "")
+            + " + reference loss (L1 + D-SSIM + alpha/scale regs"
             + (" + normal consistency" if args.gs == "2d" else "") + ") + bwd"
             + (" + training_statis" if args.anchors else "") + " + Adam step, RGB+ED")
 
 
-def secondary(args, dev):
-    """BASELINE configs[1] (decode-inclusive, 500k anchors) and configs[2] (2DGS) through the
-    same step, measured after the headline workload is freed (N = 1 only)."""
+def parallelism(args, world):
+    if args.mode == "chunk":
+        return (f"per-chunk: one chunk (seed = rank) per GPU, no collectives (x{world})" if world > 1
+                else "single GPU (per-chunk mapping)")
+    return (f"DDP over views (x{world}): one scene, a camera per rank, bucketed RCCL all-reduce of every "
+            f"gradient launched from backward hooks" if world > 1 else "single GPU (DDP mapping, no collective at N=1)")
+
+
+def secondary_names(args, world):
+    names = ["c4", "c5"] if world > 1 else ["c2-anchors", "c3", "c4", "c5"]
+    return [n for n in names if n != args.config]
+
+
+def secondary(args, rank, world, dev):
+    """The other BASELINE configs through the same step (each rank runs its part; rank 0
+    returns the lines), measured after the headline workload is freed."""
     out = []
-    for name, kw in (("configs[1] Block_small coarse: 500k anchors, 1080p, 3DGS", dict(anchors=500_000)),
-                     ("configs[2] Block_small fine: 2DGS surfels, depth + normal outputs, 1080p", dict(gs="2d"))):
-        a = argparse.Namespace(**vars(args))
-        a.steps, a.warmup = min(args.steps, 10), min(args.warmup, 3)
-        for k, v in kw.items():
-            setattr(a, k, v)
-        r = measure(a, 0, 1, dev)
-        roof = roofline(a, r)
-        out.append({"config": name, "workload": workload_name(a), "value": round(a.steps / r["dt"], 3),
-                    "unit": "views/s", "ms_per_step": round(r["dt"] / a.steps * 1e3, 3), "steps": a.steps,
-                    "warmup": a.warmup, "gaussians": int(r["wl"].last_colors.shape[0]),
-                    "n_isects": r["isects_after"],
-                    "roofline": None if roof is None else {k: roof[k] for k in (
-                        "bound", "kernel", "achieved", "frac", "frac_executed", "kernel_avg_ms")},
-                    "kernels": r["kernels"]})
+    for name in secondary_names(args, world):
+        a = parse(["--config", name, "--steps", str(min(args.steps, 10)), "--warmup", str(min(args.warmup, 3)),
+                   "--width", str(args.width), "--height", str(args.height)] + (["--no-timing"] if args.no_timing else []))
+        a = resolve(a, world)
+        r = measure(a, rank, world, dev)
+        if rank == 0:
+            roof = roofline(a, r)
+            out.append({"config": name, "label": CONFIGS[name]["label"], "workload": workload_name(a),
+                        "parallelism": parallelism(a, world), "n_gpus": world,
+                        "value": round(world * a.steps / r["dt"], 3), "unit": "views/s",
+                        "ms_per_step": round(r["dt"] / a.steps * 1e3, 3), "steps": a.steps, "warmup": a.warmup,
+                        "gaussians": int(r["wl"].last_colors.shape[0]), "n_isects": r["isects_after"],
+                        "roofline": None if roof is None else {k: roof[k] for k in (
+                            "bound", "kernel", "achieved", "frac", "frac_executed", "kernel_avg_ms")},
+                        "kernels": r["kernels"]})
         del r
         torch.cuda.empty_cache()
     return out
 
 
 def main():
-    args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    args = resolve(parse(), world)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -493,8 +563,8 @@ def main():
     wl, dt = res["wl"], res["dt"]
     roof = roofline(args, res) if rank == 0 else None
     cpu = None
-    if (rank == 0 and world == 1 and not args.no_cpu_baseline and args.gs == "3d" and not args.anchors
-            and args.sh_degree is None):
+    if (rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2" and args.gs == "3d"
+            and args.sh_degree is None and not args.anchors):
         cpu = cpu_baseline(args, wl)
     line = None
     if rank == 0:
@@ -503,20 +573,20 @@ def main():
             "metric": METRIC, "value": round(world * args.steps / dt, 3), "unit": "views/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic (seeded c2 scene, SURVEY 8(d); no dataset in the environment)",
-            "config": {"workload": workload_name(args),
+            "data": "synthetic (seeded scenes of SURVEY 8(d); no dataset in the environment)",
+            "config": {"workload": workload_name(args), "config": args.config, "label": CONFIGS[args.config]["label"],
                        "gaussians": int(wl.last_colors.shape[0]), "width": args.width, "height": args.height,
-                       "parallelism": (f"per-chunk, one scene per GPU, no collectives (x{world})"
-                                       if args.mode == "chunk" else
-                                       f"DDP over views (x{world}), RCCL all-reduce of the gradients from hooks")},
+                       "parallelism": parallelism(args, world)},
             "roofline": roof, "cpu_baseline": cpu, "quality": psnr_parity(args), "kernels": res["kernels"],
             "kernels_source": "HIP events of every kernel over a separate pass after the timed region",
             "hbm_kernels": hbm_kernels(wl, res["kernels"], res["isects_after"]),
         }
-    if rank == 0 and world == 1 and not args.no_secondary and not args.anchors and args.gs == "3d":
-        del res, wl
-        torch.cuda.empty_cache()
-        line["secondary"] = secondary(args, dev)
+    del res, wl
+    torch.cuda.empty_cache()
+    if not args.no_secondary:
+        sec = secondary(args, rank, world, dev)
+        if rank == 0:
+            line["secondary"] = sec
     if rank == 0:
         print(json.dumps(line))
     if world > 1:

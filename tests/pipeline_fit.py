@@ -1,0 +1,162 @@
+"""Equal-iteration training through the reference-pinned pipeline (TEST INFRASTRUCTURE).
+
+One reference train step (train.py:150-277) on an anchor model, twice:
+
+* CPU chain (the oracle): LoD-free prefilter_voxel (anchor projection radii > 0, oracle
+  proj3d_fwd) -> generate_neural_gaussians restated in torch (oracle/decode_ref.py, pinned to
+  tests/golden/decode_*.npz) -> the C-oracle rasterization as an autograd Function
+  (oracle/autograd.py) -> the loss head restated in torch (oracle/loss_ref.py, pinned to
+  tests/golden/losses.npz) -> backward -> torch.optim.Adam(eps=1e-15) (scene/lod_model.py:320);
+* HIP chain (the product): decode.prefilter -> decode.decode -> gsplat_api.rasterization /
+  rasterization_2dgs -> loss.fused_loss -> backward -> optim.Adam.
+
+Both start from the same initial anchor model and fit the same target render (the CPU
+chain's render of a second, "true" anchor model) with the fine-stage loss weights and
+learning rates of config/base/small_scene/fine.yaml (0.8 L1 + 0.2 D-SSIM + 0.01 scale
+regulariser + 0.05 sky opacity + 0.05 opacity entropy; the normal term starts at iteration
+7000, after this run).  `fit()` returns the final PSNR against the target.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from horizongs_amd.synthetic import make_scene
+
+HEADS = ("opacity", "cov", "color")
+# config/base/small_scene/fine.yaml initial learning rates (position lr 0: the anchors stay)
+LR = dict(feat=0.0075, offset=0.001, scaling=0.007, opacity=0.002, cov=0.004, color=0.008)
+
+
+def anchor_model(A, W, H, seed, param_seed, view_dim=3, color_dim=3, n_off=10, feat_std=0.5):
+    """Anchors placed like the c2 scene (seed: pixel-uniform, depth U[2,10]); parameters from
+    param_seed: feat ~ N(0, feat_std), offsets ~ N(0, 0.5) (x exp(scaling[:3]) ~ 0.05), _scaling = ln 0.05 + N(0, 0.1), MLPs with
+    nn.Linear's default init (scene/lod_model.py:67-84 shapes)."""
+    sc = make_scene(A, W, H, seed=seed)
+    g = torch.Generator().manual_seed(param_seed)
+    p = dict(anchor=sc.means.clone(), feat=torch.randn(A, 32, generator=g) * feat_std,
+             offset=torch.randn(A, n_off, 3, generator=g) * 0.5,
+             scaling=(math.log(0.05) + torch.randn(A, 6, generator=g) * 0.1).float())
+    torch.manual_seed(param_seed + 1)
+    for h, o in zip(HEADS, (n_off, 7 * n_off, color_dim * n_off)):
+        l1, l2 = torch.nn.Linear(32 + view_dim, 32), torch.nn.Linear(32, o)
+        p[f"{h}_w1"], p[f"{h}_b1"] = l1.weight.detach().clone(), l1.bias.detach().clone()
+        p[f"{h}_w2"], p[f"{h}_b2"] = l2.weight.detach().clone(), l2.bias.detach().clone()
+    cfg = dict(viewmats=sc.viewmats, Ks=sc.Ks, W=W, H=H, view_dim=view_dim, color_dim=color_dim, n_off=n_off,
+               cam_center=torch.zeros(3), sh_degree=None if color_dim == 3 else int(round((color_dim // 3) ** 0.5)) - 1)
+    return p, cfg
+
+
+def _lr(name):
+    for k, v in LR.items():
+        if name.startswith(k):
+            return v
+    raise KeyError(name)
+
+
+def _mlps(p):
+    return {k: v for k, v in p.items() if k.split("_")[0] in HEADS}
+
+
+# ----------------------------------------------------------------------------- CPU chain
+def cpu_render(p, cfg, gs="3d", dtype=torch.float32):
+    """-> (image [3,H,W], alpha [H,W], scaling [M,3]) through the oracle chain."""
+    from oracle import autograd as OA
+    from oracle import decode_ref as D
+    from oracle import oracle as O
+    W, H = cfg["W"], cfg["H"]
+    anchor = p["anchor"].to(dtype)
+    with torch.no_grad():  # prefilter_voxel: anchors as Gaussians, first three scales, identity rotation
+        q = np.zeros((anchor.shape[0], 4), np.float32)
+        q[:, 0] = 1
+        r, _, _, _ = O.proj3d_fwd(p["anchor"].numpy(), q, torch.exp(p["scaling"][:, :3].detach()).numpy(),
+                                  cfg["viewmats"].numpy(), cfg["Ks"].numpy(), W, H)
+        vis = torch.from_numpy(r[0] > 0)
+    mlps = {k: v.to(dtype) for k, v in _mlps(p).items()}
+    xyz, _, col, op, scal, rot, _ = D.decode_torch(anchor[vis], p["feat"].to(dtype)[vis], p["offset"].to(dtype)[vis],
+                                                   p["scaling"].to(dtype)[vis], cfg["cam_center"].to(dtype), mlps,
+                                                   cfg["view_dim"], cfg["n_off"], cfg["color_dim"])
+    rc = dict(viewmats=cfg["viewmats"], Ks=cfg["Ks"], W=W, H=H, sh_degree=cfg["sh_degree"], bg=torch.zeros(1, 3),
+              mode="RGB+ED")
+    out, ra = OA.rasterization(xyz, rot, scal, op.reshape(-1), col, rc, gs=gs)
+    return out[0, ..., :3].permute(2, 0, 1), ra[0, ..., 0], scal
+
+
+def cpu_loss(p, cfg, gt, gs="3d"):
+    from oracle import loss_ref as LR_
+    img, alpha, scal = cpu_render(p, cfg, gs)
+    return LR_.loss(img, gt, None, 0.2, alpha, 0.05, 0.05, scal, 0.01)[0]
+
+
+# ----------------------------------------------------------------------------- HIP chain
+def gpu_render(p, cfg, gs="3d"):
+    from horizongs_amd import decode as HD
+    from horizongs_amd import gsplat_api as G
+    W, H = cfg["W"], cfg["H"]
+    dev = p["feat"].device
+    vm, K = cfg["viewmats"].to(dev), cfg["Ks"].to(dev)
+    A = p["anchor"].shape[0]
+    quats = torch.zeros(A, 4, device=dev)
+    quats[:, 0] = 1
+    with torch.no_grad():
+        _, vis_idx = HD.prefilter(p["anchor"], torch.exp(p["scaling"].detach()), quats, vm[0], K[0], W, H)
+    xyz, _, col, op, scal, rot, _ = HD.decode(p["anchor"], p["feat"], p["offset"], p["scaling"],
+                                              cfg["cam_center"].to(dev), _mlps(p), vis_idx, cfg["view_dim"],
+                                              cfg["n_off"], cfg["color_dim"])
+    bg = torch.zeros(1, 3, device=dev)
+    if gs == "3d":
+        out, ra, _ = G.rasterization(xyz, rot, scal, op.reshape(-1), col, vm, K, W, H, packed=False, backgrounds=bg,
+                                     render_mode="RGB+ED", sh_degree=cfg["sh_degree"])
+    else:
+        (out, ra, *_), _ = G.rasterization_2dgs(xyz, rot, scal, op.reshape(-1), col, vm, K, W, H, packed=False,
+                                                backgrounds=bg, render_mode="RGB+ED", sh_degree=cfg["sh_degree"])
+    return out[0].permute(2, 0, 1), ra[0, ..., 0], scal
+
+
+def gpu_loss(p, cfg, gt, gs="3d"):
+    from horizongs_amd.loss import fused_loss
+    img, alpha, scal = gpu_render(p, cfg, gs)
+    return fused_loss(img, gt, None, 0.2, alpha, 0.05, 0.05, scal, 0.01)[0]
+
+
+# ----------------------------------------------------------------------------- fit
+def psnr(img, gt):
+    mse = float(((img[:3].detach().cpu().double() - gt.cpu().double()) ** 2).mean())
+    return 10 * math.log10(1.0 / mse)
+
+
+def fit(p0, cfg, gt, iters, gs="3d", device="cpu"):
+    """`iters` Adam steps of the chain on `device` from p0; returns (final PSNR, losses)."""
+    on_gpu = device != "cpu"
+    p = {k: v.to(device).clone().requires_grad_(k != "anchor") for k, v in p0.items()}
+    if on_gpu:
+        from horizongs_amd.optim import Adam
+    else:
+        Adam = torch.optim.Adam
+    opt = Adam([{"params": [p[k]], "lr": _lr(k)} for k in p if k != "anchor"], lr=0.0, eps=1e-15)
+    gt_d = gt.to(device)
+    loss_fn, render = (gpu_loss, gpu_render) if on_gpu else (cpu_loss, cpu_render)
+    losses = []
+    for _ in range(iters):
+        opt.zero_grad(set_to_none=True)
+        loss = loss_fn(p, cfg, gt_d, gs)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.detach()))
+    with torch.no_grad():
+        img = render(p, cfg, gs)[0]
+    return psnr(img, gt), losses
+
+
+def target(n, W, H, seed, gs="3d"):
+    """The fit's ground truth: an explicit seeded Gaussian scene (make_scene, scales 0.005-0.03)
+    rendered through the CPU chain's rasterizer -- not an anchor model, so the fit saturates
+    at a realistic PSNR instead of converging to an exact copy."""
+    from oracle import autograd as OA
+    sc = make_scene(n, W, H, seed=seed, scale_range=(0.005, 0.03))
+    rc = dict(viewmats=sc.viewmats, Ks=sc.Ks, W=W, H=H, bg=torch.zeros(1, 3), mode="RGB+ED")
+    with torch.no_grad():
+        out, _ = OA.rasterization(sc.means, sc.quats, sc.scales, sc.opacities, sc.colors, rc, gs=gs)
+    return out[0, ..., :3].permute(2, 0, 1).contiguous()

@@ -98,7 +98,7 @@ def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None
             continue
         rates["v_" + k] = cond_close(v.cpu().numpy(), gr32[k], gr64[k], "v_" + k, rel_floor=0, env=genv[k])
     print("strict 1e-5/1e-4 pass rates:", {k: round(float(v), 6) for k, v in rates.items()}, "stats", stats)
-    return stats, rates, dict(out=out, alpha=alpha, meta=meta, r32=r32, r64=r64)
+    return stats, rates, dict(out=out, alpha=alpha, meta=meta, r32=r32, r64=r64, grads=got, gr32=gr32, gr64=gr64)
 
 
 def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):

@@ -62,5 +62,30 @@ def test_launcher_noop(bench, monkeypatch, argv, world):
 
 def test_parser_has_modes(bench, monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--mode", "ddp", "--gpus", "2", "--no-secondary"])
-    a = bench.parse()
+    a = bench.resolve(bench.parse(), 2)
     assert a.mode == "ddp" and a.gpus == 2 and a.no_secondary
+
+
+@pytest.mark.parametrize("argv,world,expect", [
+    ([], 1, dict(config="c2", gs="3d", anchors=0, sh_degree=None, mode="chunk")),
+    ([], 8, dict(config="c2", gs="3d", anchors=0, mode="ddp")),
+    (["--config", "c4"], 1, dict(gs="3d", anchors=500_000, sh_degree=2, view_dim=0, mode="chunk")),
+    (["--config", "c4"], 8, dict(mode="chunk")),
+    (["--config", "c5"], 4, dict(anchors=1_000_000, sh_degree=None, view_dim=3, mode="ddp")),
+    (["--gs", "2d"], 1, dict(config="c3", gs="2d", anchors=0)),
+    (["--anchors", "1000"], 1, dict(config="c2-anchors", anchors=1000, view_dim=3)),
+    (["--config", "c5", "--mode", "chunk"], 2, dict(mode="chunk")),
+])
+def test_configs_resolve(bench, argv, world, expect):
+    """--config fills the workload of BASELINE configs c2-c5 (c4: SH2 chunk, view_dim 0, no
+    collectives; c5: 1M anchors, DDP); the c2 headline trains one scene DDP over views at N > 1."""
+    a = bench.resolve(bench.parse(argv), world)
+    for k, v in expect.items():
+        assert getattr(a, k) == v, (k, getattr(a, k), v)
+
+
+def test_secondary_lines_per_world(bench):
+    a = bench.resolve(bench.parse([]), 1)
+    assert bench.secondary_names(a, 1) == ["c2-anchors", "c3", "c4", "c5"]
+    assert bench.secondary_names(bench.resolve(bench.parse([]), 8), 8) == ["c4", "c5"]
+    assert "c4" not in bench.secondary_names(bench.resolve(bench.parse(["--config", "c4"]), 2), 2)

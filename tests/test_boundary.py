@@ -92,3 +92,39 @@ def test_unsupported_options_raise():
     with pytest.raises(NotImplementedError):
         G.rasterization(torch.zeros(1, 3), torch.ones(1, 4), torch.ones(1, 3), torch.ones(1), torch.ones(1, 3),
                         torch.eye(4)[None], torch.eye(3)[None], 8, 8, packed=True)
+
+
+def _render_calls():
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "render_calls.json")) as f:
+        return json.load(f)
+
+
+def test_reference_call_sites_bind():
+    """Every gsplat call of the reference's renderer (tests/golden/render_calls.json, extracted
+    from gaussian_renderer/render.py:40-76,149-186 by scripts/extract_render_calls.py) binds to the
+    drop-in surface: the same positional arity and keyword names, through the same import paths."""
+    import importlib
+    import inspect
+    rc = _render_calls()
+    assert len(rc["calls"]) == 4 and rc["meta_keys_read"] == ["means2d", "radii"]
+    for imp in rc["imports"]:  # `import gsplat`, `from gsplat.cuda._wrapper import ...`
+        mod = importlib.import_module(imp["module"])
+        for n in imp.get("names", []):
+            assert callable(getattr(mod, n)), (imp, n)
+    import gsplat
+    from gsplat.cuda import _wrapper
+    for c in rc["calls"]:
+        fn = getattr(gsplat, c["function"]) if c["callee"].startswith("gsplat.") else getattr(_wrapper, c["function"])
+        ba = inspect.signature(fn).bind(*c["args"], **c["kwargs"])  # raises TypeError on any mismatch
+        assert set(ba.arguments) >= set(c["kwargs"]), c["line"]
+
+
+def test_reference_call_site_unpack_shapes():
+    """The recorded result structures (render.py:40 -> 3 names; :56 -> ((6 names), info); the
+    prefilter's 5-way unpack at :189) are the ones gsplat_api returns (GPU side:
+    tests/test_gpu_parity.py::test_reference_call_sites_run)."""
+    shapes = {c["function"]: c.get("unpacked_at", {}).get("shape", c["target"]) for c in _render_calls()["calls"]}
+    assert len(shapes["rasterization"]) == 3
+    assert len(shapes["rasterization_2dgs"]) == 2 and len(shapes["rasterization_2dgs"][0]) == 6
+    assert len(shapes["fully_fused_projection"]) == 5 and len(shapes["fully_fused_projection_2dgs"]) == 5

@@ -5,8 +5,9 @@ set_gs_mask (scene/lod_model.py:292-296) + generate_explicit_gaussians
 * LoD mask and gathers bit-exact vs the torch restatement (oracle/explicit_ref.py), forward
   and backward, including empty / full masks, ragged sizes and SH0 (no f_rest);
 * c4's SH2 scene (2M Gaussians, 1080p) through the explicit path vs the C oracle on a band;
-* c5's size (10M SH2 Gaussians, 1080p) rendered through the explicit path: property checks
-  (there is no oracle at this size), with the render time printed."""
+* c5's size (10M SH2 Gaussians, 1080p): one train step through the explicit path (loss,
+  backward, HIP Adam) with full-size properties, and the rasterization vs the C oracle on a
+  band of rows of the same frame; the forward and step times are printed."""
 import time
 from types import SimpleNamespace
 
@@ -95,37 +96,87 @@ def test_c4_sh2_explicit_band_vs_oracle():
 
 
 @pytest.mark.slow
-def test_c5_10m_sh2_explicit_render():
-    """c5 size: 10M explicit SH2 Gaussians at 1920x1080 through the explicit render path."""
+def test_c5_10m_sh2_explicit_train_step():
+    """c5 size: 10M explicit SH2 Gaussians at 1920x1080 through one train step of the explicit
+    path -- set_gs_mask -> generate_explicit_gaussians -> rasterization (SH2, RGB+ED) -> the
+    fused loss head -> backward -> HIP Adam -- with properties at full size (finite loss and
+    gradients, dropped rows untouched, bit-reproducible forward, run-to-run backward agreement)
+    and the rasterization's forward + every gradient vs the C oracle on a band of rows of the
+    same 7M-Gaussian frame."""
+    from horizongs_amd.loss import fused_loss
+    from horizongs_amd.optim import Adam
     n = 10_000_000
     m, sc = _model(n, 9, seed=5)
     m.street_levels, m.standard_dist = 3, 40.0
     vm, K = sc.viewmats.to(DEV), sc.Ks.to(DEV)
     bg = torch.zeros(1, 3, device=DEV)
+    target = torch.rand(3, sc.height, sc.width, generator=torch.Generator().manual_seed(6)).to(DEV)
+    names = ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
+    for k in names:
+        setattr(m, k, getattr(m, k).clone().requires_grad_(True))
 
     def render():
         mask = HX.set_gs_mask(m, torch.zeros(3, device=DEV), 1.0)
         xyz, color, opac, scal, rot, deg, _ = HX.generate_explicit_gaussians(m, mask)
         out, alpha, meta = G.rasterization(xyz, rot, scal, opac.squeeze(-1), color, vm, K, sc.width, sc.height,
                                            packed=False, sh_degree=deg, backgrounds=bg, render_mode="RGB+ED")
-        return out, alpha, meta, xyz.shape[0]
+        return out, alpha, meta, mask, (xyz, color, opac, scal, rot)
+
+    def step_grads():
+        for k in names:
+            getattr(m, k).grad = None
+        out, alpha, meta, mask, dec = render()
+        img = out[0].permute(2, 0, 1)
+        loss = fused_loss(img, target, None, 0.2, alpha[0, ..., 0], 0.05, 0.05, dec[3], 0.01)[0]
+        loss.backward()
+        return loss, out, alpha, meta, mask, dec, [getattr(m, k).grad.clone() for k in names]
 
     with torch.no_grad():
-        out, alpha, meta, M = render()  # warm-up (allocations)
+        out0, _, _, _, _ = render()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        reps = 5
-        for _ in range(reps):
-            out, alpha, meta, M = render()
+        for _ in range(3):
+            out0, alpha0, meta0, _, dec0 = render()
         torch.cuda.synchronize()
-        ms = (time.perf_counter() - t0) / reps * 1e3
-    a = alpha
-    assert M > 5_000_000
-    assert torch.isfinite(out).all() and float(a.min()) >= 0.0 and float(a.max()) <= 1.0
-    assert float(a.mean()) > 0.5
+        ms_fwd = (time.perf_counter() - t0) / 3 * 1e3
+    loss, out, alpha, meta, mask, dec, grads = step_grads()
+    M = dec[0].shape[0]
+    assert M > 5_000_000 and torch.isfinite(loss)
+    assert torch.equal(out.detach(), out0)  # atomic-free forward: every bit reproduces
+    a = alpha.detach()
+    assert torch.isfinite(out).all() and float(a.min()) >= 0.0 and float(a.max()) <= 1.0 and float(a.mean()) > 0.5
     ids = meta["isect_ids"]
     assert int(meta["tiles_per_gauss"].sum()) == ids.numel() and bool((ids[1:] >= ids[:-1]).all())
-    out2, _, _, _ = render()  # atomic-free forward: every bit reproduces
-    assert torch.equal(out2, out)
-    print(f"c5 explicit render: {M} of {n} Gaussians kept, {ids.numel()} intersections, {ms:.2f} ms/view "
-          f"(LoD mask + gather + rasterization fwd, SH2, 1080p)")
+    drop = ~mask
+    for k, gk in zip(names, grads):
+        assert torch.isfinite(gk).all(), k
+        assert float(gk[drop].abs().max()) == 0.0, k  # rows the LoD mask dropped get no gradient
+        assert float(gk[mask].abs().max()) > 0.0, k
+    # the backward accumulates with float atomics: a second run agrees to rounding
+    _, _, _, _, _, _, grads2 = step_grads()
+    for k, g1, g2 in zip(names, grads, grads2):
+        tol = 1e-5 + 1e-3 * float(g1.abs().max())
+        assert float((g1 - g2).abs().max()) <= tol, k
+    # HIP Adam step over the six tensors: dropped rows stay, kept rows move
+    before = [getattr(m, k).detach().clone() for k in names]
+    opt = Adam([{"params": [getattr(m, k)], "lr": 1e-3} for k in names], lr=0.0, eps=1e-15)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss, *_ = step_grads()
+    opt.step()
+    torch.cuda.synchronize()
+    ms_step = (time.perf_counter() - t0) * 1e3
+    for k, b in zip(names, before):
+        p = getattr(m, k).detach()
+        assert torch.equal(p[drop], b[drop]), k
+        assert not torch.equal(p[mask], b[mask]), k
+    print(f"c5 explicit: {M} of {n} Gaussians kept, {ids.numel()} intersections, forward {ms_fwd:.2f} ms/view, "
+          f"train step (fwd + loss + bwd + Adam over 10M x 59 floats) {ms_step:.2f} ms")
+    # the rasterization of this frame vs the oracle on rows 0-63: forward and every gradient
+    xyz, color, opac, scal, rot = (t.detach().cpu() for t in dec0)
+    sub = SimpleNamespace(means=xyz, quats=rot, scales=scal, opacities=opac.reshape(-1), colors=color,
+                          viewmats=sc.viewmats, Ks=sc.Ks, width=sc.width, height=sc.height)
+    del out, alpha, meta, grads, grads2, dec, out0, dec0
+    torch.cuda.empty_cache()
+    (max_tile, replay, stopped), _, _ = RP.run_3dgs(sub, "RGB+ED", None, rows=64, seed=8, sh=2)
+    assert max_tile >= 1024 and stopped > 0.05, (max_tile, replay, stopped)

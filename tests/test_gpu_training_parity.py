@@ -123,3 +123,43 @@ def test_psnr_parity_2dgs():
     print(res)
     assert psnr_cpu > psnr_init + 3.0
     assert abs(psnr_gpu - psnr_cpu) <= 0.05, res
+
+
+# ----------------------------------------------------------------------------- anchor pipeline
+def _pipeline_parity(gs):
+    """200 equal Adam iterations of the whole reference train step on an anchor model
+    (5k anchors, 160x120; tests/pipeline_fit.py): prefilter -> decode -> rasterization ->
+    loss head -> backward -> Adam, HIP chain vs the CPU chain whose decode and loss stages are
+    pinned to the reference's own goldens.  Final PSNRs against the same target within 0.05 dB."""
+    from tests import pipeline_fit as PF
+    A, W, H, iters = 5000, 160, 120, 200
+    gt = PF.target(40000, W, H, seed=31, gs=gs)
+    p0, cfg = PF.anchor_model(A, W, H, seed=32, param_seed=200)
+    with torch.no_grad():
+        psnr_init = PF.psnr(PF.cpu_render(p0, cfg, gs)[0], gt)
+    psnr_cpu, loss_cpu = PF.fit(p0, cfg, gt, iters, gs=gs)
+    psnr_gpu, loss_gpu = PF.fit(p0, cfg, gt, iters, gs=gs, device="cuda")
+    res = dict(psnr_init_db=round(psnr_init, 4), psnr_ref_db=round(psnr_cpu, 4), psnr_hip_db=round(psnr_gpu, 4),
+               psnr_delta_db=round(psnr_gpu - psnr_cpu, 4), iterations=iters, anchors=A, width=W, height=H,
+               loss_first=[round(loss_cpu[0], 6), round(loss_gpu[0], 6)],
+               loss_last=[round(loss_cpu[-1], 6), round(loss_gpu[-1], 6)],
+               reference=("CPU chain: oracle/decode_ref.decode_torch (pinned to tests/golden/decode_*.npz) -> "
+                          f"C-oracle rasterization{'_2dgs' if gs == '2d' else ''} (oracle/autograd.py) -> "
+                          "oracle/loss_ref.loss (pinned to tests/golden/losses.npz) -> torch.optim.Adam(eps=1e-15); "
+                          "fine-stage loss weights and learning rates (config/base/small_scene/fine.yaml)"))
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", f"psnr_pipeline_{gs}gs.json"), "w") as f:
+        json.dump(res, f)
+    print(res)
+    # the first losses see identical parameters: the two chains agree before any divergence
+    assert abs(loss_gpu[0] - loss_cpu[0]) <= 1e-5 + 1e-4 * abs(loss_cpu[0]), res
+    assert psnr_cpu > psnr_init + 10.0  # the fit actually fits
+    assert abs(psnr_gpu - psnr_cpu) <= 0.05, res
+
+
+def test_psnr_parity_pipeline_3dgs():
+    _pipeline_parity("3d")
+
+
+def test_psnr_parity_pipeline_2dgs():
+    _pipeline_parity("2d")
