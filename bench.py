@@ -267,18 +267,21 @@ class Workload:
                                                  normals_from_depth=nfd.reshape(H, W, 3).permute(2, 0, 1),
                                                  lambda_normal=0.05)
         loss = fused_loss(img, self.target, None, 0.2, alpha.reshape(H, W), 0.05, 0.05, scales, 0.01, **aux)[0]
-        ddp = self.args.mode == "ddp"
+        ddp = self.args.mode == "ddp" and self.allreduce.active
         if ddp:
             self.allreduce.begin()  # gradient hooks launch the bucket all-reduces during the backward
         loss.backward()
-        if ddp:
-            self.allreduce.finish()
         if self.args.anchors:  # densification statistics of this view (train.py:258-262)
             HDn.training_statis(self.stats_model, self.stats_opt,
                                 dict(selection_mask=sel, visible_mask=visible, viewspace_points=meta["means2d"],
                                      visibility_filter=meta["radii"][0] > 0, opacity=opac, radii=meta["radii"][0]),
                                 W, H)
-        self.optimizer.step()  # train.py:274-277 (zero_grad(set_to_none) = the grad reset above)
+        if ddp:
+            # train.py:274-277 per bucket: each bucket's Adam launch follows its own all-reduce and
+            # overlaps the later buckets' collectives
+            self.allreduce.finish(step=self.optimizer.step_params)
+        else:
+            self.optimizer.step()  # train.py:274-277 (zero_grad(set_to_none) = the grad reset above)
         self.meta = meta
         return loss
 

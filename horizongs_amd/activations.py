@@ -30,9 +30,12 @@ class _Activate(torch.autograd.Function):
         n = scales.shape[0]
         v_ls = torch.empty_like(scales) if ctx.needs_input_grad[0] else None
         v_lg = torch.empty_like(opac) if ctx.needs_input_grad[1] else None
-        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
-        N.call("hgsr_activate_bwd", n, ptr(scales), ptr(opac), ptr(c(v_scales)), ptr(c(v_opac)), ptr(v_ls),
-               ptr(v_lg), N.stream(scales.device))
+        # contiguous copies held in locals until the launch is enqueued: a temporary freed
+        # inside the call could hand its block to the next temporary (aliased inputs)
+        vs = None if v_scales is None else v_scales.contiguous()
+        vo = None if v_opac is None else v_opac.contiguous()
+        N.call("hgsr_activate_bwd", n, ptr(scales), ptr(opac), ptr(vs), ptr(vo), ptr(v_ls), ptr(v_lg),
+               N.stream(scales.device))
         return v_ls, v_lg
 
 

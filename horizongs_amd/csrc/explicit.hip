@@ -63,7 +63,8 @@ __global__ __launch_bounds__(256) void explicit_count_kernel(int64_t N, const fl
     if (threadIdx.x == 0) block_cnt[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
 }
 
-// exclusive scan of nb block counts (nb <= 65536 per launch plan: 10M Gaussians -> 9,766)
+// exclusive scan of nb block counts in one workgroup: each of the 1024 lanes walks nb / 1024 counts
+// serially (host check nb <= 2^20, i.e. <= 2^30 Gaussians; 10M Gaussians -> 9,766 blocks, 10 per lane)
 __global__ __launch_bounds__(1024) void explicit_scan_kernel(int nb, const int32_t* __restrict__ cnt,
                                                              int64_t* __restrict__ base,
                                                              int64_t* __restrict__ total) {

@@ -53,10 +53,11 @@ def lod_mask(anchor, level, extra_level, cam_center, res_scale, standard_dist, f
     _check_dev(anchor, level, extra_level, cam_center)
     A = anchor.shape[0]
     mask = torch.empty(A, dtype=torch.uint8, device=anchor.device)
-    N.call("hgsr_lod_mask", A, ptr(_f32(anchor)), ptr(level.reshape(-1).to(torch.int32).contiguous()),
-           ptr(_f32(extra_level.reshape(-1))), ptr(_f32(cam_center.reshape(3))), float(res_scale),
-           float(standard_dist), float(math.log2(fork)), int(street_levels) - 1, ptr(mask),
-           N.stream(anchor.device))
+    # converted inputs held in locals until the launch is enqueued (no aliased temporaries)
+    an, lv = _f32(anchor), level.reshape(-1).to(torch.int32).contiguous()
+    el, cc = _f32(extra_level.reshape(-1)), _f32(cam_center.reshape(3))
+    N.call("hgsr_lod_mask", A, ptr(an), ptr(lv), ptr(el), ptr(cc), float(res_scale), float(standard_dist),
+           float(math.log2(fork)), int(street_levels) - 1, ptr(mask), N.stream(anchor.device))
     return mask.bool()
 
 
@@ -107,8 +108,9 @@ def prefilter(anchor, scales, quats, viewmat, K, width, height, lod=None, eps2d=
         keep = [lv, el, cc]
         args = [ptr(lv), ptr(el), ptr(cc), float(lod.get("res_scale", 1.0)), float(lod["standard_dist"]),
                 float(math.log2(lod["fork"])), int(lod["street_levels"]) - 1]
-    N.call("hgsr_anchor_prefilter", A, ptr(_f32(anchor)), ptr(_f32(quats)), sc.data_ptr(), stride,
-           ptr(_f32(viewmat.reshape(4, 4))), ptr(_f32(K.reshape(3, 3))), int(width), int(height), float(eps2d),
+    an, qs, vm, kk = _f32(anchor), _f32(quats), _f32(viewmat.reshape(4, 4)), _f32(K.reshape(3, 3))
+    N.call("hgsr_anchor_prefilter", A, ptr(an), ptr(qs), sc.data_ptr(), stride, ptr(vm), ptr(kk), int(width),
+           int(height), float(eps2d),
            float(near_plane), float(far_plane), *args, ptr(vis), s)
     ws_b = N.size_query("hgsr_explicit_ws_bytes", A)
     ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)

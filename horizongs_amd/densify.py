@@ -77,10 +77,11 @@ def training_statis(model, opt, render_pkg, width, height):
     else:
         rank = (torch.cumsum(sel8, 0, dtype=torch.int32) - sel8).contiguous()
     gmax = opt.growing_type == "max"
+    # converted inputs held in locals until the launch is enqueued (no aliased temporaries)
+    f8, g2 = _as_u8(filt), grad.reshape(-1, 2).float().contiguous()
+    op, rd = opacity.float().contiguous(), (radii.to(torch.int32).contiguous() if gmax else None)
     N.call("hgsr_training_statis", Av, noff, int(width), int(height), int(opt.pruning_type == "max"), int(gmax),
-           ptr(vis_idx), ptr(sel8), ptr(rank), ptr(_as_u8(filt)),
-           ptr(grad.reshape(-1, 2).float().contiguous()), ptr(opacity.float().contiguous()),
-           ptr(radii.to(torch.int32).contiguous()) if gmax else None,
+           ptr(vis_idx), ptr(sel8), ptr(rank), ptr(f8), ptr(g2), ptr(op), ptr(rd),
            ptr(_state(model.anchor_opacity_accum, "anchor_opacity_accum")),
            ptr(_state(model.anchor_demon, "anchor_demon")),
            ptr(_state(model.offset_gradient_accum, "offset_gradient_accum")),
@@ -130,8 +131,8 @@ def weed_out(model, positions, levels):
         return torch.ones(n, dtype=torch.bool, device=positions.device)
     cams = model.cam_infos.float().contiguous()
     mask = torch.empty(n, dtype=torch.uint8, device=positions.device)
-    N.call("hgsr_weed_out", n, ptr(positions.float().contiguous()), ptr(levels.reshape(-1).to(torch.int32).contiguous()),
-           cams.shape[0], ptr(cams), float(model.standard_dist), float(model.fork), int(model.street_levels),
+    pos, lv = positions.float().contiguous(), levels.reshape(-1).to(torch.int32).contiguous()
+    N.call("hgsr_weed_out", n, ptr(pos), ptr(lv), cams.shape[0], ptr(cams), float(model.standard_dist), float(model.fork), int(model.street_levels),
            _D2L[model.dist2level], float(model.weed_ratio), ptr(mask), N.stream(positions.device))
     return mask.bool()
 
@@ -146,19 +147,23 @@ def scatter_max_ts(src, index, dim=0, out=None, dim_size=None):
     return scatter_max(src, idx, dim_size), None
 
 
-def bind(lod_model_module, basic_model_module=None):
+def bind(lod_model_module, basic_model_module=None, base_model_module=None):
     """Point the reference's densification at the HIP primitives; its own
     GaussianLoDModel.anchor_growing (scene/lod_model.py:487-596) then runs unchanged:
 
-        import scene.lod_model, scene.basic_model
+        import scene.lod_model, scene.basic_model, scene.base_model
         from horizongs_amd import densify as hd
-        hd.bind(scene.lod_model, scene.basic_model)
+        hd.bind(scene.lod_model, scene.basic_model, scene.base_model)
 
     * module-level torch_scatter.scatter_max of scene/lod_model.py:20,558 -> scatter_max_ts
+      (and of scene/base_model.py:439, the Scaffold-style GaussianModel's anchor_growing, when
+      base_model_module is given)
     * BasicModel.get_remove_duplicates (basic_model.py:179-190) -> remove_duplicates (hash set)
     * GaussianLoDModel.weed_out (lod_model.py:236-249) -> weed_out
     * BasicModel.training_statis (basic_model.py:96-144) -> training_statis (one kernel)"""
     lod_model_module.scatter_max = scatter_max_ts
+    if base_model_module is not None:
+        base_model_module.scatter_max = scatter_max_ts
     lod = lod_model_module.GaussianLoDModel
     lod.weed_out = lambda self, positions, levels: weed_out(self, positions, levels)
     base = basic_model_module.BasicModel if basic_model_module is not None else lod

@@ -89,10 +89,11 @@ class _Project3D(torch.autograd.Function):
         v_means = torch.empty_like(means)
         v_quats = torch.empty_like(quats)
         v_scales = torch.empty_like(scales)
-        v_means2d, v_depths, v_conics = _grads_or_zeros((v_means2d, v_depths, v_conics), (C, Ng), (2, None, 3), means)
+        v_means2d, v_depths, v_conics = (_f32(g) for g in _grads_or_zeros((v_means2d, v_depths, v_conics), (C, Ng),
+                                                                           (2, None, 3), means))
         N.call("hgsr_project3d_bwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks), width,
-               height, eps2d, ptr(radii), ptr(conics), ptr(_f32(v_means2d)), ptr(_f32(v_depths)),
-               ptr(_f32(v_conics)), ptr(v_means), ptr(v_quats), ptr(v_scales), N.stream(means.device))
+               height, eps2d, ptr(radii), ptr(conics), ptr(v_means2d), ptr(v_depths), ptr(v_conics), ptr(v_means),
+               ptr(v_quats), ptr(v_scales), N.stream(means.device))
         if ctx.needs_input_grad[3]:
             raise NotImplementedError("hgsr: gradients w.r.t. viewmats are not supported")
         return v_means, v_quats, v_scales, None, None, None, None, None, None, None, None
@@ -144,11 +145,11 @@ class _Project2D(torch.autograd.Function):
         v_means = torch.empty_like(means)
         v_quats = torch.empty_like(quats)
         v_scales = torch.empty_like(scales)
-        v_means2d, v_depths, v_rt, v_normals = _grads_or_zeros((v_means2d, v_depths, v_rt, v_normals), (C, Ng),
-                                                               (2, None, (3, 3), 3), means)
+        v_means2d, v_depths, v_rt, v_normals = (_f32(g) for g in _grads_or_zeros(
+            (v_means2d, v_depths, v_rt, v_normals), (C, Ng), (2, None, (3, 3), 3), means))
         N.call("hgsr_project2d_bwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks), width,
-               height, ptr(radii), ptr(rt), ptr(_f32(v_means2d)), ptr(_f32(v_depths)), ptr(_f32(v_rt)),
-               ptr(_f32(v_normals)), ptr(v_means), ptr(v_quats), ptr(v_scales), N.stream(means.device))
+               height, ptr(radii), ptr(rt), ptr(v_means2d), ptr(v_depths), ptr(v_rt), ptr(v_normals), ptr(v_means),
+               ptr(v_quats), ptr(v_scales), N.stream(means.device))
         if ctx.needs_input_grad[3]:
             raise NotImplementedError("hgsr: gradients w.r.t. viewmats are not supported")
         return v_means, v_quats, v_scales, None, None, None, None, None, None, None
@@ -189,8 +190,9 @@ class _SH(torch.autograd.Function):
         n, K = coeffs.shape[0], coeffs.shape[1]
         v_coeffs = torch.empty_like(coeffs)
         v_dirs = torch.zeros_like(dirs) if ctx.needs_input_grad[1] else None
-        N.call("hgsr_sh_bwd", ctx.degree, K, n, ptr(dirs), ptr(coeffs), ptr(masks), ptr(_f32(v_colors)),
-               ptr(v_coeffs), ptr(v_dirs), N.stream(dirs.device))
+        vc = _f32(v_colors)
+        N.call("hgsr_sh_bwd", ctx.degree, K, n, ptr(dirs), ptr(coeffs), ptr(masks), ptr(vc), ptr(v_coeffs),
+               ptr(v_dirs), N.stream(dirs.device))
         return None, v_dirs, v_coeffs, None
 
 
@@ -777,8 +779,9 @@ class _DepthToNormal(torch.autograd.Function):
         C, H, W = d.shape
         st = (ct.c_int64 * 3)(*d.stride())
         v_depth = torch.empty((C, H, W), dtype=torch.float32, device=d.device)
+        vn = _f32(v_normals)
         N.call("hgsr_depth_normal_bwd", C, H, W, d.data_ptr(), ct.cast(st, ct.c_void_p), ptr(c2w), ptr(K),
-               int(z_depth), int(from_viewmat), ptr(_f32(v_normals)), ptr(v_depth), N.stream(d.device))
+               int(z_depth), int(from_viewmat), ptr(vn), ptr(v_depth), N.stream(d.device))
         return v_depth.reshape(shape), None, None, None, None
 
 

@@ -46,9 +46,18 @@ class GradientAllReduce:
       single-GPU training would), while one that some ranks did not reach averages their
       zeros in (the reference's mean over the views of a batch).
 
-    Usage per step: ``red.begin()`` before backward, ``loss.backward()``, ``red.finish()``
-    before the optimizer step.  ``red()`` = begin-less synchronous form for grads already
-    computed."""
+    * ``finish(step=...)`` applies the optimizer bucket by bucket: bucket b's parameters are
+      stepped (one fused HIP Adam launch over just them) as soon as b's collective completes,
+      while the collectives of the later buckets are still running on RCCL's stream -- the
+      optimizer overlaps the communication instead of waiting for all of it.  Adam is
+      elementwise, so the per-bucket launches give bit-identical parameters to one launch
+      over everything (tests/test_multigpu_gloo.py).
+
+    Usage per step: ``red.begin()`` before backward, ``loss.backward()``, then either
+    ``red.finish()`` + ``optimizer.step()`` or ``red.finish(step=optimizer.step_params)``.
+    Exactly ONE backward may run between begin() and finish(): a gradient that arrives for a
+    bucket already in flight raises.  ``red()`` = begin-less synchronous form for grads
+    already computed."""
 
     def __init__(self, params_or_optimizer, bucket_mb: float = 64.0, group=None):
         self.source = params_or_optimizer
@@ -127,8 +136,10 @@ class GradientAllReduce:
             return
         bi, k = self._where[id(p)]
         b = self.buckets[bi]
-        if b["launched"]:
-            return
+        if b["launched"] or b["ready"][k]:
+            raise RuntimeError("hgsr GradientAllReduce: a second gradient arrived for a parameter in this step (its "
+                               "bucket's all-reduce may already be in flight); exactly one backward is allowed "
+                               "between begin() and finish()")
         n = p.numel()
         dst = b["flat"][b["offs"][k]:b["offs"][k] + n].view_as(p)
         torch.mul(p.grad, 1.0 / self.world, out=dst)
@@ -151,15 +162,23 @@ class GradientAllReduce:
             self._launch(self.buckets[self._next])
             self._next += 1
 
-    def finish(self) -> None:
-        """Launch what the backward left (in bucket order), wait, set the averaged grads."""
+    @property
+    def active(self) -> bool:
+        return self._active()
+
+    def finish(self, step=None) -> None:
+        """Launch what the backward left (in bucket order), wait, set the averaged grads.
+        step(params): optional per-bucket optimizer step, issued on the current stream right
+        after each bucket's collective (overlapping the remaining ones)."""
         if not self._active():
+            if step is not None:
+                step(self._params())
             return
         while self._next < len(self.buckets):
             self._launch(self.buckets[self._next])
             self._next += 1
         for b in self.buckets:
-            b["work"].wait()
+            b["work"].wait()  # NCCL/RCCL: the current stream waits for the collective; the host does not
             pres = b["flat"][b["n"]:].tolist() if not all(b["ready"]) else None
             for k, p in enumerate(b["params"]):
                 n = p.numel()
@@ -167,6 +186,8 @@ class GradientAllReduce:
                     p.grad = None  # no rank produced a gradient
                 elif not b["ready"][k]:
                     p.grad = b["flat"][b["offs"][k]:b["offs"][k] + n].view_as(p)
+            if step is not None:
+                step(b["params"])
 
     def __call__(self) -> None:
         """Synchronous form: average gradients that are already in place (no overlap)."""

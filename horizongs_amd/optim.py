@@ -45,7 +45,14 @@ class Adam(torch.optim.Optimizer):
         super().__init__(params, defaults)
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step_params(self, params):
+        """Step only `params` (a subset of the groups' parameters, e.g. one all-reduce bucket:
+        multigpu.GradientAllReduce.finish(step=...)).  Adam is elementwise: stepping the
+        parameters in several subsets is bit-identical to one step over all of them."""
+        self.step(only={id(p) for p in params})
+
+    @torch.no_grad()
+    def step(self, closure=None, only=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -62,7 +69,7 @@ class Adam(torch.optim.Optimizer):
             lr = float(group["lr"])
             for p in group["params"]:
                 g = p.grad
-                if g is None:
+                if g is None or (only is not None and id(p) not in only):
                     continue
                 if g.is_sparse:
                     raise RuntimeError("hgsr Adam does not support sparse gradients")

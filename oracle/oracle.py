@@ -292,3 +292,19 @@ def set_envelope(on, dtype=np.float64):
 def set_hitform(form, dtype=np.float32):
     """2DGS hit evaluation of one build: 0 gsplat's per-pixel cross product, 1 the plane form."""
     _fn(dtype, "set_hitform")(I32(int(form)))
+
+
+_TSC_KEEP = {}
+
+
+def set_threshold_scale(tsc, dtype=np.float32):
+    """Per-pixel threshold variants of one build ([C, rows, W] multipliers of the alpha floor,
+    the T stop, the 0.999 clamp switch and the 2DGS branch; None = nominal), see hgsr_oracle.c."""
+    key = np.dtype(dtype).name
+    if tsc is None:
+        _TSC_KEEP.pop(key, None)
+        _fn(dtype, "set_threshold_scale")(None)
+        return
+    arr = np.ascontiguousarray(tsc, dtype=dtype)
+    _TSC_KEEP[key] = arr  # the library keeps the pointer: hold the array
+    _fn(dtype, "set_threshold_scale")(_p(arr))

@@ -22,9 +22,25 @@ def _campos(viewmats):
 
 
 class _Band:
+    tsc = None  # per-pixel threshold variants [C, rows, W] (hgsr_oracle.c set_threshold_scale)
+
     @property
     def Hr(self):
         return self.H if self.rows is None else min(self.rows, self.H)
+
+    def _thresholds(self):
+        """Context: the raster calls inside use this instance's per-pixel threshold variants."""
+        band = self
+
+        class _Ctx:
+            def __enter__(self):
+                if band.tsc is not None:
+                    O.set_threshold_scale(band.tsc, band.dt)
+
+            def __exit__(self, *exc):
+                if band.tsc is not None:
+                    O.set_threshold_scale(None, band.dt)
+        return _Ctx()
 
 
 class Raster3D(_Band):
@@ -75,9 +91,10 @@ class Raster3D(_Band):
                                                                    self.tw, self.th, dtype=dt)
         self.offsets = O.isect_offsets(self.isect_ids, C, self.tw, self.th)
         self.opac_c = np.ascontiguousarray(np.broadcast_to(self.opacities, (C, Nn)), dt)
-        self.rc_raw, self.ra, self.last, self.stopped, self.margin, self.gmargin = O.raster3d_fwd(
-            self.means2d, self.conics, self.cols, self.opac_c, self.bg_r, self.W, self.Hr, self.ts, self.offsets,
-            self.flatten_ids, dtype=dt, return_stopped=True)
+        with self._thresholds():
+            self.rc_raw, self.ra, self.last, self.stopped, self.margin, self.gmargin = O.raster3d_fwd(
+                self.means2d, self.conics, self.cols, self.opac_c, self.bg_r, self.W, self.Hr, self.ts, self.offsets,
+                self.flatten_ids, dtype=dt, return_stopped=True)
         out = self.rc_raw.copy()
         if self.mode in ("ED", "RGB+ED"):
             out[..., -1:] = self.rc_raw[..., -1:] / np.maximum(self.ra, dt(1e-10))
@@ -96,9 +113,10 @@ class Raster3D(_Band):
             v_ra = v_ra + np.where(self.ra >= dt(1e-10), -g * self.rc_raw[..., -1:] / (den * den), 0).astype(dt)
             v_rc = v_rc.copy()
             v_rc[..., -1:] = g / den
-        vm2, vcon, vcol, vop = O.raster3d_bwd(self.means2d, self.conics, self.cols, self.opac_c, self.bg_r, self.W,
-                                              self.Hr, self.ts, self.offsets, self.flatten_ids, self.ra, self.last,
-                                              v_rc, v_ra, dtype=dt)
+        with self._thresholds():
+            vm2, vcon, vcol, vop = O.raster3d_bwd(self.means2d, self.conics, self.cols, self.opac_c, self.bg_r,
+                                                  self.W, self.Hr, self.ts, self.offsets, self.flatten_ids, self.ra,
+                                                  self.last, v_rc, v_ra, dtype=dt)
         v_depths = np.zeros((C, Nn), dt)
         if self.mode in ("RGB+D", "RGB+ED", "D", "ED"):
             v_depths += vcol[..., -1]
@@ -147,9 +165,10 @@ class Raster3D(_Band):
             v_rc[..., -1:] = k * g / den
         O.set_envelope(True, dt)
         try:
-            vm2, vcon, vcol, vop = O.raster3d_bwd(self.means2d, self.conics, self.cols, self.opac_c, self.bg_r,
-                                                  self.W, self.Hr, self.ts, self.offsets, self.flatten_ids, self.ra,
-                                                  self.last, v_rc, v_ra, dtype=dt)
+            with self._thresholds():
+                vm2, vcon, vcol, vop = O.raster3d_bwd(self.means2d, self.conics, self.cols, self.opac_c, self.bg_r,
+                                                      self.W, self.Hr, self.ts, self.offsets, self.flatten_ids,
+                                                      self.ra, self.last, v_rc, v_ra, dtype=dt)
         finally:
             O.set_envelope(False, dt)
         v_depths = np.zeros((C, Nn), dt)
@@ -232,10 +251,11 @@ class Raster2D(_Band):
         self.offsets = O.isect_offsets(self.isect_ids, C, self.tw, self.th)
         self.opac_c = np.ascontiguousarray(np.broadcast_to(self.opacities, (C, Nn)), dt)
         O.set_hitform(self.hitform, dt)
-        (self.rc_raw, self.ra, self.rn, self.rd, self.rm, self.last,
-         self.med, self.stopped, self.margin, self.gmargin) = O.raster2d_fwd(self.means2d, self.rt, self.cols, self.opac_c, self.normals,
-                                                  self.bg_r, self.W, self.Hr, self.ts, self.offsets, self.flatten_ids,
-                                                  dtype=dt, return_stopped=True)
+        with self._thresholds():
+            (self.rc_raw, self.ra, self.rn, self.rd, self.rm, self.last, self.med, self.stopped, self.margin,
+             self.gmargin) = O.raster2d_fwd(self.means2d, self.rt, self.cols, self.opac_c, self.normals, self.bg_r,
+                                            self.W, self.Hr, self.ts, self.offsets, self.flatten_ids, dtype=dt,
+                                            return_stopped=True)
         O.set_hitform(0, dt)
         out = self.rc_raw.copy()
         if self.mode == "RGB+ED":
@@ -257,10 +277,11 @@ class Raster2D(_Band):
             v_rc[..., -1:] = g / den
         O.set_hitform(self.hitform, dt)
         try:
-            vm2, vrt, vcol, vop, vn, vdens = O.raster2d_bwd(
-                self.means2d, self.rt, self.cols, self.opac_c, self.normals, self.bg_r, self.W, self.Hr, self.ts,
-                self.offsets, self.flatten_ids, self.ra, self.last, v_rc, v_ra, np.asarray(v_render_normals_cam, dt),
-                dtype=dt)
+            with self._thresholds():
+                vm2, vrt, vcol, vop, vn, vdens = O.raster2d_bwd(
+                    self.means2d, self.rt, self.cols, self.opac_c, self.normals, self.bg_r, self.W, self.Hr, self.ts,
+                    self.offsets, self.flatten_ids, self.ra, self.last, v_rc, v_ra,
+                    np.asarray(v_render_normals_cam, dt), dtype=dt)
         finally:
             O.set_hitform(0, dt)
         v_depths = vcol[..., -1].copy()
@@ -288,10 +309,11 @@ class Raster2D(_Band):
             v_rc[..., -1:] = k * g / den
         O.set_envelope(True, dt)
         try:
-            vm2, vrt, vcol, vop, vn, vdens = O.raster2d_bwd(
-                self.means2d, self.rt, self.cols, self.opac_c, self.normals, self.bg_r, self.W, self.Hr, self.ts,
-                self.offsets, self.flatten_ids, self.ra, self.last, v_rc, v_ra,
-                np.abs(np.asarray(v_render_normals_cam, dt)), dtype=dt)
+            with self._thresholds():
+                vm2, vrt, vcol, vop, vn, vdens = O.raster2d_bwd(
+                    self.means2d, self.rt, self.cols, self.opac_c, self.normals, self.bg_r, self.W, self.Hr, self.ts,
+                    self.offsets, self.flatten_ids, self.ra, self.last, v_rc, v_ra,
+                    np.abs(np.asarray(v_render_normals_cam, dt)), dtype=dt)
         finally:
             O.set_envelope(False, dt)
         v_depths = vcol[..., -1].copy()

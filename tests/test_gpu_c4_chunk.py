@@ -73,7 +73,7 @@ def test_c4_golden_chain():
                     ref=cfg["last"], **{"d_" + k: v.grad for k, v in {**ins, **ws}.items()})
 
     c32, c64 = cpu_chain(torch.float32), cpu_chain(torch.float64)
-    assert c32["ref"].isect_ids.size > 200  # the visible golden Gaussians do reach the image
+    assert c32["ref"].isect_ids.size > 50  # the visible golden Gaussians do reach the image
 
     t = lambda x: torch.from_numpy(np.asarray(x)).to(DEV)
     ins = {"feat": t(g["anchor_feat"]), "offset": t(g["offset"]), "scaling_raw": t(g["scaling"])}

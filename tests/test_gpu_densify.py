@@ -154,3 +154,45 @@ def test_anchor_growing_matches_reference():
         got = getattr(m, n).cpu().numpy()
         assert got.shape == g["out" + n].shape, n
         np.testing.assert_allclose(got, g["out" + n], rtol=1e-6, atol=1e-7, err_msg=n)
+
+
+def test_bind_drives_reference_shaped_classes():
+    """densify.bind() on stand-in modules shaped like the reference's (scene/lod_model.py with a
+    module-level `scatter_max`, scene/basic_model.py's BasicModel, scene/base_model.py): the
+    stand-in GaussianLoDModel.anchor_growing reaches the primitives ONLY through what bind()
+    installed, with the reference's own call shapes -- self.get_remove_duplicates(grid_coords,
+    selected_grid_coords_unique) (lod_model.py:538), self.weed_out(candidate_anchor, new_level)
+    (:550), scatter_max(new_feat, inverse.unsqueeze(1).expand(-1, F), dim=0)[0] (:558, the
+    expanded 2-D index and dim_size=None) -- and must reproduce the reference's golden output."""
+    import types
+    from horizongs_amd import densify as HD
+    g = np.load(os.path.join(GOLD, "anchor_growing.npz"))
+    basic = types.ModuleType("scene.basic_model")
+    lod = types.ModuleType("scene.lod_model")
+    base = types.ModuleType("scene.base_model")
+    basic.BasicModel = type("BasicModel", (), {})
+    lod.scatter_max = base.scatter_max = None  # torch_scatter is absent: bind() must provide it
+
+    class GaussianLoDModel(_LoDShim, basic.BasicModel):
+        def anchor_growing(self, grads, opt, offset_mask):
+            mod = lod
+
+            class Prims:  # the reference's call shapes, resolved through the bound names
+                remove_duplicates = staticmethod(lambda grid, cand: self.get_remove_duplicates(grid, cand))
+                weed_out = staticmethod(lambda model, pos, levels: model.weed_out(pos, levels))
+                scatter_max = staticmethod(lambda src, inverse, n: mod.scatter_max(
+                    src, inverse.unsqueeze(1).expand(-1, src.size(1)), dim=0)[0])
+            Dn.anchor_growing(self, grads, opt, offset_mask, Prims)
+
+    lod.GaussianLoDModel = GaussianLoDModel
+    HD.bind(lod, basic, base)
+    assert lod.scatter_max is HD.scatter_max_ts and base.scatter_max is HD.scatter_max_ts
+    m = GaussianLoDModel(g)
+    opt = SimpleNamespace(update_ratio=0.5, densify_grad_threshold=0.0002, extra_ratio=0.25, extra_up=0.01,
+                          overlap=False)
+    m.anchor_growing(torch.from_numpy(g["grads"]).to(DEV), opt, torch.from_numpy(g["offset_mask"]).to(DEV))
+    for n in ("_anchor", "_offset", "_anchor_feat", "_scaling", "_rotation", "_level", "_extra_level",
+              "anchor_demon", "anchor_opacity_accum"):
+        got = getattr(m, n).cpu().numpy()
+        assert got.shape == g["out" + n].shape, n
+        np.testing.assert_allclose(got, g["out" + n], rtol=1e-6, atol=1e-7, err_msg=n)

@@ -114,3 +114,29 @@ def test_adam_state_dict_round_trip():
     o2 = Adam([{"params": [mine[0]], "lr": 1e-3}], lr=0.0, eps=1e-15)
     o2.load_state_dict(sd)
     assert float(o2.state[mine[0]]["step"]) == 1.0
+
+
+def test_adam_step_params_subsets_bit_identical():
+    """Adam.step_params (one fused launch per all-reduce bucket, multigpu.GradientAllReduce
+    .finish(step=...)) stepping the parameters in subsets gives bit-identical parameters and
+    state to one step over all of them."""
+    from horizongs_amd.optim import Adam
+    shapes = [(300_001, 3), (4096,), (70, 32), (5,), (123, 7), (1,)]
+    g = torch.Generator().manual_seed(9)
+    base = [torch.randn(s, generator=g) for s in shapes]
+    pa = [b.to(DEV).clone().requires_grad_(True) for b in base]
+    pb = [b.to(DEV).clone().requires_grad_(True) for b in base]
+    oa = Adam([{"params": [p], "lr": 1e-3 * (i + 1)} for i, p in enumerate(pa)], lr=0.0, eps=1e-15)
+    ob = Adam([{"params": [p], "lr": 1e-3 * (i + 1)} for i, p in enumerate(pb)], lr=0.0, eps=1e-15)
+    for t in range(3):
+        for a, b in zip(pa, pb):
+            gr = torch.randn(a.shape, generator=g).to(DEV)
+            a.grad, b.grad = gr.clone(), gr.clone()
+        oa.step()
+        for sub in ([pb[5], pb[0]], [pb[2]], [pb[1], pb[3], pb[4]]):  # buckets in reverse-ish order
+            ob.step_params(sub)
+        torch.cuda.synchronize()
+        for a, b in zip(pa, pb):
+            assert torch.equal(a, b)
+            assert torch.equal(oa.state[a]["exp_avg_sq"], ob.state[b]["exp_avg_sq"])
+            assert float(oa.state[a]["step"]) == float(ob.state[b]["step"]) == t + 1

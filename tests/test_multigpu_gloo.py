@@ -132,7 +132,23 @@ def _train(n_steps, views_per_step, reduce_fn=None, reducer=None):
     return grads, [p.detach().clone() for p in params]
 
 
-def _ddp_worker(rank, world, port, q):
+def _step_subset(opt, subset, log):
+    """Per-bucket optimizer step on the CPU (stand-in for optim.Adam.step_params, whose HIP
+    kernel needs a device): torch's Adam skips parameters without a gradient."""
+    ids = {id(p) for p in subset}
+    log.append(sorted(ids))
+    stash = []
+    for g in opt.param_groups:
+        for p in g["params"]:
+            if id(p) not in ids and p.grad is not None:
+                stash.append((p, p.grad))
+                p.grad = None
+    opt.step()
+    for p, gr in stash:
+        p.grad = gr
+
+
+def _ddp_worker(rank, world, port, q, per_bucket=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -140,36 +156,68 @@ def _ddp_worker(rank, world, port, q):
         params = _make_params()
         opt = _optimizer(params)
         red = GradientAllReduce(opt, bucket_mb=0.0012)  # ~300 floats: several buckets
-        grads = []
+        grads, calls = [], []
         for step in range(3):
             if step == 1:
                 params = _grow(opt, params)
             opt.zero_grad(set_to_none=True)
             red.begin()
             _view_loss(params, rank).backward()  # one view per rank, gradients averaged by the hooks
-            red.finish()
-            grads.append([None if p.grad is None else p.grad.clone() for p in params])
-            opt.step()
+            if per_bucket:  # each bucket's parameters stepped right after its own collective
+                log = []
+                red.finish(step=lambda ps: _step_subset(opt, ps, log))
+                calls.append((len(log), sorted(i for ids in log for i in ids) == sorted(id(p) for p in params)))
+                grads.append([None if p.grad is None else p.grad.clone() for p in params])
+            else:
+                red.finish()
+                grads.append([None if p.grad is None else p.grad.clone() for p in params])
+                opt.step()
+        # exactly one backward between begin() and finish(): a second one raises
+        red.begin()
+        _view_loss(params, rank).backward(retain_graph=True)
+        err = None
+        try:
+            _view_loss(params, rank).backward()
+        except RuntimeError as e:
+            err = str(e)
+        red.finish()
         npy = lambda t: None if t is None else t.detach().numpy().copy()  # noqa: E731
-        q.put((rank, [[npy(g) for g in gs] for gs in grads], [npy(p) for p in params], len(red.buckets)))
+        q.put((rank, [[npy(g) for g in gs] for gs in grads], [npy(p) for p in params], len(red.buckets), calls, err))
     finally:
         dist.destroy_process_group()
 
 
-def test_ddp_two_ranks_match_one_rank_two_views():
+def _run_ddp(per_bucket):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q, per_bucket)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+def test_ddp_per_bucket_step_equals_one_step():
+    """finish(step=...) steps each bucket as its collective lands (the optimizer overlapping
+    the remaining all-reduces): every parameter once per step, bit-identical parameters to
+    finish() + one optimizer step; a second backward before finish() raises."""
+    one, per = _run_ddp(False), _run_ddp(True)
+    for (r1, g1, p1, nb, _, err1), (r2, g2, p2, _, calls, err2) in zip(one, per):
+        assert nb >= 2 and all(n == nb and full for n, full in calls), calls
+        for a, b in zip(p1, p2):
+            assert (a == b).all(), r1  # bit for bit
+        assert err1 and err2 and "exactly one backward" in err1
+
+
+def test_ddp_two_ranks_match_one_rank_two_views():
+    res = _run_ddp(False)
     ref_grads, ref_params = _train(3, [0, 1])
-    for rank, grads, params, n_buckets in res:
+    for rank, grads, params, n_buckets, _, _ in res:
         assert n_buckets >= 2
         for step, (gs, rs) in enumerate(zip(grads, ref_grads)):
             for k, (g, r) in enumerate(zip(gs, rs)):
