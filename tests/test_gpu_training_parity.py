@@ -149,9 +149,10 @@ def _pipeline_parity(gs):
     fin_self, win_self, _ = PF.fit(pert, cfg, gt, iters, gs=gs)
     res = dict(psnr_init_db=round(psnr_init, 4), psnr_ref_db=round(win_cpu, 4), psnr_hip_db=round(win_gpu, 4),
                psnr_delta_db=round(win_gpu - win_cpu, 4), psnr_metric="mean MSE of the last 50 iterations' renders",
-               final_iterate=dict(ref_db=round(fin_cpu, 4), hip_db=round(fin_gpu, 4), delta_db=round(fin_gpu - fin_cpu, 4),
-                                  ref_perturbed_1e-6_delta_db=round(fin_self - fin_cpu, 4)),
-               window_ref_perturbed_1e-6_delta_db=round(win_self - win_cpu, 4),
+               final_iterate={"ref_db": round(fin_cpu, 4), "hip_db": round(fin_gpu, 4),
+                              "delta_db": round(fin_gpu - fin_cpu, 4),
+                              "ref_perturbed_1e-6_delta_db": round(fin_self - fin_cpu, 4)},
+               window_ref_perturbed_delta_db=round(win_self - win_cpu, 4),
                iterations=iters, anchors=A, width=W, height=H,
                loss_first=[round(loss_cpu[0], 6), round(loss_gpu[0], 6)],
                loss_last=[round(loss_cpu[-1], 6), round(loss_gpu[-1], 6)],
