@@ -58,7 +58,8 @@ class Raster2DFn(torch.autograd.Function):
         dt = np.float64 if means.dtype == torch.float64 else np.float32
         r = OP.Raster2D(_np(means, dt), _np(quats, dt), _np(scales, dt), _np(opacities, dt), _np(colors, dt),
                         _np(cfg["viewmats"], dt), _np(cfg["Ks"], dt), cfg["W"], cfg["H"],
-                        backgrounds=_np(cfg.get("bg"), dt), render_mode=cfg.get("mode", "RGB+ED"), dtype=dt)
+                        backgrounds=_np(cfg.get("bg"), dt), render_mode=cfg.get("mode", "RGB+ED"), dtype=dt,
+                        hitform=cfg.get("hitform", 0))
         out, ra, rn = r.forward()
         ctx.r = r
         ctx.rn_shape = rn.shape

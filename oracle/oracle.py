@@ -294,17 +294,23 @@ def set_hitform(form, dtype=np.float32):
     _fn(dtype, "set_hitform")(I32(int(form)))
 
 
-_TSC_KEEP = {}
+_FLIP_KEEP = {}
 
 
-def set_threshold_scale(tsc, dtype=np.float32):
-    """Per-pixel threshold variants of one build ([C, rows, W] multipliers of the alpha floor,
-    the T stop, the 0.999 clamp switch and the 2DGS branch; None = nominal), see hgsr_oracle.c."""
+def set_flips(flips, dtype=np.float32):
+    """Near-threshold branch forcing of one build (hgsr_oracle.c set_flips): flips = None, or a
+    dict of [C, rows, W] arrays: {"target"} (target mode: the raster forward takes the other
+    branch at the decision whose margin equals target and fills "idx" / "kind" / "out") or
+    {"idx", "kind", "out"} (forced mode).  The arrays are held until the next call."""
     key = np.dtype(dtype).name
-    if tsc is None:
-        _TSC_KEEP.pop(key, None)
-        _fn(dtype, "set_threshold_scale")(None)
+    if flips is None:
+        _FLIP_KEEP.pop(key, None)
+        _fn(dtype, "set_flips")(None, None, None, None)
         return
-    arr = np.ascontiguousarray(tsc, dtype=dtype)
-    _TSC_KEEP[key] = arr  # the library keeps the pointer: hold the array
-    _fn(dtype, "set_threshold_scale")(_p(arr))
+    _FLIP_KEEP[key] = flips
+    for k, t in (("idx", np.int64), ("kind", np.int32), ("out", np.int32)):
+        assert flips[k].dtype == t and flips[k].flags["C_CONTIGUOUS"], k
+    tgt = flips.get("target")
+    if tgt is not None:
+        assert tgt.dtype == np.dtype(dtype) and tgt.flags["C_CONTIGUOUS"]
+    _fn(dtype, "set_flips")(_p(tgt), _p(flips["idx"]), _p(flips["kind"]), _p(flips["out"]))

@@ -22,25 +22,43 @@ def _campos(viewmats):
 
 
 class _Band:
-    tsc = None  # per-pixel threshold variants [C, rows, W] (hgsr_oracle.c set_threshold_scale)
+    # near-threshold branch forcing of the raster calls (hgsr_oracle.c set_flips): None, or a
+    # dict of [C, rows, W] arrays {"target"} + outputs {"idx", "kind", "out"} (target mode) /
+    # {"idx", "kind", "out"} (forced mode)
+    flips = None
 
     @property
     def Hr(self):
         return self.H if self.rows is None else min(self.rows, self.H)
 
     def _thresholds(self):
-        """Context: the raster calls inside use this instance's per-pixel threshold variants."""
+        """Context: the raster calls inside use this instance's branch forcing."""
         band = self
 
         class _Ctx:
             def __enter__(self):
-                if band.tsc is not None:
-                    O.set_threshold_scale(band.tsc, band.dt)
+                if band.flips is not None:
+                    O.set_flips(band.flips, band.dt)
 
             def __exit__(self, *exc):
-                if band.tsc is not None:
-                    O.set_threshold_scale(None, band.dt)
+                if band.flips is not None:
+                    O.set_flips(None, band.dt)
         return _Ctx()
+
+    def flip_closest(self, target):
+        """Target mode: at every pixel with target > 0 take the other branch at the decision
+        whose margin equals target (pass a nominal forward's own `margin` there: the pixel's
+        closest call); call before forward().  The decision found is left in
+        flips["idx" / "kind" / "out"] (out = its NOMINAL outcome)."""
+        shape = (self.viewmats.shape[0], self.Hr, self.W)
+        self.flips = {"target": np.ascontiguousarray(target, self.dt), "idx": np.full(shape, -1, np.int64),
+                      "kind": np.zeros(shape, np.int32), "out": np.zeros(shape, np.int32)}
+
+    def force(self, idx, kind, out):
+        """Forced mode: at list index idx[pix] the decision of kind[pix] (1 alpha floor, 2 stop;
+        0 = none) takes outcome out[pix]."""
+        self.flips = {"idx": np.ascontiguousarray(idx, np.int64), "kind": np.ascontiguousarray(kind, np.int32),
+                      "out": np.ascontiguousarray(out, np.int32)}
 
 
 class Raster3D(_Band):

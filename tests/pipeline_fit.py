@@ -68,8 +68,10 @@ def _mlps(p):
 
 
 # ----------------------------------------------------------------------------- CPU chain
-def cpu_render(p, cfg, gs="3d", dtype=torch.float32):
-    """-> (image [3,H,W], alpha [H,W], scaling [M,3]) through the oracle chain."""
+def cpu_render(p, cfg, gs="3d", dtype=None):
+    """-> (image [3,H,W], alpha [H,W], scaling [M,3]) through the oracle chain (cfg["dtype"]:
+    its precision, float32 by default; cfg["hitform"]: the 2DGS oracle's hit evaluation)."""
+    dtype = dtype or cfg.get("dtype", torch.float32)
     from oracle import autograd as OA
     from oracle import decode_ref as D
     from oracle import oracle as O
@@ -86,7 +88,7 @@ def cpu_render(p, cfg, gs="3d", dtype=torch.float32):
                                                    p["scaling"].to(dtype)[vis], cfg["cam_center"].to(dtype), mlps,
                                                    cfg["view_dim"], cfg["n_off"], cfg["color_dim"])
     rc = dict(viewmats=cfg["viewmats"], Ks=cfg["Ks"], W=W, H=H, sh_degree=cfg["sh_degree"], bg=torch.zeros(1, 3),
-              mode="RGB+ED")
+              mode="RGB+ED", hitform=cfg.get("hitform", 0))
     out, ra = OA.rasterization(xyz, rot, scal, op.reshape(-1), col, rc, gs=gs)
     return out[0, ..., :3].permute(2, 0, 1), ra[0, ..., 0], scal
 
@@ -94,7 +96,7 @@ def cpu_render(p, cfg, gs="3d", dtype=torch.float32):
 def cpu_loss(p, cfg, gt, gs="3d"):
     from oracle import loss_ref as LR_
     img, alpha, scal = cpu_render(p, cfg, gs)
-    return LR_.loss(img, gt, None, 0.2, alpha, 0.05, 0.05, scal, 0.01)[0], img
+    return LR_.loss(img, gt.to(img.dtype), None, 0.2, alpha, 0.05, 0.05, scal, 0.01)[0], img
 
 
 # ----------------------------------------------------------------------------- HIP chain

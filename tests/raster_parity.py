@@ -9,14 +9,13 @@ Pixels whose discrete decisions (alpha vs 1/255, T vs 1e-4, the 0.999 clamp, the
 surface / low-pass branch) sit within a few ulps of a threshold can legitimately go either
 way in any other correct f32 evaluation order.  They are not waved through:
 
-1. value decisions: each such pixel's branch is RESOLVED -- the f64 oracle is re-run with every
-   threshold raised and lowered by a ladder of multiples of the ambiguity margin
-   (hgsr_oracle.c set_threshold_scale), and the GPU pixel must equal (its last contributor
-   index exactly, its values within the bar) the nominal branch or one of those
-   (`resolve_branches`; the counts per branch are printed and returned);
+1. value decisions: each such pixel's branch is RESOLVED -- the f64 oracle is re-run taking the
+   OTHER branch at exactly that pixel's closest decision (hgsr_oracle.c branch forcing), and the
+   GPU pixel must equal (its last contributor index exactly, its values within the bar) the
+   nominal or the flipped branch (`resolve_branches`; the counts are printed and returned);
 2. gradients: a second backward of the same forward runs WITHOUT zeroing those pixels'
-   upstream gradient, against the f32 / f64 oracle evaluated with each pixel's resolved branch
-   (per-pixel threshold variants).  Only pixels whose sole near-threshold decision switches a
+   upstream gradient, against the f32 / f64 oracle forced onto the branch the GPU took at each
+   of them.  Only pixels whose sole near-threshold decision switches a
    gradient path and leaves the value unchanged (the 0.999 clamp, the 2DGS surface / low-pass
    branch: invisible in any output) keep a zero upstream gradient there, and are counted.
 
@@ -45,65 +44,65 @@ def gpu_last(out):
     return last
 
 
-# threshold-variant ladder (multiples of the ambiguity margin delta): the T <= 1e-4 stop's
-# margin is per composited step (oracle margin / (1 + 0.02 ncomp)), so a stop decision within
-# delta of its threshold after k steps sits up to delta (1 + 0.02 k) away in raw relative terms
-BRANCH_LADDER = (2.0, 8.0, 32.0)
+def resolve_branches(make64, r32, r64, amb, vals, last):
+    """Branch the GPU took at every ambiguous pixel.
 
-
-def resolve_branches(make64, r32, r64, amb, vals, last, delta, alt32=None):
-    """Branch of every ambiguous pixel: 0 nominal, +s thresholds raised by s delta, -s lowered.
-
-    make64(tsc) -> a forwarded f64 oracle with per-pixel threshold scale tsc; vals: list of
-    (GPU image [C,rows,W,K], f32 oracle image, f64 oracle image, attribute name of the
-    variant's image); last: GPU last ids [C,rows,W].  A pixel matches a branch when its last
-    contributor is that branch's and every value is within ATOL + RTOL |b| + 3 |b32 - b64|.
-    Returns (per-pixel relative threshold offset [C,rows,W] (0 = nominal), counts)."""
+    make64(target) -> a forwarded f64 oracle that takes the other branch at each pixel's
+    closest decision (hgsr_oracle.c branch forcing, target = the nominal f64 margin); vals:
+    list of (GPU image [C,rows,W,K], f32 oracle image, f64 oracle image, attribute name of the
+    image on the oracle object); last: GPU last ids [C,rows,W].  A pixel matches a branch when
+    its last contributor is that branch's and every value is within ATOL + RTOL |b| +
+    3 |b32 - b64|.  Returns (forced decisions {"idx", "kind", "out"} [C,rows,W] that reproduce
+    the GPU's branch at every ambiguous pixel -- the nominal outcome where the GPU matched the
+    nominal branch, the flipped one where it matched that -- and the counts)."""
     amb = np.asarray(amb, bool)
-    choice = np.zeros(amb.shape, np.float64)
-    if not amb.any():
-        return choice, {"ambiguous": 0}
     shape = amb.shape
-    last = np.asarray(last)
-    e32 = []
-    for a, b32, b64, attr in vals:
-        e = np.abs(np.asarray(b32, np.float64) - b64)
-        if alt32 is not None:
-            e = np.maximum(e, np.abs(np.asarray(alt32[attr], np.float64) - b64))
-        e32.append(e)
-    done = np.zeros(shape, bool)
+    forced = {"idx": np.full(shape, -1, np.int64), "kind": np.zeros(shape, np.int32),
+              "out": np.zeros(shape, np.int32)}
     counts = {"ambiguous": int(amb.sum())}
+    if not amb.any():
+        return forced, counts
+    last = np.asarray(last)
+    e32 = [np.abs(np.asarray(b32, np.float64) - b64) for _, b32, b64, _ in vals]
+    rf = make64(np.where(amb, r64.margin, 0.0))
+    fl = rf.flips
+    has = amb & (fl["kind"] > 0)
 
-    def match(rv, key, off):
-        ok = amb & ~done & (last == rv.last)
+    def err(rv, cand):
+        """per pixel: max over values of |GPU - branch| / bar (inf off the candidates or when the
+        last contributor differs); <= 1 is a match"""
+        x = np.where(cand & (last == rv.last), 0.0, np.inf)
         for (a, _, _, attr), e in zip(vals, e32):
             b = np.asarray(getattr(rv, attr), np.float64)
             bar = ATOL + RTOL * np.abs(b) + 3.0 * e
-            ok &= (np.abs(np.asarray(a, np.float64) - b) <= bar).reshape(shape + (-1,)).all(-1)
-        choice[ok] = off
-        done[...] |= ok
-        counts[key] = int(ok.sum())
+            x = np.maximum(x, (np.abs(np.asarray(a, np.float64) - b) / bar).reshape(shape + (-1,)).max(-1))
+        return x
 
-    match(r64, "nominal", 0.0)
-    for s in BRANCH_LADDER:
-        for sign in (1, -1):
-            if (amb & ~done).any():
-                off = sign * s * delta
-                match(make64(np.full(shape, 1.0 + off)), f"{'+' if sign > 0 else '-'}{s:g}d", off)
-    left = amb & ~done
-    counts["unmatched"] = int(left.sum())
+    # the closer of the two branches (both can lie within the bar where the flip moves the
+    # values only a little; the gradient check then uses the one the GPU evaluated)
+    e_nom, e_flp = err(r64, amb), err(rf, has)
+    flp = (e_flp <= 1.0) & (e_flp < e_nom)
+    nom = (e_nom <= 1.0) & ~flp
+    # where the GPU matched a branch, force the decision found to the GPU's outcome
+    sel = (nom | flp) & has
+    forced["idx"][sel] = fl["idx"][sel]
+    forced["kind"][sel] = fl["kind"][sel]
+    forced["out"][sel] = np.where(flp, 1 - fl["out"], fl["out"])[sel]
+    counts.update(nominal=int(nom.sum()), flipped=int(flp.sum()), unmatched=int((amb & ~nom & ~flp).sum()),
+                  flip_kinds={"alpha_floor": int((flp & (fl["kind"] == 1)).sum()),
+                              "stop": int((flp & (fl["kind"] == 2)).sum())})
+    left = amb & ~nom & ~flp
     if left.any():
-        idx = np.argwhere(left)[:6]
         rows = []
-        for p in idx:
+        for p in np.argwhere(left)[:6]:
             p = tuple(p)
-            rows.append(dict(pix=p, gpu_last=int(last[p]), f64_last=int(r64.last[p]), f32_last=int(r32.last[p]),
-                             margin=float(r32.margin[p]), gpu=np.asarray(vals[0][0])[p].tolist(),
-                             f64=np.asarray(vals[0][2])[p].tolist(), gpu_alpha=float(np.asarray(vals[1][0])[p]),
-                             f64_alpha=float(np.asarray(vals[1][2])[p])))
-        raise AssertionError(f"{counts['unmatched']} near-threshold pixels match no branch of the oracle: {counts} "
-                             f"{rows}")
-    return choice, counts
+            rows.append(dict(pix=p, gpu_last=int(last[p]), f64_last=int(r64.last[p]), flip_last=int(rf.last[p]),
+                             f32_last=int(r32.last[p]), margin=float(r64.margin[p]), kind=int(fl["kind"][p]),
+                             gpu=np.asarray(vals[0][0])[p].tolist(), f64=np.asarray(vals[0][2])[p].tolist(),
+                             flip=np.asarray(getattr(rf, vals[0][3]))[p].tolist()))
+        raise AssertionError(f"{counts['unmatched']} near-threshold pixels match neither branch of the oracle: "
+                             f"{counts} {rows}")
+    return forced, counts
 
 
 def depth_stats(ref):
@@ -182,20 +181,19 @@ def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None
         rates["v_" + k] = cond_close(v.cpu().numpy(), gr32[k], gr64[k], "v_" + k, rel_floor=0, env=genv[k])
     # near-threshold pixels: resolve the branch the GPU took, then check the gradients again with
     # their upstream gradient kept, against the oracle evaluated on those branches
-    def make64(tsc):
+    def make64(target):
         r = OP.Raster3D(*args, dtype=np.float64, **kw)
-        r.tsc = tsc
+        r.flip_closest(target)
         r.forward()
         return r
     vals = [(o, rc, r64.render_colors, "render_colors"),
             (alpha.detach()[:, :rr].cpu().numpy(), ra, r64.ra, "ra")]
-    choice, counts = resolve_branches(make64, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy(), DELTA_3D)
+    forced, counts = resolve_branches(make64, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy())
     gonly = gamb & ~amb  # a gradient-path switch only (the 0.999 clamp): invisible in every output
     rates["branches"] = counts
     rates["grad_only_ambiguous_px"] = int(gonly.sum())
     if amb.any():
         got = {k: v.clone() for k, v in got.items()}
-        tsc = 1.0 + choice
         g2 = torch.Generator().manual_seed(seed + 1000)
         keep2 = torch.from_numpy(~gonly)[..., None].float()
         vrc2 = torch.randn(rc.shape, generator=g2) * keep2
@@ -209,9 +207,9 @@ def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None
             leaves[k].grad = None
         ((out * vrc_full.to(DEV)).sum() + (alpha * vra_full.to(DEV)).sum()).backward()
         rv = {}
-        for dt in (np.float32, np.float64):
+        for dt in (np.float32, np.float64):  # both precisions forced onto the GPU's branches
             rv[dt] = OP.Raster3D(*args, dtype=dt, **kw)
-            rv[dt].tsc = tsc.astype(dt)
+            rv[dt].force(**forced)
             rv[dt].forward()
         gv32 = rv[np.float32].backward(vrc2.numpy(), vra2.numpy())
         gv64 = rv[np.float64].backward(vrc2.numpy(), vra2.numpy())
@@ -290,15 +288,19 @@ def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
                                      alt32=gr32b[k])
     # near-threshold pixels: resolve the GPU's branch, then the gradients again with their upstream kept
 
-    def make64(tsc):
+    def make64(target):
         r = OP.Raster2D(*args, dtype=np.float64, **kw)
-        r.tsc = tsc
+        r.flip_closest(target)
         r.forward()
         return r
-    vals = [(o, rc, r64.render_colors, "render_colors"), (alpha.detach()[:, :rr].cpu().numpy(), ra, r64.ra, "ra"),
-            (normals.detach()[:, :rr].cpu().numpy(), rn, r64.rn, "rn")]
-    choice, counts = resolve_branches(make64, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy(), DELTA_2D,
-                                      alt32={"render_colors": rb, "ra": r32b.ra, "rn": r32b.rn})
+    # the f32 error of each value: the larger of the two hit forms' (the kernels use the plane form)
+    vals = [(o, np.where(np.abs(rb - r64.render_colors) > np.abs(rc - r64.render_colors), rb, rc),
+             r64.render_colors, "render_colors"),
+            (alpha.detach()[:, :rr].cpu().numpy(), np.where(np.abs(r32b.ra - r64.ra) > np.abs(ra - r64.ra), r32b.ra, ra),
+             r64.ra, "ra"),
+            (normals.detach()[:, :rr].cpu().numpy(), np.where(np.abs(r32b.rn - r64.rn) > np.abs(rn - r64.rn), r32b.rn,
+                                                              rn), r64.rn, "rn")]
+    forced, counts = resolve_branches(make64, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy())
     # gradient-path switches only (the 0.999 clamp; the surface / low-pass branch of sigma =
     # min(g3, g2)/2, continuous in value): invisible in every output, so unresolvable
     gonly = gamb & ~amb
@@ -306,7 +308,6 @@ def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
     rates["grad_only_ambiguous_px"] = int(gonly.sum())
     if amb.any():
         got = {k: v.clone() for k, v in got.items()}
-        tsc = 1.0 + choice
         g2 = torch.Generator().manual_seed(seed + 1000)
         keep2 = torch.from_numpy(~gonly)[..., None].float()
         ups = [torch.randn(t.shape, generator=g2) * keep2 for t in (rc, ra, rn)]
@@ -320,7 +321,7 @@ def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
         rv = {}
         for key, dt, hf in (("32", np.float32, 0), ("32b", np.float32, 1), ("64", np.float64, 0)):
             rv[key] = OP.Raster2D(*args, dtype=dt, hitform=hf, **kw)
-            rv[key].tsc = tsc.astype(dt)
+            rv[key].force(**forced)
             rv[key].forward()
         un = [u.numpy() for u in ups]
         gv = {k: r.backward(*un) for k, r in rv.items()}
