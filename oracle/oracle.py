@@ -294,23 +294,21 @@ def set_hitform(form, dtype=np.float32):
     _fn(dtype, "set_hitform")(I32(int(form)))
 
 
-_FLIP_KEEP = {}
+NEAR_K = 8  # hgsr_oracle.c NEAR_K
+_NEAR_KEEP = {}
 
 
-def set_flips(flips, dtype=np.float32):
-    """Near-threshold branch forcing of one build (hgsr_oracle.c set_flips): flips = None, or a
-    dict of [C, rows, W] arrays: {"target"} (target mode: the raster forward takes the other
-    branch at the decision whose margin equals target and fills "idx" / "kind" / "out") or
-    {"idx", "kind", "out"} (forced mode).  The arrays are held until the next call."""
+def set_near(near, dtype=np.float32):
+    """Near-threshold decision lists of one build (hgsr_oracle.c set_near): None, or a dict with
+    "thr" (> 0: record mode, 0: force mode) and arrays "n" [P] int32, "idx" [P,K] int64, "kind" /
+    "out" [P,K] int32, "m" [P,K] float64 (P = C x rows x W).  Held until the next call."""
     key = np.dtype(dtype).name
-    if flips is None:
-        _FLIP_KEEP.pop(key, None)
-        _fn(dtype, "set_flips")(None, None, None, None)
+    if near is None:
+        _NEAR_KEEP.pop(key, None)
+        _fn(dtype, "set_near")(ct.c_double(0.0), None, None, None, None, None)
         return
-    _FLIP_KEEP[key] = flips
-    for k, t in (("idx", np.int64), ("kind", np.int32), ("out", np.int32)):
-        assert flips[k].dtype == t and flips[k].flags["C_CONTIGUOUS"], k
-    tgt = flips.get("target")
-    if tgt is not None:
-        assert tgt.dtype == np.dtype(dtype) and tgt.flags["C_CONTIGUOUS"]
-    _fn(dtype, "set_flips")(_p(tgt), _p(flips["idx"]), _p(flips["kind"]), _p(flips["out"]))
+    for k, t in (("n", np.int32), ("idx", np.int64), ("kind", np.int32), ("out", np.int32), ("m", np.float64)):
+        assert near[k].dtype == t and near[k].flags["C_CONTIGUOUS"], k
+    _NEAR_KEEP[key] = near
+    _fn(dtype, "set_near")(ct.c_double(float(near["thr"])), _p(near["n"]), _p(near["idx"]), _p(near["kind"]),
+                           _p(near["out"]), _p(near["m"]))

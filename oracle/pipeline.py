@@ -22,43 +22,46 @@ def _campos(viewmats):
 
 
 class _Band:
-    # near-threshold branch forcing of the raster calls (hgsr_oracle.c set_flips): None, or a
-    # dict of [C, rows, W] arrays {"target"} + outputs {"idx", "kind", "out"} (target mode) /
-    # {"idx", "kind", "out"} (forced mode)
-    flips = None
+    # near-threshold decision lists of the raster calls (hgsr_oracle.c set_near): None, or the
+    # dict of oracle.set_near (record mode: thr > 0, filled by forward(); force mode: thr = 0)
+    decisions = None
 
     @property
     def Hr(self):
         return self.H if self.rows is None else min(self.rows, self.H)
 
     def _thresholds(self):
-        """Context: the raster calls inside use this instance's branch forcing."""
+        """Context: the raster calls inside use this instance's decision lists."""
         band = self
 
         class _Ctx:
             def __enter__(self):
-                if band.flips is not None:
-                    O.set_flips(band.flips, band.dt)
+                if band.decisions is not None:
+                    O.set_near(band.decisions, band.dt)
 
             def __exit__(self, *exc):
-                if band.flips is not None:
-                    O.set_flips(None, band.dt)
+                if band.decisions is not None:
+                    O.set_near(None, band.dt)
         return _Ctx()
 
-    def flip_closest(self, target):
-        """Target mode: at every pixel with target > 0 take the other branch at the decision
-        whose margin equals target (pass a nominal forward's own `margin` there: the pixel's
-        closest call); call before forward().  The decision found is left in
-        flips["idx" / "kind" / "out"] (out = its NOMINAL outcome)."""
-        shape = (self.viewmats.shape[0], self.Hr, self.W)
-        self.flips = {"target": np.ascontiguousarray(target, self.dt), "idx": np.full(shape, -1, np.int64),
-                      "kind": np.zeros(shape, np.int32), "out": np.zeros(shape, np.int32)}
+    def _shape(self):
+        return (self.viewmats.shape[0], self.Hr, self.W)
 
-    def force(self, idx, kind, out):
-        """Forced mode: at list index idx[pix] the decision of kind[pix] (1 alpha floor, 2 stop;
-        0 = none) takes outcome out[pix]."""
-        self.flips = {"idx": np.ascontiguousarray(idx, np.int64), "kind": np.ascontiguousarray(kind, np.int32),
-                      "out": np.ascontiguousarray(out, np.int32)}
+    def record_near(self, thr):
+        """Record mode: forward() lists every decision with margin < thr per pixel."""
+        P = int(np.prod(self._shape()))
+        K = O.NEAR_K
+        self.decisions = {"thr": float(thr), "n": np.zeros(P, np.int32), "idx": np.full((P, K), -1, np.int64),
+                     "kind": np.zeros((P, K), np.int32), "out": np.zeros((P, K), np.int32),
+                     "m": np.zeros((P, K), np.float64)}
+
+    def force_near(self, near):
+        """Force mode: the listed decisions take the listed outcomes (forward and backward)."""
+        self.decisions = {"thr": 0.0, "n": np.ascontiguousarray(near["n"], np.int32),
+                     "idx": np.ascontiguousarray(near["idx"], np.int64),
+                     "kind": np.ascontiguousarray(near["kind"], np.int32),
+                     "out": np.ascontiguousarray(near["out"], np.int32),
+                     "m": np.ascontiguousarray(near.get("m", np.zeros(near["idx"].shape)), np.float64)}
 
 
 class Raster3D(_Band):

@@ -9,10 +9,12 @@ Pixels whose discrete decisions (alpha vs 1/255, T vs 1e-4, the 0.999 clamp, the
 surface / low-pass branch) sit within a few ulps of a threshold can legitimately go either
 way in any other correct f32 evaluation order.  They are not waved through:
 
-1. value decisions: each such pixel's branch is RESOLVED -- the f64 oracle is re-run taking the
-   OTHER branch at exactly that pixel's closest decision (hgsr_oracle.c branch forcing), and the
-   GPU pixel must equal (its last contributor index exactly, its values within the bar) the
-   nominal or the flipped branch (`resolve_branches`; the counts are printed and returned);
+1. value decisions: each such pixel's branch is RESOLVED -- every decision within 0.1 % of its
+   threshold in the f32 or the f64 oracle is listed, and the f64 oracle is re-run forced onto
+   candidate branches (the f64 outcomes, the f32 outcomes, the f32 outcomes with its closest or
+   second-closest call inverted; hgsr_oracle.c decision lists); the GPU pixel must equal one of
+   them (its last contributor index exactly, its values within the bar) (`resolve_branches`;
+   the counts per branch are printed and returned);
 2. gradients: a second backward of the same forward runs WITHOUT zeroing those pixels'
    upstream gradient, against the f32 / f64 oracle forced onto the branch the GPU took at each
    of them.  Only pixels whose sole near-threshold decision switches a
@@ -44,65 +46,109 @@ def gpu_last(out):
     return last
 
 
-def resolve_branches(make64, r32, r64, amb, vals, last):
-    """Branch the GPU took at every ambiguous pixel.
+NEAR_THR = 1e-3  # decisions listed per pixel: margin below 0.1 %
 
-    make64(target) -> a forwarded f64 oracle that takes the other branch at each pixel's
-    closest decision (hgsr_oracle.c branch forcing, target = the nominal f64 margin); vals:
-    list of (GPU image [C,rows,W,K], f32 oracle image, f64 oracle image, attribute name of the
-    image on the oracle object); last: GPU last ids [C,rows,W].  A pixel matches a branch when
-    its last contributor is that branch's and every value is within ATOL + RTOL |b| +
-    3 |b32 - b64|.  Returns (forced decisions {"idx", "kind", "out"} [C,rows,W] that reproduce
-    the GPU's branch at every ambiguous pixel -- the nominal outcome where the GPU matched the
-    nominal branch, the flipped one where it matched that -- and the counts)."""
+
+def _merge_lists(pix, src, other, flip=None):
+    """One pixel's decision list: every decision near the threshold in EITHER precision, with the
+    outcome of `src` (falling back to `other`, whose margin there is >= NEAR_THR in src's
+    evaluation, so both agree), optionally with the decision flip = (idx, kind) inverted."""
+    ent = {}
+    for lst in (other, src):  # src last: its outcomes win
+        n = min(int(lst["n"][pix]), lst["idx"].shape[1])
+        for k in range(n):
+            ent[(int(lst["idx"][pix, k]), int(lst["kind"][pix, k]))] = (int(lst["out"][pix, k]), float(lst["m"][pix, k]))
+    if flip is not None and flip in ent:
+        o, m = ent[flip]
+        ent[flip] = (1 - o, m)
+    return ent
+
+
+def _closest(pix, lst, j):
+    """(idx, kind) of the j-th smallest-margin decision listed for pixel pix, or None"""
+    n = min(int(lst["n"][pix]), lst["idx"].shape[1])
+    if n <= j:
+        return None
+    k = int(np.argsort(lst["m"][pix, :n])[j])
+    return int(lst["idx"][pix, k]), int(lst["kind"][pix, k])
+
+
+def resolve_branches(make, r32, r64, amb, vals, last):
+    """Branch the GPU took at every near-threshold pixel.
+
+    make(dtype, near) -> a forwarded oracle of that precision with decision lists `near` (None:
+    record mode at NEAR_THR; a dict: force mode, hgsr_oracle.c set_near); vals: list of (GPU
+    image [C,rows,W,K], f32 oracle image, f64 oracle image, attribute name of the image on the
+    oracle object); last: GPU last ids [C,rows,W].
+
+    Every decision within NEAR_THR of its threshold in the f32 or the f64 evaluation is listed
+    per pixel; the candidate branches are: the f64 outcomes, the f32 outcomes, and the f32
+    outcomes with the closest or second-closest call flipped -- each evaluated in f64, forced.
+    A pixel matches a candidate when its last contributor is the candidate's and every value is
+    within ATOL + RTOL |b| + 3 |b32 - b64|; the closest match wins.  Returns (decision lists
+    that reproduce the GPU's branch at every near-threshold pixel, counts)."""
     amb = np.asarray(amb, bool)
     shape = amb.shape
-    forced = {"idx": np.full(shape, -1, np.int64), "kind": np.zeros(shape, np.int32),
-              "out": np.zeros(shape, np.int32)}
+    P, K = int(np.prod(shape)), O_NEAR_K()
+    forced = {"n": np.zeros(P, np.int32), "idx": np.full((P, K), -1, np.int64), "kind": np.zeros((P, K), np.int32),
+              "out": np.zeros((P, K), np.int32)}
     counts = {"ambiguous": int(amb.sum())}
     if not amb.any():
         return forced, counts
+    l32, l64 = make(np.float32, None).decisions, make(np.float64, None).decisions
+    over = amb.reshape(-1) & ((l32["n"] > K) | (l64["n"] > K))
+    counts["list_overflow"] = int(over.sum())
+    pixels = np.flatnonzero(amb.reshape(-1) & ~over)
+    names = ("f64", "f32", "f32_flip0", "f32_flip1")
+    cand_lists = []
+    for ci in range(len(names)):
+        lst = {k: v.copy() for k, v in forced.items()}
+        for p in pixels:
+            if ci == 0:
+                ent = _merge_lists(p, l64, l32)
+            else:
+                ent = _merge_lists(p, l32, l64, None if ci == 1 else _closest(p, l32, ci - 2))
+            for k, ((idx, kind), (o, _)) in enumerate(sorted(ent.items())[:K]):
+                lst["idx"][p, k], lst["kind"][p, k], lst["out"][p, k] = idx, kind, o
+            lst["n"][p] = min(len(ent), K)
+        cand_lists.append(lst)
     last = np.asarray(last)
     e32 = [np.abs(np.asarray(b32, np.float64) - b64) for _, b32, b64, _ in vals]
-    rf = make64(np.where(amb, r64.margin, 0.0))
-    fl = rf.flips
-    has = amb & (fl["kind"] > 0)
 
-    def err(rv, cand):
-        """per pixel: max over values of |GPU - branch| / bar (inf off the candidates or when the
-        last contributor differs); <= 1 is a match"""
-        x = np.where(cand & (last == rv.last), 0.0, np.inf)
+    def err(rv):
+        x = np.where(amb & (last == rv.last), 0.0, np.inf)
         for (a, _, _, attr), e in zip(vals, e32):
             b = np.asarray(getattr(rv, attr), np.float64)
             bar = ATOL + RTOL * np.abs(b) + 3.0 * e
             x = np.maximum(x, (np.abs(np.asarray(a, np.float64) - b) / bar).reshape(shape + (-1,)).max(-1))
         return x
 
-    # the closer of the two branches (both can lie within the bar where the flip moves the
-    # values only a little; the gradient check then uses the one the GPU evaluated)
-    e_nom, e_flp = err(r64, amb), err(rf, has)
-    flp = (e_flp <= 1.0) & (e_flp < e_nom)
-    nom = (e_nom <= 1.0) & ~flp
-    # where the GPU matched a branch, force the decision found to the GPU's outcome
-    sel = (nom | flp) & has
-    forced["idx"][sel] = fl["idx"][sel]
-    forced["kind"][sel] = fl["kind"][sel]
-    forced["out"][sel] = np.where(flp, 1 - fl["out"], fl["out"])[sel]
-    counts.update(nominal=int(nom.sum()), flipped=int(flp.sum()), unmatched=int((amb & ~nom & ~flp).sum()),
-                  flip_kinds={"alpha_floor": int((flp & (fl["kind"] == 1)).sum()),
-                              "stop": int((flp & (fl["kind"] == 2)).sum())})
-    left = amb & ~nom & ~flp
+    errs = np.stack([err(make(np.float64, lst)) for lst in cand_lists])  # [4, C, rows, W]
+    best = np.argmin(errs, 0)
+    ok = amb & (np.min(errs, 0) <= 1.0)
+    for ci, name in enumerate(names):
+        sel = (ok & (best == ci)).reshape(-1)
+        counts[name] = int(sel.sum())
+        for k in forced:
+            forced[k][sel] = cand_lists[ci][k][sel]
+    left = amb & ~ok
+    counts["unmatched"] = int(left.sum())
     if left.any():
         rows = []
         for p in np.argwhere(left)[:6]:
             p = tuple(p)
-            rows.append(dict(pix=p, gpu_last=int(last[p]), f64_last=int(r64.last[p]), flip_last=int(rf.last[p]),
-                             f32_last=int(r32.last[p]), margin=float(r64.margin[p]), kind=int(fl["kind"][p]),
-                             gpu=np.asarray(vals[0][0])[p].tolist(), f64=np.asarray(vals[0][2])[p].tolist(),
-                             flip=np.asarray(getattr(rf, vals[0][3]))[p].tolist()))
-        raise AssertionError(f"{counts['unmatched']} near-threshold pixels match neither branch of the oracle: "
-                             f"{counts} {rows}")
+            q = int(np.ravel_multi_index(p, shape))
+            rows.append(dict(pix=p, gpu_last=int(last[p]), f64_last=int(r64.last[p]), f32_last=int(r32.last[p]),
+                             err=[float(e[p]) for e in errs], n32=int(l32["n"][q]), n64=int(l64["n"][q]),
+                             gpu=np.asarray(vals[0][0])[p].tolist(), f64=np.asarray(vals[0][2])[p].tolist()))
+        raise AssertionError(f"{counts['unmatched']} near-threshold pixels match no branch of the oracle: {counts} "
+                             f"{rows}")
     return forced, counts
+
+
+def O_NEAR_K():
+    from oracle import oracle as O
+    return O.NEAR_K
 
 
 def depth_stats(ref):
@@ -181,14 +227,17 @@ def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None
         rates["v_" + k] = cond_close(v.cpu().numpy(), gr32[k], gr64[k], "v_" + k, rel_floor=0, env=genv[k])
     # near-threshold pixels: resolve the branch the GPU took, then check the gradients again with
     # their upstream gradient kept, against the oracle evaluated on those branches
-    def make64(target):
-        r = OP.Raster3D(*args, dtype=np.float64, **kw)
-        r.flip_closest(target)
+    def make(dt, near):
+        r = OP.Raster3D(*args, dtype=dt, **kw)
+        if near is None:
+            r.record_near(NEAR_THR)
+        else:
+            r.force_near(near)
         r.forward()
         return r
     vals = [(o, rc, r64.render_colors, "render_colors"),
             (alpha.detach()[:, :rr].cpu().numpy(), ra, r64.ra, "ra")]
-    forced, counts = resolve_branches(make64, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy())
+    forced, counts = resolve_branches(make, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy())
     gonly = gamb & ~amb  # a gradient-path switch only (the 0.999 clamp): invisible in every output
     rates["branches"] = counts
     rates["grad_only_ambiguous_px"] = int(gonly.sum())
@@ -209,7 +258,7 @@ def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None
         rv = {}
         for dt in (np.float32, np.float64):  # both precisions forced onto the GPU's branches
             rv[dt] = OP.Raster3D(*args, dtype=dt, **kw)
-            rv[dt].force(**forced)
+            rv[dt].force_near(forced)
             rv[dt].forward()
         gv32 = rv[np.float32].backward(vrc2.numpy(), vra2.numpy())
         gv64 = rv[np.float64].backward(vrc2.numpy(), vra2.numpy())
@@ -288,9 +337,12 @@ def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
                                      alt32=gr32b[k])
     # near-threshold pixels: resolve the GPU's branch, then the gradients again with their upstream kept
 
-    def make64(target):
-        r = OP.Raster2D(*args, dtype=np.float64, **kw)
-        r.flip_closest(target)
+    def make(dt, near):
+        r = OP.Raster2D(*args, dtype=dt, **kw)
+        if near is None:
+            r.record_near(NEAR_THR)
+        else:
+            r.force_near(near)
         r.forward()
         return r
     # the f32 error of each value: the larger of the two hit forms' (the kernels use the plane form)
@@ -300,7 +352,7 @@ def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
              r64.ra, "ra"),
             (normals.detach()[:, :rr].cpu().numpy(), np.where(np.abs(r32b.rn - r64.rn) > np.abs(rn - r64.rn), r32b.rn,
                                                               rn), r64.rn, "rn")]
-    forced, counts = resolve_branches(make64, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy())
+    forced, counts = resolve_branches(make, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy())
     # gradient-path switches only (the 0.999 clamp; the surface / low-pass branch of sigma =
     # min(g3, g2)/2, continuous in value): invisible in every output, so unresolvable
     gonly = gamb & ~amb
@@ -321,7 +373,7 @@ def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
         rv = {}
         for key, dt, hf in (("32", np.float32, 0), ("32b", np.float32, 1), ("64", np.float64, 0)):
             rv[key] = OP.Raster2D(*args, dtype=dt, hitform=hf, **kw)
-            rv[key].force(**forced)
+            rv[key].force_near(forced)
             rv[key].forward()
         un = [u.numpy() for u in ups]
         gv = {k: r.backward(*un) for k, r in rv.items()}

@@ -9,6 +9,7 @@ import json
 import math
 import os
 
+import numpy as np
 import pytest
 import torch
 
@@ -176,3 +177,29 @@ def test_psnr_parity_pipeline_3dgs():
 
 def test_psnr_parity_pipeline_2dgs():
     _pipeline_parity("2d")
+
+
+@pytest.mark.parametrize("gs", ["3d", "2d"])
+def test_pipeline_step_gradients(gs):
+    """One step of the PSNR-parity pipeline (tests/pipeline_fit.py) at its initial parameters: the
+    loss and the gradient of every trained tensor (anchor features, offsets, scalings, the twelve
+    MLP tensors) of the HIP chain against the CPU chain in f32 (checker) and f64 (truth), per
+    element with conditioning (oracle/checks.cond_close).  The per-step statement behind the
+    equal-iteration PSNR comparison."""
+    from oracle.checks import cond_close
+    from tests import pipeline_fit as PF
+    W, H = 160, 120
+    gt = PF.target(40000, W, H, seed=31, gs=gs)
+    p0, cfg = PF.anchor_model(5000, W, H, seed=32, param_seed=200)
+    res = {}
+    for name, dev, dt in (("gpu", "cuda", None), ("f32", "cpu", torch.float32), ("f64", "cpu", torch.float64)):
+        p = {k: v.to(dev).clone().requires_grad_(k != "anchor") for k, v in p0.items()}
+        c = dict(cfg)
+        if dt is not None:
+            c["dtype"] = dt
+        loss = (PF.gpu_loss if dev == "cuda" else PF.cpu_loss)(p, c, gt.to(dev), gs)[0]
+        loss.backward()
+        res[name] = (float(loss), {k: v.grad.detach().cpu().double().numpy() for k, v in p.items() if k != "anchor"})
+    cond_close(np.array([res["gpu"][0]]), np.array([res["f32"][0]]), np.array([res["f64"][0]]), "loss")
+    for k in res["gpu"][1]:
+        cond_close(res["gpu"][1][k], res["f32"][1][k], res["f64"][1][k], "d_" + k)
