@@ -294,6 +294,12 @@ def set_hitform(form, dtype=np.float32):
     _fn(dtype, "set_hitform")(I32(int(form)))
 
 
+def set_alphaform(form, dtype=np.float32):
+    """3DGS alpha evaluation of one build: 0 gsplat's exp(-sigma), 1 the kernels' log2(e)-scaled
+    conic with explicit FMAs and exp2 (hgsr_oracle.c vis3)."""
+    _fn(dtype, "set_alphaform")(I32(int(form)))
+
+
 NEAR_K = 8  # hgsr_oracle.c NEAR_K
 _NEAR_KEEP = {}
 

@@ -69,9 +69,10 @@ class Raster3D(_Band):
 
     def __init__(self, means, quats, scales, opacities, colors, viewmats, Ks, W, H, sh_degree=None,
                  backgrounds=None, render_mode="RGB+ED", eps2d=0.3, near=0.01, far=1e10, tile_size=16,
-                 dtype=np.float32, rows=None):
+                 dtype=np.float32, rows=None, alphaform=0):
         self.dt = dtype
         self.rows = rows  # rasterise only image rows [0, rows) (banded checks); None = all
+        self.alphaform = alphaform  # 3DGS alpha evaluation form (hgsr_oracle.c vis3)
         c = lambda a: None if a is None else np.ascontiguousarray(a, dtype=dtype)  # noqa: E731
         self.means, self.quats, self.scales = c(means), c(quats), c(scales)
         self.opacities, self.colors = c(opacities), c(colors)
@@ -112,10 +113,14 @@ class Raster3D(_Band):
                                                                    self.tw, self.th, dtype=dt)
         self.offsets = O.isect_offsets(self.isect_ids, C, self.tw, self.th)
         self.opac_c = np.ascontiguousarray(np.broadcast_to(self.opacities, (C, Nn)), dt)
-        with self._thresholds():
-            self.rc_raw, self.ra, self.last, self.stopped, self.margin, self.gmargin = O.raster3d_fwd(
-                self.means2d, self.conics, self.cols, self.opac_c, self.bg_r, self.W, self.Hr, self.ts, self.offsets,
-                self.flatten_ids, dtype=dt, return_stopped=True)
+        O.set_alphaform(self.alphaform, dt)
+        try:
+            with self._thresholds():
+                self.rc_raw, self.ra, self.last, self.stopped, self.margin, self.gmargin = O.raster3d_fwd(
+                    self.means2d, self.conics, self.cols, self.opac_c, self.bg_r, self.W, self.Hr, self.ts,
+                    self.offsets, self.flatten_ids, dtype=dt, return_stopped=True)
+        finally:
+            O.set_alphaform(0, dt)
         out = self.rc_raw.copy()
         if self.mode in ("ED", "RGB+ED"):
             out[..., -1:] = self.rc_raw[..., -1:] / np.maximum(self.ra, dt(1e-10))
@@ -134,10 +139,14 @@ class Raster3D(_Band):
             v_ra = v_ra + np.where(self.ra >= dt(1e-10), -g * self.rc_raw[..., -1:] / (den * den), 0).astype(dt)
             v_rc = v_rc.copy()
             v_rc[..., -1:] = g / den
-        with self._thresholds():
-            vm2, vcon, vcol, vop = O.raster3d_bwd(self.means2d, self.conics, self.cols, self.opac_c, self.bg_r,
-                                                  self.W, self.Hr, self.ts, self.offsets, self.flatten_ids, self.ra,
-                                                  self.last, v_rc, v_ra, dtype=dt)
+        O.set_alphaform(self.alphaform, dt)
+        try:
+            with self._thresholds():
+                vm2, vcon, vcol, vop = O.raster3d_bwd(self.means2d, self.conics, self.cols, self.opac_c, self.bg_r,
+                                                      self.W, self.Hr, self.ts, self.offsets, self.flatten_ids,
+                                                      self.ra, self.last, v_rc, v_ra, dtype=dt)
+        finally:
+            O.set_alphaform(0, dt)
         v_depths = np.zeros((C, Nn), dt)
         if self.mode in ("RGB+D", "RGB+ED", "D", "ED"):
             v_depths += vcol[..., -1]

@@ -49,15 +49,17 @@ def gpu_last(out):
 NEAR_THR = 1e-3  # decisions listed per pixel: margin below 0.1 %
 
 
-def _merge_lists(pix, src, other, flip=None):
-    """One pixel's decision list: every decision near the threshold in EITHER precision, with the
-    outcome of `src` (falling back to `other`, whose margin there is >= NEAR_THR in src's
-    evaluation, so both agree), optionally with the decision flip = (idx, kind) inverted."""
+def _merge_lists(pix, src, flip=None):
+    """One pixel's decision list: the decisions `src` took within NEAR_THR of their thresholds,
+    with its outcomes, optionally with the decision flip = (idx, kind) inverted.  Only src's own
+    decisions are forced: a decision src did not list had a margin >= NEAR_THR on src's
+    trajectory, so the forced f64 run -- on the same trajectory up to there -- decides it the same
+    way by itself.  (Another precision's outcomes must not fill the gaps: once one earlier
+    decision differs, its later decisions belong to a different trajectory.)"""
     ent = {}
-    for lst in (other, src):  # src last: its outcomes win
-        n = min(int(lst["n"][pix]), lst["idx"].shape[1])
-        for k in range(n):
-            ent[(int(lst["idx"][pix, k]), int(lst["kind"][pix, k]))] = (int(lst["out"][pix, k]), float(lst["m"][pix, k]))
+    n = min(int(src["n"][pix]), src["idx"].shape[1])
+    for k in range(n):
+        ent[(int(src["idx"][pix, k]), int(src["kind"][pix, k]))] = (int(src["out"][pix, k]), float(src["m"][pix, k]))
     if flip is not None and flip in ent:
         o, m = ent[flip]
         ent[flip] = (1 - o, m)
@@ -73,17 +75,20 @@ def _closest(pix, lst, j):
     return int(lst["idx"][pix, k]), int(lst["kind"][pix, k])
 
 
-def resolve_branches(make, r32, r64, amb, vals, last):
+def resolve_branches(make, r32, r64, amb, vals, last, alt32=None):
     """Branch the GPU took at every near-threshold pixel.
 
     make(dtype, near) -> a forwarded oracle of that precision with decision lists `near` (None:
     record mode at NEAR_THR; a dict: force mode, hgsr_oracle.c set_near); vals: list of (GPU
     image [C,rows,W,K], f32 oracle image, f64 oracle image, attribute name of the image on the
-    oracle object); last: GPU last ids [C,rows,W].
+    oracle object); last: GPU last ids [C,rows,W] (indices into the f32 oracle's intersection
+    list, which the GPU's equals); alt32(near) -> a second correct f32
+    evaluation in record mode (2DGS: the plane-form hit the kernels use), or None.
 
-    Every decision within NEAR_THR of its threshold in the f32 or the f64 evaluation is listed
-    per pixel; the candidate branches are: the f64 outcomes, the f32 outcomes, and the f32
-    outcomes with the closest or second-closest call flipped -- each evaluated in f64, forced.
+    Every decision within NEAR_THR of its threshold is listed per pixel and evaluation; the
+    candidate branches are: the f64 outcomes, the f32 outcomes, and the f32
+    outcomes with the closest or second-closest call flipped (and the same three for alt32's
+    outcomes) -- each evaluated in f64, forced.
     A pixel matches a candidate when its last contributor is the candidate's and every value is
     within ATOL + RTOL |b| + 3 |b32 - b64|; the closest match wins.  Returns (decision lists
     that reproduce the GPU's branch at every near-threshold pixel, counts)."""
@@ -96,34 +101,39 @@ def resolve_branches(make, r32, r64, amb, vals, last):
     if not amb.any():
         return forced, counts
     l32, l64 = make(np.float32, None).decisions, make(np.float64, None).decisions
-    over = amb.reshape(-1) & ((l32["n"] > K) | (l64["n"] > K))
+    srcs = [("f32", l32)] + ([] if alt32 is None else [("f32b", alt32(None).decisions)])
+    over = amb.reshape(-1) & ((l64["n"] > K) | np.any([ls["n"] > K for _, ls in srcs], 0))
     counts["list_overflow"] = int(over.sum())
     pixels = np.flatnonzero(amb.reshape(-1) & ~over)
-    names = ("f64", "f32", "f32_flip0", "f32_flip1")
+    # (name, the evaluation whose listed outcomes are forced, which of its calls to flip)
+    cands = [("f64", l64, None)]
+    for nm, ls in srcs:
+        cands += [(nm, ls, None), (nm + "_flip0", ls, 0), (nm + "_flip1", ls, 1)]
+    names = tuple(c[0] for c in cands)
     cand_lists = []
-    for ci in range(len(names)):
+    for _, src, fl in cands:
         lst = {k: v.copy() for k, v in forced.items()}
         for p in pixels:
-            if ci == 0:
-                ent = _merge_lists(p, l64, l32)
-            else:
-                ent = _merge_lists(p, l32, l64, None if ci == 1 else _closest(p, l32, ci - 2))
+            ent = _merge_lists(p, src, None if fl is None else _closest(p, src, fl))
             for k, ((idx, kind), (o, _)) in enumerate(sorted(ent.items())[:K]):
                 lst["idx"][p, k], lst["kind"][p, k], lst["out"][p, k] = idx, kind, o
             lst["n"][p] = min(len(ent), K)
         cand_lists.append(lst)
+    # last contributors compared as Gaussian ids: the f32 and f64 binnings can order the
+    # intersection lists differently (the GPU's list is the f32 oracle's, bit for bit)
     last = np.asarray(last)
+    gid = r32.flatten_ids[last]
     e32 = [np.abs(np.asarray(b32, np.float64) - b64) for _, b32, b64, _ in vals]
 
     def err(rv):
-        x = np.where(amb & (last == rv.last), 0.0, np.inf)
+        x = np.where(amb & (gid == rv.flatten_ids[rv.last]), 0.0, np.inf)
         for (a, _, _, attr), e in zip(vals, e32):
             b = np.asarray(getattr(rv, attr), np.float64)
             bar = ATOL + RTOL * np.abs(b) + 3.0 * e
             x = np.maximum(x, (np.abs(np.asarray(a, np.float64) - b) / bar).reshape(shape + (-1,)).max(-1))
         return x
 
-    errs = np.stack([err(make(np.float64, lst)) for lst in cand_lists])  # [4, C, rows, W]
+    errs = np.stack([err(make(np.float64, lst)) for lst in cand_lists])  # [candidates, C, rows, W]
     best = np.argmin(errs, 0)
     ok = amb & (np.min(errs, 0) <= 1.0)
     for ci, name in enumerate(names):
@@ -138,7 +148,8 @@ def resolve_branches(make, r32, r64, amb, vals, last):
         for p in np.argwhere(left)[:6]:
             p = tuple(p)
             q = int(np.ravel_multi_index(p, shape))
-            rows.append(dict(pix=p, gpu_last=int(last[p]), f64_last=int(r64.last[p]), f32_last=int(r32.last[p]),
+            rows.append(dict(pix=p, gpu_last=int(gid[p]), f64_last=int(r64.flatten_ids[r64.last[p]]),
+                             f32_last=int(r32.flatten_ids[r32.last[p]]),
                              err=[float(e[p]) for e in errs], n32=int(l32["n"][q]), n64=int(l64["n"][q]),
                              gpu=np.asarray(vals[0][0])[p].tolist(), f64=np.asarray(vals[0][2])[p].tolist()))
         raise AssertionError(f"{counts['unmatched']} near-threshold pixels match no branch of the oracle: {counts} "
@@ -237,7 +248,13 @@ def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None
         return r
     vals = [(o, rc, r64.render_colors, "render_colors"),
             (alpha.detach()[:, :rr].cpu().numpy(), ra, r64.ra, "ra")]
-    forced, counts = resolve_branches(make, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy())
+
+    def make_k(near):  # the kernels' alpha form (log2(e)-scaled conic, FMAs, exp2), f32
+        r = OP.Raster3D(*args, alphaform=1, **kw)
+        r.record_near(NEAR_THR)
+        r.forward()
+        return r
+    forced, counts = resolve_branches(make, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy(), alt32=make_k)
     gonly = gamb & ~amb  # a gradient-path switch only (the 0.999 clamp): invisible in every output
     rates["branches"] = counts
     rates["grad_only_ambiguous_px"] = int(gonly.sum())
@@ -352,7 +369,12 @@ def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
              r64.ra, "ra"),
             (normals.detach()[:, :rr].cpu().numpy(), np.where(np.abs(r32b.rn - r64.rn) > np.abs(rn - r64.rn), r32b.rn,
                                                               rn), r64.rn, "rn")]
-    forced, counts = resolve_branches(make, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy())
+    def make_b(near):  # the plane-form hit the kernels evaluate, f32
+        r = OP.Raster2D(*args, hitform=1, **kw)
+        r.record_near(NEAR_THR)
+        r.forward()
+        return r
+    forced, counts = resolve_branches(make, r32, r64, amb, vals, gpu_last(out)[:, :rr].cpu().numpy(), alt32=make_b)
     # gradient-path switches only (the 0.999 clamp; the surface / low-pass branch of sigma =
     # min(g3, g2)/2, continuous in value): invisible in every output, so unresolvable
     gonly = gamb & ~amb
