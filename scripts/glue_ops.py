@@ -33,7 +33,13 @@ def main():
         if not kern:
             continue
         frames = [f for f in (ev.stack or []) if ROOT in f and "glue_ops.py" not in f]
-        where = frames[0].replace(ROOT + "/", "") if frames else "?"
+        where = frames[0].replace(ROOT + "/", "") if frames else ""
+        # inside the backward there is no Python stack: name the autograd node / parent ops
+        par, chain = ev.cpu_parent, []
+        while par is not None and len(chain) < 3:
+            chain.append(par.name.replace("autograd::engine::evaluate_function: ", "bwd:"))
+            par = par.cpu_parent
+        where = (where + " " + " < ".join(chain)).strip() or "?"
         key = (ev.name, where)
         r = rows.setdefault(key, [0, 0.0, set()])
         r[0] += len(kern)

@@ -17,11 +17,14 @@ regulariser + 0.05 sky opacity + 0.05 opacity entropy; the normal term starts at
 7000, after this run).  `fit()` returns the final-iterate PSNR against the target and the
 PSNR of the last iterations' renders (the smoothed training curve).
 
-The chain is chaotic: the opacity gate (tanh > 0) and the per-pixel threshold decisions are
-discrete, so round-off differences grow into different trajectories.  The CPU chain
-against itself with its initial parameters perturbed by 1e-6 (relative) already ends
-~0.1 dB apart in final-iterate PSNR, while the window PSNRs agree to ~0.02 dB -- the
-trajectories differ in the phase of Adam's oscillation, not in quality.
+At the config's learning rates the chain is chaotic: the opacity gate (tanh > 0), the anchor
+prefilter and the per-pixel threshold decisions are discrete, so round-off differences grow
+into different trajectories.  Measured on the 2DGS chain (CPU, 200 iterations): four runs
+from initialisations perturbed by 1e-6 (relative) end with window PSNRs 30.88-31.02 dB (sd
+0.06 dB), i.e. at those rates no two f32 evaluations can agree to 0.05 dB.  With every
+learning rate scaled by 0.3 the same pair of runs ends 0.010 dB apart (window) / 0.002 dB
+(final iterate) and the fit still gains ~17.6 dB over its initialisation, so the parity test
+uses LR_SCALE: the comparison then resolves the pipelines, not the chain's sensitivity.
 """
 from __future__ import annotations
 
@@ -35,6 +38,7 @@ from horizongs_amd.synthetic import make_scene
 HEADS = ("opacity", "cov", "color")
 # config/base/small_scene/fine.yaml initial learning rates (position lr 0: the anchors stay)
 LR = dict(feat=0.0075, offset=0.001, scaling=0.007, opacity=0.002, cov=0.004, color=0.008)
+LR_SCALE = 0.3  # the parity test's rate scale (see the module docstring)
 
 
 def anchor_model(A, W, H, seed, param_seed, view_dim=3, color_dim=3, n_off=10, feat_std=0.5):
@@ -136,18 +140,18 @@ def psnr(img, gt):
     return 10 * math.log10(1.0 / mse)
 
 
-def fit(p0, cfg, gt, iters, gs="3d", device="cpu", window=50):
-    """`iters` Adam steps of the chain on `device` from p0.  Returns (final-iterate PSNR,
-    window PSNR, losses): the window PSNR is 10 log10(1 / mean MSE) of the renders of the last
-    `window` iterations (the training curve smoothed over Adam's iteration-to-iteration
-    oscillation, ~2 % in the loss at constant learning rate)."""
+def fit(p0, cfg, gt, iters, gs="3d", device="cpu", window=50, lr_scale=1.0):
+    """`iters` Adam steps of the chain on `device` from p0, every learning rate times lr_scale.
+    Returns (final-iterate PSNR, window PSNR, losses): the window PSNR is 10 log10(1 / mean MSE)
+    of the renders of the last `window` iterations (the training curve smoothed over Adam's
+    iteration-to-iteration oscillation, ~2 % in the loss at constant learning rate)."""
     on_gpu = device != "cpu"
     p = {k: v.to(device).clone().requires_grad_(k != "anchor") for k, v in p0.items()}
     if on_gpu:
         from horizongs_amd.optim import Adam
     else:
         Adam = torch.optim.Adam
-    opt = Adam([{"params": [p[k]], "lr": _lr(k)} for k in p if k != "anchor"], lr=0.0, eps=1e-15)
+    opt = Adam([{"params": [p[k]], "lr": lr_scale * _lr(k)} for k in p if k != "anchor"], lr=0.0, eps=1e-15)
     gt_d = gt.to(device)
     loss_fn, render = (gpu_loss, gpu_render) if on_gpu else (cpu_loss, cpu_render)
     losses, mses = [], []

@@ -90,7 +90,7 @@ def resolve_branches(make, r32, r64, amb, vals, last, alt32=None):
     outcomes with the closest or second-closest call flipped (and the same three for alt32's
     outcomes) -- each evaluated in f64, forced.
     A pixel matches a candidate when its last contributor is the candidate's and every value is
-    within ATOL + RTOL |b| + 3 |b32 - b64|; the closest match wins.  Returns (decision lists
+    within ATOL + RTOL |b| + 3 |b32 - b64|; the first match in preference order wins.  Returns (decision lists
     that reproduce the GPU's branch at every near-threshold pixel, counts)."""
     amb = np.asarray(amb, bool)
     shape = amb.shape
@@ -105,10 +105,16 @@ def resolve_branches(make, r32, r64, amb, vals, last, alt32=None):
     over = amb.reshape(-1) & ((l64["n"] > K) | np.any([ls["n"] > K for _, ls in srcs], 0))
     counts["list_overflow"] = int(over.sum())
     pixels = np.flatnonzero(amb.reshape(-1) & ~over)
-    # (name, the evaluation whose listed outcomes are forced, which of its calls to flip)
-    cands = [("f64", l64, None)]
-    for nm, ls in srcs:
+    # (name, the evaluation whose listed outcomes are forced, which of its calls to flip), in
+    # order of preference: the evaluation that reproduces the kernels' arithmetic first (alt32:
+    # its decisions are the GPU's up to the hardware exp2's last ulp), f64 last.  The first
+    # candidate within the value bar wins, not the closest: a keep / skip decision whose
+    # contribution is below the value bar cannot be told apart by the render, only by its
+    # gradient, so the branch is taken from the evaluation most likely to share it.
+    cands = []
+    for nm, ls in srcs[::-1]:
         cands += [(nm, ls, None), (nm + "_flip0", ls, 0), (nm + "_flip1", ls, 1)]
+    cands.append(("f64", l64, None))
     names = tuple(c[0] for c in cands)
     cand_lists = []
     for _, src, fl in cands:
@@ -134,8 +140,9 @@ def resolve_branches(make, r32, r64, amb, vals, last, alt32=None):
         return x
 
     errs = np.stack([err(make(np.float64, lst)) for lst in cand_lists])  # [candidates, C, rows, W]
-    best = np.argmin(errs, 0)
-    ok = amb & (np.min(errs, 0) <= 1.0)
+    fits = errs <= 1.0
+    best = np.argmax(fits, 0)  # the first fitting candidate in preference order
+    ok = amb & fits.any(0)
     for ci, name in enumerate(names):
         sel = (ok & (best == ci)).reshape(-1)
         counts[name] = int(sel.sum())
