@@ -243,6 +243,7 @@ class Workload:
                                                                self.cam_center, self.mlps, vis_idx, self.view_dim, 10,
                                                                self.color_dim)
             opac = opac.reshape(-1)
+            self.last_av = sel.numel() // 10  # visible anchors of this view (decode MFMA accounting)
         else:
             xyz, quats, cols = self.means, self.quats, self.colors
             # scaling_activation = exp, opacity_activation = sigmoid: one fused HIP pass each way
@@ -304,6 +305,47 @@ def hbm_kernels(wl, kernels, n_isects):
         if k in kernels:
             gbs = nbytes / (kernels[k]["avg_ms"] * 1e-3) / 1e9
             out[k] = {"bytes": nbytes, "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 3)}
+    return out
+
+
+def decode_mfma(wl, kernels):
+    """MFMA utilisation of the fused anchor decode (csrc/decode.hip), forward and backward.
+
+    Every MLP product runs on v_mfma_f32_16x16x4_f32 (2,048 FLOP, 32 SIMD-cycles each) on a
+    16-anchor wave tile; the counts per wave tile follow the kernels' loops (K1 = 32 + view_dim
+    inputs, KS = ceil(K1 / 4) k-steps, output tiles T = ceil(rows / 16) per head):
+      forward  : hidden 2 KS per head x 3 + second layer 8 T per head (+ the count pass: the
+                 opacity head again, 2 KS + 8);
+      backward : per head launch (colour head chunked by <= 5 output tiles) hidden 2 KS +
+                 recomputed Y (8 x all T, opacity / cov) + dW2 8 nt + dH 8 nt + dW1 and dX
+                 8 ceil(K1 / 16) each.
+    busy = MFMA FLOP / kernel time / 157.3 TFLOP/s (= the f32 MFMA peak at 64 FLOP/clk/SIMD),
+    which is SQ_VALU_MFMA_BUSY_CYCLES / (SIMD count x kernel cycles) at the peak clock: the
+    r02 PMC pass measured exactly 374 x 32 SIMD-cycles per wave tile for the RGB model."""
+    av = getattr(wl, "last_av", None)
+    if not av or not kernels:
+        return None
+    K1 = 32 + wl.view_dim
+    KS = (K1 + 3) // 4
+    kt = (K1 + 15) // 16
+    T = [1, 5, (wl.color_dim * 10 + 15) // 16]  # opacity 10, cov 70, colour color_dim x 10 rows
+    fwd = 3 * 2 * KS + 8 * sum(T) + (2 * KS + 8)
+    bwd = 0
+    for h in range(3):
+        chunks = [min(5, T[h] - t0) for t0 in range(0, T[h], 5)]
+        for nt in chunks:
+            bwd += 2 * KS + (8 * T[h] if h < 2 else 0) + 16 * nt + 16 * kt
+    tiles = (av + 63) // 64 * 4
+    out = {"visible_anchors": av, "mfma_per_wave_tile": {"decode_fwd+count": fwd, "decode_bwd": bwd}}
+    for name, n in (("decode_bwd", bwd), ("decode_fwd", fwd)):
+        key = name if name in kernels else None
+        if key is None:
+            continue
+        t = kernels[key]["avg_ms"] * 1e-3
+        if name == "decode_fwd" and "decode_count" in kernels:
+            t += kernels["decode_count"]["avg_ms"] * 1e-3
+        tf = tiles * n * 2048 / t / 1e12
+        out[name] = {"tflops": round(tf, 2), "busy": round(tf / FP32_PEAK_TFLOPS, 4)}
     return out
 
 
@@ -547,6 +589,7 @@ def secondary(args, rank, world, dev):
                         "gaussians": int(r["wl"].last_colors.shape[0]), "n_isects": r["isects_after"],
                         "roofline": None if roof is None else {k: roof[k] for k in (
                             "bound", "kernel", "achieved", "frac", "frac_executed", "kernel_avg_ms")},
+                        "decode_mfma": decode_mfma(r["wl"], r["kernels"]) if a.anchors else None,
                         "kernels": r["kernels"]})
         del r
         torch.cuda.empty_cache()
