@@ -162,7 +162,8 @@ def _pipeline_parity(gs):
                reference=("CPU chain: oracle/decode_ref.decode_torch (pinned to tests/golden/decode_*.npz) -> "
                           f"C-oracle rasterization{'_2dgs' if gs == '2d' else ''} (oracle/autograd.py) -> "
                           "oracle/loss_ref.loss (pinned to tests/golden/losses.npz) -> torch.optim.Adam(eps=1e-15); "
-                          "fine-stage loss weights and learning rates (config/base/small_scene/fine.yaml)"))
+                          "fine-stage loss weights (config/base/small_scene/fine.yaml), its learning rates x "
+                          f"{ls}"))
     os.makedirs("gpurun_out", exist_ok=True)
     with open(os.path.join("gpurun_out", f"psnr_pipeline_{gs}gs.json"), "w") as f:
         json.dump(res, f)
@@ -170,7 +171,8 @@ def _pipeline_parity(gs):
     # the first losses see identical parameters: the two chains agree before any divergence
     assert abs(loss_gpu[0] - loss_cpu[0]) <= 1e-5 + 1e-4 * abs(loss_cpu[0]), res
     assert win_cpu > psnr_init + 10.0  # the fit actually fits
-    assert abs(win_self - win_cpu) <= 0.02, res  # the chain itself is not chaotic at these rates
+    # the chain's own noise floor (a 1e-6 perturbation of its initialisation) is below the bar
+    assert abs(win_self - win_cpu) <= 0.05, res
     assert abs(win_gpu - win_cpu) <= 0.05, res
 
 
