@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes as ct
+import gc
 import json
 import os
 import sys
@@ -453,6 +454,9 @@ def measure(args, rank, world, dev):
     for _ in range(args.warmup):
         wl.step()
     torch.cuda.synchronize(dev)
+    # the objects of the scene setup (and of an earlier workload in this process) are collected
+    # now, not by a generation-2 pass inside the timed steps
+    gc.collect()
     # the optimizer moves the scene: intersections before / after the timed steps show the drift
     isects_before = wl.meta["flatten_ids"].numel() if args.warmup else None
     timing = not args.no_timing
