@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         float4 g0[2][NB + 1], g1[2][NB + 1], col[2][NB + 1];
     } sr;
     __shared__ int32_t s_id[2][NB];
-    __shared__ uint8_t s_list[4][NB];
+    __shared__ __attribute__((aligned(16))) uint8_t s_list[4][NB];  // read back as 32-bit words
     __shared__ int32_t s_last[4];
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -422,6 +422,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     uint8_t* my_list = s_list[wave];
     uint32_t stepped = 0;  // compacted list entries this wave stepped (bench roofline only)
     const int slot = lane >> 4;  // pass-2 Gaussian slot of this lane
+    const int slot8 = 8 * slot;
     // pass-2 output lane roles: after the 16-lane tree every lane of a row holds the six
     // sigma sums (and |v_xy|) and each quad one colour channel; lane r16 = 4 q + 3 adds its
     // quad's channel, lanes 0-2 / 4-6 the sums 0-2 / 3-5, lanes 8 / 9 the |v_xy| pair (ABS)
@@ -505,7 +506,8 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         if (n_mine > 0) {
             // the list comes back into registers once per batch; the loop reads
             // entries with readlane so no LDS index read sits on the critical path
-            const int lst0 = my_list[lane], lst1 = my_list[64 + lane];
+            // (four 8-bit entries per lane: lanes 0-31 hold the whole list)
+            const uint32_t lstp = reinterpret_cast<const uint32_t*>(my_list)[lane & 31];
             // pass 1: composite record t for this lane's pixel (branch-free: a padding entry
             // is the zero-opacity dummy and composites nothing); returns fac and v_sigma
             auto step = [&](const int t, float& F, float& V) {
@@ -534,7 +536,20 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                 V = -araw * va2;  // dL/dsigma (unscaled sigma)
             };
             // pass 2 over 4 composited steps (records ts[0..3], values F/V in pass-1 layout)
-            auto pass2 = [&](const int li, float (&F)[4], float (&V)[4]) {
+            auto pass2 = [&](const uint32_t packed, float (&F)[4], float (&V)[4]) {
+                // this lane's Gaussian (step `slot`), extracted from the group's packed list
+                // entries: its position and id reads are independent and go out before the
+                // transpose
+                const int t = (int)__builtin_amdgcn_ubfe(packed, slot8, 8);
+                float4 g0;
+                if (ABS) {
+                    g0 = sr.g0[cur][t];
+                } else {
+                    const float2 xy = *reinterpret_cast<const float2*>(&sr.g0[cur][t]);
+                    g0 = make_float4(xy.x, xy.y, 0.f, 0.f);
+                }
+                const float g1x = ABS ? sr.g1[cur][t].x : 0.f;
+                const int sid = s_id[cur][t < NB ? t : 0];
                 // transpose: lane bit 5 <-> register bit 1, lane bit 4 <-> register bit 0
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
@@ -551,17 +566,14 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                     V[q] = __uint_as_float(v[0]); V[q + 1] = __uint_as_float(v[1]);
                 }
                 // now F[m], V[m]: step `slot`, pixel (column cx, row y0 + 2m)
-                const int t = my_list[li + slot];  // this lane's Gaussian (list entry li + slot)
-                const float4 g0 = sr.g0[cur][t];
                 const float dx = g0.x - p2.pxc, dy0 = g0.y - p2.py0c;
                 float S0, Sy, Syy, P[4], A0 = 0.f, A1 = 0.f;
                 float ax = 0.f, ay = 0.f, bx = 0.f, c2 = 0.f;
                 if (ABS) {
-                    const float4 g1 = sr.g1[cur][t];
                     ax = 2.f * g0.z * dx;
                     bx = g0.w * dx;
                     ay = g0.w;
-                    c2 = 2.f * g1.x;
+                    c2 = 2.f * g1x;
                 }
                 // the sums start from the first pixel's terms (an add to +0 is not foldable)
 #pragma unroll
@@ -633,19 +645,17 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                     v = qcol ? g[6] : v;
                     if (ABS) v = r16 == 8 ? kLn2 * A0 : r16 == 9 ? kLn2 * A1 : v;
                     if (koff >= 0 && t < NB && v != 0.f)
-                        atomicAdd(acc_rows + (int64_t)s_id[cur][t] * kRec3 + koff, v);
+                        atomicAdd(acc_rows + (int64_t)sid * kRec3 + koff, v);
                 }
             };
-            auto group = [&](const int lst, const int i0, const int li) {
+            for (int i = 0; i < n_mine; i += 4) {
+                // the group's four list entries in one scalar register
+                const uint32_t packed = (uint32_t)__builtin_amdgcn_readlane((int)lstp, i >> 2);
                 float F[4], V[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) step(__builtin_amdgcn_readlane(lst, i0 + q), F[q], V[q]);
-                pass2(li, F, V);
-            };
-            // two loops instead of a per-step select between the list halves
-            const int n0 = min(n_mine, 64);
-            for (int i = 0; i < n0; i += 4) group(lst0, i, i);
-            for (int i = 64; i < n_mine; i += 4) group(lst1, i - 64, i);
+                for (int q = 0; q < 4; ++q) step((int)((packed >> (8 * q)) & 0xffu), F[q], V[q]);
+                pass2(packed, F, V);
+            }
         }
         lds_barrier();
     }
