@@ -197,6 +197,11 @@ struct TransposeReduce {
     }
 };
 
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {  // lane-shuffled copy of x (bound_ctrl: 0 for invalid)
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
 // Where a raster call's channels come from.  gsplat's rasterize_to_pixels takes
 // colors [C,N,D] and opacities [C,N]; rasterization() itself concatenates the depth
 // and repeats shared colours/opacities over cameras, which the fused entry points do

@@ -285,10 +285,6 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
 // split3.  A 16-lane DPP tree finishes the sums (colours pre-permuted per lane class so
 // that the first two levels transpose instead of add).  Two transposed inputs replace
 // the ten reduced outputs of a per-step wave reduction.
-template <int CTRL>
-__device__ __forceinline__ float dpp(float x) {  // lane-shuffled copy of x (bound_ctrl: 0 for invalid)
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
-}
 
 // 8 waves / SIMD (64 VGPRs; the register budget costs two spilled values outside the
 // step loop): 0.789 -> 0.776 ms at c2
