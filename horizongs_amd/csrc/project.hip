@@ -250,7 +250,9 @@ __global__ __launch_bounds__(256) void anchor_prefilter_kernel(
 
 // ---------------------------------------------------------------- 3DGS bwd
 // One lane per Gaussian, looping over cameras: deterministic accumulation.
-// 3 waves per SIMD (<= 168 VGPRs, a few spills): 0.079 -> 0.071 ms at 2M Gaussians; 4 spills heavily
+// 3 waves per SIMD (<= 168 VGPRs, a few spills): 0.079 -> 0.071 ms at 2M Gaussians; 4 spills heavily.
+// Branch-free camera loop with every load of a camera consumed at one point: 0.071 -> 0.059-0.066 ms
+// (the same for project3d_fwd / project2d_bwd measured no change)
 __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
     int C, int N, const float* __restrict__ means, const float4* __restrict__ quats,
     const float* __restrict__ scales, const float* __restrict__ viewmats,
@@ -267,20 +269,41 @@ __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
     float vm_acc[3] = {0.f, 0.f, 0.f};
     float vs_acc[3] = {0.f, 0.f, 0.f};
     float4 vq_acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    bool any = false;
-    Mat3 Rq, cov;
+    // branch-free camera loop: every load of a camera is issued together and consumed at
+    // one point (one memory round trip per camera -- camera 0's together with the
+    // Gaussian's own -- instead of a radius load, a branch and then the rest in three
+    // waits); a culled pair's contributions are computed from whatever it holds and
+    // selected away
+    int32_t rad;
+    float3 cn, vcn;
+    float2 vm2;
+    float vdep;
+    auto load_cam = [&](int64_t o) {
+        rad = radii[o];
+        cn = ld3(conics + o * 3);
+        vcn = ld3(v_conics + o * 3);
+        vm2 = v_means2d[o];
+        vdep = v_depths[o];
+    };
+#define HGSR_CAM_READY asm volatile("" ::"v"(rad), "v"(cn.x), "v"(cn.y), "v"(cn.z), "v"(vcn.x), "v"(vcn.y), \
+                                    "v"(vcn.z), "v"(vm2.x), "v"(vm2.y), "v"(vdep))
+    load_cam(g);
+    HGSR_CAM_READY;
+    asm volatile("" ::"v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w), "v"(s3.x),
+                 "v"(s3.y), "v"(s3.z));
+    Mat3 Rq;
+    const Mat3 cov = covar_from_qs(q, s3, Rq);
     for (int c = 0; c < C; ++c) {
-        const int64_t o = (int64_t)c * N + g;
-        if (radii[o] <= 0) continue;
-        if (!any) {
-            cov = covar_from_qs(q, s3, Rq);
-            any = true;
+        if (c > 0) {
+            load_cam((int64_t)c * N + g);
+            HGSR_CAM_READY;
         }
+#undef HGSR_CAM_READY
+        const bool live = rad > 0;
         const View v = load_view(viewmats + c * 16, Ks + c * 9);
         const Lims L = make_lims(v, W, H);
-        const float Ci[2][2] = {{conics[o * 3], conics[o * 3 + 1]}, {conics[o * 3 + 1], conics[o * 3 + 2]}};
-        const float vCi[2][2] = {{v_conics[o * 3], 0.5f * v_conics[o * 3 + 1]},
-                                 {0.5f * v_conics[o * 3 + 1], v_conics[o * 3 + 2]}};
+        const float Ci[2][2] = {{cn.x, cn.y}, {cn.y, cn.z}};
+        const float vCi[2][2] = {{vcn.x, 0.5f * vcn.y}, {0.5f * vcn.y, vcn.z}};
         float T1[2][2], vc2[2][2];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -323,7 +346,6 @@ __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
                     for (int k = 0; k < 3; ++k) acc += (vc2[a][b2] + vc2[b2][a]) * J[b2][k] * covc.m[k][j];
                 vJ[a][j] = acc;
             }
-        const float2 vm2 = v_means2d[o];
         float vmc[3];
         vmc[0] = v.fx * rz * vm2.x;
         vmc[1] = v.fy * rz * vm2.y;
@@ -341,9 +363,12 @@ __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
         } else {
             vmc[2] += v.fy * ty * rz3 * vJ[1][2];
         }
-        vmc[2] += v_depths[o];
+        vmc[2] += vdep;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) vm_acc[j] += v.R.m[0][j] * vmc[0] + v.R.m[1][j] * vmc[1] + v.R.m[2][j] * vmc[2];
+        for (int j = 0; j < 3; ++j) {
+            const float d = v.R.m[0][j] * vmc[0] + v.R.m[1][j] * vmc[1] + v.R.m[2][j] * vmc[2];
+            vm_acc[j] += live ? d : 0.f;
+        }
         const Mat3 vcov = mm3(mm3_at(v.R, vcovc), v.R);
         Mat3 Mm, vsym;
 #pragma unroll
@@ -360,9 +385,15 @@ __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
 #pragma unroll
             for (int j = 0; j < 3; ++j) vRq.m[i][j] = vM.m[i][j] * s[j];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) vs_acc[j] += Rq.m[0][j] * vM.m[0][j] + Rq.m[1][j] * vM.m[1][j] + Rq.m[2][j] * vM.m[2][j];
+        for (int j = 0; j < 3; ++j) {
+            const float d = Rq.m[0][j] * vM.m[0][j] + Rq.m[1][j] * vM.m[1][j] + Rq.m[2][j] * vM.m[2][j];
+            vs_acc[j] += live ? d : 0.f;
+        }
         const float4 vq = quat_to_rotmat_vjp(q, vRq);
-        vq_acc.x += vq.x; vq_acc.y += vq.y; vq_acc.z += vq.z; vq_acc.w += vq.w;
+        vq_acc.x += live ? vq.x : 0.f;
+        vq_acc.y += live ? vq.y : 0.f;
+        vq_acc.z += live ? vq.z : 0.f;
+        vq_acc.w += live ? vq.w : 0.f;
     }
     // overwrite semantics: a Gaussian culled in every camera gets zeros
 #pragma unroll
