@@ -219,7 +219,10 @@ __global__ __launch_bounds__(256, 3) void loss_fwd_kernel(int C, int H, int W, I
                                                        float* __restrict__ dmaps, float* __restrict__ partials) {
     __shared__ LossFwdSmem sm;
     const int tiles_x = (W + kLT - 1) / kLT;
-    const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
+    // logical tile = XCD-contiguous remap of the dispatch index: the tiles of one XCD are a band
+    // of neighbours, so the 5-px halos they share are L2 hits of that XCD, not HBM re-reads
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int bx = blk % tiles_x, by = blk / tiles_x;
     const int x0 = bx * kLT - kLR, y0 = by * kLT - kLR;
     const int64_t HW = (int64_t)H * W;
     const int tid = threadIdx.x;
@@ -260,7 +263,7 @@ __global__ __launch_bounds__(256, 3) void loss_fwd_kernel(int C, int H, int W, I
     float dreg = 0.f;
     if (sr.s) {
         const int64_t per = (sr.n + gridDim.x - 1) / gridDim.x;
-        const int64_t g0 = (int64_t)blockIdx.x * per, g1 = min(sr.n, g0 + per);
+        const int64_t g0 = (int64_t)blk * per, g1 = min(sr.n, g0 + per);
         for (int64_t g = g0 + tid; g < g1; g += 256) dreg += row_prod(sr.s + g * sr.k, sr.k);
     }
     const int tx = tid & (kLT - 1), qd = tid / kLT;  // vertical pass: column, row quad
@@ -314,13 +317,13 @@ __global__ __launch_bounds__(256, 3) void loss_fwd_kernel(int C, int H, int W, I
     for (int q = 0; q < 3; ++q) aux[q] = block_sum(aux[q], sm.red);
     if (tid == 0) {
         const int64_t nt = gridDim.x;
-        partials[blockIdx.x] = l1;
-        partials[nt + blockIdx.x] = ss;
-        partials[2 * nt + blockIdx.x] = sky;
-        partials[3 * nt + blockIdx.x] = ent;
-        partials[4 * nt + blockIdx.x] = dreg;
+        partials[blk] = l1;
+        partials[nt + blk] = ss;
+        partials[2 * nt + blk] = sky;
+        partials[3 * nt + blk] = ent;
+        partials[4 * nt + blk] = dreg;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) partials[(5 + q) * nt + blockIdx.x] = aux[q];
+        for (int q = 0; q < 3; ++q) partials[(5 + q) * nt + blk] = aux[q];
     }
 }
 
@@ -451,7 +454,8 @@ __global__ __launch_bounds__(256, 3) void loss_bwd_kernel(int C, int H, int W, I
     __shared__ LossBwdSmem sm;
     const int tid = threadIdx.x;
     const int tiles_x = (W + kLT - 1) / kLT;
-    const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);  // as in loss_fwd_kernel
+    const int bx = blk % tiles_x, by = blk / tiles_x;
     const int x0 = bx * kLT - kLR, y0 = by * kLT - kLR;
     const int64_t HW = (int64_t)H * W;
     const int tx = tid & (kLT - 1), qd = tid / kLT;
@@ -493,7 +497,7 @@ __global__ __launch_bounds__(256, 3) void loss_bwd_kernel(int C, int H, int W, I
     }
     if (g_scaling) {  // d mean_i prod_j s_ij / d s_ij = prod_{l != j} s_il / n
         const int64_t per = (sr.n + gridDim.x - 1) / gridDim.x;
-        const int64_t g0 = (int64_t)blockIdx.x * per, g1 = min(sr.n, g0 + per);
+        const int64_t g0 = (int64_t)blk * per, g1 = min(sr.n, g0 + per);
         for (int64_t g = g0 + tid; g < g1; g += 256) {
             const float* s = sr.s + g * sr.k;
             for (int j = 0; j < sr.k; ++j) {
