@@ -1,7 +1,7 @@
 // K16: densification on device.
 //
-//  * training_statis   <- scene/basic_model.py:96-144: one lane per visible anchor walks
-//                         its n_offsets slots in order (deterministic, no atomics): opacity
+//  * training_statis   <- scene/basic_model.py:96-144: one lane per (visible anchor, slot),
+//                         whole anchors per workgroup (deterministic, no atomics): opacity
 //                         mean/max per anchor, visit count, per-slot grad-norm / radius /
 //                         opacity / denominator updates for the selected, visible slots;
 //  * voxel dedup       <- scene/basic_model.py:179-190 get_remove_duplicates: the O(M*A)
@@ -37,64 +37,58 @@ struct StatisState {
     float* offset_opacity_accum;   // [A*noff] (max mode)
 };
 
-// One lane per visible anchor, its slots unrolled (noff <= kStatMaxOff) so that every
-// memory access of a level is issued for all slots before any is used: the selection
-// bytes and ranks, then the Gaussian gathers and the old accumulator values, then the
-// stores -- three exposed latencies per anchor instead of ~4 per slot.  Each slot's
-// accumulators are written by exactly one lane (deterministic).
+// One lane per (visible anchor, slot): a workgroup holds kStatAnch whole anchors (kStatAnch *
+// n_offsets lanes), so the selection bytes / ranks, the Gaussian gathers and the per-slot
+// accumulators are read and written by consecutive lanes (a lane per anchor walking its
+// slots touched every cache line n_offsets times).  Each slot's accumulators are written by
+// exactly one lane; the per-anchor opacity sum and count go through LDS and are formed by the
+// anchor's slot-0 lane in slot order (the arithmetic of a sequential walk: deterministic).
 constexpr int kStatMaxOff = 16;
-__global__ __launch_bounds__(256) void training_statis_kernel(int Av, int noff, float half_w, float half_h,
-                                                              int pruning_max, int growing_max, StatisIn in,
-                                                              StatisState st) {
-    const int a = blockIdx.x * 256 + threadIdx.x;
-    if (a >= Av) return;
-    const int64_t id = in.vis_idx[a];
-    bool sel[kStatMaxOff];
-    int64_t m[kStatMaxOff];
-#pragma unroll
-    for (int k = 0; k < kStatMaxOff; ++k) {
-        const int64_t j = (int64_t)a * noff + k;
-        sel[k] = k < noff && in.sel[j];
-        m[k] = k < noff ? in.sel_rank[j] : 0;
+constexpr int kStatAnch = 32;  // anchors per workgroup (<= 512 lanes)
+__global__ __launch_bounds__(kStatAnch * kStatMaxOff) void training_statis_kernel(
+    int Av, int noff, float half_w, float half_h, int pruning_max, int growing_max, StatisIn in, StatisState st) {
+    __shared__ float s_o[kStatAnch * kStatMaxOff];
+    __shared__ uint8_t s_sel[kStatAnch * kStatMaxOff];
+    const int t = threadIdx.x, la = t / noff, k = t - la * noff;
+    const int a = blockIdx.x * kStatAnch + la;
+    const bool lane_ok = la < kStatAnch && a < Av;
+    const int64_t j = (int64_t)a * noff + k;
+    const int64_t id = lane_ok ? in.vis_idx[a] : 0;
+    const bool sel = lane_ok && in.sel[j];
+    const int64_t mk = sel ? in.sel_rank[j] : 0;
+    const int64_t gslot = id * noff + k;
+    const float o = sel ? in.opacity[mk] : 0.f;
+    const bool flt = sel && in.filt[mk];
+    const float gx = flt ? in.grad[mk * 2] : 0.f, gy = flt ? in.grad[mk * 2 + 1] : 0.f;
+    const float acc = flt ? st.offset_gradient_accum[gslot] : 0.f;
+    const float den = flt ? st.offset_denom[gslot] : 0.f;
+    const float mr = (flt && growing_max) ? st.max_radii2D[gslot] : 0.f;
+    const float oa = (flt && growing_max) ? st.offset_opacity_accum[gslot] : 0.f;
+    const float rad = (flt && growing_max) ? (float)in.radii[mk] : 0.f;
+    if (flt) {
+        // grad[:, 0] *= W/2, grad[:, 1] *= H/2, then the 2-norm (basic_model.py:128-131)
+        const float sx = gx * half_w, sy = gy * half_h;
+        const float gn = sqrtf(sx * sx + sy * sy);
+        if (growing_max) {
+            st.offset_gradient_accum[gslot] = fmaxf(acc, fabsf(gn));
+            st.max_radii2D[gslot] = fmaxf(mr, rad);
+            st.offset_opacity_accum[gslot] = oa + o;
+        } else {
+            st.offset_gradient_accum[gslot] = acc + gn;
+        }
+        st.offset_denom[gslot] = den + 1.f;
     }
-    float o[kStatMaxOff], gx[kStatMaxOff], gy[kStatMaxOff], acc[kStatMaxOff], den[kStatMaxOff];
-    float mr[kStatMaxOff], oa[kStatMaxOff], rad[kStatMaxOff];
-    bool flt[kStatMaxOff];
-#pragma unroll
-    for (int k = 0; k < kStatMaxOff; ++k) {
-        const int64_t mk = sel[k] ? m[k] : 0;
-        const int64_t gslot = id * noff + k;
-        o[k] = sel[k] ? in.opacity[mk] : 0.f;
-        flt[k] = sel[k] && in.filt[mk];
-        gx[k] = flt[k] ? in.grad[mk * 2] : 0.f;
-        gy[k] = flt[k] ? in.grad[mk * 2 + 1] : 0.f;
-        acc[k] = flt[k] ? st.offset_gradient_accum[gslot] : 0.f;
-        den[k] = flt[k] ? st.offset_denom[gslot] : 0.f;
-        mr[k] = (flt[k] && growing_max) ? st.max_radii2D[gslot] : 0.f;
-        oa[k] = (flt[k] && growing_max) ? st.offset_opacity_accum[gslot] : 0.f;
-        rad[k] = (flt[k] && growing_max) ? (float)in.radii[mk] : 0.f;
-    }
+    s_o[t] = o;
+    s_sel[t] = sel;
+    __syncthreads();
+    if (!lane_ok || k != 0) return;
     const float a_old = st.anchor_opacity_accum[id], d_old = st.anchor_demon[id];
     float osum = 0.f;
     int cnt = 0;
-#pragma unroll
-    for (int k = 0; k < kStatMaxOff; ++k) {
-        if (!sel[k]) continue;
-        osum += o[k];
+    for (int q = 0; q < noff; ++q) {
+        if (!s_sel[t + q]) continue;
+        osum += s_o[t + q];
         ++cnt;
-        if (!flt[k]) continue;
-        const int64_t gslot = id * noff + k;
-        // grad[:, 0] *= W/2, grad[:, 1] *= H/2, then the 2-norm (basic_model.py:128-131)
-        const float sx = gx[k] * half_w, sy = gy[k] * half_h;
-        const float gn = sqrtf(sx * sx + sy * sy);
-        if (growing_max) {
-            st.offset_gradient_accum[gslot] = fmaxf(acc[k], fabsf(gn));
-            st.max_radii2D[gslot] = fmaxf(mr[k], rad[k]);
-            st.offset_opacity_accum[gslot] = oa[k] + o[k];
-        } else {
-            st.offset_gradient_accum[gslot] = acc[k] + gn;
-        }
-        st.offset_denom[gslot] = den[k] + 1.f;
     }
     if (pruning_max) {
         st.anchor_opacity_accum[id] = fmaxf(a_old, fabsf(osum));
@@ -273,8 +267,9 @@ extern "C" int hgsr_training_statis(int Av, int n_offsets, int width, int height
     const StatisState st{anchor_opacity_accum, anchor_demon, offset_gradient_accum, offset_denom, max_radii2D,
                          offset_opacity_accum};
     KernelTimer kt("training_statis", as_stream(stream));
-    hipLaunchKernelGGL(training_statis_kernel, dim3(blocks_for(Av)), dim3(256), 0, as_stream(stream), Av, n_offsets,
-                       0.5f * (float)width, 0.5f * (float)height, pruning_max, growing_max, in, st);
+    hipLaunchKernelGGL(training_statis_kernel, dim3((Av + kStatAnch - 1) / kStatAnch), dim3(kStatAnch * n_offsets), 0,
+                       as_stream(stream), Av, n_offsets, 0.5f * (float)width, 0.5f * (float)height, pruning_max,
+                       growing_max, in, st);
     return check_launch("training_statis");
 }
 
