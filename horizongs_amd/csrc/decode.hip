@@ -327,7 +327,7 @@ struct DecodeOut {
     int32_t* slot_row;  // [Av*noff] output row or -1 (kept for the backward)
 };
 
-template <int KSTEPS, int W2R>
+template <int KSTEPS, int W2R, bool COLOR = true>
 __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs mp,
                                                          const int32_t* __restrict__ vis_idx,
                                                          const float* __restrict__ anchor,
@@ -337,7 +337,8 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
                                                          const float* __restrict__ cam,
                                                          const int32_t* __restrict__ tile_off, DecodeOut out) {
     __shared__ DecodeSmem<96, W2R, 80> sm;
-    stage_weights(sm, mp, d, 96, d.rows);
+    // without the colour head (decode_color_kernel writes it) only the opacity and cov rows
+    stage_weights(sm, mp, d, 96, COLOR ? d.rows : d.row0[2]);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
     const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
     const int noff = d.noff, cd = d.cd;
@@ -396,7 +397,6 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
         // hidden layer of the cov and colour heads
         const float* sx = sm.x[wave];
         const f32x4 hc0 = layer1_tile<KSTEPS>(sm, sx, 2), hc1 = layer1_tile<KSTEPS>(sm, sx, 3);
-        const f32x4 hl0 = layer1_tile<KSTEPS>(sm, sx, 4), hl1 = layer1_tile<KSTEPS>(sm, sx, 5);
         // cov head -> LDS, then scaling / rotation / position per kept slot
         float* syw = sm.y[wave];
         for (int ot = 0; ot < d.T[1]; ++ot) {
@@ -431,7 +431,9 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
                 out.xyz[(int64_t)p * 3 + q] = anc[it][q] + o;
             }
         }
+        if (!COLOR) continue;
         // colour head straight from the accumulators (linear output)
+        const f32x4 hl0 = layer1_tile<KSTEPS>(sm, sx, 4), hl1 = layer1_tile<KSTEPS>(sm, sx, 5);
         for (int ot = 0; ot < d.T[2]; ++ot) {
             const f32x4 y = layer2_tile(sm, d.row0[2] + ot * 16, hl0, hl1);
             if (a0 + i >= d.Av) continue;
@@ -447,10 +449,86 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
     }
 }
 
-// ---------------------------------------------------------------- backward
 // wave-level LDS ordering point: all of this wave's LDS operations have completed and the
 // compiler may not move memory operations across it (no workgroup barrier)
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Colour head alone, for models whose second layer exceeds the 128-row plan (SH colour
+// heads: 27 x 10 outputs).  With every head's W2 in LDS the fused forward fits one workgroup
+// per CU; split, the fused pass (opacity + cov, 128 rows) and this pass (the colour head's W1
+// and W2 only, 61 KB) run two each.  The output rows of the kept slots come from slot_row,
+// which the fused pass wrote; X rows are prefetched one tile ahead as there.
+constexpr int kDecColRows = 272;  // colour W2 rows of this pass (17 tiles: SH2 x 10 offsets)
+struct DecodeColorSmem {
+    float w1[32 * kDecS];
+    float b1[32];
+    float w2[kDecColRows * kDecS];
+    float b2[kDecColRows];
+    float x[4][16 * kDecS];
+    int pos[4][16 * 16];
+};
+
+template <int KSTEPS>
+__global__ __launch_bounds__(256) void decode_color_kernel(DecodeDims d, MlpPtrs mp,
+                                                           const int32_t* __restrict__ vis_idx,
+                                                           const float* __restrict__ anchor,
+                                                           const float* __restrict__ feat,
+                                                           const float* __restrict__ cam,
+                                                           const int32_t* __restrict__ slot_row,
+                                                           float* __restrict__ color) {
+    __shared__ DecodeColorSmem sm;
+    const int K1 = kDecF + d.vd, O = d.O[2], rows = d.T[2] * 16;
+    for (int e = threadIdx.x; e < 32 * kDecS; e += 256) {
+        const int h = e / kDecS, k = e - h * kDecS;
+        sm.w1[e] = k < K1 ? mp.w1[2][h * K1 + k] : 0.f;
+    }
+    if (threadIdx.x < 32) sm.b1[threadIdx.x] = mp.b1[2][threadIdx.x];
+    for (int e = threadIdx.x; e < rows * kDecF; e += 256) {
+        const int row = e / kDecF, h = e - row * kDecF;
+        sm.w2[row * kDecS + w2_col(h)] = row < O ? mp.w2[2][row * kDecF + h] : 0.f;
+    }
+    for (int row = threadIdx.x; row < rows; row += 256) sm.b2[row] = row < O ? mp.b2[2][row] : 0.f;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
+    const int noff = d.noff, cd = d.cd;
+    XPrefetch px;
+    if (blockIdx.x < (unsigned)n_tiles) {
+        x_issue_id(px, vis_idx, blockIdx.x * kDecTile + wave * 16, d.Av);
+        x_issue_data(px, feat, anchor, d.vd);
+    }
+    __syncthreads();  // weights staged
+    float* sx = sm.x[wave];
+    int* pos = sm.pos[wave];
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        wave_lds_sync();  // this wave's previous tile is done with its x / pos arrays
+        const int a0 = t * kDecTile + wave * 16;
+        float ov[3], dist;
+        x_store(px, sx, d.vd, cam, ov, dist);
+        for (int sl = lane; sl < 16 * noff; sl += 64) {
+            const int a = sl / noff;
+            pos[sl] = a0 + a < d.Av ? slot_row[(int64_t)a0 * noff + sl] : -1;
+        }
+        const int tn = t + gridDim.x;
+        if (tn < n_tiles) x_issue_id(px, vis_idx, tn * kDecTile + wave * 16, d.Av);
+        wave_lds_sync();
+        const f32x4 h0 = layer1_tile<KSTEPS>(sm, sx, 0), h1 = layer1_tile<KSTEPS>(sm, sx, 1);
+        if (tn < n_tiles) x_issue_data(px, feat, anchor, d.vd);
+        for (int ot = 0; ot < d.T[2]; ++ot) {
+            const f32x4 y = layer2_tile(sm, ot * 16, h0, h1);
+            if (a0 + i >= d.Av) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int o = ot * 16 + 4 * g + r;
+                if (o >= cd * noff) continue;
+                const int k = o / cd;
+                const int p = pos[i * noff + k];
+                if (p >= 0) color[(int64_t)p * cd + (o - k * cd)] = y[r];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- backward
 
 // Developer instrumentation (variant builds with -DHGSR_DECODE_PROF only): per-head, per-phase
 // shader-clock totals of the backward; every boundary drains the wave's memory counters so a
@@ -1050,10 +1128,26 @@ extern "C" int hgsr_decode_fwd(int Av, int F, int view_dim, int n_offsets, int c
 #define LAUNCH_DF(KS, R)                                                                                      \
     hipLaunchKernelGGL((decode_fwd_kernel<KS, R>), dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor, \
                        feat, offset, scaling_raw, cam_center, off, out)
-    // LDS sized to the model: RGB heads fit 128 second-layer rows (2 workgroups per CU)
+    // LDS sized to the model: RGB heads fit 128 second-layer rows (2 workgroups per CU); an SH
+    // colour head of up to 272 rows runs as its own pass after the opacity / cov pass (2
+    // workgroups per CU each instead of 1 for all 368 rows at once)
     if (d.rows <= 128) {
         if (view_dim == 3) LAUNCH_DF(9, 128);
         else LAUNCH_DF(8, 128);
+    } else if (d.row0[2] <= 128 && d.T[2] * 16 <= kDecColRows) {
+        if (view_dim == 3)
+            hipLaunchKernelGGL((decode_fwd_kernel<9, 128, false>), dim3(decode_grid(Av)), dim3(256), 0, s, d, mp,
+                               vis_idx, anchor, feat, offset, scaling_raw, cam_center, off, out);
+        else
+            hipLaunchKernelGGL((decode_fwd_kernel<8, 128, false>), dim3(decode_grid(Av)), dim3(256), 0, s, d, mp,
+                               vis_idx, anchor, feat, offset, scaling_raw, cam_center, off, out);
+        if (int st = check_launch("decode_fwd")) return st;
+        if (view_dim == 3)
+            hipLaunchKernelGGL(decode_color_kernel<9>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
+                               feat, cam_center, slot_row, color);
+        else
+            hipLaunchKernelGGL(decode_color_kernel<8>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
+                               feat, cam_center, slot_row, color);
     } else {
         if (view_dim == 3) LAUNCH_DF(9, kDecMaxRows);
         else LAUNCH_DF(8, kDecMaxRows);
