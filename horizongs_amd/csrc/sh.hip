@@ -136,6 +136,113 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int K, int64_t n, const flo
     v_dirs[i * 3 + 2] += (gu2 - dot * uz) * inv;
 }
 
+// rasterization()'s SH colours in one pass each way (gsplat rendering: dirs = means - campos,
+// colors = spherical_harmonics(dirs, coeffs, masks = radii > 0), clamp_min(colors + 0.5, 0)):
+// no dirs tensor, no elementwise offset / clamp kernels and no clamp mask in the backward,
+// whose v_means (= v_dirs) is written directly.  Lane per Gaussian, cameras in a loop
+// (deterministic sums over cameras for shared coefficients).
+template <int DEG>
+__device__ __forceinline__ bool sh_rgb_eval(int K, const float* __restrict__ m, const float* __restrict__ cp,
+                                            const float* __restrict__ c, bool on, float (&u)[3], float& inv,
+                                            float (&b)[(DEG + 1) * (DEG + 1)], float (&r)[3]) {
+    constexpr int NB = (DEG + 1) * (DEG + 1);
+    r[0] = r[1] = r[2] = 0.f;
+    if (!on) return false;
+    const float x = m[0] - cp[0], y = m[1] - cp[1], z = m[2] - cp[2];
+    inv = 1.0f / sqrtf(x * x + y * y + z * z);
+    u[0] = x * inv, u[1] = y * inv, u[2] = z * inv;
+    sh_basis<DEG>(u[0], u[1], u[2], b);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        r[0] += b[k] * c[k * 3 + 0];
+        r[1] += b[k] * c[k * 3 + 1];
+        r[2] += b[k] * c[k * 3 + 2];
+    }
+    return true;
+}
+
+template <int DEG>
+__global__ __launch_bounds__(256) void sh_rgb_fwd_kernel(int C, int N, int K, const float* __restrict__ means,
+                                                         const float* __restrict__ campos,
+                                                         const float* __restrict__ coeffs, int shared,
+                                                         const int32_t* __restrict__ radii,
+                                                         float* __restrict__ colors) {
+    constexpr int NB = (DEG + 1) * (DEG + 1);
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= N) return;
+    for (int c = 0; c < C; ++c) {
+        const int64_t i = (int64_t)c * N + g;
+        float u[3], inv, b[NB], r[3];
+        sh_rgb_eval<DEG>(K, means + (int64_t)g * 3, campos + c * 3, coeffs + (shared ? g : i) * K * 3,
+                         radii[i] > 0, u, inv, b, r);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) colors[i * 3 + q] = fmaxf(r[q] + 0.5f, 0.0f);
+    }
+}
+
+template <int DEG>
+__global__ __launch_bounds__(256) void sh_rgb_bwd_kernel(int C, int N, int K, const float* __restrict__ means,
+                                                         const float* __restrict__ campos,
+                                                         const float* __restrict__ coeffs, int shared,
+                                                         const int32_t* __restrict__ radii,
+                                                         const float* __restrict__ v_colors,
+                                                         float* __restrict__ v_coeffs, float* __restrict__ v_means) {
+    constexpr int NB = (DEG + 1) * (DEG + 1);
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= N) return;
+    float vm[3] = {0.f, 0.f, 0.f};
+    float vsum[NB * 3];  // shared coefficients: summed over cameras
+#pragma unroll
+    for (int k = 0; k < NB * 3; ++k) vsum[k] = 0.f;
+    for (int c = 0; c < C; ++c) {
+        const int64_t i = (int64_t)c * N + g;
+        const float* cf = coeffs + (shared ? g : i) * K * 3;
+        float u[3], inv, b[NB], r[3];
+        const bool on = sh_rgb_eval<DEG>(K, means + (int64_t)g * 3, campos + c * 3, cf, radii[i] > 0, u, inv, b, r);
+        // clamp_min backward: the gradient passes where colour + 0.5 >= 0
+        float gq[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) gq[q] = (on && r[q] + 0.5f >= 0.0f) ? v_colors[i * 3 + q] : 0.f;
+        if (shared) {
+#pragma unroll
+            for (int k = 0; k < NB; ++k)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) vsum[k * 3 + q] += b[k] * gq[q];
+        } else {
+            float* vc = v_coeffs + i * K * 3;
+#pragma unroll
+            for (int k = 0; k < NB; ++k)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) vc[k * 3 + q] = on ? b[k] * gq[q] : 0.f;
+            for (int k = NB * 3; k < K * 3; ++k) vc[k] = 0.f;
+        }
+        if (DEG < 1 || !on || !v_means) continue;
+        float bx[NB], by[NB], bz[NB];
+        sh_basis_grad<DEG>(u[0], u[1], u[2], bx, by, bz);
+        float gu0 = 0.f, gu1 = 0.f, gu2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const float vb = cf[k * 3] * gq[0] + cf[k * 3 + 1] * gq[1] + cf[k * 3 + 2] * gq[2];
+            gu0 += vb * bx[k];
+            gu1 += vb * by[k];
+            gu2 += vb * bz[k];
+        }
+        const float dot = gu0 * u[0] + gu1 * u[1] + gu2 * u[2];
+        vm[0] += (gu0 - dot * u[0]) * inv;
+        vm[1] += (gu1 - dot * u[1]) * inv;
+        vm[2] += (gu2 - dot * u[2]) * inv;
+    }
+    if (shared) {
+        float* vc = v_coeffs + (int64_t)g * K * 3;
+#pragma unroll
+        for (int k = 0; k < NB * 3; ++k) vc[k] = vsum[k];
+        for (int k = NB * 3; k < K * 3; ++k) vc[k] = 0.f;
+    }
+    if (v_means)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) v_means[(int64_t)g * 3 + q] = vm[q];
+}
+
 }  // namespace hgsr
 
 using namespace hgsr;
@@ -175,4 +282,50 @@ extern "C" int hgsr_sh_bwd(int degree, int K, int64_t n, const float* dirs, cons
         default: hipLaunchKernelGGL(sh_bwd_kernel<3>, grid, dim3(256), 0, s, K, n, dirs, coeffs, masks, v_colors, v_coeffs, v_dirs); break;
     }
     return check_launch("sh_bwd");
+}
+
+extern "C" int hgsr_sh_rgb_fwd(int degree, int C, int N, int K, const float* means, const float* campos,
+                               const float* coeffs, int shared, const int32_t* radii, float* colors,
+                               hgsr_stream_t stream) {
+    HGSR_REQUIRE(degree >= 0 && degree <= 3, "sh degree %d unsupported (0..3)", degree);
+    HGSR_REQUIRE(K >= (degree + 1) * (degree + 1), "K=%d too small for degree %d", K, degree);
+    HGSR_REQUIRE(C >= 1 && N >= 0, "bad dims C=%d N=%d", C, N);
+    if (N == 0) return HGSR_OK;
+    HGSR_REQUIRE(means && campos && coeffs && radii && colors, "null pointer");
+    dim3 grid((unsigned)((N + 255) / 256));
+    hipStream_t s = as_stream(stream);
+    KernelTimer kt("sh_fwd", s);
+#define SH_RGB_F(D) hipLaunchKernelGGL(sh_rgb_fwd_kernel<D>, grid, dim3(256), 0, s, C, N, K, means, campos, coeffs, \
+                                       shared, radii, colors)
+    switch (degree) {
+        case 0: SH_RGB_F(0); break;
+        case 1: SH_RGB_F(1); break;
+        case 2: SH_RGB_F(2); break;
+        default: SH_RGB_F(3); break;
+    }
+#undef SH_RGB_F
+    return check_launch("sh_rgb_fwd");
+}
+
+extern "C" int hgsr_sh_rgb_bwd(int degree, int C, int N, int K, const float* means, const float* campos,
+                               const float* coeffs, int shared, const int32_t* radii, const float* v_colors,
+                               float* v_coeffs, float* v_means, hgsr_stream_t stream) {
+    HGSR_REQUIRE(degree >= 0 && degree <= 3, "sh degree %d unsupported (0..3)", degree);
+    HGSR_REQUIRE(K >= (degree + 1) * (degree + 1), "K=%d too small for degree %d", K, degree);
+    HGSR_REQUIRE(C >= 1 && N >= 0, "bad dims C=%d N=%d", C, N);
+    if (N == 0) return HGSR_OK;
+    HGSR_REQUIRE(means && campos && coeffs && radii && v_colors && v_coeffs, "null pointer");
+    dim3 grid((unsigned)((N + 255) / 256));
+    hipStream_t s = as_stream(stream);
+    KernelTimer kt("sh_bwd", s);
+#define SH_RGB_B(D) hipLaunchKernelGGL(sh_rgb_bwd_kernel<D>, grid, dim3(256), 0, s, C, N, K, means, campos, coeffs, \
+                                       shared, radii, v_colors, v_coeffs, v_means)
+    switch (degree) {
+        case 0: SH_RGB_B(0); break;
+        case 1: SH_RGB_B(1); break;
+        case 2: SH_RGB_B(2); break;
+        default: SH_RGB_B(3); break;
+    }
+#undef SH_RGB_B
+    return check_launch("sh_rgb_bwd");
 }

@@ -196,6 +196,34 @@ class _SH(torch.autograd.Function):
         return None, v_dirs, v_coeffs, None
 
 
+class _SHColors(torch.autograd.Function):
+    """rasterization()'s SH colour path (dirs = means - campos, masked SH evaluation,
+    clamp_min(+0.5, 0)) as one native call each way: hgsr_sh_rgb_{fwd,bwd}."""
+
+    @staticmethod
+    def forward(ctx, degree, means, campos, coeffs, radii):
+        C, Ng = radii.shape
+        K = coeffs.shape[-2]
+        shared = coeffs.dim() == 3
+        colors = torch.empty((C, Ng, 3), dtype=torch.float32, device=means.device)
+        N.call("hgsr_sh_rgb_fwd", degree, C, Ng, K, ptr(means), ptr(campos), ptr(coeffs), int(shared), ptr(radii),
+               ptr(colors), N.stream(means.device))
+        ctx.save_for_backward(means, campos, coeffs, radii)
+        ctx.degree = degree
+        return colors
+
+    @staticmethod
+    def backward(ctx, v_colors):
+        means, campos, coeffs, radii = ctx.saved_tensors
+        C, Ng = radii.shape
+        v_coeffs = torch.empty_like(coeffs)
+        v_means = torch.empty_like(means) if ctx.needs_input_grad[1] else None
+        vc = _f32(v_colors)
+        N.call("hgsr_sh_rgb_bwd", ctx.degree, C, Ng, coeffs.shape[-2], ptr(means), ptr(campos), ptr(coeffs),
+               int(coeffs.dim() == 3), ptr(radii), ptr(vc), ptr(v_coeffs), ptr(v_means), N.stream(means.device))
+        return None, v_means, None, v_coeffs, None
+
+
 def spherical_harmonics(degrees_to_use: int, dirs: torch.Tensor, coeffs: torch.Tensor,
                         masks: Optional[torch.Tensor] = None) -> torch.Tensor:
     """gsplat spherical_harmonics: dirs [..., 3], coeffs [..., K, 3] -> colors [..., 3] (degree <= 3)."""
@@ -206,7 +234,11 @@ def spherical_harmonics(degrees_to_use: int, dirs: torch.Tensor, coeffs: torch.T
     batch = dirs.shape[:-1]
     d = _f32(dirs.reshape(-1, 3))
     c = _f32(coeffs.reshape(-1, K, 3))
-    m = None if masks is None else masks.reshape(-1).to(torch.uint8).contiguous()
+    if masks is None:
+        m = None
+    else:  # bool -> uint8 is a free view (same bytes), any other dtype a converting copy
+        m = masks.reshape(-1).contiguous()
+        m = m.view(torch.uint8) if m.dtype == torch.bool else m.to(torch.uint8)
     out = _SH.apply(int(degrees_to_use), d, c, m)
     return out.reshape(batch + (3,))
 
@@ -680,11 +712,13 @@ def _colors_for_raster(means, colors, viewmats, radii, sh_degree, C):
     """Colours per raster call: [N,D] (shared over cameras) or [C,N,D]."""
     if sh_degree is None:
         return colors
-    campos = _camera_centers(viewmats)
-    dirs = means[None, :, :] - campos[:, None, :]
-    shs = colors.expand(C, -1, -1, -1) if colors.dim() == 3 else colors
-    out = spherical_harmonics(sh_degree, dirs, shs, masks=radii > 0)
-    return torch.clamp_min(out + 0.5, 0.0)
+    # gsplat: dirs = means - campos, spherical_harmonics(masks = radii > 0), clamp_min(+0.5, 0),
+    # fused into one native call each way (no dirs tensor, no elementwise glue)
+    _check_cuda(means, colors, viewmats)
+    K = colors.shape[-2]
+    assert colors.shape[-1] == 3 and colors.dim() in (3, 4) and (sh_degree + 1) ** 2 <= K, "bad SH coefficients"
+    campos = _f32(_camera_centers(viewmats.detach()))
+    return _SHColors.apply(int(sh_degree), _f32(means), campos, _f32(colors), radii.contiguous())
 
 
 def _with_depth(colors, backgrounds, depths, render_mode, C):

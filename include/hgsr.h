@@ -94,6 +94,19 @@ int hgsr_sh_fwd(int degree, int K, int64_t n, const float* dirs, const float* co
 int hgsr_sh_bwd(int degree, int K, int64_t n, const float* dirs, const float* coeffs,
                 const uint8_t* masks, const float* v_colors, float* v_coeffs, float* v_dirs,
                 hgsr_stream_t stream);
+/* rasterization()'s colour path for sh_degree != None in one call each way
+ * (gsplat rendering.py as HorizonGS calls it from gaussian_renderer/render.py:40-54:
+ * dirs = means - campos[c]; colors = spherical_harmonics(sh_degree, dirs, coeffs,
+ * masks = radii > 0); colors = clamp_min(colors + 0.5, 0)).  means [N,3], campos [C,3],
+ * coeffs [N,K,3] (shared = 1) or [C,N,K,3], radii [C,N] -> colors [C,N,3] (written).
+ * The backward writes v_coeffs (summed over cameras when shared) and v_means [N,3]
+ * (nullable; overwritten, = the gradient through dirs). */
+int hgsr_sh_rgb_fwd(int degree, int C, int N, int K, const float* means, const float* campos,
+                    const float* coeffs, int shared, const int32_t* radii, float* colors,
+                    hgsr_stream_t stream);
+int hgsr_sh_rgb_bwd(int degree, int C, int N, int K, const float* means, const float* campos,
+                    const float* coeffs, int shared, const int32_t* radii, const float* v_colors,
+                    float* v_coeffs, float* v_means, hgsr_stream_t stream);
 
 /* ---- K5/K6/K7: tile intersection, sort, tile offsets ---------------------
  * Replaces gsplat isect_tiles(sort=True) + cub DeviceRadixSort + isect_offset_encode
