@@ -138,6 +138,42 @@ def test_sh_fwd_bwd(deg):
     grad_close(d.grad.cpu().numpy(), vd_ref, "v_dirs")
 
 
+@pytest.mark.parametrize("deg", [0, 1, 2, 3])
+@pytest.mark.parametrize("C,shared", [(1, True), (2, True), (2, False)])
+def test_sh_rgb_fused(deg, C, shared):
+    """rasterization()'s fused SH colour step (hgsr_sh_rgb_fwd/bwd) against the C oracle's SH
+    on dirs = means - campos per camera, masks = radii > 0, then clamp_min(+0.5, 0) and its
+    gradient mask (gsplat rendering as render.py calls it); shared coefficients sum their
+    gradient over the cameras, v_means sums v_dirs over the cameras."""
+    g = torch.Generator().manual_seed(10 * deg + C + int(shared))
+    n, K = 4000, 16
+    means = torch.randn(n, 3, generator=g) * 2.0
+    campos = torch.randn(C, 3, generator=g) * 0.5 + torch.tensor([0.0, 0.0, -6.0])
+    coeffs = torch.randn(*((n, K, 3) if shared else (C, n, K, 3)), generator=g) * 0.4
+    radii = (torch.rand(C, n, generator=g) > 0.2).to(torch.int32) * 3
+    vo = torch.randn(C, n, 3, generator=g)
+    m, cf = to_dev(means, coeffs)
+    m.requires_grad_(True)
+    cf.requires_grad_(True)
+    cols = G._SHColors.apply(deg, m, campos.to(DEV), cf, radii.to(DEV))
+    (cols * vo.to(DEV)).sum().backward()
+    ref, vc_ref, vm_ref = [], [], np.zeros((n, 3), np.float32)
+    for c in range(C):
+        dirs = (means - campos[c]).numpy()
+        cc = (coeffs if shared else coeffs[c]).numpy()
+        mask = (radii[c] > 0).numpy()
+        pre = O.sh_fwd(deg, dirs, cc, mask) + 0.5
+        ref.append(np.maximum(pre, 0.0))
+        gv = np.where(pre >= 0.0, vo[c].numpy(), 0.0).astype(np.float32)
+        vc, vd = O.sh_bwd(deg, dirs, cc, gv, mask)
+        vc_ref.append(vc)
+        vm_ref += vd
+    close(cols.detach().cpu().numpy(), np.stack(ref), name="fused sh colors")
+    vc_ref = np.sum(vc_ref, axis=0) if shared else np.stack(vc_ref)
+    grad_close(cf.grad.cpu().numpy(), vc_ref, "fused v_coeffs")
+    grad_close(m.grad.cpu().numpy(), vm_ref, "fused v_means")
+
+
 def test_sh_matches_reference_golden():
     import os
     gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "sh_eval.npz"))
