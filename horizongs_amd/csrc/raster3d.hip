@@ -275,7 +275,9 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
 // Backward "input transpose".  Per step a wave composites one Gaussian over its 8x8
 // quadrant (pass 1) and keeps only two numbers per pixel: fac = alpha T (the colour
 // weight) and v_sigma.  Every 4 steps the 4 x 2 registers are transposed across the
-// wave (v_permlane32_swap, v_permlane16_swap) so that lane L = 16 s + r holds step s's
+// wave through LDS (four 8-B writes, two 16-B reads per lane; measured 623-635 -> 585 us
+// at c2 against eight v_permlane32/16_swap, which cost ~3 VALU slots each) so that lane
+// L = 16 s + r holds step s's
 // values for the 4 pixels r + 16 m (m = 0..3) -- one pixel column, rows y0, y0+2, y0+4,
 // y0+6 -- and accumulates the 10 gradient values of that Gaussian over them in
 // registers (pass 2).  With dx constant down a column the sigma moments factor:
@@ -286,10 +288,10 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
 // that the first two levels transpose instead of add).  Two transposed inputs replace
 // the ten reduced outputs of a per-step wave reduction.
 
-// 8 waves / SIMD (64 VGPRs; the register budget costs two spilled values outside the
-// step loop): 0.789 -> 0.776 ms at c2
+// 7 waves / SIMD: the LDS transpose buffer (8 KB per workgroup) allows 7 workgroups per CU;
+// 72 VGPRs (two spilled values outside the step loop)
 #ifndef HGSR_BWD_WAVES_N
-#define HGSR_BWD_WAVES_N 8
+#define HGSR_BWD_WAVES_N 7
 #endif
 #if HGSR_BWD_WAVES_N > 0
 #define HGSR_BWD_WAVES __attribute__((amdgpu_waves_per_eu(HGSR_BWD_WAVES_N, 8)))
@@ -320,6 +322,8 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     __shared__ int32_t s_id[2][NB];
     __shared__ __attribute__((aligned(16))) uint8_t s_list[4][NB];  // read back as 32-bit words
     __shared__ int32_t s_last[4];
+    // pass-1 -> pass-2 transpose through LDS: [step s][column lane r][pixel m][F, V]
+    __shared__ __attribute__((aligned(16))) float s_tp[4][4 * 16 * 4 * 2];
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
@@ -546,20 +550,18 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                 }
                 const float g1x = ABS ? sr.g1[cur][t].x : 0.f;
                 const int sid = s_id[cur][t < NB ? t : 0];
-                // transpose: lane bit 5 <-> register bit 1, lane bit 4 <-> register bit 0
+                {
+                    // lane L = pixel r + 16 m writes (F[s], V[s]) at [s][r][m]; lane 16 s + r reads
+                    // its step's column [s][r][0..3] (a wave's LDS operations complete in order)
+                    float* tp = s_tp[wave];
+                    const int rr = lane & 15, mm = lane >> 4;
 #pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(F[q]), __float_as_uint(F[q + 2]), false, false);
-                    F[q] = __uint_as_float(a[0]); F[q + 2] = __uint_as_float(a[1]);
-                    auto v = __builtin_amdgcn_permlane32_swap(__float_as_uint(V[q]), __float_as_uint(V[q + 2]), false, false);
-                    V[q] = __uint_as_float(v[0]); V[q + 2] = __uint_as_float(v[1]);
-                }
-#pragma unroll
-                for (int q = 0; q < 4; q += 2) {
-                    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(F[q]), __float_as_uint(F[q + 1]), false, false);
-                    F[q] = __uint_as_float(a[0]); F[q + 1] = __uint_as_float(a[1]);
-                    auto v = __builtin_amdgcn_permlane16_swap(__float_as_uint(V[q]), __float_as_uint(V[q + 1]), false, false);
-                    V[q] = __uint_as_float(v[0]); V[q + 1] = __uint_as_float(v[1]);
+                    for (int q = 0; q < 4; ++q)
+                        *reinterpret_cast<float2*>(tp + ((q * 16 + rr) * 4 + mm) * 2) = make_float2(F[q], V[q]);
+                    const float4 lo = *reinterpret_cast<const float4*>(tp + ((slot * 16 + rr) * 4) * 2);
+                    const float4 hi = *reinterpret_cast<const float4*>(tp + ((slot * 16 + rr) * 4) * 2 + 4);
+                    F[0] = lo.x; V[0] = lo.y; F[1] = lo.z; V[1] = lo.w;
+                    F[2] = hi.x; V[2] = hi.y; F[3] = hi.z; V[3] = hi.w;
                 }
                 // now F[m], V[m]: step `slot`, pixel (column cx, row y0 + 2m)
                 const float dx = g0.x - p2.pxc, dy0 = g0.y - p2.py0c;
