@@ -118,6 +118,17 @@ __device__ __forceinline__ void stage_floats(const float* __restrict__ src, int 
     for (int e = done + threadIdx.x; e < count; e += 256) dst[e] = src[e];
 }
 
+// A grid-wide memset folded into a kernel that is not HBM-bound (the raster forwards clear
+// the backward's accumulator rows): workgroup b of the grid clears its share
+// [b n4 / nwg, (b+1) n4 / nwg) of the n4 float4s.  Called after the kernel's last load, so
+// no later vmcnt wait covers these stores.
+__device__ __forceinline__ void zero_share(float4* __restrict__ p, int64_t n4) {
+    if (!p) return;
+    const int64_t nwg = gridDim.x, b = blockIdx.x;
+    const int64_t a = b * n4 / nwg, z = (b + 1) * n4 / nwg;
+    for (int64_t q = a + threadIdx.x; q < z; q += blockDim.x) p[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }

@@ -253,7 +253,8 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     const int32_t* __restrict__ flatten_ids, float* __restrict__ render_colors, float* __restrict__ render_alphas,
     float* __restrict__ render_normals,
     float* __restrict__ render_distort, float* __restrict__ render_median, int32_t* __restrict__ last_ids,
-    int32_t* __restrict__ median_ids, uint64_t* __restrict__ qmask, int64_t qstride) {
+    int32_t* __restrict__ median_ids, uint64_t* __restrict__ qmask, int64_t qstride, float4* __restrict__ zero_rows,
+    int64_t zero_n4) {
     constexpr int NB = kFwd2Batch;
     // one LDS object: every component of record t sits at a compile-time offset from one address
     __shared__ struct {
@@ -368,6 +369,9 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
         last_ids[tc.pix] = cur;
         median_ids[tc.pix] = med_idx;
     }
+    // the backward's accumulator rows, cleared here (after the last load) instead of by a
+    // memset on the step's critical path
+    zero_share(zero_rows, zero_n4);
 }
 
 __device__ __forceinline__ int32_t wave_max2(int32_t v) {
@@ -721,7 +725,7 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
                                float* render_alphas, float* render_normals, float* render_distort,
                                float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s,
-                               uint64_t* qmask = nullptr);
+                               uint64_t* qmask = nullptr, float* zero_rows = nullptr, size_t zero_bytes = 0);
 
 static int raster2d_fwd_impl(int C, int N, int D, const float* means2d, const float* rt, const ChanSrc& cs,
                              const float* normals, const float* backgrounds, int bg_ch, int ed_ch, int width,
@@ -752,15 +756,17 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
                                float* render_alphas, float* render_normals, float* render_distort,
                                float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s,
-                               uint64_t* qmask) {
+                               uint64_t* qmask, float* zero_rows, size_t zero_bytes) {
     const dim3 grid(C * tile_w * tile_h);
+    float4* const z4 = reinterpret_cast<float4*>(zero_rows);
+    const int64_t zn4 = (int64_t)(zero_bytes / sizeof(float4));
     const int64_t qstride = qmask_stride(n_isects, (int64_t)C * tile_w * tile_h);
     KernelTimer kt("raster2d_fwd", s);
 #define LAUNCH_F2(DD)                                                                                            \
     hipLaunchKernelGGL(raster2d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,     \
                        backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,           \
                        render_alphas, render_normals, render_distort, render_median, last_ids, median_ids, qmask,   \
-                       qstride)
+                       qstride, z4, zn4)
     switch (D) {
         case 1: LAUNCH_F2(1); break;
         case 2: LAUNCH_F2(2); break;
@@ -828,8 +834,8 @@ extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, in
                                         const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                                         float* render_normals, float* render_distort, float* render_median,
                                         int32_t* last_ids, int32_t* median_ids, const void* records,
-                                        size_t records_bytes, void* qmask, size_t qmask_bytes,
-                                        hgsr_stream_t stream) {
+                                        size_t records_bytes, void* qmask, size_t qmask_bytes, void* bwd_ws,
+                                        size_t bwd_ws_bytes, hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || with_depth), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !with_depth), "expected_depth needs depths");
     const int D = Dc + (with_depth ? 1 : 0);
@@ -841,10 +847,14 @@ extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, in
     HGSR_REQUIRE(n_isects == 0 || (flatten_ids && records), "null pointer");
     HGSR_REQUIRE(!qmask || qmask_bytes >= (size_t)(4 * qmask_stride(n_isects, (int64_t)C * tile_w * tile_h)) * 8,
                  "raster2d_fwd_packed: quadrant-mask buffer too small");
+    // bwd_ws (nullable): the backward's workspace, whose accumulator rows this launch clears
+    const size_t rows_b = (size_t)C * N * kRec2 * sizeof(float);
+    HGSR_REQUIRE(!bwd_ws || (bwd_ws_bytes >= rows_b && (reinterpret_cast<uintptr_t>(bwd_ws) & 15) == 0),
+                 "raster2d_fwd_packed: bwd_ws too small or not 16-B aligned");
     return raster2d_fwd_launch(C, D, (const Rec2*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
                                tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
                                render_normals, render_distort, render_median, last_ids, median_ids,
-                               as_stream(stream), (uint64_t*)qmask);
+                               as_stream(stream), (uint64_t*)qmask, (float*)bwd_ws, bwd_ws ? rows_b : 0);
 }
 
 extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
@@ -860,7 +870,8 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* render_alphas, const int32_t* last_ids, const float* v_render_colors,
                              const float* v_render_alphas, const float* v_render_normals, float* v_means2d,
                              float* v_rt, const ChanDst& cd, float* v_normals, float* v_densify,
-                             const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream, const uint64_t* qmask = nullptr) {
+                             const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream, const uint64_t* qmask = nullptr,
+                             bool rows_zeroed = false) {
     if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
                  "raster2d_bwd workspace too small");
@@ -889,7 +900,8 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     const size_t rows_b = ((size_t)C * N * kRec2 * sizeof(float) + 255) & ~(size_t)255;
     float* rows = (float*)ws;
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
-    if (int st = memset_async(rows, (size_t)C * N * kRec2 * sizeof(float), s, "raster2d_bwd")) return st;
+    if (!rows_zeroed)  // else hgsr_raster2d_fwd_packed cleared them (bwd_ws)
+        if (int st = memset_async(rows, (size_t)C * N * kRec2 * sizeof(float), s, "raster2d_bwd")) return st;
     const Rec2* rec = (const Rec2*)fwd_ws;
     if (!rec) {
         Rec2* own = (Rec2*)((char*)ws + rows_b);
@@ -948,7 +960,8 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                                        const float* v_render_normals, float* v_means2d, float* v_ray_transforms,
                                        float* v_colors, float* v_depths, float* v_opacities, float* v_normals,
                                        float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
-                                       const void* qmask, size_t qmask_bytes, hgsr_stream_t stream) {
+                                       const void* qmask, size_t qmask_bytes, int ws_zeroed,
+                                       hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !depths), "expected_depth needs depths");
     HGSR_REQUIRE(!depths || v_depths, "null pointer");
@@ -963,5 +976,5 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                              expected_depth ? Dc : -1, render_colors, width, height, tile_size, tile_w, tile_h,
                              isect_offsets, n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
                              v_render_alphas, v_render_normals, v_means2d, v_ray_transforms, cd, v_normals,
-                             v_densify, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask);
+                             v_densify, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask, ws_zeroed != 0);
 }

@@ -159,7 +159,8 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
     int bg_ch, int ed_ch, const int32_t* __restrict__ offsets, int64_t n_isects,
     const int32_t* __restrict__ flatten_ids, float* __restrict__ render_colors, float* __restrict__ render_alphas,
-    int32_t* __restrict__ last_ids, uint64_t* __restrict__ qmask, int64_t qstride) {
+    int32_t* __restrict__ last_ids, uint64_t* __restrict__ qmask, int64_t qstride, float4* __restrict__ zero_rows,
+    int64_t zero_n4) {
     // slot kFwdBatch is a zero-opacity dummy used to pad the per-wave lists
     __shared__ float4 s_g0[kFwdBatch + 1];
     __shared__ float4 s_g1[kFwdBatch + 1];
@@ -264,6 +265,9 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
         }
         last_ids[tc.pix] = cur;
     }
+    // the backward's accumulator rows, cleared here (after the last load: no wait covers
+    // these stores) instead of by a memset on the step's critical path
+    zero_share(zero_rows, zero_n4);
 }
 
 __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
@@ -754,7 +758,8 @@ extern "C" size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D) {
 static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backgrounds, int bg_ch, int ed_ch,
                                int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
-                               float* render_alphas, int32_t* last_ids, hipStream_t s, uint64_t* qmask = nullptr);
+                               float* render_alphas, int32_t* last_ids, hipStream_t s, uint64_t* qmask = nullptr,
+                               float* zero_rows = nullptr, size_t zero_bytes = 0);
 
 static int raster3d_fwd_impl(int C, int N, int D, const float* means2d, const float* conics, const ChanSrc& cs,
                              const float* backgrounds, int bg_ch, int ed_ch, int width, int height, int tile_size,
@@ -777,14 +782,17 @@ static int raster3d_fwd_impl(int C, int N, int D, const float* means2d, const fl
 static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backgrounds, int bg_ch, int ed_ch,
                                int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
-                               float* render_alphas, int32_t* last_ids, hipStream_t s, uint64_t* qmask) {
+                               float* render_alphas, int32_t* last_ids, hipStream_t s, uint64_t* qmask,
+                               float* zero_rows, size_t zero_bytes) {
     const dim3 grid(C * tile_w * tile_h);
+    float4* const z4 = reinterpret_cast<float4*>(zero_rows);
+    const int64_t zn4 = (int64_t)(zero_bytes / sizeof(float4));
     const int64_t qstride = qmask_stride(n_isects, (int64_t)C * tile_w * tile_h);
     KernelTimer kt("raster3d_fwd", s);
 #define LAUNCH_F(DD)                                                                                           \
     hipLaunchKernelGGL(raster3d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,    \
                        backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,          \
-                       render_alphas, last_ids, qmask, qstride)
+                       render_alphas, last_ids, qmask, qstride, z4, zn4)
     switch (D) {
         case 1: LAUNCH_F(1); break;
         case 2: LAUNCH_F(2); break;
@@ -844,7 +852,8 @@ extern "C" int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, in
                                         int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
                                         const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                                         int32_t* last_ids, const void* records, size_t records_bytes,
-                                        void* qmask, size_t qmask_bytes, hgsr_stream_t stream) {
+                                        void* qmask, size_t qmask_bytes, void* bwd_ws, size_t bwd_ws_bytes,
+                                        hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || with_depth), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !with_depth), "expected_depth needs depths");
     const int D = Dc + (with_depth ? 1 : 0);
@@ -854,9 +863,13 @@ extern "C" int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, in
     HGSR_REQUIRE(n_isects == 0 || (flatten_ids && records), "null pointer");
     HGSR_REQUIRE(!qmask || qmask_bytes >= hgsr_raster3d_qmask_bytes(C, tile_w, tile_h, n_isects),
                  "raster3d_fwd_packed: quadrant-mask buffer too small");
+    // bwd_ws (nullable): the backward's workspace, whose accumulator rows this launch clears
+    const size_t rows_b = (size_t)C * N * kRec3 * sizeof(float);
+    HGSR_REQUIRE(!bwd_ws || (bwd_ws_bytes >= rows_b && (reinterpret_cast<uintptr_t>(bwd_ws) & 15) == 0),
+                 "raster3d_fwd_packed: bwd_ws too small or not 16-B aligned");
     return raster3d_fwd_launch(C, D, (const Rec3*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
                                tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
-                               last_ids, as_stream(stream), (uint64_t*)qmask);
+                               last_ids, as_stream(stream), (uint64_t*)qmask, (float*)bwd_ws, bwd_ws ? rows_b : 0);
 }
 
 extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
@@ -872,7 +885,7 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* render_alphas, const int32_t* last_ids, const float* v_render_colors,
                              const float* v_render_alphas, float* v_means2d, float* v_conics, const ChanDst& cd,
                              float* v_means2d_abs, const void* fwd_ws, void* ws, size_t ws_bytes,
-                             hgsr_stream_t stream, const uint64_t* qmask = nullptr) {
+                             hgsr_stream_t stream, const uint64_t* qmask = nullptr, bool rows_zeroed = false) {
     if (int st = check_raster(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
                  "raster3d_bwd workspace too small");
@@ -899,7 +912,8 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                  "null pointer");
     const size_t rows_b = ((size_t)C * N * kRec3 * sizeof(float) + 255) & ~(size_t)255;
     float* rows = (float*)ws;
-    if (int st = memset_async(rows, (size_t)C * N * kRec3 * sizeof(float), s, "raster3d_bwd")) return st;
+    if (!rows_zeroed)  // else hgsr_raster3d_fwd_packed cleared them (bwd_ws)
+        if (int st = memset_async(rows, (size_t)C * N * kRec3 * sizeof(float), s, "raster3d_bwd")) return st;
     // the forward's packed records when the caller kept them, else pack again
     const Rec3* rec = (const Rec3*)fwd_ws;
     if (!rec) {
@@ -962,7 +976,7 @@ extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2
                                        const float* v_render_colors, const float* v_render_alphas,
                                        float* v_means2d, float* v_conics, float* v_colors, float* v_depths,
                                        float* v_opacities, float* v_means2d_abs, const void* fwd_ws, void* ws,
-                                       size_t ws_bytes, const void* qmask, size_t qmask_bytes,
+                                       size_t ws_bytes, const void* qmask, size_t qmask_bytes, int ws_zeroed,
                                        hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!qmask || qmask_bytes >= hgsr_raster3d_qmask_bytes(C, tile_w, tile_h, n_isects),
@@ -977,5 +991,6 @@ extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2
     return raster3d_bwd_impl(C, N, D, means2d, conics, cs, backgrounds, Dc, expected_depth ? Dc : -1,
                              render_colors, width, height, tile_size, tile_w, tile_h, isect_offsets, n_isects,
                              flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, v_means2d,
-                             v_conics, cd, v_means2d_abs, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask);
+                             v_conics, cd, v_means2d_abs, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask,
+                             ws_zeroed != 0);
 }

@@ -24,6 +24,8 @@ import math
 import threading
 from typing import Optional, Tuple
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -403,6 +405,28 @@ class _Raster3D(torch.autograd.Function):
         return v_means2d, v_conics, v_colors, v_opac, v_bg, None, None, None, None, None, None
 
 
+def _bwd_ws(size_fn, ctx, C, Ng, D, dev):
+    """The raster backward's workspace (records reused), allocated by the forward when a
+    backward can follow: the forward kernel clears its accumulator rows while it composites,
+    so the backward needs no memset (hgsr_raster{3,2}d_fwd_packed bwd_ws)."""
+    ctx.bwd_ws = None
+    if not any(ctx.needs_input_grad) or os.environ.get("HGSR_RASTER_PREZERO", "1") == "0":  # (A/B knob)
+        return None
+    ws_b = N.size_query(size_fn, C, Ng, D, 1)
+    ctx.bwd_ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+    return ctx.bwd_ws
+
+
+def _take_bwd_ws(ctx, ws_b, dev):
+    """(workspace, rows already zero) for the backward: the forward's pre-cleared one once,
+    else a fresh one the backward clears itself (a second backward through the same graph)."""
+    ws = getattr(ctx, "bwd_ws", None)
+    ctx.bwd_ws = None
+    if ws is not None and ws.numel() >= ws_b:
+        return ws, 1
+    return torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev), 0
+
+
 class _Raster3DFused(torch.autograd.Function):
     """rasterization()'s colour assembly + rasterize_to_pixels + ED normalisation as one
     native call each way (hgsr_raster3d_{fwd,bwd}_fused): colours shared over cameras or
@@ -442,10 +466,12 @@ class _Raster3DFused(torch.autograd.Function):
             # the forward's per-quadrant culling bits, read back by the backward
             q_b = N.size_query("hgsr_raster3d_qmask_bytes", C, tw, th, flatten_ids.numel())
             qmask = torch.empty(q_b, dtype=torch.uint8, device=dev)
+            # the backward's workspace, its accumulator rows cleared by this forward launch
+            bwd_ws = _bwd_ws("hgsr_raster3d_bwd_ws_bytes", ctx, C, Ng, D, dev)
             N.call("hgsr_raster3d_fwd_packed", C, Ng, Dc, int(depths is not None), int(expected_depth),
                    ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
                    ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(ws),
-                   ws.numel(), ptr(qmask), q_b, N.stream(dev))
+                   ws.numel(), ptr(qmask), q_b, ptr(bwd_ws), 0 if bwd_ws is None else bwd_ws.numel(), N.stream(dev))
         else:
             ws_b = N.size_query("hgsr_raster3d_fwd_ws_bytes", C, Ng, D)
             ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
@@ -477,14 +503,14 @@ class _Raster3DFused(torch.autograd.Function):
         v_abs = torch.empty_like(means2d) if absgrad else None
         fwd_ws = ctx.fwd_ws
         ws_b = N.size_query("hgsr_raster3d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
-        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+        ws, zeroed = _take_bwd_ws(ctx, ws_b, dev)
         v_rc, v_ra = _f32(v_rc), _f32(v_ra)
         N.call("hgsr_raster3d_bwd_fused", C, Ng, Dc, ptr(means2d), ptr(conics), ptr(colors), int(col_shared),
                ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(backgrounds), width, height,
                tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
                ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_means2d), ptr(v_conics), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_abs), ptr(fwd_ws),
-               ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(), N.stream(dev))
+               ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(), zeroed, N.stream(dev))
         if absgrad:
             means2d.absgrad = v_abs
         v_bg = None
@@ -619,10 +645,13 @@ class _Raster2DFused(torch.autograd.Function):
             # the forward's per-quadrant culling bits, read back by the backward
             q_b = N.size_query("hgsr_raster3d_qmask_bytes", C, tw, th, flatten_ids.numel())
             qmask = torch.empty(q_b, dtype=torch.uint8, device=dev)
+            # the backward's workspace, its accumulator rows cleared by this forward launch
+            bwd_ws = _bwd_ws("hgsr_raster2d_bwd_ws_bytes", ctx, C, Ng, D, dev)
             N.call("hgsr_raster2d_fwd_packed", C, Ng, Dc, int(depths is not None), int(expected_depth),
                    ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
                    ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(rn), ptr(rd), ptr(rm),
-                   ptr(last), ptr(med), ptr(ws), ws.numel(), ptr(qmask), q_b, N.stream(dev))
+                   ptr(last), ptr(med), ptr(ws), ws.numel(), ptr(qmask), q_b, ptr(bwd_ws),
+                   0 if bwd_ws is None else bwd_ws.numel(), N.stream(dev))
         else:
             ws_b = N.size_query("hgsr_raster2d_fwd_ws_bytes", C, Ng, D)
             ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
@@ -657,7 +686,7 @@ class _Raster2DFused(torch.autograd.Function):
         v_dens = torch.empty_like(means2d)
         fwd_ws = ctx.fwd_ws
         ws_b = N.size_query("hgsr_raster2d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
-        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+        ws, zeroed = _take_bwd_ws(ctx, ws_b, dev)
         v_rc, v_ra, v_rn = _f32(v_rc), _f32(v_ra), _f32(v_rn)
         N.call("hgsr_raster2d_bwd_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors), int(col_shared),
                ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(normals), ptr(backgrounds),
@@ -665,7 +694,7 @@ class _Raster2DFused(torch.autograd.Function):
                ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_rn), ptr(v_means2d), ptr(v_rt), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_normals),
                ptr(v_dens), ptr(fwd_ws), ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(),
-               N.stream(dev))
+               zeroed, N.stream(dev))
         v_bg = None
         if backgrounds is not None and ctx.needs_input_grad[7]:
             v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))

@@ -195,7 +195,10 @@ int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * hgsr_raster3d_bwd_fused's fwd_ws.  qmask (nullable, hgsr_raster3d_qmask_bytes) receives
  * the forward's per-quadrant culling bits of every tile list, which hgsr_raster3d_bwd_fused
  * (given the same buffer) reads instead of repeating the culling tests; caller-allocated,
- * OVERWRITTEN where the forward visits a tile (the backward reads only those bits). */
+ * OVERWRITTEN where the forward visits a tile (the backward reads only those bits).
+ * bwd_ws (nullable, 16-B aligned, >= hgsr_raster3d_bwd_ws_bytes(C, N, D, 1)): the workspace
+ * the backward will get; the forward clears its accumulator rows while it composites (HBM
+ * is idle there), so hgsr_raster3d_bwd_fused given it with ws_zeroed = 1 skips its memset. */
 size_t hgsr_raster3d_qmask_bytes(int C, int tile_w, int tile_h, int64_t n_isects);
 int hgsr_raster3d_pack_fused(int C, int N, int Dc, const float* means2d, const float* conics,
                              const float* colors, int colors_shared, const float* depths,
@@ -206,7 +209,8 @@ int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_
                              int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
                              const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                              int32_t* last_ids, const void* records, size_t records_bytes,
-                             void* qmask, size_t qmask_bytes, hgsr_stream_t stream);
+                             void* qmask, size_t qmask_bytes, void* bwd_ws, size_t bwd_ws_bytes,
+                             hgsr_stream_t stream);
 /* vjp of hgsr_raster3d_fwd_fused: v_colors in the colours' layout (shared colours
  * summed over cameras in camera order), v_depths [C,N] (when depths), v_opacities
  * in the opacities' layout; render_colors is the forward output (needed for ED);
@@ -221,7 +225,7 @@ int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             const float* v_render_colors, const float* v_render_alphas,
                             float* v_means2d, float* v_conics, float* v_colors, float* v_depths,
                             float* v_opacities, float* v_means2d_abs, const void* fwd_ws, void* ws,
-                            size_t ws_bytes, const void* qmask, size_t qmask_bytes,
+                            size_t ws_bytes, const void* qmask, size_t qmask_bytes, int ws_zeroed,
                             hgsr_stream_t stream);
 
 /* ---- K11/K12: 2DGS surfel rasterization -----------------------------------
@@ -270,7 +274,8 @@ int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * surfel records (ws, hgsr_raster2d_fwd_ws_bytes) are packed while the host reads the
  * intersection count, then composited; they stay valid as hgsr_raster2d_bwd_fused's fwd_ws.
  * qmask (nullable; size hgsr_raster3d_qmask_bytes, the same layout): the forward's
- * per-quadrant culling bits, read by hgsr_raster2d_bwd_fused instead of repeating the tests. */
+ * per-quadrant culling bits, read by hgsr_raster2d_bwd_fused instead of repeating the tests.
+ * bwd_ws / ws_zeroed: as hgsr_raster3d_fwd_packed (size hgsr_raster2d_bwd_ws_bytes(C, N, D, 1)). */
 int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                              const float* colors, int colors_shared, const float* depths,
                              const float* opacities, int opacities_shared, const float* normals, void* ws,
@@ -281,7 +286,8 @@ int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_
                              const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                              float* render_normals, float* render_distort, float* render_median,
                              int32_t* last_ids, int32_t* median_ids, const void* records,
-                             size_t records_bytes, void* qmask, size_t qmask_bytes, hgsr_stream_t stream);
+                             size_t records_bytes, void* qmask, size_t qmask_bytes, void* bwd_ws,
+                             size_t bwd_ws_bytes, hgsr_stream_t stream);
 int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                             const float* colors, int colors_shared, const float* depths,
                             int expected_depth, const float* opacities, int opacities_shared,
@@ -293,7 +299,7 @@ int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             const float* v_render_normals, float* v_means2d, float* v_ray_transforms,
                             float* v_colors, float* v_depths, float* v_opacities, float* v_normals,
                             float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
-                            const void* qmask, size_t qmask_bytes,
+                            const void* qmask, size_t qmask_bytes, int ws_zeroed,
                             hgsr_stream_t stream);
 
 /* ---- K14: anchor -> neural-Gaussian decode --------------
