@@ -18,6 +18,9 @@
 //  * opacity > 0 compaction is order-preserving (anchor-major, then offset) with
 //    wave ballots + a per-tile offset table from a count pass and a scan;
 //  * the colour head (pure linear) is stored straight from the accumulators.
+#include <map>
+#include <mutex>
+
 #include "common.h"
 
 namespace hgsr {
@@ -1161,6 +1164,34 @@ static int bwd_grid(int Av) {
     return n_tiles < 1024 ? (n_tiles > 0 ? n_tiles : 1) : 1024;
 }
 
+// Workgroups of one decode_bwd launch: at most what is resident at once on the device (the
+// kernel's occupancy x CUs), so the grid-stride tiles run in one round.  1024 workgroups of
+// the 3-per-CU opacity head left a second round a third full.
+static int bwd_grid_resident(const void* kernel, int Av) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, int> cache;  // (device, kernel) -> resident workgroups
+    int dev = 0;
+    static const bool fixed = getenv("HGSR_DEC_GRID_FIXED") != nullptr;  // (A/B knob: the old 1024 cap)
+    if (fixed || hipGetDevice(&dev) != hipSuccess) return bwd_grid(Av);
+    int resident = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find({dev, kernel});
+        if (it != cache.end()) {
+            resident = it->second;
+        } else {
+            int per_cu = 0, n_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess ||
+                hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                per_cu = n_cu = 0;
+            resident = per_cu * n_cu;
+            cache[{dev, kernel}] = resident;
+        }
+    }
+    const int g = bwd_grid(Av);  // the workspace bound
+    return resident > 0 && resident < g ? resident : g;
+}
+
 extern "C" size_t hgsr_decode_bwd_ws_bytes(int Av) {
     const size_t parts = ((size_t)bwd_grid(Av) * 4 * bwd_partial_floats(kBwdChunk) * sizeof(float) + 255) & ~(size_t)255;
     return parts + (size_t)kRedGroups * bwd_partial_floats(kBwdChunk) * sizeof(double);
@@ -1184,7 +1215,7 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
     const MlpPtrs mp = mlp_ptrs(mlp);
     const DecodeGrads gr{g_xyz, g_offsets, g_color, g_opacity, g_scaling, g_rot, d_anchor, d_feat, d_offset, d_scaling};
     hipStream_t s = as_stream(stream);
-    const int grid = bwd_grid(Av);
+    int grid = bwd_grid(Av);
     float* partials = (float*)ws;
     double* level2 = (double*)((char*)ws + (((size_t)grid * 4 * bwd_partial_floats(kBwdChunk) * sizeof(float) + 255) &
                                             ~(size_t)255));
@@ -1197,8 +1228,11 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
         for (int t0 = 0; t0 < d.T[head]; t0 += chunk) {
             const int nt = d.T[head] - t0 < chunk ? d.T[head] - t0 : chunk;
 #define LAUNCH_DB(KS, HD, NTT)                                                                                 \
-    hipLaunchKernelGGL((decode_bwd_kernel<KS, HD, NTT>), dim3(grid), dim3(256), 0, s, d, mp, t0, nt, vis_idx,       \
-                       anchor, feat, offset, scaling_raw, cam_center, slot_row, gr, partials)
+    do {                                                                                                       \
+        grid = bwd_grid_resident(reinterpret_cast<const void*>(&decode_bwd_kernel<KS, HD, NTT>), Av);          \
+        hipLaunchKernelGGL((decode_bwd_kernel<KS, HD, NTT>), dim3(grid), dim3(256), 0, s, d, mp, t0, nt, vis_idx,   \
+                           anchor, feat, offset, scaling_raw, cam_center, slot_row, gr, partials);              \
+    } while (0)
 #define LAUNCH_DB_NT(KS, HD) \
     do {                                                               \
         if (nt <= 1) LAUNCH_DB(KS, HD, 1);                             \
