@@ -1065,6 +1065,34 @@ static int decode_grid(int Av) {
     return n_tiles < 1024 ? (n_tiles > 0 ? n_tiles : 1) : 1024;
 }
 
+// Workgroups of one decode launch (grid-stride over 64-anchor tiles): at most what is resident at once on the device (the
+// kernel's occupancy x CUs), so the grid-stride tiles run in one round.  1024 workgroups of
+// the 3-per-CU opacity-head backward left a second round a third full.
+static int grid_resident(const void* kernel, int Av) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, int> cache;  // (device, kernel) -> resident workgroups
+    int dev = 0;
+    static const bool fixed = getenv("HGSR_DEC_GRID_FIXED") != nullptr;  // (A/B knob: the old 1024 cap)
+    if (fixed || hipGetDevice(&dev) != hipSuccess) return decode_grid(Av);
+    int resident = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find({dev, kernel});
+        if (it != cache.end()) {
+            resident = it->second;
+        } else {
+            int per_cu = 0, n_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess ||
+                hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                per_cu = n_cu = 0;
+            resident = per_cu * n_cu;
+            cache[{dev, kernel}] = resident;
+        }
+    }
+    const int g = decode_grid(Av);  // the backward's workspace bound
+    return resident > 0 && resident < g ? resident : g;
+}
+
 static MlpPtrs mlp_ptrs(const float* const* w) {
     MlpPtrs mp;
     for (int h = 0; h < 3; ++h) {
@@ -1101,10 +1129,10 @@ extern "C" int hgsr_decode_count(int Av, int F, int view_dim, int n_offsets, int
     int32_t* cnt = (int32_t*)((char*)ws + (((size_t)(n_tiles + 1) * 4 + 255) & ~(size_t)255));
     KernelTimer kt("decode_count", s);
     if (view_dim == 3)
-        hipLaunchKernelGGL(decode_count_kernel<9>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
+        hipLaunchKernelGGL(decode_count_kernel<9>, dim3(grid_resident(reinterpret_cast<const void*>(&decode_count_kernel<9>), Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
                            feat, cam_center, cnt, av_dev);
     else
-        hipLaunchKernelGGL(decode_count_kernel<8>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
+        hipLaunchKernelGGL(decode_count_kernel<8>, dim3(grid_resident(reinterpret_cast<const void*>(&decode_count_kernel<8>), Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
                            feat, cam_center, cnt, av_dev);
     if (int st = check_launch("decode_count")) return st;
     hipLaunchKernelGGL(decode_scan_kernel, dim3(1), dim3(1024), 0, s, n_tiles, cnt, off, total, av_dev);
@@ -1129,7 +1157,7 @@ extern "C" int hgsr_decode_fwd(int Av, int F, int view_dim, int n_offsets, int c
     hipStream_t s = as_stream(stream);
     KernelTimer kt("decode_fwd", s);
 #define LAUNCH_DF(KS, R)                                                                                      \
-    hipLaunchKernelGGL((decode_fwd_kernel<KS, R>), dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor, \
+    hipLaunchKernelGGL((decode_fwd_kernel<KS, R>), dim3(grid_resident(reinterpret_cast<const void*>(&decode_fwd_kernel<KS, R>), Av)), dim3(256), 0, s, d, mp, vis_idx, anchor, \
                        feat, offset, scaling_raw, cam_center, off, out)
     // LDS sized to the model: RGB heads fit 128 second-layer rows (2 workgroups per CU); an SH
     // colour head of up to 272 rows runs as its own pass after the opacity / cov pass (2
@@ -1139,17 +1167,17 @@ extern "C" int hgsr_decode_fwd(int Av, int F, int view_dim, int n_offsets, int c
         else LAUNCH_DF(8, 128);
     } else if (d.row0[2] <= 128 && d.T[2] * 16 <= kDecColRows) {
         if (view_dim == 3)
-            hipLaunchKernelGGL((decode_fwd_kernel<9, 128, false>), dim3(decode_grid(Av)), dim3(256), 0, s, d, mp,
+            hipLaunchKernelGGL((decode_fwd_kernel<9, 128, false>), dim3(grid_resident(reinterpret_cast<const void*>(&decode_fwd_kernel<9, 128, false>), Av)), dim3(256), 0, s, d, mp,
                                vis_idx, anchor, feat, offset, scaling_raw, cam_center, off, out);
         else
-            hipLaunchKernelGGL((decode_fwd_kernel<8, 128, false>), dim3(decode_grid(Av)), dim3(256), 0, s, d, mp,
+            hipLaunchKernelGGL((decode_fwd_kernel<8, 128, false>), dim3(grid_resident(reinterpret_cast<const void*>(&decode_fwd_kernel<8, 128, false>), Av)), dim3(256), 0, s, d, mp,
                                vis_idx, anchor, feat, offset, scaling_raw, cam_center, off, out);
         if (int st = check_launch("decode_fwd")) return st;
         if (view_dim == 3)
-            hipLaunchKernelGGL(decode_color_kernel<9>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
+            hipLaunchKernelGGL(decode_color_kernel<9>, dim3(grid_resident(reinterpret_cast<const void*>(&decode_color_kernel<9>), Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
                                feat, cam_center, slot_row, color);
         else
-            hipLaunchKernelGGL(decode_color_kernel<8>, dim3(decode_grid(Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
+            hipLaunchKernelGGL(decode_color_kernel<8>, dim3(grid_resident(reinterpret_cast<const void*>(&decode_color_kernel<8>), Av)), dim3(256), 0, s, d, mp, vis_idx, anchor,
                                feat, cam_center, slot_row, color);
     } else {
         if (view_dim == 3) LAUNCH_DF(9, kDecMaxRows);
@@ -1164,33 +1192,6 @@ static int bwd_grid(int Av) {
     return n_tiles < 1024 ? (n_tiles > 0 ? n_tiles : 1) : 1024;
 }
 
-// Workgroups of one decode_bwd launch: at most what is resident at once on the device (the
-// kernel's occupancy x CUs), so the grid-stride tiles run in one round.  1024 workgroups of
-// the 3-per-CU opacity head left a second round a third full.
-static int bwd_grid_resident(const void* kernel, int Av) {
-    static std::mutex mu;
-    static std::map<std::pair<int, const void*>, int> cache;  // (device, kernel) -> resident workgroups
-    int dev = 0;
-    static const bool fixed = getenv("HGSR_DEC_GRID_FIXED") != nullptr;  // (A/B knob: the old 1024 cap)
-    if (fixed || hipGetDevice(&dev) != hipSuccess) return bwd_grid(Av);
-    int resident = 0;
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        auto it = cache.find({dev, kernel});
-        if (it != cache.end()) {
-            resident = it->second;
-        } else {
-            int per_cu = 0, n_cu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess ||
-                hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                per_cu = n_cu = 0;
-            resident = per_cu * n_cu;
-            cache[{dev, kernel}] = resident;
-        }
-    }
-    const int g = bwd_grid(Av);  // the workspace bound
-    return resident > 0 && resident < g ? resident : g;
-}
 
 extern "C" size_t hgsr_decode_bwd_ws_bytes(int Av) {
     const size_t parts = ((size_t)bwd_grid(Av) * 4 * bwd_partial_floats(kBwdChunk) * sizeof(float) + 255) & ~(size_t)255;
@@ -1229,7 +1230,7 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
             const int nt = d.T[head] - t0 < chunk ? d.T[head] - t0 : chunk;
 #define LAUNCH_DB(KS, HD, NTT)                                                                                 \
     do {                                                                                                       \
-        grid = bwd_grid_resident(reinterpret_cast<const void*>(&decode_bwd_kernel<KS, HD, NTT>), Av);          \
+        grid = grid_resident(reinterpret_cast<const void*>(&decode_bwd_kernel<KS, HD, NTT>), Av);          \
         hipLaunchKernelGGL((decode_bwd_kernel<KS, HD, NTT>), dim3(grid), dim3(256), 0, s, d, mp, t0, nt, vis_idx,   \
                            anchor, feat, offset, scaling_raw, cam_center, slot_row, gr, partials);              \
     } while (0)
