@@ -587,6 +587,7 @@ struct DepthQ {
     uint32_t lo;
     int shift;
 };
+template <int IB = 11>
 __device__ __forceinline__ DepthQ depth_q(uint32_t mn, uint32_t mx) {
     __shared__ uint32_t s_red[8];
     // wave min / max over the network's in-wave lane exchanges (DPP / swizzle / permlane)
@@ -606,18 +607,22 @@ __device__ __forceinline__ DepthQ depth_q(uint32_t mn, uint32_t mx) {
     mx = max(max(s_red[4], s_red[5]), max(s_red[6], s_red[7]));
     const uint32_t span = mx - mn;
     const int bits = span ? 32 - __clz((int)span) : 0;
-    return {mn, bits > 20 ? bits - 20 : 0};
+    constexpr int DB = 31 - IB;  // depth bits: every real key stays below the ~0 padding
+    return {mn, bits > DB ? bits - DB : 0};
 }
 
+template <int IB = 11>
 __device__ __forceinline__ uint32_t key32(uint64_t k, int i, DepthQ q) {
-    return ((((uint32_t)(k >> 32) - q.lo) >> q.shift) << 11) | (uint32_t)i;
+    return ((((uint32_t)(k >> 32) - q.lo) >> q.shift) << IB) | (uint32_t)i;
 }
 
 template <int E>
 __device__ __forceinline__ void sort32_and_emit(const uint64_t* keys, int n, uint64_t* smem, int64_t hi,
                                                 int64_t* __restrict__ isect_ids, int32_t* __restrict__ flatten_ids) {
-    uint64_t* full = smem;                                  // [2048] full keys by local index
-    uint32_t* s32 = reinterpret_cast<uint32_t*>(smem + 2048);  // 32-bit network scratch
+    constexpr int NF = 256 * E > 2048 ? 256 * E : 2048;    // full keys held (2048 up to E = 8)
+    constexpr int IB = NF > 2048 ? 12 : 11;                 // local index bits of the 32-bit key
+    uint64_t* full = smem;                                  // [NF] full keys by local index
+    uint32_t* s32 = reinterpret_cast<uint32_t*>(smem + NF);  // 32-bit network scratch
     const int t = threadIdx.x;
     uint64_t kk[E];
     uint32_t mn = ~0u, mx = 0u;
@@ -631,18 +636,18 @@ __device__ __forceinline__ void sort32_and_emit(const uint64_t* keys, int n, uin
             mx = max(mx, (uint32_t)(kk[r] >> 32));
         }
     }
-    const DepthQ q = depth_q(mn, mx);
+    const DepthQ q = depth_q<IB>(mn, mx);
     uint32_t v[E];
 #pragma unroll
     for (int r = 0; r < E; ++r) {
         const int i = r * 256 + t;
-        v[r] = i < n ? key32(kk[r], i, q) : ~0u;
+        v[r] = i < n ? key32<IB>(kk[r], i, q) : ~0u;
     }
     to_blocked<uint32_t, E>(v, s32);  // its barriers also publish full[]
     bitonic_regs<uint32_t, E>(v, s32, n);
     uint64_t w[E];
 #pragma unroll
-    for (int r = 0; r < E; ++r) w[r] = v[r] == ~0u ? ~0ull : full[v[r] & 2047u];
+    for (int r = 0; r < E; ++r) w[r] = v[r] == ~0u ? ~0ull : full[v[r] & ((1u << IB) - 1u)];
     // boundary exchange in the network scratch (its last reads were before bitonic_regs' barrier)
     if (!fix_runs<E>(w, reinterpret_cast<uint64_t*>(s32)))
         bitonic_regs<uint64_t, E>(w, smem, n);  // rare: many equal depths
@@ -764,30 +769,38 @@ __device__ void merge_runs(const uint64_t* __restrict__ src, uint64_t* __restric
     }
 }
 
+// BIG = false: the bins of <= kSortCap keys (24.6 KB of LDS); BIG = true: the larger ones,
+// launched only when some bin exceeds kSortCap (anchor scenes: 1M anchors put most bins just
+// above 2048), with the LDS for a 4096-key sort (49 KB: 4096 full keys + the 32-bit network's
+// scratch) so those bins sort in LDS instead of by chunk merges through global memory.
+template <bool BIG>
 __global__ __launch_bounds__(256) void tile_sort_kernel(int n_bins, int n_tiles, int tile_bits,
                                                         const int32_t* __restrict__ offsets,
                                                         int64_t n_isects, uint64_t* __restrict__ keys,
                                                         uint64_t* __restrict__ tmp,
                                                         int64_t* __restrict__ isect_ids,
                                                         int32_t* __restrict__ flatten_ids) {
-    // 64-bit network scratch, or (32-bit path) 2048 full keys + the 32-bit network's scratch
-    __shared__ uint64_t s_keys[2048 + 4 * kSortPitch];
+    // 64-bit network scratch, or (32-bit path) the full keys + the 32-bit network's scratch
+    __shared__ uint64_t s_keys[BIG ? 4096 + 8 * kSortPitch : 2048 + 4 * kSortPitch];
     const int bin = blockIdx.x;
     const int64_t start = offsets[bin];
     const int64_t end = bin + 1 < n_bins ? (int64_t)offsets[bin + 1] : n_isects;
     const int n = (int)(end - start);
-    if (n <= 0) return;
+    if (n <= 0 || (n <= kSortCap) == BIG) return;
     const int cam = bin / n_tiles, tile = bin - cam * n_tiles;
     const int64_t hi = ((int64_t)cam << (32 + tile_bits)) | ((int64_t)tile << 32);
-    if (n <= kSortCap) {
+    if constexpr (!BIG) {
         if (n <= 256) sort_and_emit<1>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         else if (n <= 512) sort32_and_emit<2>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         else if (n <= 1024) sort32_and_emit<4>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         else if (n <= 1280) sort32_split_and_emit<1>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         else sort32_and_emit<8>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
         return;
+    } else if (n <= 2 * kSortCap) {
+        sort32_and_emit<16>(keys + start, n, s_keys, hi, isect_ids + start, flatten_ids + start);
+        return;
     }
-    // large bin: LDS-sorted chunks, then merge passes ping-ponging keys <-> tmp
+    // larger bins: LDS-sorted chunks, then merge passes ping-ponging keys <-> tmp
     uint64_t* a = keys + start;
     uint64_t* b = tmp + start;
     for (int c0 = 0; c0 < n; c0 += kSortCap) {
@@ -988,8 +1001,11 @@ extern "C" int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const 
     }
     if (int st = check_launch("isect_emit")) return st;
     KernelTimer kt("tile_sort", s);
-    hipLaunchKernelGGL(tile_sort_kernel, dim3(g.n_bins), dim3(256), 0, s, g.n_bins, g.n_tiles,
+    hipLaunchKernelGGL(tile_sort_kernel<false>, dim3(g.n_bins), dim3(256), 0, s, g.n_bins, g.n_tiles,
                        nbits64(g.n_tiles), isect_offsets, n_isects, keys, tmp, isect_ids, flatten_ids);
+    if (max_bin > kSortCap)
+        hipLaunchKernelGGL(tile_sort_kernel<true>, dim3(g.n_bins), dim3(256), 0, s, g.n_bins, g.n_tiles,
+                           nbits64(g.n_tiles), isect_offsets, n_isects, keys, tmp, isect_ids, flatten_ids);
     return check_launch("tile_sort");
 }
 

@@ -272,6 +272,41 @@ def test_isect_split_sort_bins():
     np.testing.assert_array_equal(goffs.cpu().numpy(), offs)
 
 
+def test_isect_large_bins():
+    """Bins above 2048 keys (anchor scenes) go to the large-bin launch: 2049-4096 keys sort in
+    LDS as 32-bit keys with a 12-bit local index (4096-key network), larger ones by chunk
+    merges.  Exact order at the size edges with distinct, fix-up-repaired and heavily repeated
+    depths (fallback to the 64-bit network), next to ordinary bins of the other launch."""
+    rng = np.random.default_rng(12)
+    sizes = [2049, 4096, 3000, 900, 2500, 4097, 6100, 2048, 3333, 3500]
+    m2, d = [], []
+    for k, c in enumerate(sizes):
+        m2.append(np.tile([16.0 * k + 8.0, 8.0], (c, 1)))
+        if k in (2, 6):
+            dk = rng.choice(rng.uniform(1, 50, 60), c)  # ~50-100 equal depths per value
+        elif k == 8:
+            dk = np.repeat(rng.uniform(1, 50, (c + 1) // 2), 2)[:c]  # equal pairs
+        elif k == 9:
+            dk = np.float32(7.0) + np.float32(1e-6) * rng.integers(0, 64, c)  # narrow span
+        else:
+            dk = rng.uniform(0.5, 80.0, c)
+        d.append(dk)
+    perm = rng.permutation(sum(sizes))
+    m2 = np.concatenate(m2)[perm].astype(np.float32)[None]
+    d = np.concatenate(d)[perm].astype(np.float32)[None]
+    r = np.ones((1, m2.shape[1]), np.int32)
+    tw, th = len(sizes), 1
+    tpg, ids, fl = O.isect_tiles(m2, r, d, 16, tw, th)
+    offs = O.isect_offsets(ids, 1, tw, th)
+    counts = np.diff(np.concatenate([offs.reshape(-1), [len(ids)]]))
+    assert counts.tolist() == sizes
+    gr, gm2, gd = to_dev(torch.from_numpy(r), torch.from_numpy(m2), torch.from_numpy(d))
+    gtpg, gids, gfl, goffs = G._isect_binned(gm2, gr, 16, tw, th, gd)
+    np.testing.assert_array_equal(gids.cpu().numpy(), ids)
+    np.testing.assert_array_equal(gfl.cpu().numpy(), fl)
+    np.testing.assert_array_equal(goffs.cpu().numpy(), offs)
+
+
 def test_isect_empty():
     r = torch.zeros(1, 10, dtype=torch.int32, device=DEV)
     m2 = torch.zeros(1, 10, 2, device=DEV)
