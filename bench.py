@@ -472,9 +472,18 @@ def measure(args, rank, world, dev):
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    step_t = [] if os.environ.get("HGSR_BENCH_STEP_TIMES") else None  # (diagnostic: host time per step)
+    seg0 = torch.cuda.memory_stats(dev).get("segment.all.allocated") if step_t is not None else None
     for _ in range(args.steps):
         wl.step()
+        if step_t is not None:
+            step_t.append(time.perf_counter())
     torch.cuda.synchronize(dev)
+    if step_t is not None:
+        ms = torch.cuda.memory_stats(dev)
+        print("step ms:", " ".join(f"{(b - a) * 1e3:.2f}" for a, b in zip([t0] + step_t[:-1], step_t)),
+              "| segments allocated", ms.get("segment.all.allocated"), "- before", seg0,
+              "| alloc retries", ms.get("num_alloc_retries"), "| gc counts", gc.get_count(), file=sys.stderr)
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
