@@ -451,23 +451,25 @@ def measure(args, rank, world, dev):
     """Warm up, time exactly args.steps steps (barrier + synchronize on both sides, max over
     ranks), then a per-kernel breakdown pass.  Returns the measurements of this workload."""
     wl = Workload(args, rank, dev)
-    for _ in range(args.warmup):
-        wl.step()
-    torch.cuda.synchronize(dev)
-    # the objects of the scene setup (and of an earlier workload in this process) are collected
-    # now, not by a generation-2 pass inside the timed steps
-    gc.collect()
-    # the optimizer moves the scene: intersections before / after the timed steps show the drift
-    isects_before = wl.meta["flatten_ids"].numel() if args.warmup else None
     timing = not args.no_timing
     # live HIP events inside the timed region on the dominant kernel only (the roofline);
     # the per-kernel breakdown comes from a separate pass after it
     dominant = "raster3d_bwd" if args.gs == "3d" else "raster2d_bwd"
-    if timing:
+    if timing:  # event pool and pair counters created now, not between the warmup and the timed steps
         NAT.call("hgsr_timing_reset")
         NAT.call("hgsr_timing_only", dominant.encode())
-        NAT.call("hgsr_timing_enable", 1)
         NAT.call("hgsr_timing_pairs", None, 1)  # the backward counts its visited / stepped pairs on the device
+    # the objects of the scene setup (and of an earlier workload in this process) are collected
+    # before the warmup: no generation-2 pass inside the timed steps, and no idle GPU between
+    # the warmup and the timed steps (a collection there left the first timed steps ~10 % slower)
+    gc.collect()
+    for _ in range(args.warmup):
+        wl.step()
+    torch.cuda.synchronize(dev)
+    # the optimizer moves the scene: intersections before / after the timed steps show the drift
+    isects_before = wl.meta["flatten_ids"].numel() if args.warmup else None
+    if timing:
+        NAT.call("hgsr_timing_enable", 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)

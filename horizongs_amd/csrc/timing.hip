@@ -20,6 +20,7 @@ std::vector<hipEvent_t> g_pool;
 std::vector<Rec> g_recs;
 size_t g_next = 0;
 constexpr size_t kMaxRecs = 1 << 16;
+constexpr size_t kPrealloc = 256;  // events created by hgsr_timing_enable
 std::string g_only;  // record only this kernel (empty = all)
 // device counters of the timed raster bwd: [0] (pixel, Gaussian) pairs visited (gsplat's span),
 // [1] lane-pairs stepped (compacted list entries x 64)
@@ -28,6 +29,16 @@ constexpr size_t kPairBytes = (size_t)kPairSlots * 2 * 16 * sizeof(unsigned long
 }  // namespace
 
 bool timing_on() { return g_on; }
+
+// the event pool is filled by reset / enable, outside the region being timed (creating
+// events there costs host time inside it); called with g_mu held
+static void prefill_pool() {
+    while (g_pool.size() < kPrealloc) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) break;
+        g_pool.push_back(e);
+    }
+}
 
 int timing_begin(const char* name, hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -84,6 +95,7 @@ using namespace hgsr;
 extern "C" int hgsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_on = on != 0;
+    if (g_on) prefill_pool();
     return HGSR_OK;
 }
 
@@ -96,6 +108,12 @@ extern "C" int hgsr_timing_only(const char* kernel) {
 extern "C" int hgsr_timing_pairs(unsigned long long* out, int reset) {
     std::lock_guard<std::mutex> lk(g_mu);
     unsigned long long v = 0;
+    // a reset allocates the counters now: their synchronous hipMalloc / hipMemset must not
+    // fall inside the timed steps (the first counted launch would drain the queue)
+    if (!g_pairs && reset) {
+        if (hipMalloc(&g_pairs, kPairBytes) != hipSuccess) return HGSR_ELAUNCH;
+        if (hipMemset(g_pairs, 0, kPairBytes) != hipSuccess) return HGSR_ELAUNCH;
+    }
     if (g_pairs) {
         if (int st = read_pairs(0, &v)) return st;
         if (reset && hipMemset(g_pairs, 0, kPairBytes) != hipSuccess) return HGSR_ELAUNCH;
@@ -117,6 +135,7 @@ extern "C" int hgsr_timing_reset(void) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_recs.clear();
     g_next = 0;
+    prefill_pool();
     return HGSR_OK;
 }
 
