@@ -602,8 +602,12 @@ def secondary(args, rank, world, dev):
                         "value": round(world * a.steps / r["dt"], 3), "unit": "views/s",
                         "ms_per_step": round(r["dt"] / a.steps * 1e3, 3), "steps": a.steps, "warmup": a.warmup,
                         "gaussians": int(r["wl"].last_colors.shape[0]), "n_isects": r["isects_after"],
-                        "roofline": None if roof is None else {k: roof[k] for k in (
-                            "bound", "kernel", "achieved", "frac", "frac_executed", "kernel_avg_ms")},
+                        "roofline": None if roof is None else dict(
+                            {k: roof[k] for k in ("bound", "kernel", "achieved", "frac", "frac_executed",
+                                                  "kernel_avg_ms", "pairs_per_launch", "executed_pairs_per_launch")},
+                            note=("frac prices gsplat's visited (pixel, Gaussian) pairs, including those the "
+                                  "per-quadrant culling skips, so it exceeds 1 where culling removes most of them "
+                                  "(clustered neural Gaussians); frac_executed prices the work actually executed")),
                         "decode_mfma": decode_mfma(r["wl"], r["kernels"]) if a.anchors else None,
                         "kernels": r["kernels"]})
         del r
