@@ -12,7 +12,12 @@
 
 namespace hgsr {
 
-constexpr int kFwd2Batch = 128;
+#ifndef HGSR_FWD2_BATCH
+#define HGSR_FWD2_BATCH 64
+#endif
+// records per forward batch (a multiple of 64): 64 -> 64 VGPRs, 12.6 KB of LDS, 8 waves / SIMD;
+// raster2d_fwd 0.682 -> 0.633 ms at c3 against 128 (25 KB, 6 waves)
+constexpr int kFwd2Batch = HGSR_FWD2_BATCH;
 constexpr int kBwd2Batch = 64;
 constexpr int kRec2 = 24;  // floats per accumulator row (96 B): 15 + D colour + 2 abs xy <= 21 used
 
