@@ -574,6 +574,8 @@ class _Raster2D(torch.autograd.Function):
         ctx.cfg = (width, height, tile_size)
         ctx.fwd_ws = ws  # packed surfel records, reused by the backward
         ctx.mark_non_differentiable(rd, rm)
+        ctx.set_materialize_grads(False)  # no zero-filled image grads for distort / median per step
+        ctx.out_shapes = (rc.shape, ra.shape, rn.shape)
         return rc, ra, rn, rd, rm
 
     @staticmethod
@@ -593,7 +595,8 @@ class _Raster2D(torch.autograd.Function):
         fwd_ws = ctx.fwd_ws
         ws_b = N.size_query("hgsr_raster2d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
         ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
-        v_rc, v_ra, v_rn = _f32(v_rc), _f32(v_ra), _f32(v_rn)
+        v_rc, v_ra, v_rn = (_f32(g if g is not None else torch.zeros(sh, dtype=torch.float32, device=dev))
+                            for g, sh in zip((v_rc, v_ra, v_rn), ctx.out_shapes))
         N.call("hgsr_raster2d_bwd", C, Ng, D, ptr(means2d), ptr(rt), ptr(colors), ptr(opacities), ptr(normals),
                ptr(backgrounds), width, height, tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
                ptr(flatten_ids) if flatten_ids.numel() else None, ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
@@ -666,6 +669,8 @@ class _Raster2DFused(torch.autograd.Function):
         ctx.fwd_ws = ws  # packed surfel records, reused by the backward
         ctx.qmask = qmask  # the forward's quadrant culling bits, reused by the backward
         ctx.mark_non_differentiable(rd, rm)
+        ctx.set_materialize_grads(False)  # no zero-filled image grads for distort / median per step
+        ctx.out_shapes = (rc.shape, ra.shape, rn.shape)
         return rc, ra, rn, rd, rm
 
     @staticmethod
@@ -687,7 +692,8 @@ class _Raster2DFused(torch.autograd.Function):
         fwd_ws = ctx.fwd_ws
         ws_b = N.size_query("hgsr_raster2d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
         ws, zeroed = _take_bwd_ws(ctx, ws_b, dev)
-        v_rc, v_ra, v_rn = _f32(v_rc), _f32(v_ra), _f32(v_rn)
+        v_rc, v_ra, v_rn = (_f32(g if g is not None else torch.zeros(sh, dtype=torch.float32, device=dev))
+                            for g, sh in zip((v_rc, v_ra, v_rn), ctx.out_shapes))
         N.call("hgsr_raster2d_bwd_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors), int(col_shared),
                ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(normals), ptr(backgrounds),
                width, height, tile_size, tw, th, ptr(offsets), flatten_ids.numel(),

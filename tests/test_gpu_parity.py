@@ -514,3 +514,35 @@ def test_reference_call_sites_run():
         else:
             radii = res[0]
             assert radii.shape == (1, 300) and bool((radii > 0).any())
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_2dgs_unused_outputs_get_no_grad_tensors(fused):
+    """The 2DGS raster Functions do not materialise zero grads (distort / median never have
+    one; colours-only losses leave alphas / normals without one): the gradients must equal
+    those of the same loss with the unused outputs added at weight 0 (up to the float-atomic
+    summation order of the backward's accumulator rows, which differs run to run)."""
+    sc = scene(n=300, seed=41)
+    means, quats, scales, opac, cols, vm, K = to_dev(sc.means, sc.quats, sc.scales, sc.opacities, sc.colors,
+                                                     sc.viewmats, sc.Ks)
+    W, H = sc.width, sc.height
+    grads = []
+    for weigh_all in (False, True):
+        ps = [t.clone().requires_grad_(True) for t in (means, quats, scales, opac, cols)]
+        if fused:
+            (rc, ra, rn, _nfd, rd, rm), _ = G.rasterization_2dgs(*ps, vm, K, W, H, render_mode="RGB+ED")
+        else:
+            rad, m2, dep, rt, nrm = G.fully_fused_projection_2dgs(ps[0], ps[1], ps[2], vm, None, K, W, H)
+            tw, th = (W + 15) // 16, (H + 15) // 16
+            _, ids, fl = G.isect_tiles(m2, rad, dep, 16, tw, th)
+            offs = G.isect_offset_encode(ids, 1, tw, th)
+            c4 = torch.cat([ps[4][None], dep[..., None]], dim=-1)
+            rc, ra, rn, rd, rm = G.rasterize_to_pixels_2dgs(m2, rt, c4, torch.sigmoid(ps[3])[None].contiguous(),
+                                                             nrm, None, W, H, 16, offs, fl)
+        loss = (rc[..., :3] * torch.linspace(0.1, 1.0, 3, device=DEV)).sum()
+        if weigh_all:
+            loss = loss + 0.0 * ra.sum() + 0.0 * rn.sum()
+        loss.backward()
+        grads.append([p.grad.clone() for p in ps])
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
