@@ -186,8 +186,10 @@ class Workload:
         # the reference optimizer (scene/lod_model.py:320): Adam(eps=1e-15), one group per tensor,
         # stepped every iteration (train.py:274-277) -- one fused HIP launch here
         self.optimizer = Adam([{"params": [p], "lr": lr} for p, lr in groups], lr=0.0, eps=1e-15)
-        # DDP over views: buckets follow the optimizer's current groups (densify surgery safe)
-        self.allreduce = GradientAllReduce(self.optimizer, bucket_mb=64.0)
+        # DDP over views: buckets follow the optimizer's current groups (densify surgery safe); the
+        # anchor model buckets _offset / _scaling / the cov MLP first: the decode backward hands
+        # their gradients over after its first head, so their all-reduce runs under the rest of it
+        self.allreduce = GradientAllReduce(self.optimizer, bucket_mb=64.0, order=getattr(self, "ddp_order", None))
 
     def _init_anchors(self, args, seed, dev):
         """SURVEY 8(d) decode-inclusive c2: anchors placed like the c2 Gaussians, feat ~ N(0, 0.1),
@@ -211,6 +213,7 @@ class Workload:
         self.cam_center = torch.zeros(3, device=dev)
         self.params = [self.anchor, self.feat, self.offset, self.scaling_raw] + [
             p for m in self.mlps for p in m.parameters()]
+        self.ddp_order = [self.offset, self.scaling_raw, *self.mlps[1].parameters(), self.feat, self.anchor]
         self.anchor_quats = torch.zeros(A, 4, device=dev)
         self.anchor_quats[:, 0] = 1.0  # get_rotation at init (_rotation is not trained)
         # LoD inputs of set_anchor_mask (every synthetic anchor on level 0: the test runs, all pass)

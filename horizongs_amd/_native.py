@@ -40,7 +40,7 @@ _SIGS = {
     "hgsr_isect_ws1_bytes": (SZ, [I, I, I, I]),
     "hgsr_isect_ws2_bytes": (SZ, [I64, I64]),
     "hgsr_isect_count": (I, [I, I, P, P, I, I, I, P, P, P, P, SZ, P]),
-    "hgsr_isect_emit_sorted": (I, [I, I, P, P, P, I, I, I, P, I64, I64, P, P, P, SZ, P, SZ, P]),
+    "hgsr_isect_emit_sorted": (I, [I, I, P, P, P, I, I, I, P, I64, I64, P, P, P, SZ, P, SZ, P, P]),
     "hgsr_isect_emit_unsorted": (I, [I, I, P, P, P, I, I, I, P, P, P, P]),
     "hgsr_isect_offset_encode": (I, [I64, P, I, I, I, P, P]),
     "hgsr_raster3d_fwd_ws_bytes": (SZ, [I, I, I]),
@@ -55,12 +55,12 @@ _SIGS = {
     "hgsr_raster3d_qmask_bytes": (SZ, [I, I, I, I64]),
     "hgsr_raster3d_pack_fused": (I, [I, I, I, P, P, P, I, P, P, I, P, SZ, P]),
     "hgsr_raster3d_fwd_packed": (I, [I, I, I, I, I, P, I, I, I, I, I, P, I64, P, P, P, P, P, SZ, P, SZ, P, SZ,
-                                     P]),
+                                     P, P]),
     "hgsr_raster2d_fwd_ws_bytes": (SZ, [I, I, I]),
     "hgsr_raster2d_fwd": (I, [I, I, I, P, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, SZ, P]),
     "hgsr_raster2d_pack_fused": (I, [I, I, I, P, P, P, I, P, P, I, P, P, SZ, P]),
     "hgsr_raster2d_fwd_packed": (I, [I, I, I, I, I, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, SZ, P, SZ,
-                                     P, SZ, P]),
+                                     P, SZ, P, P]),
     "hgsr_raster2d_bwd_ws_bytes": (SZ, [I, I, I, I]),
     "hgsr_raster2d_bwd": (I, [I, I, I, P, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, P,
                               P, P, P, P, SZ, P]),
@@ -73,7 +73,7 @@ _SIGS = {
     "hgsr_decode_count": (I, [I, I, I, I, I, P, P, P, P, P, P, SZ, P, P, P]),
     "hgsr_decode_fwd": (I, [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P]),
     "hgsr_decode_bwd_ws_bytes": (SZ, [I]),
-    "hgsr_decode_bwd": (I, [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P]),
+    "hgsr_decode_bwd": (I, [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, SZ, P]),
     "hgsr_loss_ws_bytes": (SZ, [I, I, I]),
     "hgsr_training_statis": (I, [I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "hgsr_voxel_dedup_ws_bytes": (SZ, [I64]),

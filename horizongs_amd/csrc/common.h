@@ -105,6 +105,9 @@ __host__ __device__ __forceinline__ int64_t qmask_word0(int64_t start, int64_t b
 __host__ __device__ __forceinline__ int64_t qmask_stride(int64_t n_isects, int64_t n_bins) {
     return (n_isects + 63) / 64 + n_bins + 4;
 }
+// the stride of a caller-sized quadrant-mask buffer (4 arrays of 64-bit words): forward and
+// backward derive it from the same buffer, which may be sized for a capacity above n_isects
+inline int64_t qmask_stride_of(size_t qmask_bytes) { return (int64_t)(qmask_bytes / (4 * sizeof(uint64_t))); }
 
 // count floats from src to LDS dst (16-B aligned) as float4 runs when src allows
 __device__ __forceinline__ void stage_floats(const float* __restrict__ src, int count, float* dst) {

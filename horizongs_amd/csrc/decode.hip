@@ -1065,28 +1065,28 @@ static int decode_grid(int Av) {
     return n_tiles < 1024 ? (n_tiles > 0 ? n_tiles : 1) : 1024;
 }
 
-// Workgroups of one decode launch (grid-stride over 64-anchor tiles): at most what is resident at once on the device (the
-// kernel's occupancy x CUs), so the grid-stride tiles run in one round.  1024 workgroups of
-// the 3-per-CU opacity-head backward left a second round a third full.
+// Workgroups of one decode launch (grid-stride over 64-anchor tiles): what an MI355X holds
+// resident at once (the kernel's occupancy per CU x 256 CUs), so the grid-stride tiles run in
+// one round (1024 workgroups of the 3-per-CU opacity-head backward left a second round a third
+// full).  The CU count is the MI355X's constant, not the device's: the backward's weight
+// gradients are summed over per-workgroup partials, so the grid fixes their summation order,
+// and a grid that depended on the device (a partitioned GPU, another SKU) would change their
+// last bits from machine to machine.  The occupancy is a property of the compiled gfx950 code.
+constexpr int kGridCUs = 256;
 static int grid_resident(const void* kernel, int Av) {
     static std::mutex mu;
-    static std::map<std::pair<int, const void*>, int> cache;  // (device, kernel) -> resident workgroups
-    int dev = 0;
-    static const bool fixed = getenv("HGSR_DEC_GRID_FIXED") != nullptr;  // (A/B knob: the old 1024 cap)
-    if (fixed || hipGetDevice(&dev) != hipSuccess) return decode_grid(Av);
+    static std::map<const void*, int> cache;  // kernel -> resident workgroups
     int resident = 0;
     {
         std::lock_guard<std::mutex> lk(mu);
-        auto it = cache.find({dev, kernel});
+        auto it = cache.find(kernel);
         if (it != cache.end()) {
             resident = it->second;
         } else {
-            int per_cu = 0, n_cu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess ||
-                hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                per_cu = n_cu = 0;
-            resident = per_cu * n_cu;
-            cache[{dev, kernel}] = resident;
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess) per_cu = 0;
+            resident = per_cu * kGridCUs;
+            cache[kernel] = resident;
         }
     }
     const int g = decode_grid(Av);  // the backward's workspace bound
@@ -1203,8 +1203,8 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
                                const float* cam_center, const float* const* mlp, const int32_t* slot_row,
                                const float* g_xyz, const float* g_offsets, const float* g_color,
                                const float* g_opacity, const float* g_scaling, const float* g_rot, float* d_anchor,
-                               float* d_feat, float* d_offset, float* d_scaling, float* const* d_mlp, void* ws,
-                               size_t ws_bytes, hgsr_stream_t stream) {
+                               float* d_feat, float* d_offset, float* d_scaling, float* const* d_mlp, int head_mask,
+                               void* ws, size_t ws_bytes, hgsr_stream_t stream) {
     const DecodeDims d = decode_dims(Av, view_dim, n_offsets, color_dim);
     if (int st = check_decode(Av, F, view_dim, n_offsets, color_dim, d)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_decode_bwd_ws_bytes(Av), "decode_bwd workspace too small");
@@ -1222,7 +1222,13 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
                                             ~(size_t)255));
     const int K1 = kDecF + view_dim;
     KernelTimer kt("decode_bwd", s);
-    for (int head = 0; head < 3; ++head) {
+    // the cov head first: after it d_offset, d_scaling and the cov weights are final, so a
+    // caller (multi-GPU) can start reducing them while the opacity and colour heads run
+    static const int kOrder[3] = {1, 0, 2};
+    const int mask = head_mask ? head_mask : 7;
+    for (int hi = 0; hi < 3; ++hi) {
+        const int head = kOrder[hi];
+        if (!((mask >> head) & 1)) continue;
         // up to 5 output tiles per launch (the cov head in one launch; measured: splitting it
         // into 3 + 2 tiles gains nothing, its time is the per-tile work, not the accumulators)
         const int chunk = kBwdChunk;

@@ -256,13 +256,26 @@ __global__ __launch_bounds__(1024) void isect_binscan_kernel(int n_bins, const i
 }
 
 // ---------------------------------------------------------------- stage 4
+// Deferred count (info != nullptr): the emission was sized by the host from a capacity
+// (cap keys, bins up to mb_cap) before it read the count; info = {n_isects, largest bin,
+// overflow}.  Every block tests the capacity itself, block 0 publishes the verdict in
+// info[2] for the sort and raster kernels that follow on the stream, and an overflowed
+// emission writes nothing (the host re-runs it at the exact size).
+__device__ __forceinline__ bool emit_overflow(int64_t* info, int64_t cap, int64_t mb_cap) {
+    if (!info) return false;
+    const bool ovf = info[0] > cap || info[1] > mb_cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) info[2] = ovf ? 1 : 0;
+    return ovf;
+}
+
 __global__ __launch_bounds__(256) void isect_emit_lds_kernel(
     int64_t CN, int N, int per_block, const float2* __restrict__ means2d,
     const int32_t* __restrict__ radii, const float* __restrict__ depths, int tile_size, int tw,
     int th, int n_tiles, int n_bins, const int32_t* __restrict__ offsets,
     const int32_t* __restrict__ blockhist, const int32_t* __restrict__ chunk_pre, uint64_t* __restrict__ keys,
-    int phases) {
+    int phases, int64_t* __restrict__ info, int64_t cap, int64_t mb_cap) {
     extern __shared__ __attribute__((aligned(16))) int s_cur[];
+    if (emit_overflow(info, cap, mb_cap)) return;
     // Logical block = XCD-contiguous remap of the dispatch index: the blocks resident on one
     // XCD hold consecutive slices of every bin, so their scattered 8-B key writes to a bin
     // land in adjacent addresses of the same L2 and leave it as whole lines.
@@ -321,7 +334,9 @@ __global__ __launch_bounds__(256) void isect_emit_lds_kernel(
 __global__ __launch_bounds__(256) void isect_emit_global_kernel(
     int64_t CN, int N, const float2* __restrict__ means2d, const int32_t* __restrict__ radii,
     const float* __restrict__ depths, int tile_size, int tw, int th, int n_tiles,
-    int32_t* __restrict__ cursor, uint64_t* __restrict__ keys) {
+    int32_t* __restrict__ cursor, uint64_t* __restrict__ keys, int64_t* __restrict__ info, int64_t cap,
+    int64_t mb_cap) {
+    if (emit_overflow(info, cap, mb_cap)) return;
     const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (o >= CN) return;
     const int32_t r = radii[o];
@@ -779,12 +794,14 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(int n_bins, int n_tiles,
                                                         int64_t n_isects, uint64_t* __restrict__ keys,
                                                         uint64_t* __restrict__ tmp,
                                                         int64_t* __restrict__ isect_ids,
-                                                        int32_t* __restrict__ flatten_ids) {
+                                                        int32_t* __restrict__ flatten_ids,
+                                                        const int64_t* __restrict__ info) {
     // 64-bit network scratch, or (32-bit path) the full keys + the 32-bit network's scratch
     __shared__ uint64_t s_keys[BIG ? 4096 + 8 * kSortPitch : 2048 + 4 * kSortPitch];
+    if (info && info[2]) return;  // deferred count over capacity: nothing was emitted
     const int bin = blockIdx.x;
     const int64_t start = offsets[bin];
-    const int64_t end = bin + 1 < n_bins ? (int64_t)offsets[bin + 1] : n_isects;
+    const int64_t end = bin + 1 < n_bins ? (int64_t)offsets[bin + 1] : (info ? info[0] : n_isects);
     const int n = (int)(end - start);
     if (n <= 0 || (n <= kSortCap) == BIG) return;
     const int cam = bin / n_tiles, tile = bin - cam * n_tiles;
@@ -974,7 +991,9 @@ extern "C" int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const 
                                       const float* depths, int tile_size, int tile_w, int tile_h,
                                       const int32_t* isect_offsets, int64_t n_isects, int64_t max_bin,
                                       int64_t* isect_ids, int32_t* flatten_ids, void* ws1, size_t ws1_bytes,
-                                      void* ws2, size_t ws2_bytes, hgsr_stream_t stream) {
+                                      void* ws2, size_t ws2_bytes, int64_t* isect_info, hgsr_stream_t stream) {
+    // isect_info (nullable): deferred count -- n_isects / max_bin are then capacities and the
+    // device-resident count decides (emit_overflow)
     HGSR_REQUIRE(C >= 1 && N >= 0 && tile_size > 0 && tile_w > 0 && tile_h > 0, "bad dims");
     HGSR_REQUIRE(ws1_bytes >= hgsr_isect_ws1_bytes(C, N, tile_w, tile_h), "isect ws1 too small");
     HGSR_REQUIRE(ws2_bytes >= hgsr_isect_ws2_bytes(n_isects, max_bin), "isect ws2 too small");
@@ -991,21 +1010,22 @@ extern "C" int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const 
         hipLaunchKernelGGL(isect_emit_lds_kernel, dim3(g.n_blocks), dim3(256), g.n_bins * 4, s, g.CN, N,
                            g.per_block, reinterpret_cast<const float2*>(means2d), radii, depths, tile_size,
                            tile_w, tile_h, g.n_tiles, g.n_bins, isect_offsets, w.blockhist, w.chunk_pre, keys,
-                           emit_phases(tile_h));
+                           emit_phases(tile_h), isect_info, n_isects, max_bin);
     } else {
         hipLaunchKernelGGL(copy_i32_kernel, dim3((g.n_bins + 255) / 256), dim3(256), 0, s, g.n_bins,
                            isect_offsets, w.cursor);
         hipLaunchKernelGGL(isect_emit_global_kernel, dim3((unsigned)((g.CN + 255) / 256)), dim3(256), 0, s, g.CN,
                            N, reinterpret_cast<const float2*>(means2d), radii, depths, tile_size, tile_w, tile_h,
-                           g.n_tiles, w.cursor, keys);
+                           g.n_tiles, w.cursor, keys, isect_info, n_isects, max_bin);
     }
     if (int st = check_launch("isect_emit")) return st;
     KernelTimer kt("tile_sort", s);
     hipLaunchKernelGGL(tile_sort_kernel<false>, dim3(g.n_bins), dim3(256), 0, s, g.n_bins, g.n_tiles,
-                       nbits64(g.n_tiles), isect_offsets, n_isects, keys, tmp, isect_ids, flatten_ids);
+                       nbits64(g.n_tiles), isect_offsets, n_isects, keys, tmp, isect_ids, flatten_ids, isect_info);
     if (max_bin > kSortCap)
         hipLaunchKernelGGL(tile_sort_kernel<true>, dim3(g.n_bins), dim3(256), 0, s, g.n_bins, g.n_tiles,
-                           nbits64(g.n_tiles), isect_offsets, n_isects, keys, tmp, isect_ids, flatten_ids);
+                           nbits64(g.n_tiles), isect_offsets, n_isects, keys, tmp, isect_ids, flatten_ids,
+                           isect_info);
     return check_launch("tile_sort");
 }
 

@@ -29,8 +29,11 @@ struct Tile2 {
     int64_t pix;
 };
 
+// info (nullable): a deferred count's device-resident {n_isects, largest bin, overflow}, as
+// in raster3d.hip tile_ctx
 __device__ __forceinline__ Tile2 tile2_ctx(int C, int W, int H, int tw, int th,
-                                           const int32_t* __restrict__ offsets, int64_t n_isects) {
+                                           const int32_t* __restrict__ offsets, int64_t n_isects,
+                                           const int64_t* __restrict__ info = nullptr) {
     Tile2 t;
     const int n_tiles = tw * th;
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -45,7 +48,9 @@ __device__ __forceinline__ Tile2 tile2_ctx(int C, int W, int H, int tw, int th,
     t.py = (float)t.i + 0.5f;
     const int64_t bin = (int64_t)t.cam * n_tiles + t.tile;
     t.start = offsets[bin];
-    t.end = (bin == (int64_t)C * n_tiles - 1) ? (int32_t)n_isects : offsets[bin + 1];
+    const int64_t n = info ? info[0] : n_isects;
+    t.end = (bin == (int64_t)C * n_tiles - 1) ? (int32_t)n : offsets[bin + 1];
+    if (info && info[2]) t.end = t.start;
     t.pix = ((int64_t)t.cam * H + t.i) * W + t.j;
     return t;
 }
@@ -259,7 +264,7 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     float* __restrict__ render_normals,
     float* __restrict__ render_distort, float* __restrict__ render_median, int32_t* __restrict__ last_ids,
     int32_t* __restrict__ median_ids, uint64_t* __restrict__ qmask, int64_t qstride, float4* __restrict__ zero_rows,
-    int64_t zero_n4) {
+    int64_t zero_n4, const int64_t* __restrict__ isect_info) {
     constexpr int NB = kFwd2Batch;
     // one LDS object: every component of record t sits at a compile-time offset from one address;
     // double-buffered and filled by LDS-DMA one batch ahead (no staging VGPRs: 96 -> 72 VGPRs)
@@ -268,7 +273,7 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     } sr;
     __shared__ uint8_t s_list[4][NB];
     __shared__ int s_vote[2][4];
-    const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects);
+    const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects, isect_info);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
@@ -330,7 +335,10 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
             if (qw && lane == k && k * 64 < cnt) qw[k] = m;  // only words holding records of this tile
         }
         if (n_mine == 0) continue;
-        const int lst0 = my_list[lane], lst1 = my_list[64 + lane];
+        static_assert(NB == 64 || NB == 128, "list registers hold 64 or 128 entries");
+        const int lst0 = my_list[lane];
+        // the second half exists only for 128-record batches (s_list rows are NB long)
+        const int lst1 = NB > 64 ? my_list[(NB > 64 ? 64 : 0) + lane] : 0;
         auto step = [&](const int t) {
             const float4 r0 = s_r0[t], r1 = s_r1[t], r2 = s_r2[t], c = s_col[t], r4 = s_r4[t];
             const Hit2 h = hit2(r0, r1, r2, tc.px, tc.py);
@@ -360,7 +368,7 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
             step(__builtin_amdgcn_readlane(lst0, i));
             if (__all(T < 0.f)) break;
         }
-        if (i == n0)
+        if (NB > 64 && i == n0)
             for (; i < n_mine; ++i) {
                 step(__builtin_amdgcn_readlane(lst1, i - 64));
                 if (__all(T < 0.f)) break;
@@ -739,7 +747,8 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
                                float* render_alphas, float* render_normals, float* render_distort,
                                float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s,
-                               uint64_t* qmask = nullptr, float* zero_rows = nullptr, size_t zero_bytes = 0);
+                               uint64_t* qmask = nullptr, int64_t qstride = 0, float* zero_rows = nullptr,
+                               size_t zero_bytes = 0, const int64_t* isect_info = nullptr);
 
 static int raster2d_fwd_impl(int C, int N, int D, const float* means2d, const float* rt, const ChanSrc& cs,
                              const float* normals, const float* backgrounds, int bg_ch, int ed_ch, int width,
@@ -770,17 +779,17 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
                                float* render_alphas, float* render_normals, float* render_distort,
                                float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s,
-                               uint64_t* qmask, float* zero_rows, size_t zero_bytes) {
+                               uint64_t* qmask, int64_t qstride, float* zero_rows, size_t zero_bytes,
+                               const int64_t* isect_info) {
     const dim3 grid(C * tile_w * tile_h);
     float4* const z4 = reinterpret_cast<float4*>(zero_rows);
     const int64_t zn4 = (int64_t)(zero_bytes / sizeof(float4));
-    const int64_t qstride = qmask_stride(n_isects, (int64_t)C * tile_w * tile_h);
     KernelTimer kt("raster2d_fwd", s);
 #define LAUNCH_F2(DD)                                                                                            \
     hipLaunchKernelGGL(raster2d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,     \
                        backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,           \
                        render_alphas, render_normals, render_distort, render_median, last_ids, median_ids, qmask,   \
-                       qstride, z4, zn4)
+                       qstride, z4, zn4, isect_info)
     switch (D) {
         case 1: LAUNCH_F2(1); break;
         case 2: LAUNCH_F2(2); break;
@@ -849,7 +858,7 @@ extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, in
                                         float* render_normals, float* render_distort, float* render_median,
                                         int32_t* last_ids, int32_t* median_ids, const void* records,
                                         size_t records_bytes, void* qmask, size_t qmask_bytes, void* bwd_ws,
-                                        size_t bwd_ws_bytes, hgsr_stream_t stream) {
+                                        size_t bwd_ws_bytes, const int64_t* isect_info, hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || with_depth), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !with_depth), "expected_depth needs depths");
     const int D = Dc + (with_depth ? 1 : 0);
@@ -868,7 +877,8 @@ extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, in
     return raster2d_fwd_launch(C, D, (const Rec2*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
                                tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
                                render_normals, render_distort, render_median, last_ids, median_ids,
-                               as_stream(stream), (uint64_t*)qmask, (float*)bwd_ws, bwd_ws ? rows_b : 0);
+                               as_stream(stream), (uint64_t*)qmask, qmask_stride_of(qmask_bytes), (float*)bwd_ws,
+                               bwd_ws ? rows_b : 0, isect_info);
 }
 
 extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
@@ -885,7 +895,7 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* v_render_alphas, const float* v_render_normals, float* v_means2d,
                              float* v_rt, const ChanDst& cd, float* v_normals, float* v_densify,
                              const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream, const uint64_t* qmask = nullptr,
-                             bool rows_zeroed = false) {
+                             size_t qmask_bytes = 0, bool rows_zeroed = false) {
     if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
                  "raster2d_bwd workspace too small");
@@ -924,7 +934,7 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     }
     const dim3 grid(C * tile_w * tile_h);
     unsigned long long* const pairs = timing_pair_counter("raster2d_bwd");
-    const int64_t qstride = qmask_stride(n_isects, (int64_t)C * tile_w * tile_h);
+    const int64_t qstride = qmask_stride_of(qmask_bytes);
 #define LAUNCH_B2(DD)                                                                                             \
     {                                                                                                             \
         KernelTimer kt("raster2d_bwd", s);                                                                        \
@@ -990,5 +1000,6 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                              expected_depth ? Dc : -1, render_colors, width, height, tile_size, tile_w, tile_h,
                              isect_offsets, n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
                              v_render_alphas, v_render_normals, v_means2d, v_ray_transforms, cd, v_normals,
-                             v_densify, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask, ws_zeroed != 0);
+                             v_densify, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask, qmask_bytes,
+                             ws_zeroed != 0);
 }

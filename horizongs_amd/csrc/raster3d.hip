@@ -34,8 +34,12 @@ struct TileCtx {
     int64_t pix;
 };
 
+// info (nullable): the device-resident {n_isects, largest bin, overflow} of a deferred
+// intersection count (hgsr_isect_emit_sorted with isect_info): the last bin ends at info[0],
+// and an overflowed emission (capacity exceeded; the host re-runs it) leaves every tile empty
 __device__ __forceinline__ TileCtx tile_ctx(int C, int W, int H, int tw, int th,
-                                            const int32_t* __restrict__ offsets, int64_t n_isects) {
+                                            const int32_t* __restrict__ offsets, int64_t n_isects,
+                                            const int64_t* __restrict__ info = nullptr) {
     TileCtx t;
     const int n_tiles = tw * th;
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -50,7 +54,9 @@ __device__ __forceinline__ TileCtx tile_ctx(int C, int W, int H, int tw, int th,
     t.py = (float)t.i + 0.5f;
     const int64_t bin = (int64_t)t.cam * n_tiles + t.tile;
     t.start = offsets[bin];
-    t.end = (bin == (int64_t)C * n_tiles - 1) ? (int32_t)n_isects : offsets[bin + 1];
+    const int64_t n = info ? info[0] : n_isects;
+    t.end = (bin == (int64_t)C * n_tiles - 1) ? (int32_t)n : offsets[bin + 1];
+    if (info && info[2]) t.end = t.start;
     t.pix = ((int64_t)t.cam * H + t.i) * W + t.j;
     return t;
 }
@@ -160,7 +166,7 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     int bg_ch, int ed_ch, const int32_t* __restrict__ offsets, int64_t n_isects,
     const int32_t* __restrict__ flatten_ids, float* __restrict__ render_colors, float* __restrict__ render_alphas,
     int32_t* __restrict__ last_ids, uint64_t* __restrict__ qmask, int64_t qstride, float4* __restrict__ zero_rows,
-    int64_t zero_n4) {
+    int64_t zero_n4, const int64_t* __restrict__ isect_info) {
     // slot kFwdBatch is a zero-opacity dummy used to pad the per-wave lists
     __shared__ float4 s_g0[kFwdBatch + 1];
     __shared__ float4 s_g1[kFwdBatch + 1];
@@ -170,7 +176,7 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     // keeps the offset, rebased once per batch
     __shared__ uint32_t s_list[4][kFwdBatch + 4];
     __shared__ int s_vote[2][4];
-    const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
+    const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects, isect_info);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;   // centre of this wave's quadrant
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
@@ -759,7 +765,8 @@ static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backg
                                int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
                                float* render_alphas, int32_t* last_ids, hipStream_t s, uint64_t* qmask = nullptr,
-                               float* zero_rows = nullptr, size_t zero_bytes = 0);
+                               int64_t qstride = 0, float* zero_rows = nullptr, size_t zero_bytes = 0,
+                               const int64_t* isect_info = nullptr);
 
 static int raster3d_fwd_impl(int C, int N, int D, const float* means2d, const float* conics, const ChanSrc& cs,
                              const float* backgrounds, int bg_ch, int ed_ch, int width, int height, int tile_size,
@@ -783,16 +790,15 @@ static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backg
                                int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
                                float* render_alphas, int32_t* last_ids, hipStream_t s, uint64_t* qmask,
-                               float* zero_rows, size_t zero_bytes) {
+                               int64_t qstride, float* zero_rows, size_t zero_bytes, const int64_t* isect_info) {
     const dim3 grid(C * tile_w * tile_h);
     float4* const z4 = reinterpret_cast<float4*>(zero_rows);
     const int64_t zn4 = (int64_t)(zero_bytes / sizeof(float4));
-    const int64_t qstride = qmask_stride(n_isects, (int64_t)C * tile_w * tile_h);
     KernelTimer kt("raster3d_fwd", s);
 #define LAUNCH_F(DD)                                                                                           \
     hipLaunchKernelGGL(raster3d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,    \
                        backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,          \
-                       render_alphas, last_ids, qmask, qstride, z4, zn4)
+                       render_alphas, last_ids, qmask, qstride, z4, zn4, isect_info)
     switch (D) {
         case 1: LAUNCH_F(1); break;
         case 2: LAUNCH_F(2); break;
@@ -853,7 +859,7 @@ extern "C" int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, in
                                         const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                                         int32_t* last_ids, const void* records, size_t records_bytes,
                                         void* qmask, size_t qmask_bytes, void* bwd_ws, size_t bwd_ws_bytes,
-                                        hgsr_stream_t stream) {
+                                        const int64_t* isect_info, hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || with_depth), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !with_depth), "expected_depth needs depths");
     const int D = Dc + (with_depth ? 1 : 0);
@@ -867,9 +873,12 @@ extern "C" int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, in
     const size_t rows_b = (size_t)C * N * kRec3 * sizeof(float);
     HGSR_REQUIRE(!bwd_ws || (bwd_ws_bytes >= rows_b && (reinterpret_cast<uintptr_t>(bwd_ws) & 15) == 0),
                  "raster3d_fwd_packed: bwd_ws too small or not 16-B aligned");
+    // the quadrant-mask stride follows the buffer (sized for the capacity of a deferred count;
+    // the backward, given the same buffer, derives the same stride)
     return raster3d_fwd_launch(C, D, (const Rec3*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
                                tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
-                               last_ids, as_stream(stream), (uint64_t*)qmask, (float*)bwd_ws, bwd_ws ? rows_b : 0);
+                               last_ids, as_stream(stream), (uint64_t*)qmask, qmask_stride_of(qmask_bytes),
+                               (float*)bwd_ws, bwd_ws ? rows_b : 0, isect_info);
 }
 
 extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
@@ -885,7 +894,8 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* render_alphas, const int32_t* last_ids, const float* v_render_colors,
                              const float* v_render_alphas, float* v_means2d, float* v_conics, const ChanDst& cd,
                              float* v_means2d_abs, const void* fwd_ws, void* ws, size_t ws_bytes,
-                             hgsr_stream_t stream, const uint64_t* qmask = nullptr, bool rows_zeroed = false) {
+                             hgsr_stream_t stream, const uint64_t* qmask = nullptr, size_t qmask_bytes = 0,
+                             bool rows_zeroed = false) {
     if (int st = check_raster(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
                  "raster3d_bwd workspace too small");
@@ -923,7 +933,7 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     }
     const dim3 grid(C * tile_w * tile_h);
     unsigned long long* const pairs = timing_pair_counter("raster3d_bwd");
-    const int64_t qstride = qmask_stride(n_isects, (int64_t)C * tile_w * tile_h);
+    const int64_t qstride = qmask_stride_of(qmask_bytes);
     const bool abs = v_means2d_abs != nullptr;
 #define LAUNCH_B(DD, AA)                                                                                       \
     {                                                                                                          \
@@ -992,5 +1002,5 @@ extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2
                              render_colors, width, height, tile_size, tile_w, tile_h, isect_offsets, n_isects,
                              flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, v_means2d,
                              v_conics, cd, v_means2d_abs, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask,
-                             ws_zeroed != 0);
+                             qmask_bytes, ws_zeroed != 0);
 }

@@ -212,6 +212,9 @@ class _Decode(torch.autograd.Function):
         del arr
         ctx.save_for_backward(anchor, feat, offset, scaling_raw, cam_center, vis_idx, slot_row, *w)
         ctx.cfg = cfg
+        # the autograd inputs whose gradients are final after the backward's cov head (handed to
+        # an early-gradient hook, set_early_grad_hook); weights[4:8] are the cov head's
+        ctx.inputs = (offset, scaling_raw, *weights[4:8])
         sel = mask.view(torch.bool)  # 0/1 bytes: a view, no conversion kernel
         # the output row of every selected slot IS the exclusive cumsum of the selection mask:
         # training_statis takes it from here instead of recomputing it
@@ -242,11 +245,31 @@ class _Decode(torch.autograd.Function):
         ws_b = N.size_query("hgsr_decode_bwd_ws_bytes", Av)
         ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
         g = [None if x is None else _f32(x) for x in (g_xyz, g_offs, g_color, g_opac, g_scaling, g_rot)]
-        N.call("hgsr_decode_bwd", Av, F, view_dim, n_off, color_dim, ptr(vis_idx), ptr(anchor), ptr(feat),
-               ptr(offset), ptr(scaling_raw), ptr(cam_center), mlp, ptr(slot_row), *[ptr(x) for x in g],
-               ptr(d_anchor), ptr(d_feat), ptr(d_offset), ptr(d_scaling), dmlp, ptr(ws), ws_b, N.stream(dev))
+        hook = _EARLY_GRAD[0]
+        # with a data-parallel reducer attached: the cov head first (head_mask 2), whose end makes
+        # d_offset, d_scaling and the cov weights final; their all-reduce is launched while the
+        # opacity and colour heads run (head_mask 5).  Otherwise all heads in one call.
+        for mask in ((2, 5) if hook is not None else (0,)):
+            N.call("hgsr_decode_bwd", Av, F, view_dim, n_off, color_dim, ptr(vis_idx), ptr(anchor), ptr(feat),
+                   ptr(offset), ptr(scaling_raw), ptr(cam_center), mlp, ptr(slot_row), *[ptr(x) for x in g],
+                   ptr(d_anchor), ptr(d_feat), ptr(d_offset), ptr(d_scaling), dmlp, mask, ptr(ws), ws_b,
+                   N.stream(dev))
+            if mask == 2:
+                src = ctx.inputs  # (offset, scaling_raw, the four cov-head tensors), the autograd inputs
+                hook([(src[0], d_offset), (src[1], d_scaling)] + list(zip(src[2:], d_w[4:8])))
         del arr, darr
         return (d_anchor, d_feat, d_offset, d_scaling, None, None, None, *d_w)
+
+
+_EARLY_GRAD = [None]
+
+
+def set_early_grad_hook(fn):
+    """fn([(input tensor, its final gradient), ...]) is called by the decode backward as soon as
+    the listed gradients are final on the stream (before the rest of the backward is enqueued):
+    multigpu.GradientAllReduce installs its early-reduction entry here for the duration of a
+    data-parallel step.  None removes it."""
+    _EARLY_GRAD[0] = fn
 
 
 def decode(anchor, feat, offset, scaling_raw, cam_center, mlps, visible=None, view_dim=3, n_offsets=10,

@@ -253,6 +253,24 @@ def _tile_grid(width, height, tile_size):
 
 
 _pinned = threading.local()
+# Deferred intersection count: rasterization() enqueues the emission, the sort
+# and the raster forward into capacity-sized buffers BEFORE it reads the count, so the one
+# host wait of a view lands behind queued work instead of draining the queue.  The capacity
+# comes from the previous view of the same camera grid; an overflow (device-detected, the
+# kernels then write nothing) is redone at the exact size.  HGSR_DEFER_ISECT=0: the
+# synchronous order (count -> host -> emit), as gsplat does it.
+_DEFER = os.environ.get("HGSR_DEFER_ISECT", "1") != "0"
+_pred = {}  # (device, C, tile_w, tile_h) -> (n_isects, largest bin) of the last view
+_CAP_GRAIN = 1 << 18  # capacities in steps of 256K keys: stable sizes for the caching allocator
+
+
+def _capacity(n, max_bin):
+    """(key capacity, largest-bin capacity) for a view predicted to have n keys: 12.5 % + 64K of
+    headroom; bins sort in classes (<= 2048 keys: one launch, <= 4096: the big-bin launch, more:
+    merge scratch), so the bin capacity is the class of the predicted largest bin."""
+    cap = (int(n * 1.125) + 65536 + _CAP_GRAIN - 1) // _CAP_GRAIN * _CAP_GRAIN
+    m = int(max_bin * 1.125) + 64
+    return cap, (2048 if m <= 2048 else (4096 if m <= 4096 else 1 << 30))
 
 
 def _host_info_buffer():
@@ -275,29 +293,38 @@ def _isect_count(means2d, radii, tile_size, tile_width, tile_height, depths):
     radii = radii.contiguous()
     tpg = torch.empty((C, Ng), dtype=torch.int32, device=dev)
     offsets = torch.empty((C, tile_height, tile_width), dtype=torch.int32, device=dev)
-    info = torch.empty(2, dtype=torch.int64, device=dev)
+    info = torch.empty(3, dtype=torch.int64, device=dev)  # {n_isects, largest bin, overflow (deferred)}
     ws1_b = N.size_query("hgsr_isect_ws1_bytes", C, Ng, tile_width, tile_height)
     ws1 = torch.empty(max(ws1_b, 1), dtype=torch.uint8, device=dev)
     s = N.stream(dev)
     N.call("hgsr_isect_count", C, Ng, ptr(m2), ptr(radii), tile_size, tile_width, tile_height, ptr(tpg),
            ptr(offsets), ptr(info), ptr(ws1), ws1_b, s)
     host = _host_info_buffer()
-    host.copy_(info, non_blocking=True)
+    host.copy_(info[:2], non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
-    return (m2, dep, radii, tpg, offsets, ws1, ws1_b, host, ev, tile_size, tile_width, tile_height)
+    return (m2, dep, radii, tpg, offsets, ws1, ws1_b, host, ev, info, tile_size, tile_width, tile_height)
+
+
+def _isect_count_host(st):
+    """Wait for the count's copy (not for the queue behind it) -> (n_isects, largest bin);
+    remembered as the next view's capacity prediction."""
+    m2, radii, host, ev, tw, th = st[0], st[2], st[7], st[8], st[11], st[12]
+    ev.synchronize()
+    n_isects, max_bin = int(host[0]), int(host[1])
+    _pred[(m2.device.index, radii.shape[0], tw, th)] = (n_isects, max_bin)
+    return n_isects, max_bin
 
 
 @torch.no_grad()
 def _isect_finish(st):
-    """Stage 2: wait for the count (the one host sync of a view; gsplat has it too), then
-    emit + sort -> (tiles_per_gauss, isect_ids, flatten_ids, isect_offsets)."""
-    m2, dep, radii, tpg, offsets, ws1, ws1_b, host, ev, tile_size, tile_width, tile_height = st
+    """Stage 2, synchronous: wait for the count (gsplat's host sync), then emit + sort ->
+    (tiles_per_gauss, isect_ids, flatten_ids, isect_offsets)."""
+    m2, dep, radii, tpg, offsets, ws1, ws1_b, host, ev, info, tile_size, tile_width, tile_height = st
     C, Ng = radii.shape
     dev = m2.device
     s = N.stream(dev)
-    ev.synchronize()
-    n_isects, max_bin = int(host[0]), int(host[1])
+    n_isects, max_bin = _isect_count_host(st)
     isect_ids = torch.empty(n_isects, dtype=torch.int64, device=dev)
     flatten_ids = torch.empty(n_isects, dtype=torch.int32, device=dev)
     if n_isects > 0:
@@ -305,8 +332,48 @@ def _isect_finish(st):
         ws2 = torch.empty(ws2_b, dtype=torch.uint8, device=dev)
         N.call("hgsr_isect_emit_sorted", C, Ng, ptr(m2), ptr(radii), ptr(dep), tile_size, tile_width,
                tile_height, ptr(offsets), n_isects, max_bin, ptr(isect_ids), ptr(flatten_ids), ptr(ws1), ws1_b,
-               ptr(ws2), ws2_b, s)
+               ptr(ws2), ws2_b, None, s)
     return tpg, isect_ids, flatten_ids, offsets
+
+
+class _Deferred:
+    """Capacity-sized intersection arrays of a deferred count; n is set by _isect_resolve."""
+    __slots__ = ("ids", "flat", "ws2", "info", "cap", "mbcap", "n")
+
+
+@torch.no_grad()
+def _isect_emit_deferred(st):
+    """Stage 2 enqueued before the count is read (None without a prediction for this camera
+    grid: the first view takes the synchronous path)."""
+    if not _DEFER:
+        return None
+    m2, dep, radii, tpg, offsets, ws1, ws1_b, host, ev, info, tile_size, tile_width, tile_height = st
+    C, Ng = radii.shape
+    p = _pred.get((m2.device.index, C, tile_width, tile_height))
+    if p is None:
+        return None
+    dev = m2.device
+    d = _Deferred()
+    d.cap, d.mbcap = _capacity(*p)
+    d.ids = torch.empty(d.cap, dtype=torch.int64, device=dev)
+    d.flat = torch.empty(d.cap, dtype=torch.int32, device=dev)
+    ws2_b = N.size_query("hgsr_isect_ws2_bytes", d.cap, d.mbcap)
+    d.ws2 = torch.empty(ws2_b, dtype=torch.uint8, device=dev)
+    d.info, d.n = info, None
+    N.call("hgsr_isect_emit_sorted", C, Ng, ptr(m2), ptr(radii), ptr(dep), tile_size, tile_width, tile_height,
+           ptr(offsets), d.cap, d.mbcap, ptr(d.ids), ptr(d.flat), ptr(ws1), ws1_b, ptr(d.ws2), ws2_b, ptr(info),
+           N.stream(dev))
+    return d
+
+
+def _isect_resolve(st, d):
+    """After the raster forward is enqueued: read the count (its copy finished long ago, so the
+    host does not drain the queue).  True when it fit the capacities; d.n = n_isects."""
+    n_isects, max_bin = _isect_count_host(st)
+    if n_isects > d.cap or max_bin > d.mbcap:
+        return False  # the kernels wrote nothing: the caller redoes it at the exact size
+    d.n = n_isects
+    return True
 
 
 def _isect_binned(means2d, radii, tile_size, tile_width, tile_height, depths):
@@ -405,12 +472,16 @@ class _Raster3D(torch.autograd.Function):
         return v_means2d, v_conics, v_colors, v_opac, v_bg, None, None, None, None, None, None
 
 
-def _bwd_ws(size_fn, ctx, C, Ng, D, dev):
+def _bwd_ws(size_fn, ctx, C, Ng, D, dev, grad_mode):
     """The raster backward's workspace (records reused), allocated by the forward when a
     backward can follow: the forward kernel clears its accumulator rows while it composites,
-    so the backward needs no memset (hgsr_raster{3,2}d_fwd_packed bwd_ws)."""
+    so the backward needs no memset (hgsr_raster{3,2}d_fwd_packed bwd_ws).  grad_mode is the
+    CALLER's torch.is_grad_enabled() (inside forward() grad mode is always off, and
+    needs_input_grad follows requires_grad only): an evaluation render under no_grad()
+    allocates and clears nothing."""
     ctx.bwd_ws = None
-    if not any(ctx.needs_input_grad) or os.environ.get("HGSR_RASTER_PREZERO", "1") == "0":  # (A/B knob)
+    if (not grad_mode or not any(ctx.needs_input_grad)
+            or os.environ.get("HGSR_RASTER_PREZERO", "1") == "0"):  # (A/B knob)
         return None
     ws_b = N.size_query(size_fn, C, Ng, D, 1)
     ctx.bwd_ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
@@ -449,7 +520,8 @@ class _Raster3DFused(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means2d, conics, colors, depths, opacities, backgrounds, width, height, tile_size,
-                isect_offsets, flatten_ids, expected_depth, absgrad, records=None):
+                isect_offsets, flatten_ids, expected_depth, absgrad, records=None, grad_mode=True, deferred=None):
+        """deferred (_Deferred): flatten_ids is its capacity-sized array, the count device-resident."""
         C, Ng = means2d.shape[:2]
         Dc = 0 if colors is None else colors.shape[-1]
         D = Dc + (0 if depths is None else 1)
@@ -467,11 +539,12 @@ class _Raster3DFused(torch.autograd.Function):
             q_b = N.size_query("hgsr_raster3d_qmask_bytes", C, tw, th, flatten_ids.numel())
             qmask = torch.empty(q_b, dtype=torch.uint8, device=dev)
             # the backward's workspace, its accumulator rows cleared by this forward launch
-            bwd_ws = _bwd_ws("hgsr_raster3d_bwd_ws_bytes", ctx, C, Ng, D, dev)
+            bwd_ws = _bwd_ws("hgsr_raster3d_bwd_ws_bytes", ctx, C, Ng, D, dev, grad_mode)
             N.call("hgsr_raster3d_fwd_packed", C, Ng, Dc, int(depths is not None), int(expected_depth),
                    ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
                    ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(ws),
-                   ws.numel(), ptr(qmask), q_b, ptr(bwd_ws), 0 if bwd_ws is None else bwd_ws.numel(), N.stream(dev))
+                   ws.numel(), ptr(qmask), q_b, ptr(bwd_ws), 0 if bwd_ws is None else bwd_ws.numel(),
+                   None if deferred is None else ptr(deferred.info), N.stream(dev))
         else:
             ws_b = N.size_query("hgsr_raster3d_fwd_ws_bytes", C, Ng, D)
             ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
@@ -485,6 +558,7 @@ class _Raster3DFused(torch.autograd.Function):
         ctx.cfg = (width, height, tile_size, expected_depth, absgrad, Dc, col_shared, op_shared)
         ctx.fwd_ws = ws  # packed raster records, reused by the backward
         ctx.qmask = qmask
+        ctx.deferred = deferred
         return rc, ra
 
     @staticmethod
@@ -505,10 +579,10 @@ class _Raster3DFused(torch.autograd.Function):
         ws_b = N.size_query("hgsr_raster3d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
         ws, zeroed = _take_bwd_ws(ctx, ws_b, dev)
         v_rc, v_ra = _f32(v_rc), _f32(v_ra)
+        n_is = flatten_ids.numel() if ctx.deferred is None else ctx.deferred.n  # exact once resolved
         N.call("hgsr_raster3d_bwd_fused", C, Ng, Dc, ptr(means2d), ptr(conics), ptr(colors), int(col_shared),
                ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(backgrounds), width, height,
-               tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
-               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
+               tile_size, tw, th, ptr(offsets), n_is, ptr(flatten_ids) if n_is else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_means2d), ptr(v_conics), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_abs), ptr(fwd_ws),
                ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(), zeroed, N.stream(dev))
         if absgrad:
@@ -517,7 +591,7 @@ class _Raster3DFused(torch.autograd.Function):
         if backgrounds is not None and ctx.needs_input_grad[5]:
             v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))
         return (v_means2d, v_conics, v_colors, v_depths, v_opac, v_bg, None, None, None, None, None, None, None,
-                None)
+                None, None, None)
 
 
 def rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_height, tile_size, isect_offsets,
@@ -627,7 +701,7 @@ class _Raster2DFused(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means2d, rt, colors, depths, opacities, normals, densify, backgrounds, width, height,
-                tile_size, isect_offsets, flatten_ids, expected_depth, records=None):
+                tile_size, isect_offsets, flatten_ids, expected_depth, records=None, grad_mode=True, deferred=None):
         C, Ng = means2d.shape[:2]
         Dc = 0 if colors is None else colors.shape[-1]
         D = Dc + (0 if depths is None else 1)
@@ -649,12 +723,13 @@ class _Raster2DFused(torch.autograd.Function):
             q_b = N.size_query("hgsr_raster3d_qmask_bytes", C, tw, th, flatten_ids.numel())
             qmask = torch.empty(q_b, dtype=torch.uint8, device=dev)
             # the backward's workspace, its accumulator rows cleared by this forward launch
-            bwd_ws = _bwd_ws("hgsr_raster2d_bwd_ws_bytes", ctx, C, Ng, D, dev)
+            bwd_ws = _bwd_ws("hgsr_raster2d_bwd_ws_bytes", ctx, C, Ng, D, dev, grad_mode)
             N.call("hgsr_raster2d_fwd_packed", C, Ng, Dc, int(depths is not None), int(expected_depth),
                    ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
                    ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(rn), ptr(rd), ptr(rm),
                    ptr(last), ptr(med), ptr(ws), ws.numel(), ptr(qmask), q_b, ptr(bwd_ws),
-                   0 if bwd_ws is None else bwd_ws.numel(), N.stream(dev))
+                   0 if bwd_ws is None else bwd_ws.numel(), None if deferred is None else ptr(deferred.info),
+                   N.stream(dev))
         else:
             ws_b = N.size_query("hgsr_raster2d_fwd_ws_bytes", C, Ng, D)
             ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
@@ -668,6 +743,7 @@ class _Raster2DFused(torch.autograd.Function):
         ctx.cfg = (width, height, tile_size, expected_depth, Dc, col_shared, op_shared)
         ctx.fwd_ws = ws  # packed surfel records, reused by the backward
         ctx.qmask = qmask  # the forward's quadrant culling bits, reused by the backward
+        ctx.deferred = deferred
         ctx.mark_non_differentiable(rd, rm)
         ctx.set_materialize_grads(False)  # no zero-filled image grads for distort / median per step
         ctx.out_shapes = (rc.shape, ra.shape, rn.shape)
@@ -694,10 +770,10 @@ class _Raster2DFused(torch.autograd.Function):
         ws, zeroed = _take_bwd_ws(ctx, ws_b, dev)
         v_rc, v_ra, v_rn = (_f32(g if g is not None else torch.zeros(sh, dtype=torch.float32, device=dev))
                             for g, sh in zip((v_rc, v_ra, v_rn), ctx.out_shapes))
+        n_is = flatten_ids.numel() if ctx.deferred is None else ctx.deferred.n  # exact once resolved
         N.call("hgsr_raster2d_bwd_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors), int(col_shared),
                ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(normals), ptr(backgrounds),
-               width, height, tile_size, tw, th, ptr(offsets), flatten_ids.numel(),
-               ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
+               width, height, tile_size, tw, th, ptr(offsets), n_is, ptr(flatten_ids) if n_is else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_rn), ptr(v_means2d), ptr(v_rt), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_normals),
                ptr(v_dens), ptr(fwd_ws), ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(),
                zeroed, N.stream(dev))
@@ -705,7 +781,7 @@ class _Raster2DFused(torch.autograd.Function):
         if backgrounds is not None and ctx.needs_input_grad[7]:
             v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))
         return (v_means2d, v_rt, v_colors, v_depths, v_opac, v_normals, v_dens, v_bg, None, None, None, None, None,
-                None, None)
+                None, None, None, None)
 
 
 def rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals, densify, image_width,
@@ -795,11 +871,22 @@ def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, 
         r_in = (_f32(means2d), _f32(conics), _f32(cols) if rgb else None, _f32(depths) if with_depth else None,
                 _f32(opacities))
         records = _Raster3DFused.pack(*(t.detach() if t is not None else None for t in r_in))
-        tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
         bgs = None if (backgrounds is None or not rgb) else _f32(backgrounds)
-        render_colors, render_alphas = _Raster3DFused.apply(
-            *r_in, bgs, int(width), int(height), int(tile_size), isect_offsets.contiguous(),
-            flatten_ids.contiguous(), render_mode in ("ED", "RGB+ED"), absgrad, records)
+        args = (bgs, int(width), int(height), int(tile_size))
+        ed, grad_mode = render_mode in ("ED", "RGB+ED"), torch.is_grad_enabled()
+        tpg, isect_offsets = isect_state[3], isect_state[4]
+        d = _isect_emit_deferred(isect_state)
+        if d is not None:  # emission, sort and forward queued; then the count is read
+            render_colors, render_alphas = _Raster3DFused.apply(*r_in, *args, isect_offsets, d.flat, ed, absgrad,
+                                                                records, grad_mode, d)
+            if _isect_resolve(isect_state, d):
+                isect_ids, flatten_ids = d.ids[:d.n], d.flat[:d.n]
+            else:
+                d = None  # over capacity: nothing was emitted or composited; redo at the exact size
+        if d is None:
+            tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
+            render_colors, render_alphas = _Raster3DFused.apply(*r_in, *args, isect_offsets, flatten_ids, ed,
+                                                                absgrad, records, grad_mode)
         opac = opacities.expand(C, -1)
     else:
         tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
@@ -923,12 +1010,22 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
         r_in = (_f32(means2d), _f32(ray_transforms.reshape(C, Ng, 9)), _f32(cols) if rgb else None,
                 _f32(depths) if with_depth else None, _f32(opacities), _f32(normals))
         records = _Raster2DFused.pack(*(t.detach() if t is not None else None for t in r_in))
-        tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
         bgs = None if (backgrounds is None or not rgb) else _f32(backgrounds)
         opac = opacities.expand(C, -1)
-        render_colors, render_alphas, render_normals, render_distort, render_median = _Raster2DFused.apply(
-            *r_in[:5], r_in[5], densifications, bgs, int(width), int(height), int(tile_size),
-            isect_offsets.contiguous(), flatten_ids.contiguous(), render_mode in ("ED", "RGB+ED"), records)
+        args = (densifications, bgs, int(width), int(height), int(tile_size))
+        ed, grad_mode = render_mode in ("ED", "RGB+ED"), torch.is_grad_enabled()
+        tpg, isect_offsets = isect_state[3], isect_state[4]
+        d = _isect_emit_deferred(isect_state)
+        if d is not None:  # emission, sort and forward queued; then the count is read
+            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, d.flat, ed, records, grad_mode, d)
+            if _isect_resolve(isect_state, d):
+                isect_ids, flatten_ids = d.ids[:d.n], d.flat[:d.n]
+            else:
+                d = None  # over capacity: redo at the exact size
+        if d is None:
+            tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
+            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, flatten_ids, ed, records, grad_mode)
+        render_colors, render_alphas, render_normals, render_distort, render_median = outs
     else:
         tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
         opac = opacities.repeat(C, 1)

@@ -53,19 +53,31 @@ class GradientAllReduce:
       elementwise, so the per-bucket launches give bit-identical parameters to one launch
       over everything (tests/test_multigpu_gloo.py).
 
+    * Early gradients: between begin() and finish() the fused anchor decode's backward hands over
+      the gradients that are final after its first (cov) head -- _offset, _scaling and the cov
+      MLP -- through decode.set_early_grad_hook, so their buckets are all-reduced while the
+      opacity and colour heads still run; `order` puts those parameters in the first buckets
+      (buckets launch in bucket order on every rank).
+
     Usage per step: ``red.begin()`` before backward, ``loss.backward()``, then either
     ``red.finish()`` + ``optimizer.step()`` or ``red.finish(step=optimizer.step_params)``.
     Exactly ONE backward may run between begin() and finish(): a gradient that arrives for a
     bucket already in flight raises.  ``red()`` = begin-less synchronous form for grads
-    already computed."""
+    already computed.
 
-    def __init__(self, params_or_optimizer, bucket_mb: float = 64.0, group=None):
+    order: parameters in the order they should be bucketed (those not listed follow, in reverse
+    registration order) -- the order their gradients become final, e.g. (offset, scaling, cov MLP,
+    feat, anchor, opacity MLP, colour MLP) for the anchor model."""
+
+    def __init__(self, params_or_optimizer, bucket_mb: float = 64.0, group=None, order=None):
         self.source = params_or_optimizer
         self.group = group
+        self.order = order
         self.cap = max(1, int(bucket_mb * (1 << 20) // 4))
         self._key = None
         self._hooks = []
         self.buckets: List[dict] = []
+        self._in_step = False  # between begin() and finish(): the hooks copy into buckets
 
     # ---------------------------------------------------------------- setup
     def _params(self) -> List[torch.Tensor]:
@@ -91,7 +103,13 @@ class GradientAllReduce:
         self._hooks = []
         self.buckets = []
         cur, size = [], 0
-        for p in reversed(params):
+        seq = list(reversed(params))
+        if self.order is not None:
+            ids = {id(p) for p in params}
+            first = [p for p in self.order if id(p) in ids]
+            fid = {id(p) for p in first}
+            seq = first + [p for p in seq if id(p) not in fid]
+        for p in seq:
             n = p.numel()
             if cur and size + n > self.cap:
                 self.buckets.append(cur)
@@ -118,7 +136,7 @@ class GradientAllReduce:
         # flat = [grads of every parameter | one presence slot per parameter]
         flat = torch.empty(o + len(params), dtype=torch.float32, device=dev)
         return {"params": params, "offs": offs, "n": o, "flat": flat, "ready": [False] * len(params),
-                "work": None, "launched": False}
+                "early": [False] * len(params), "work": None, "launched": False}
 
     # ---------------------------------------------------------------- per step
     def begin(self) -> None:
@@ -129,13 +147,42 @@ class GradientAllReduce:
         self._next = 0
         for b in self.buckets:
             b["ready"] = [False] * len(b["params"])
+            b["early"] = [False] * len(b["params"])
             b["work"], b["launched"] = None, False
+        self._in_step = True
+        from . import decode
+        decode.set_early_grad_hook(self.early)
+
+    def early(self, pairs) -> None:
+        """Gradients final before the backward ends ([(parameter, gradient)], decode backward):
+        copied into their buckets now, and the buckets that became complete are launched."""
+        if not self._in_step:
+            return
+        for p, g in pairs:
+            loc = self._where.get(id(p))
+            if loc is None or g is None:
+                continue
+            b = self.buckets[loc[0]]
+            k = loc[1]
+            if b["launched"] or b["ready"][k]:
+                continue
+            dst = b["flat"][b["offs"][k]:b["offs"][k] + p.numel()].view_as(p)
+            torch.mul(g.reshape(p.shape), 1.0 / self.world, out=dst)
+            b["flat"][b["n"] + k] = 1.0
+            b["ready"][k] = b["early"][k] = True
+        self._launch_ready()
 
     def _on_grad(self, p) -> None:
-        if not self._active() or p.grad is None:
+        # hooks stay registered between steps: a backward outside begin()/finish() (e.g. before
+        # the synchronous red()) leaves the gradient alone
+        if not self._in_step or not self._active() or p.grad is None:
             return
         bi, k = self._where[id(p)]
         b = self.buckets[bi]
+        if b["early"][k]:  # handed over by early(): autograd's copy of the same gradient arrives now
+            b["early"][k] = False
+            p.grad = b["flat"][b["offs"][k]:b["offs"][k] + p.numel()].view_as(p)
+            return
         if b["launched"] or b["ready"][k]:
             raise RuntimeError("hgsr GradientAllReduce: a second gradient arrived for a parameter in this step (its "
                                "bucket's all-reduce may already be in flight); exactly one backward is allowed "
@@ -174,6 +221,9 @@ class GradientAllReduce:
             if step is not None:
                 step(self._params())
             return
+        self._in_step = False  # later gradients (a backward outside begin()/finish()) are not bucketed
+        from . import decode
+        decode.set_early_grad_hook(None)
         while self._next < len(self.buckets):
             self._launch(self.buckets[self._next])
             self._next += 1

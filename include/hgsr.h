@@ -120,7 +120,14 @@ int hgsr_sh_rgb_bwd(int degree, int C, int N, int K, const float* means, const f
  *     isect_ids [n_isects] (cam<<(32+tile_bits) | tile<<32 | depth bits) and
  *     flatten_ids [n_isects], bit-identical to a stable radix sort of gsplat's
  *     Gaussian-major emission.
- * The same `ws1` must be passed to both stages. */
+ * The same `ws1` must be passed to both stages.
+ * Deferred count (isect_info != NULL, the `info` of stage 1 allocated as 3 x int64): stage 2
+ *   is enqueued BEFORE the host reads the count, n_isects / max_bin being the caller's
+ *   capacities (isect_ids / flatten_ids / ws2 sized for them).  The kernels read the true
+ *   count from info[0..1]; when it exceeds a capacity they emit nothing and set info[2] = 1
+ *   (else 0), and hgsr_raster{3,2}d_fwd_packed given the same info composite nothing.  The
+ *   caller checks the count it copies back and re-runs stage 2 at the exact size on overflow.
+ *   Otherwise the first info[0] entries of isect_ids / flatten_ids are the sorted result. */
 size_t hgsr_isect_ws1_bytes(int C, int N, int tile_w, int tile_h);
 size_t hgsr_isect_ws2_bytes(int64_t n_isects, int64_t max_bin);
 int hgsr_isect_count(int C, int N, const float* means2d, const int32_t* radii, int tile_size,
@@ -130,7 +137,7 @@ int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const int32_t* ra
                            const float* depths, int tile_size, int tile_w, int tile_h,
                            const int32_t* isect_offsets, int64_t n_isects, int64_t max_bin,
                            int64_t* isect_ids, int32_t* flatten_ids, void* ws1,
-                           size_t ws1_bytes, void* ws2, size_t ws2_bytes,
+                           size_t ws1_bytes, void* ws2, size_t ws2_bytes, int64_t* isect_info,
                            hgsr_stream_t stream);
 /* gsplat isect_tiles(sort=False): Gaussian-major emission; cum_tiles = inclusive
  * prefix sum of tiles_per_gauss over the flattened [C*N]. */
@@ -198,7 +205,10 @@ int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * OVERWRITTEN where the forward visits a tile (the backward reads only those bits).
  * bwd_ws (nullable, 16-B aligned, >= hgsr_raster3d_bwd_ws_bytes(C, N, D, 1)): the workspace
  * the backward will get; the forward clears its accumulator rows while it composites (HBM
- * is idle there), so hgsr_raster3d_bwd_fused given it with ws_zeroed = 1 skips its memset. */
+ * is idle there), so hgsr_raster3d_bwd_fused given it with ws_zeroed = 1 skips its memset.
+ * isect_info (nullable): the deferred count of hgsr_isect_emit_sorted (n_isects is then the
+ * capacity the intersection arrays and qmask were sized for); the quadrant-mask stride is
+ * derived from qmask_bytes, so the backward must get the same buffer and size. */
 size_t hgsr_raster3d_qmask_bytes(int C, int tile_w, int tile_h, int64_t n_isects);
 int hgsr_raster3d_pack_fused(int C, int N, int Dc, const float* means2d, const float* conics,
                              const float* colors, int colors_shared, const float* depths,
@@ -210,7 +220,7 @@ int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_
                              const int32_t* flatten_ids, float* render_colors, float* render_alphas,
                              int32_t* last_ids, const void* records, size_t records_bytes,
                              void* qmask, size_t qmask_bytes, void* bwd_ws, size_t bwd_ws_bytes,
-                             hgsr_stream_t stream);
+                             const int64_t* isect_info, hgsr_stream_t stream);
 /* vjp of hgsr_raster3d_fwd_fused: v_colors in the colours' layout (shared colours
  * summed over cameras in camera order), v_depths [C,N] (when depths), v_opacities
  * in the opacities' layout; render_colors is the forward output (needed for ED);
@@ -275,7 +285,8 @@ int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * intersection count, then composited; they stay valid as hgsr_raster2d_bwd_fused's fwd_ws.
  * qmask (nullable; size hgsr_raster3d_qmask_bytes, the same layout): the forward's
  * per-quadrant culling bits, read by hgsr_raster2d_bwd_fused instead of repeating the tests.
- * bwd_ws / ws_zeroed: as hgsr_raster3d_fwd_packed (size hgsr_raster2d_bwd_ws_bytes(C, N, D, 1)). */
+ * bwd_ws / ws_zeroed / isect_info: as hgsr_raster3d_fwd_packed (size
+ * hgsr_raster2d_bwd_ws_bytes(C, N, D, 1)). */
 int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                              const float* colors, int colors_shared, const float* depths,
                              const float* opacities, int opacities_shared, const float* normals, void* ws,
@@ -287,7 +298,7 @@ int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_
                              float* render_normals, float* render_distort, float* render_median,
                              int32_t* last_ids, int32_t* median_ids, const void* records,
                              size_t records_bytes, void* qmask, size_t qmask_bytes, void* bwd_ws,
-                             size_t bwd_ws_bytes, hgsr_stream_t stream);
+                             size_t bwd_ws_bytes, const int64_t* isect_info, hgsr_stream_t stream);
 int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                             const float* colors, int colors_shared, const float* depths,
                             int expected_depth, const float* opacities, int opacities_shared,
@@ -343,8 +354,12 @@ int hgsr_decode_fwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
  * d_anchor [A,3] (nullable), d_feat [A,F], d_scaling [A,6] (d w.r.t. the raw
  * _scaling parameter) and the 12 weight gradients d_mlp (same order as mlp);
  * d_offset [A, n_offsets, 3] rows of visible anchors are written.  Weight
- * gradients are reduced in a fixed order (deterministic).  ws:
- * hgsr_decode_bwd_ws_bytes(Av). */
+ * gradients are reduced in a fixed order (deterministic; the launch grids are fixed by the
+ * compiled code, not the device, so the bits are the same on every MI355X).
+ * head_mask (bit 0 opacity, 1 cov, 2 colour; 0 = all): the heads this call runs, cov first.
+ * After the cov head d_offset, d_scaling and the cov weights are final: a data-parallel
+ * caller runs {cov}, launches their all-reduce, then {opacity, colour} (the other
+ * accumulations continue).  ws: hgsr_decode_bwd_ws_bytes(Av). */
 size_t hgsr_decode_bwd_ws_bytes(int Av);
 int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
                     const int32_t* vis_idx, const float* anchor, const float* feat,
@@ -352,8 +367,8 @@ int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
                     const float* const* mlp, const int32_t* slot_row, const float* g_xyz,
                     const float* g_offsets, const float* g_color, const float* g_opacity,
                     const float* g_scaling, const float* g_rot, float* d_anchor, float* d_feat,
-                    float* d_offset, float* d_scaling, float* const* d_mlp, void* ws,
-                    size_t ws_bytes, hgsr_stream_t stream);
+                    float* d_offset, float* d_scaling, float* const* d_mlp, int head_mask,
+                    void* ws, size_t ws_bytes, hgsr_stream_t stream);
 
 /* ---- K13: normals from the rendered depth (2DGS) -------------------------------
  * replaces the gsplat fork's depth_to_normal (torch, ~25 launches incl. two 3 x 3 x HW GEMMs

@@ -294,6 +294,12 @@ def set_hitform(form, dtype=np.float32):
     _fn(dtype, "set_hitform")(I32(int(form)))
 
 
+def set_pixmask(mask, dtype=np.float32):
+    """Raster forwards composite only pixels whose mask byte is set (hgsr_oracle.c set_pixmask;
+    None clears).  The caller keeps `mask` (uint8, C-contiguous [C*rows*W]) alive while set."""
+    _fn(dtype, "set_pixmask")(None if mask is None else _p(mask))
+
+
 def set_alphaform(form, dtype=np.float32):
     """3DGS alpha evaluation of one build: 0 gsplat's exp(-sigma), 1 the kernels' log2(e)-scaled
     conic with explicit FMAs and exp2 (hgsr_oracle.c vis3)."""

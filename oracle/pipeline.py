@@ -25,6 +25,9 @@ class _Band:
     # near-threshold decision lists of the raster calls (hgsr_oracle.c set_near): None, or the
     # dict of oracle.set_near (record mode: thr > 0, filled by forward(); force mode: thr = 0)
     decisions = None
+    # uint8 [C*rows*W] or None: the raster calls composite only these pixels (hgsr_oracle.c
+    # set_pixmask) -- for branch candidates whose other pixels are never read
+    pixmask = None
 
     @property
     def Hr(self):
@@ -38,10 +41,14 @@ class _Band:
             def __enter__(self):
                 if band.decisions is not None:
                     O.set_near(band.decisions, band.dt)
+                if band.pixmask is not None:
+                    O.set_pixmask(band.pixmask, band.dt)
 
             def __exit__(self, *exc):
                 if band.decisions is not None:
                     O.set_near(None, band.dt)
+                if band.pixmask is not None:
+                    O.set_pixmask(None, band.dt)
         return _Ctx()
 
     def _shape(self):

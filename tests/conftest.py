@@ -26,3 +26,15 @@ def oracle_mod():
     from oracle import oracle
     oracle.build()
     return oracle
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """The raster parity tests' element-wise strict rates (tests/parity_report.py), printed at
+    the end of every run so the suite's own log carries them (also with -q)."""
+    try:
+        from tests import parity_report
+    except Exception:
+        return
+    if parity_report.RECORDS:
+        terminalreporter.write_sep("=", "raster parity: strict rates")
+        terminalreporter.write_line(parity_report.table())

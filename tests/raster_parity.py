@@ -29,6 +29,7 @@ import torch
 from horizongs_amd import gsplat_api as G
 from oracle import pipeline as OP
 from oracle.checks import ATOL, DELTA_2D, DELTA_3D, MAX_GRAD_AMBIGUOUS, RTOL, ambiguous, cond_close, image_close
+from tests import parity_report as PR
 
 DEV = "cuda:0"
 # bare 1e-5 abs / 1e-4 rel pass rate the RGB image must keep against the f32 oracle
@@ -78,8 +79,9 @@ def _closest(pix, lst, j):
 def resolve_branches(make, r32, r64, amb, vals, last, alt32=None):
     """Branch the GPU took at every near-threshold pixel.
 
-    make(dtype, near) -> a forwarded oracle of that precision with decision lists `near` (None:
-    record mode at NEAR_THR; a dict: force mode, hgsr_oracle.c set_near); vals: list of (GPU
+    make(dtype, near, pixmask=None) -> a forwarded oracle of that precision with decision lists
+    `near` (None: record mode at NEAR_THR; a dict: force mode, hgsr_oracle.c set_near),
+    compositing only the pixels of pixmask when given; vals: list of (GPU
     image [C,rows,W,K], f32 oracle image, f64 oracle image, attribute name of the image on the
     oracle object); last: GPU last ids [C,rows,W] (indices into the f32 oracle's intersection
     list, which the GPU's equals); alt32(near) -> a second correct f32
@@ -139,7 +141,9 @@ def resolve_branches(make, r32, r64, amb, vals, last, alt32=None):
             x = np.maximum(x, (np.abs(np.asarray(a, np.float64) - b) / bar).reshape(shape + (-1,)).max(-1))
         return x
 
-    errs = np.stack([err(make(np.float64, lst)) for lst in cand_lists])  # [candidates, C, rows, W]
+    # each candidate forward composites only the near-threshold pixels (the only ones read)
+    pm = np.ascontiguousarray(amb.reshape(-1), np.uint8)
+    errs = np.stack([err(make(np.float64, lst, pm)) for lst in cand_lists])  # [candidates, C, rows, W]
     fits = errs <= 1.0
     best = np.argmax(fits, 0)  # the first fitting candidate in preference order
     ok = amb & fits.any(0)
@@ -243,10 +247,27 @@ def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None
         if k == "colors" and not Dc:
             continue
         rates["v_" + k] = cond_close(v.cpu().numpy(), gr32[k], gr64[k], "v_" + k, rel_floor=0, env=genv[k])
+    # element-wise report against the gsplat-form f32, the kernel-form f32 (the kernels' alpha
+    # arithmetic) and f64 (tests/parity_report.py); images on their unambiguous pixels
+    rk = OP.Raster3D(*args, alphaform=1, **kw)
+    rk.forward()
+    gk32 = rk.backward(vrc.numpy(), vra.numpy())
+    px = ~np.asarray(amb, bool)
+    for nm, sl in (("render_rgb", slice(0, Dc)), ("render_depth", slice(Dc, o.shape[-1]))):
+        if sl.stop > sl.start:
+            PR.tensor(nm, o[..., sl], rc[..., sl], rk.render_colors[..., sl], r64.render_colors[..., sl],
+                      mask=np.broadcast_to(px[..., None], o[..., sl].shape))
+    PR.tensor("render_alpha", alpha.detach()[:, :rr].cpu().numpy(), ra, rk.ra, r64.ra,
+              mask=np.broadcast_to(px[..., None], ra.shape))
+    for k, v in got.items():
+        if k == "colors" and not Dc:
+            continue
+        PR.tensor("v_" + k, v.cpu().numpy(), gr32[k], gk32[k], gr64[k])
     # near-threshold pixels: resolve the branch the GPU took, then check the gradients again with
     # their upstream gradient kept, against the oracle evaluated on those branches
-    def make(dt, near):
+    def make(dt, near, pixmask=None):
         r = OP.Raster3D(*args, dtype=dt, **kw)
+        r.pixmask = pixmask
         if near is None:
             r.record_near(NEAR_THR)
         else:
@@ -359,10 +380,21 @@ def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
     for k, v in got.items():
         rates["v_" + k] = cond_close(v.cpu().numpy(), gr32[k], gr64[k], "v_" + k, rel_floor=0, env=genv[k],
                                      alt32=gr32b[k])
+    # element-wise report: gsplat-form (per-pixel cross product) f32, kernel-form (plane-form
+    # hit) f32 and f64 (tests/parity_report.py); images on their unambiguous pixels
+    px = ~np.asarray(amb, bool)
+    for nm, a, b, k, c in (("render_rgb", o[..., :3], rc[..., :3], rb[..., :3], r64.render_colors[..., :3]),
+                           ("render_depth", o[..., 3:], rc[..., 3:], rb[..., 3:], r64.render_colors[..., 3:]),
+                           ("render_alpha", alpha.detach()[:, :rr].cpu().numpy(), ra, r32b.ra, r64.ra),
+                           ("render_normals", normals.detach()[:, :rr].cpu().numpy(), rn, r32b.rn, r64.rn)):
+        PR.tensor(nm, a, b, k, c, mask=np.broadcast_to(px[..., None], a.shape))
+    for k, v in got.items():
+        PR.tensor("v_" + k, v.cpu().numpy(), gr32[k], gr32b[k], gr64[k])
     # near-threshold pixels: resolve the GPU's branch, then the gradients again with their upstream kept
 
-    def make(dt, near):
+    def make(dt, near, pixmask=None):
         r = OP.Raster2D(*args, dtype=dt, **kw)
+        r.pixmask = pixmask
         if near is None:
             r.record_near(NEAR_THR)
         else:

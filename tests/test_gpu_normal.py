@@ -44,7 +44,8 @@ def _depth(C, H, W, seed):
     return (base[None] + 0.05 * torch.randn(C, H, W, generator=g))[..., None].float()
 
 
-@pytest.mark.parametrize("C,H,W,z_depth", [(1, 48, 64, True), (2, 37, 53, True), (1, 40, 40, False)])
+@pytest.mark.parametrize("C,H,W,z_depth", [(1, 48, 64, True), (2, 37, 53, True), (1, 40, 40, False),
+                                           (1, 1080, 1920, True)])  # c3's size (1080p)
 def test_depth_to_normal_fwd_bwd(C, H, W, z_depth):
     from horizongs_amd import gsplat_api as G
     c2w, Ks = _cams(C, W, H, seed=C * 100 + H)

@@ -10,7 +10,8 @@ C oracle (f32 checker + f64 truth, per-element conditioning of oracle/checks.py)
     backward, the `t0 = batch_end - wave_final` trimming, the workgroup early-out vote and
     the exclusive T <= 1e-4 stop;
   * the full c2 scene (2M Gaussians, 1920x1080, ~1,070 intersections per tile) through
-    gsplat.rasterization, every image and gradient, and a 320-row band of the c3 2DGS scene.
+    gsplat.rasterization, every image and gradient, and the full c3 2DGS frame (with K13,
+    the normals from its expected depth, at 1920x1080).
 
 Each test asserts the depth statistics of its own scene, so it cannot silently become
 sparse.  Pixels where the oracle took a discrete decision (alpha vs 1/255, the 0.999 clamp,
@@ -81,9 +82,39 @@ def test_dense_2dgs_multibatch():
 
 
 @pytest.mark.slow
-def test_c3_band_2dgs_vs_oracle():
-    """c3 (the c2 inputs through rasterization_2dgs) on rows 0-319 (20 tile rows)."""
+def test_c3_fullsize_2dgs_vs_oracle():
+    """c3 (the c2 inputs through rasterization_2dgs), the whole 1920x1080 frame: every image
+    and gradient vs the oracle, then K13 -- render_normals_from_depth, the normal-consistency
+    input of reference train.py:180-188, computed inside rasterization_2dgs
+    (gaussian_renderer/render.py:62-76) -- on this frame's own expected depth against the torch
+    restatement of the fork's depth_to_normal in f32 / f64, forward and backward."""
+    from horizongs_amd import gsplat_api as G
+    from oracle import torch_ref as TR
+    from oracle.checks import cond_close
+    from tests import parity_report as PR
     sc = c2()
     bg = torch.tensor([[0.2, 0.1, 0.3]])
-    (max_tile, replay, sat), _, _ = run_2dgs(sc, "RGB+ED", bg, rows=320, seed=4)
+    (max_tile, replay, sat), _, res = run_2dgs(sc, "RGB+ED", bg, seed=4)
     assert max_tile >= 1024 and replay >= 1024 and sat >= 0.10, (max_tile, replay, sat)
+    assert res["r32"].Hr == 1080
+    # K13 at full size on the GPU's expected-depth channel (viewmat = I: camera = world frame)
+    depth = res["out"].detach()[..., 3:].contiguous()
+    c2w = torch.eye(4)[None]
+    Ks = sc.Ks
+    gup = torch.randn(1, 1080, 1920, 3, generator=torch.Generator().manual_seed(11))
+    ref = {}
+    for dt in (torch.float32, torch.float64):
+        d = depth.cpu().to(dt).requires_grad_(True)
+        n = TR.depth_to_normal(d, c2w.to(dt), Ks.to(dt))
+        (n * gup.to(dt)).sum().backward()
+        ref[dt] = (n.detach().numpy(), d.grad.numpy())
+    nfd = res["nfd"].detach().cpu().numpy()
+    cond_close(nfd, ref[torch.float32][0], ref[torch.float64][0], "normals_from_depth (c3 frame)", dilate_axes=(1, 2))
+    PR.tensor("normals_from_depth", nfd, ref[torch.float32][0], ref[torch.float32][0], ref[torch.float64][0])
+    dg = depth.clone().requires_grad_(True)
+    n = G.depth_to_normal(dg, c2w.to(depth.device), Ks.to(depth.device))
+    (n * gup.to(depth.device)).sum().backward()
+    np.testing.assert_array_equal(n.detach().cpu().numpy(), nfd)  # the same kernel rasterization_2dgs ran
+    vd = dg.grad.cpu().numpy()
+    cond_close(vd, ref[torch.float32][1], ref[torch.float64][1], "v_depth of K13 (c3 frame)", dilate_axes=(1, 2))
+    PR.tensor("v_depth(K13)", vd, ref[torch.float32][1], ref[torch.float32][1], ref[torch.float64][1])

@@ -228,3 +228,133 @@ def test_ddp_two_ranks_match_one_rank_two_views():
                                                msg=f"rank {rank} step {step} p{k}")
         for p, r in zip(params, ref_params):
             torch.testing.assert_close(torch.from_numpy(p), r, rtol=1e-6, atol=1e-7)
+
+
+# ---------------------------------------------------------------------------------------
+# the synchronous form red() across steps, and bucket identity across ranks after a densify
+# ---------------------------------------------------------------------------------------
+def _sync_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        params = _make_params()
+        opt = _optimizer(params)
+        red = GradientAllReduce(opt, bucket_mb=0.0012)
+        grads, layouts, flats = [], [], []
+        for step in range(3):
+            if step == 2:
+                params = _grow(opt, params)  # densification replaces every Parameter
+            opt.zero_grad(set_to_none=True)
+            # the hooks registered by the previous red() stay in place: this backward must
+            # leave the gradients alone (they are reduced by the synchronous call below)
+            _view_loss(params, rank).backward()
+            red()
+            grads.append([None if p.grad is None else p.grad.detach().numpy().copy() for p in params])
+            layouts.append([[tuple(p.shape) for p in b["params"]] for b in red.buckets])
+            flats.append([b["flat"].detach().numpy().copy() for b in red.buckets])
+            opt.step()
+        q.put((rank, grads, layouts, flats))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sync_reduce_across_steps_and_bucket_identity():
+    """red() (begin-less synchronous form) works step after step with its hooks left
+    registered (a plain backward between steps does not raise), gives the 2-view mean every
+    step, and after a densify both ranks hold the same bucket layout and reduced contents."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sync_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, g0, l0, f0), (_, g1, l1, f1) = res
+    assert l0 == l1 and len(l0[-1]) >= 2  # same buckets, same order, after the growth too
+    for a, b in zip(f0, f1):
+        for x, y in zip(a, b):
+            assert (x == y).all()  # identical reduced bucket contents on both ranks
+    params = _make_params()
+    opt = _optimizer(params)
+    for step in range(3):  # one process, both views averaged
+        if step == 2:
+            params = _grow(opt, params)
+        opt.zero_grad(set_to_none=True)
+        (sum(_view_loss(params, v) for v in (0, 1)) / 2).backward()
+        for k, p in enumerate(params):
+            if p.grad is None:
+                assert g0[step][k] is None and g1[step][k] is None
+            else:
+                torch.testing.assert_close(torch.from_numpy(g0[step][k]), p.grad, rtol=1e-6, atol=1e-7)
+        opt.step()
+
+
+# ---------------------------------------------------------------------------------------
+# early gradients (the decode backward's cov head hands over _offset / _scaling / cov MLP
+# gradients before the backward ends) and the bucket order that launches them first
+# ---------------------------------------------------------------------------------------
+def _early_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from horizongs_amd import decode as HD
+        params = _make_params()
+        a, b, c, d = params
+        opt = _optimizer(params)
+        red = GradientAllReduce(opt, bucket_mb=0.00005, order=[b])  # one parameter per bucket, b first
+        out = []
+        for step in range(2):
+            opt.zero_grad(set_to_none=True)
+            red.begin()
+            assert HD._EARLY_GRAD[0] is not None  # installed for the step
+            loss = _view_loss(params, rank)
+            # the CPU stand-in of the decode backward: b's gradient is final "early" and handed
+            # over before the rest of the backward runs
+            gb, = torch.autograd.grad(loss, [b], retain_graph=True)
+            HD._EARLY_GRAD[0]([(b, gb)])
+            first = red.buckets[0]
+            launched_early = first["launched"] and [id(p) for p in first["params"]] == [id(b)]
+            loss.backward()
+            red.finish()
+            assert HD._EARLY_GRAD[0] is None  # removed after the step
+            out.append((launched_early, [None if p.grad is None else p.grad.detach().numpy().copy() for p in params]))
+            opt.step()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_early_gradients_launch_first_and_match():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_early_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    params = _make_params()  # one process, both views averaged, no densification
+    opt = _optimizer(params)
+    ref_grads = []
+    for _ in range(2):
+        opt.zero_grad(set_to_none=True)
+        (sum(_view_loss(params, v) for v in (0, 1)) / 2).backward()
+        ref_grads.append([None if p.grad is None else p.grad.clone() for p in params])
+        opt.step()
+    for rank, out in res:
+        for step, (launched_early, grads) in enumerate(out):
+            assert launched_early, (rank, step)  # the early bucket's collective was in flight before backward
+            for g, r in zip(grads, ref_grads[step]):
+                if r is None:
+                    assert g is None
+                else:
+                    torch.testing.assert_close(torch.from_numpy(g), r, rtol=1e-6, atol=1e-7)
