@@ -30,9 +30,9 @@ _SIGS = {
     "hgsr_version": (I, []),
     "hgsr_last_error": (ct.c_char_p, []),
     "hgsr_project3d_fwd": (I, [I, I, P, P, P, P, P, I, I, F, F, F, F, P, P, P, P, P]),
-    "hgsr_project3d_bwd": (I, [I, I, P, P, P, P, P, I, I, F, P, P, P, P, P, P, P, P, P]),
+    "hgsr_project3d_bwd": (I, [I, I, P, P, P, P, P, I, I, F, P, P, P, P, P, P, P, P, P, P]),
     "hgsr_project2d_fwd": (I, [I, I, P, P, P, P, P, I, I, F, F, F, P, P, P, P, P, P]),
-    "hgsr_project2d_bwd": (I, [I, I, P, P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P]),
+    "hgsr_project2d_bwd": (I, [I, I, P, P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P]),
     "hgsr_sh_fwd": (I, [I, I, I64, P, P, P, P, P]),
     "hgsr_sh_bwd": (I, [I, I, I64, P, P, P, P, P, P, P]),
     "hgsr_sh_rgb_fwd": (I, [I, I, I, I, P, P, P, I, P, P, P]),
@@ -60,14 +60,14 @@ _SIGS = {
     "hgsr_raster2d_fwd": (I, [I, I, I, P, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, SZ, P]),
     "hgsr_raster2d_pack_fused": (I, [I, I, I, P, P, P, I, P, P, I, P, P, SZ, P]),
     "hgsr_raster2d_fwd_packed": (I, [I, I, I, I, I, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, SZ, P, SZ,
-                                     P, SZ, P, P]),
+                                     P, SZ, P, P, P]),
     "hgsr_raster2d_bwd_ws_bytes": (SZ, [I, I, I, I]),
     "hgsr_raster2d_bwd": (I, [I, I, I, P, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, P,
                               P, P, P, P, SZ, P]),
     "hgsr_raster2d_fwd_fused": (I, [I, I, I, P, P, P, I, P, I, P, I, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P,
                                     P, P, P, SZ, P]),
     "hgsr_raster2d_bwd_fused": (I, [I, I, I, P, P, P, I, P, I, P, I, P, P, I, I, I, I, I, P, I64, P, P, P, P, P,
-                                    P, P, P, P, P, P, P, P, P, P, P, SZ, P, SZ, I, P]),
+                                    P, P, P, P, P, P, P, P, P, P, P, SZ, P, SZ, I, P, P, P]),
     "hgsr_lod_mask": (I, [I, P, P, P, P, F, F, F, I, P, P]),
     "hgsr_decode_ws_bytes": (SZ, [I]),
     "hgsr_decode_count": (I, [I, I, I, I, I, P, P, P, P, P, P, SZ, P, P, P]),

@@ -259,7 +259,8 @@ __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
     const float* __restrict__ Ks, int W, int H, const int32_t* __restrict__ radii,
     const float* __restrict__ conics, const float2* __restrict__ v_means2d,
     const float* __restrict__ v_depths, const float* __restrict__ v_conics,
-    float* __restrict__ v_means, float4* __restrict__ v_quats, float* __restrict__ v_scales) {
+    float* __restrict__ v_means, float4* __restrict__ v_quats, float* __restrict__ v_scales,
+    const float* __restrict__ v_scales_in) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= N) return;
     const float m[3] = {means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2]};
@@ -395,11 +396,12 @@ __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
         vq_acc.z += live ? vq.z : 0.f;
         vq_acc.w += live ? vq.w : 0.f;
     }
-    // overwrite semantics: a Gaussian culled in every camera gets zeros
+    // overwrite semantics: a Gaussian culled in every camera gets zeros; v_scales_in (another
+    // consumer's gradient of the scales) is added here instead of by a separate sum
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         v_means[(int64_t)g * 3 + j] = vm_acc[j];
-        v_scales[(int64_t)g * 3 + j] = vs_acc[j];
+        v_scales[(int64_t)g * 3 + j] = v_scales_in ? vs_acc[j] + v_scales_in[(int64_t)g * 3 + j] : vs_acc[j];
     }
     v_quats[g] = vq_acc;
 }
@@ -518,7 +520,7 @@ __global__ __launch_bounds__(256) void project2d_bwd_kernel(
     const float* __restrict__ ray_transforms, const float2* __restrict__ v_means2d,
     const float* __restrict__ v_depths, const float* __restrict__ v_ray_transforms,
     const float* __restrict__ v_normals, float* __restrict__ v_means, float4* __restrict__ v_quats,
-    float* __restrict__ v_scales) {
+    float* __restrict__ v_scales, const float* __restrict__ v_scales_in) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= N) return;
     const float m[3] = {means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2]};
@@ -580,9 +582,15 @@ __global__ __launch_bounds__(256) void project2d_bwd_kernel(
     // overwrite semantics: a Gaussian culled in every camera gets zeros
 #pragma unroll
     for (int j = 0; j < 3; ++j) v_means[(int64_t)g * 3 + j] = vm_acc[j];
-    v_scales[(int64_t)g * 3 + 0] = vs0;
-    v_scales[(int64_t)g * 3 + 1] = vs1;
-    v_scales[(int64_t)g * 3 + 2] = 0.f;
+    if (v_scales_in) {
+        v_scales[(int64_t)g * 3 + 0] = vs0 + v_scales_in[(int64_t)g * 3 + 0];
+        v_scales[(int64_t)g * 3 + 1] = vs1 + v_scales_in[(int64_t)g * 3 + 1];
+        v_scales[(int64_t)g * 3 + 2] = 0.f + v_scales_in[(int64_t)g * 3 + 2];
+    } else {
+        v_scales[(int64_t)g * 3 + 0] = vs0;
+        v_scales[(int64_t)g * 3 + 1] = vs1;
+        v_scales[(int64_t)g * 3 + 2] = 0.f;
+    }
     v_quats[g] = vq_acc;
 }
 
@@ -622,7 +630,8 @@ extern "C" int hgsr_project3d_bwd(int C, int N, const float* means, const float*
                                   int width, int height, float eps2d, const int32_t* radii,
                                   const float* conics, const float* v_means2d,
                                   const float* v_depths, const float* v_conics, float* v_means,
-                                  float* v_quats, float* v_scales, hgsr_stream_t stream) {
+                                  float* v_quats, float* v_scales, const float* v_scales_in,
+                                  hgsr_stream_t stream) {
     (void)eps2d;
     int st = check_common(C, N, means, quats, scales, viewmats, Ks, width, height);
     if (st) return st;
@@ -633,7 +642,7 @@ extern "C" int hgsr_project3d_bwd(int C, int N, const float* means, const float*
     hipLaunchKernelGGL(project3d_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, as_stream(stream), C, N,
                        means, reinterpret_cast<const float4*>(quats), scales, viewmats, Ks, width,
                        height, radii, conics, reinterpret_cast<const float2*>(v_means2d), v_depths,
-                       v_conics, v_means, reinterpret_cast<float4*>(v_quats), v_scales);
+                       v_conics, v_means, reinterpret_cast<float4*>(v_quats), v_scales, v_scales_in);
     return check_launch("project3d_bwd");
 }
 
@@ -661,7 +670,7 @@ extern "C" int hgsr_project2d_bwd(int C, int N, const float* means, const float*
                                   const float* ray_transforms, const float* v_means2d,
                                   const float* v_depths, const float* v_ray_transforms,
                                   const float* v_normals, float* v_means, float* v_quats,
-                                  float* v_scales, hgsr_stream_t stream) {
+                                  float* v_scales, const float* v_scales_in, hgsr_stream_t stream) {
     int st = check_common(C, N, means, quats, scales, viewmats, Ks, width, height);
     if (st) return st;
     HGSR_REQUIRE(N == 0 || (radii && ray_transforms && v_means2d && v_depths && v_ray_transforms && v_normals &&
@@ -672,7 +681,8 @@ extern "C" int hgsr_project2d_bwd(int C, int N, const float* means, const float*
     hipLaunchKernelGGL(project2d_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, as_stream(stream), C, N,
                        means, reinterpret_cast<const float4*>(quats), scales, viewmats, Ks, radii,
                        ray_transforms, reinterpret_cast<const float2*>(v_means2d), v_depths,
-                       v_ray_transforms, v_normals, v_means, reinterpret_cast<float4*>(v_quats), v_scales);
+                       v_ray_transforms, v_normals, v_means, reinterpret_cast<float4*>(v_quats), v_scales,
+                       v_scales_in);
     return check_launch("project2d_bwd");
 }
 

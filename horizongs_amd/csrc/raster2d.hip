@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     float* __restrict__ render_normals,
     float* __restrict__ render_distort, float* __restrict__ render_median, int32_t* __restrict__ last_ids,
     int32_t* __restrict__ median_ids, uint64_t* __restrict__ qmask, int64_t qstride, float4* __restrict__ zero_rows,
-    int64_t zero_n4, const int64_t* __restrict__ isect_info) {
+    int64_t zero_n4, const int64_t* __restrict__ isect_info, const float* __restrict__ normal_rot) {
     constexpr int NB = kFwd2Batch;
     // one LDS object: every component of record t sits at a compile-time offset from one address;
     // double-buffered and filled by LDS-DMA one batch ahead (no staging VGPRs: 96 -> 72 VGPRs)
@@ -384,6 +384,15 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
             if (k == ed_ch) v = v / fmaxf(alpha, 1e-10f);  // expected depth (rasterization ED)
             render_colors[tc.pix * D + k] = v;
         }
+        if (normal_rot) {
+            // world frame (rasterization_2dgs): R^T n, R = the camera's viewmat rotation
+            const float* R = normal_rot + tc.cam * 16;
+            float nw[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) nw[k] = R[k] * nacc[0] + R[4 + k] * nacc[1] + R[8 + k] * nacc[2];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) nacc[k] = nw[k];
+        }
 #pragma unroll
         for (int k = 0; k < 3; ++k) render_normals[tc.pix * 3 + k] = nacc[k];
         render_distort[tc.pix] = distort;
@@ -410,7 +419,7 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
     const float* __restrict__ v_render_alphas, const float* __restrict__ v_render_normals,
     float* __restrict__ acc_rows, unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask,
-    int64_t qstride) {
+    int64_t qstride, const float* __restrict__ normal_rot, const float* __restrict__ v_depth_extra) {
     // row layout: 0-1 xy, 2-4 sum (p-m)_x v_c, 5-7 sum (p-m)_y v_c, 8-10 sum v_c (v_c = dL/d(h_u x h_v)),
     // 11 opac, 12-14 normal, 15.. colour, then abs xy; split2 maps v_c sums to u, v, w and densify
     constexpr int KV = 15 + D + (ABS ? 2 : 0);
@@ -447,6 +456,17 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
     for (int k = 0; k < D; ++k) vo[k] = tc.inside ? v_render_colors[tc.pix * D + k] : 0.f;
 #pragma unroll
     for (int k = 0; k < 3; ++k) vn[k] = tc.inside ? v_render_normals[tc.pix * 3 + k] : 0.f;
+    if (normal_rot) {  // world-frame normal gradients back to the camera frame: R v
+        const float* R = normal_rot + tc.cam * 16;
+        float vc[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) vc[j] = R[4 * j] * vn[0] + R[4 * j + 1] * vn[1] + R[4 * j + 2] * vn[2];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) vn[j] = vc[j];
+    }
+    // the depth channel's second consumer (normals from depth, K13), added here instead of by a
+    // separate sum: the gradient w.r.t. the rendered (expected) depth value
+    if (v_depth_extra && tc.inside) vo[D - 1] += v_depth_extra[tc.pix];
     float va = tc.inside ? v_render_alphas[tc.pix] : 0.f;
     if (ed_ch >= 0 && tc.inside) {
         // ED = raw / max(alpha, 1e-10): d/d raw = 1/ac, d/d alpha = -ED/ac (alpha >= 1e-10)
@@ -748,7 +768,8 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
                                float* render_alphas, float* render_normals, float* render_distort,
                                float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s,
                                uint64_t* qmask = nullptr, int64_t qstride = 0, float* zero_rows = nullptr,
-                               size_t zero_bytes = 0, const int64_t* isect_info = nullptr);
+                               size_t zero_bytes = 0, const int64_t* isect_info = nullptr,
+                               const float* normal_rot = nullptr);
 
 static int raster2d_fwd_impl(int C, int N, int D, const float* means2d, const float* rt, const ChanSrc& cs,
                              const float* normals, const float* backgrounds, int bg_ch, int ed_ch, int width,
@@ -780,7 +801,7 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
                                float* render_alphas, float* render_normals, float* render_distort,
                                float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s,
                                uint64_t* qmask, int64_t qstride, float* zero_rows, size_t zero_bytes,
-                               const int64_t* isect_info) {
+                               const int64_t* isect_info, const float* normal_rot) {
     const dim3 grid(C * tile_w * tile_h);
     float4* const z4 = reinterpret_cast<float4*>(zero_rows);
     const int64_t zn4 = (int64_t)(zero_bytes / sizeof(float4));
@@ -789,7 +810,7 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
     hipLaunchKernelGGL(raster2d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,     \
                        backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,           \
                        render_alphas, render_normals, render_distort, render_median, last_ids, median_ids, qmask,   \
-                       qstride, z4, zn4, isect_info)
+                       qstride, z4, zn4, isect_info, normal_rot)
     switch (D) {
         case 1: LAUNCH_F2(1); break;
         case 2: LAUNCH_F2(2); break;
@@ -858,7 +879,8 @@ extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, in
                                         float* render_normals, float* render_distort, float* render_median,
                                         int32_t* last_ids, int32_t* median_ids, const void* records,
                                         size_t records_bytes, void* qmask, size_t qmask_bytes, void* bwd_ws,
-                                        size_t bwd_ws_bytes, const int64_t* isect_info, hgsr_stream_t stream) {
+                                        size_t bwd_ws_bytes, const int64_t* isect_info, const float* normal_rot,
+                                        hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || with_depth), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !with_depth), "expected_depth needs depths");
     const int D = Dc + (with_depth ? 1 : 0);
@@ -878,7 +900,7 @@ extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, in
                                tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
                                render_normals, render_distort, render_median, last_ids, median_ids,
                                as_stream(stream), (uint64_t*)qmask, qmask_stride_of(qmask_bytes), (float*)bwd_ws,
-                               bwd_ws ? rows_b : 0, isect_info);
+                               bwd_ws ? rows_b : 0, isect_info, normal_rot);
 }
 
 extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
@@ -895,7 +917,8 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* v_render_alphas, const float* v_render_normals, float* v_means2d,
                              float* v_rt, const ChanDst& cd, float* v_normals, float* v_densify,
                              const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream, const uint64_t* qmask = nullptr,
-                             size_t qmask_bytes = 0, bool rows_zeroed = false) {
+                             size_t qmask_bytes = 0, bool rows_zeroed = false, const float* normal_rot = nullptr,
+                             const float* v_depth_extra = nullptr) {
     if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
                  "raster2d_bwd workspace too small");
@@ -941,7 +964,7 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
                            tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,        \
                            flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,                \
-                           v_render_normals, rows, pairs, qmask, qstride);                                        \
+                           v_render_normals, rows, pairs, qmask, qstride, normal_rot, v_depth_extra);            \
     }                                                                                                             \
     hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s,   \
                        C, N, rows, rt, m2, reinterpret_cast<float2*>(v_means2d), v_rt, cd, v_normals,             \
@@ -985,10 +1008,12 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                                        float* v_colors, float* v_depths, float* v_opacities, float* v_normals,
                                        float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
                                        const void* qmask, size_t qmask_bytes, int ws_zeroed,
+                                       const float* normal_rot, const float* v_depth_extra,
                                        hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !depths), "expected_depth needs depths");
     HGSR_REQUIRE(!depths || v_depths, "null pointer");
+    HGSR_REQUIRE(!v_depth_extra || depths, "v_depth_extra needs the depth channel");
     HGSR_REQUIRE(!qmask || qmask_bytes >= (size_t)(4 * qmask_stride(n_isects, (int64_t)C * tile_w * tile_h)) * 8,
                  "raster2d_bwd_fused: quadrant-mask buffer too small");
     const int D = Dc + (depths ? 1 : 0);
@@ -1001,5 +1026,5 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                              isect_offsets, n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
                              v_render_alphas, v_render_normals, v_means2d, v_ray_transforms, cd, v_normals,
                              v_densify, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask, qmask_bytes,
-                             ws_zeroed != 0);
+                             ws_zeroed != 0, normal_rot, v_depth_extra);
 }

@@ -64,10 +64,56 @@ def _grads_or_zeros(grads, lead, tails, like):
     return out
 
 
+class GradSink:
+    """Hand-off of a second gradient of the projection's `scales` ("glue").
+
+    The reference loss head regularises the same activated scales the rasterizer projects
+    (train.py:163-167), so autograd would sum the loss's gradient and the projection's with a
+    separate add kernel.  The projection's forward (when a backward can follow) hangs a sink
+    on its scales tensor; the fused loss, seeing it on the tensor it regularises, puts its
+    gradient there instead of returning it, and the projection backward -- which by the graph's
+    order runs after the loss backward -- adds it inside its own kernel (v_scales_in).  A put
+    after the projection backward took the sink (a second backward) is refused, and the loss
+    then returns its gradient through autograd as usual."""
+    __slots__ = ("value", "closed")
+
+    def __init__(self):
+        self.value, self.closed = None, False
+
+    def put(self, g):
+        if self.closed:
+            return False
+        self.value = g if self.value is None else self.value + g
+        return True
+
+    def take(self):
+        self.closed = True
+        v, self.value = self.value, None
+        return v
+
+
+_GRAD_SINK = os.environ.get("HGSR_GRAD_SINK", "1") != "0"  # (A/B knob)
+# rasterization_2dgs: world-frame normals and K13 inside the fused raster Function (A/B knob)
+_FUSE_FRAME = os.environ.get("HGSR_FUSE_FRAME", "1") != "0"
+
+
+def _attach_sink(ctx, scales, grad_mode, idx):
+    ctx.sink = None
+    if _GRAD_SINK and grad_mode and ctx.needs_input_grad[idx]:
+        ctx.sink = GradSink()
+        scales._hgsr_grad_sink = ctx.sink
+
+
+def _sink_grad(ctx, like):
+    """The gradient handed over through the sink (contiguous fp32 like `like`), or None."""
+    v = None if ctx.sink is None else ctx.sink.take()
+    return None if v is None else _f32(v.reshape(like.shape))
+
+
 class _Project3D(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means, quats, scales, viewmats, Ks, width, height, eps2d, near_plane, far_plane,
-                radius_clip):
+                radius_clip, grad_mode=False):
         C, Ng = viewmats.shape[0], means.shape[0]
         dev = means.device
         radii = torch.empty((C, Ng), dtype=torch.int32, device=dev)
@@ -79,6 +125,7 @@ class _Project3D(torch.autograd.Function):
                ptr(conics), N.stream(dev))
         ctx.save_for_backward(means, quats, scales, viewmats, Ks, radii, conics)
         ctx.cfg = (width, height, eps2d)
+        _attach_sink(ctx, scales, grad_mode, 2)
         ctx.mark_non_differentiable(radii)
         ctx.set_materialize_grads(False)  # no zero-filled int grad for radii per step
         return radii, means2d, depths, conics
@@ -93,12 +140,13 @@ class _Project3D(torch.autograd.Function):
         v_scales = torch.empty_like(scales)
         v_means2d, v_depths, v_conics = (_f32(g) for g in _grads_or_zeros((v_means2d, v_depths, v_conics), (C, Ng),
                                                                            (2, None, 3), means))
+        v_in = _sink_grad(ctx, scales)
         N.call("hgsr_project3d_bwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks), width,
                height, eps2d, ptr(radii), ptr(conics), ptr(v_means2d), ptr(v_depths), ptr(v_conics), ptr(v_means),
-               ptr(v_quats), ptr(v_scales), N.stream(means.device))
+               ptr(v_quats), ptr(v_scales), ptr(v_in), N.stream(means.device))
         if ctx.needs_input_grad[3]:
             raise NotImplementedError("hgsr: gradients w.r.t. viewmats are not supported")
-        return v_means, v_quats, v_scales, None, None, None, None, None, None, None, None
+        return v_means, v_quats, v_scales, None, None, None, None, None, None, None, None, None
 
 
 def fully_fused_projection(means, covars, quats, scales, viewmats, Ks, width, height, eps2d=0.3,
@@ -116,13 +164,14 @@ def fully_fused_projection(means, covars, quats, scales, viewmats, Ks, width, he
     assert viewmats.dim() == 3 and viewmats.shape[1:] == (4, 4) and Ks.shape == (viewmats.shape[0], 3, 3)
     radii, means2d, depths, conics = _Project3D.apply(
         _f32(means), _f32(quats), _f32(scales), _f32(viewmats), _f32(Ks), int(width), int(height),
-        float(eps2d), float(near_plane), float(far_plane), float(radius_clip))
+        float(eps2d), float(near_plane), float(far_plane), float(radius_clip), torch.is_grad_enabled())
     return radii, means2d, depths, conics, None
 
 
 class _Project2D(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, means, quats, scales, viewmats, Ks, width, height, near_plane, far_plane, radius_clip):
+    def forward(ctx, means, quats, scales, viewmats, Ks, width, height, near_plane, far_plane, radius_clip,
+                grad_mode=False):
         C, Ng = viewmats.shape[0], means.shape[0]
         dev = means.device
         radii = torch.empty((C, Ng), dtype=torch.int32, device=dev)
@@ -135,6 +184,7 @@ class _Project2D(torch.autograd.Function):
                ptr(normals), N.stream(dev))
         ctx.save_for_backward(means, quats, scales, viewmats, Ks, radii, rt)
         ctx.cfg = (width, height)
+        _attach_sink(ctx, scales, grad_mode, 2)
         ctx.mark_non_differentiable(radii)
         ctx.set_materialize_grads(False)  # no zero-filled int grad for radii per step
         return radii, means2d, depths, rt, normals
@@ -149,12 +199,13 @@ class _Project2D(torch.autograd.Function):
         v_scales = torch.empty_like(scales)
         v_means2d, v_depths, v_rt, v_normals = (_f32(g) for g in _grads_or_zeros(
             (v_means2d, v_depths, v_rt, v_normals), (C, Ng), (2, None, (3, 3), 3), means))
+        v_in = _sink_grad(ctx, scales)
         N.call("hgsr_project2d_bwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks), width,
                height, ptr(radii), ptr(rt), ptr(v_means2d), ptr(v_depths), ptr(v_rt), ptr(v_normals), ptr(v_means),
-               ptr(v_quats), ptr(v_scales), N.stream(means.device))
+               ptr(v_quats), ptr(v_scales), ptr(v_in), N.stream(means.device))
         if ctx.needs_input_grad[3]:
             raise NotImplementedError("hgsr: gradients w.r.t. viewmats are not supported")
-        return v_means, v_quats, v_scales, None, None, None, None, None, None, None
+        return v_means, v_quats, v_scales, None, None, None, None, None, None, None, None
 
 
 def fully_fused_projection_2dgs(means, quats, scales, viewmats, densifications, Ks, width, height, eps2d=0.3,
@@ -169,7 +220,8 @@ def fully_fused_projection_2dgs(means, quats, scales, viewmats, densifications, 
     Ng = means.shape[0]
     assert means.shape == (Ng, 3) and quats.shape == (Ng, 4) and scales.shape == (Ng, 3), "bad Gaussian shapes"
     return _Project2D.apply(_f32(means), _f32(quats), _f32(scales), _f32(viewmats), _f32(Ks), int(width),
-                            int(height), float(near_plane), float(far_plane), float(radius_clip))
+                            int(height), float(near_plane), float(far_plane), float(radius_clip),
+                            torch.is_grad_enabled())
 
 
 # =========================================================================
@@ -701,7 +753,12 @@ class _Raster2DFused(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means2d, rt, colors, depths, opacities, normals, densify, backgrounds, width, height,
-                tile_size, isect_offsets, flatten_ids, expected_depth, records=None, grad_mode=True, deferred=None):
+                tile_size, isect_offsets, flatten_ids, expected_depth, records=None, grad_mode=True, deferred=None,
+                frame=None):
+        """frame = (viewmats [C,4,4], Ks [C,3,3], normals_from_depth) with records: render_normals
+        come out in world frame (the kernels apply R^T) and, with normals_from_depth, K13 runs on
+        the depth channel here and is a sixth output whose gradient the raster backward adds to
+        the depth channel's (no rotate / slice / sum kernels in torch)."""
         C, Ng = means2d.shape[:2]
         Dc = 0 if colors is None else colors.shape[-1]
         D = Dc + (0 if depths is None else 1)
@@ -729,8 +786,9 @@ class _Raster2DFused(torch.autograd.Function):
                    ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(rn), ptr(rd), ptr(rm),
                    ptr(last), ptr(med), ptr(ws), ws.numel(), ptr(qmask), q_b, ptr(bwd_ws),
                    0 if bwd_ws is None else bwd_ws.numel(), None if deferred is None else ptr(deferred.info),
-                   N.stream(dev))
+                   None if frame is None else ptr(frame[0]), N.stream(dev))
         else:
+            assert frame is None, "frame needs the packed records"
             ws_b = N.size_query("hgsr_raster2d_fwd_ws_bytes", C, Ng, D)
             ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
             N.call("hgsr_raster2d_fwd_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors), int(col_shared),
@@ -744,13 +802,22 @@ class _Raster2DFused(torch.autograd.Function):
         ctx.fwd_ws = ws  # packed surfel records, reused by the backward
         ctx.qmask = qmask  # the forward's quadrant culling bits, reused by the backward
         ctx.deferred = deferred
+        ctx.frame = frame
+        nfd = None
+        if frame is not None and frame[2] and depths is not None:
+            # K13 on the rendered depth channel (read in place through its strides), world frame
+            dch = rc[..., D - 1]
+            st = (ct.c_int64 * 3)(*dch.stride())
+            nfd = torch.empty((C, height, width, 3), dtype=torch.float32, device=dev)
+            N.call("hgsr_depth_normal_fwd", C, height, width, dch.data_ptr(), ct.cast(st, ct.c_void_p),
+                   ptr(frame[0]), ptr(frame[1]), 1, 1, ptr(nfd), N.stream(dev))
         ctx.mark_non_differentiable(rd, rm)
         ctx.set_materialize_grads(False)  # no zero-filled image grads for distort / median per step
         ctx.out_shapes = (rc.shape, ra.shape, rn.shape)
-        return rc, ra, rn, rd, rm
+        return rc, ra, rn, rd, rm, nfd
 
     @staticmethod
-    def backward(ctx, v_rc, v_ra, v_rn, v_rd, v_rm):
+    def backward(ctx, v_rc, v_ra, v_rn, v_rd, v_rm, v_nfd=None):
         (means2d, rt, colors, depths, opacities, normals, backgrounds, offsets, flatten_ids, rc, ra,
          last) = ctx.saved_tensors
         width, height, tile_size, expected_depth, Dc, col_shared, op_shared = ctx.cfg
@@ -771,17 +838,24 @@ class _Raster2DFused(torch.autograd.Function):
         v_rc, v_ra, v_rn = (_f32(g if g is not None else torch.zeros(sh, dtype=torch.float32, device=dev))
                             for g, sh in zip((v_rc, v_ra, v_rn), ctx.out_shapes))
         n_is = flatten_ids.numel() if ctx.deferred is None else ctx.deferred.n  # exact once resolved
+        frame, v_dep = ctx.frame, None
+        if v_nfd is not None:  # K13 backward: its depth gradient goes into the raster backward
+            dch = rc[..., D - 1]
+            st = (ct.c_int64 * 3)(*dch.stride())
+            v_dep = torch.empty((C, height, width), dtype=torch.float32, device=dev)
+            N.call("hgsr_depth_normal_bwd", C, height, width, dch.data_ptr(), ct.cast(st, ct.c_void_p),
+                   ptr(frame[0]), ptr(frame[1]), 1, 1, ptr(_f32(v_nfd)), ptr(v_dep), N.stream(dev))
         N.call("hgsr_raster2d_bwd_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors), int(col_shared),
                ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(normals), ptr(backgrounds),
                width, height, tile_size, tw, th, ptr(offsets), n_is, ptr(flatten_ids) if n_is else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_rn), ptr(v_means2d), ptr(v_rt), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_normals),
                ptr(v_dens), ptr(fwd_ws), ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(),
-               zeroed, N.stream(dev))
+               zeroed, None if frame is None else ptr(frame[0]), ptr(v_dep), N.stream(dev))
         v_bg = None
         if backgrounds is not None and ctx.needs_input_grad[7]:
             v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))
         return (v_means2d, v_rt, v_colors, v_depths, v_opac, v_normals, v_dens, v_bg, None, None, None, None, None,
-                None, None, None, None)
+                None, None, None, None, None)
 
 
 def rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals, densify, image_width,
@@ -1014,18 +1088,23 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
         opac = opacities.expand(C, -1)
         args = (densifications, bgs, int(width), int(height), int(tile_size))
         ed, grad_mode = render_mode in ("ED", "RGB+ED"), torch.is_grad_enabled()
+        # world-frame normals and (expected / raw depth channel) K13 inside the fused Function
+        _unsupported(viewmats.requires_grad or Ks.requires_grad, "rasterization_2dgs gradients w.r.t. the cameras")
+        frame = (_f32(viewmats.detach()), _f32(Ks.detach()),
+                 render_mode in ("RGB+ED", "RGB+D") and depth_mode != "median") if _FUSE_FRAME else None
         tpg, isect_offsets = isect_state[3], isect_state[4]
         d = _isect_emit_deferred(isect_state)
         if d is not None:  # emission, sort and forward queued; then the count is read
-            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, d.flat, ed, records, grad_mode, d)
+            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, d.flat, ed, records, grad_mode, d, frame)
             if _isect_resolve(isect_state, d):
                 isect_ids, flatten_ids = d.ids[:d.n], d.flat[:d.n]
             else:
                 d = None  # over capacity: redo at the exact size
         if d is None:
             tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
-            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, flatten_ids, ed, records, grad_mode)
-        render_colors, render_alphas, render_normals, render_distort, render_median = outs
+            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, flatten_ids, ed, records, grad_mode, None, frame)
+        render_colors, render_alphas, render_normals, render_distort, render_median, nfd_fused = outs
+        fused_frame = frame is not None
     else:
         tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
         opac = opacities.repeat(C, 1)
@@ -1038,15 +1117,17 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
         if render_mode in ("ED", "RGB+ED"):
             render_colors = torch.cat([render_colors[..., :-1],
                                        render_colors[..., -1:] / render_alphas.clamp(min=1e-10)], dim=-1)
+        fused_frame, nfd_fused = False, None
     # camera -> world rotations straight from the viewmats (R_c2w = R^T), no c2w tensor built
     _unsupported(viewmats.requires_grad or Ks.requires_grad, "rasterization_2dgs gradients w.r.t. the cameras")
     vm = _f32(viewmats.detach())
-    render_normals_from_depth = None
-    if render_mode in ("RGB+ED", "RGB+D"):
+    render_normals_from_depth = nfd_fused
+    if render_mode in ("RGB+ED", "RGB+D") and render_normals_from_depth is None:
         dmap = render_median if depth_mode == "median" else render_colors[..., -1:]
         _check_cuda(dmap, vm, Ks)
         render_normals_from_depth = _DepthToNormal.apply(dmap, vm, Ks.detach(), True, True)
-    render_normals = _Rotate3.apply(vm, render_normals, True)  # camera -> world frame
+    if not fused_frame:
+        render_normals = _Rotate3.apply(vm, render_normals, True)  # camera -> world frame
     meta = {
         "camera_ids": None, "gaussian_ids": None, "radii": radii, "means2d": means2d, "depths": depths,
         "ray_transforms": ray_transforms, "normals": normals, "opacities": opac, "tile_width": tw,

@@ -89,6 +89,9 @@ class _FusedLoss(torch.autograd.Function):
                ptr(alpha), ptr(scaling), n_sc, k_sc, ct.byref(terms), ptr(out), ptr(ws), ws_b, N.stream(dev))
         ctx.save_for_backward(image, gt, mask, alpha, scaling, normals, nfd, distort, depth, mono, dmask, ws)
         ctx.lams = lams
+        # the rasterizer's projection of these same scales takes this loss's scale-regulariser
+        # gradient into its own backward kernel (gsplat_api.GradSink): no separate sum
+        ctx.sink = None if scaling is None else getattr(scaling, "_hgsr_grad_sink", None)
         # nine separate 0-dim outputs: an output the caller never uses gets no gradient
         # tensor at all (None below), so the backward builds no zeros / stack glue
         ctx.set_materialize_grads(False)
@@ -118,6 +121,8 @@ class _FusedLoss(torch.autograd.Function):
                image.shape[0] - C, ptr(g_alpha), ptr(g_sc), ct.byref(aux), ptr(ws), ws.numel(), N.stream(dev))
         if g_alpha is not None:
             g_alpha = g_alpha.reshape(alpha.shape)
+        if g_sc is not None and ctx.sink is not None and ctx.sink.put(g_sc):
+            g_sc = None  # handed to the projection backward, which adds it in its kernel
         return g_img, None, None, g_alpha, g_sc, g_n, g_f, g_d, g_z, None, None, None
 
 

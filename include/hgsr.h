@@ -55,13 +55,15 @@ int hgsr_project3d_fwd(int C, int N, const float* means, const float* quats,
                        float far_plane, float radius_clip, int32_t* radii, float* means2d,
                        float* depths, float* conics, hgsr_stream_t stream);
 
-/* vjp of the above: writes (overwrites) v_means [N,3], v_quats [N,4], v_scales [N,3]. */
+/* vjp of the above: writes (overwrites) v_means [N,3], v_quats [N,4], v_scales [N,3];
+ * v_scales_in (nullable [N,3]): another consumer's gradient of the same scales (the loss
+ * head's scale regulariser), added into v_scales in the same pass. */
 int hgsr_project3d_bwd(int C, int N, const float* means, const float* quats,
                        const float* scales, const float* viewmats, const float* Ks,
                        int width, int height, float eps2d, const int32_t* radii,
                        const float* conics, const float* v_means2d, const float* v_depths,
                        const float* v_conics, float* v_means, float* v_quats, float* v_scales,
-                       hgsr_stream_t stream);
+                       const float* v_scales_in, hgsr_stream_t stream);
 
 /* ---- K1'/K10: 2DGS surfel projection -------------------------------------
  * replaces fully_fused_projection_2dgs (render.py:171-186 and inside
@@ -74,14 +76,15 @@ int hgsr_project2d_fwd(int C, int N, const float* means, const float* quats,
                        float radius_clip, int32_t* radii, float* means2d, float* depths,
                        float* ray_transforms, float* normals, hgsr_stream_t stream);
 
-/* vjp of the above: writes (overwrites) v_means, v_quats, v_scales (v_scales[:,2] = 0). */
+/* vjp of the above: writes (overwrites) v_means, v_quats, v_scales (v_scales[:,2] = 0);
+ * v_scales_in (nullable): added into v_scales, as in hgsr_project3d_bwd. */
 int hgsr_project2d_bwd(int C, int N, const float* means, const float* quats,
                        const float* scales, const float* viewmats, const float* Ks,
                        int width, int height, const int32_t* radii,
                        const float* ray_transforms, const float* v_means2d,
                        const float* v_depths, const float* v_ray_transforms,
                        const float* v_normals, float* v_means, float* v_quats,
-                       float* v_scales, hgsr_stream_t stream);
+                       float* v_scales, const float* v_scales_in, hgsr_stream_t stream);
 
 /* ---- K3: spherical-harmonics colour --------------------------------------
  * replaces gsplat spherical_harmonics (used by rasterization when sh_degree is
@@ -286,7 +289,12 @@ int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * qmask (nullable; size hgsr_raster3d_qmask_bytes, the same layout): the forward's
  * per-quadrant culling bits, read by hgsr_raster2d_bwd_fused instead of repeating the tests.
  * bwd_ws / ws_zeroed / isect_info: as hgsr_raster3d_fwd_packed (size
- * hgsr_raster2d_bwd_ws_bytes(C, N, D, 1)). */
+ * hgsr_raster2d_bwd_ws_bytes(C, N, D, 1)).
+ * normal_rot (nullable, the viewmats [C,4,4]): render_normals are written in world frame,
+ * R^T n (rasterization_2dgs' frame), and hgsr_raster2d_bwd_fused given the same matrices
+ * takes world-frame v_render_normals.  v_depth_extra (nullable, [C,H,W]): a second gradient
+ * of the depth channel (K13's, the normals from the rendered depth), added per pixel by the
+ * backward kernel instead of by a separate sum. */
 int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                              const float* colors, int colors_shared, const float* depths,
                              const float* opacities, int opacities_shared, const float* normals, void* ws,
@@ -298,7 +306,8 @@ int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_
                              float* render_normals, float* render_distort, float* render_median,
                              int32_t* last_ids, int32_t* median_ids, const void* records,
                              size_t records_bytes, void* qmask, size_t qmask_bytes, void* bwd_ws,
-                             size_t bwd_ws_bytes, const int64_t* isect_info, hgsr_stream_t stream);
+                             size_t bwd_ws_bytes, const int64_t* isect_info, const float* normal_rot,
+                             hgsr_stream_t stream);
 int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                             const float* colors, int colors_shared, const float* depths,
                             int expected_depth, const float* opacities, int opacities_shared,
@@ -311,7 +320,7 @@ int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             float* v_colors, float* v_depths, float* v_opacities, float* v_normals,
                             float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
                             const void* qmask, size_t qmask_bytes, int ws_zeroed,
-                            hgsr_stream_t stream);
+                            const float* normal_rot, const float* v_depth_extra, hgsr_stream_t stream);
 
 /* ---- K14: anchor -> neural-Gaussian decode --------------
  * replaces scene/lod_model.py:286-290 set_anchor_mask (LoD mask, dist2level
