@@ -374,24 +374,34 @@ def pmc_traffic(args):
 
 def psnr_parity(args):
     """The "PSNR delta vs ref" half of the metric: equal-iteration training parity measured by
-    tests/test_gpu_training_parity.py -- 200 Adam iterations of the whole train step on an
-    anchor model (prefilter -> fused decode -> rasterization -> fused loss -> HIP Adam) against
-    the CPU chain whose decode and loss stages are pinned to the reference's goldens.  Training
-    to convergence cannot run inside a timed bench step, so the newest figure is quoted: the
-    one the GPU suite wrote in this tree (gpurun_out/, the same box) if present, else the
-    newest committed profiles/rNN_psnr_pipeline_*.json."""
+    tests/test_gpu_training_parity.py -- the whole train step on an anchor model (prefilter ->
+    fused decode -> rasterization -> fused loss -> HIP Adam) against the CPU chain whose decode
+    and loss stages are pinned to the reference's goldens: at scale (50k anchors, 480x270, 500
+    iterations; test_psnr_parity_at_scale_*) and small (5k anchors, 160x120, 200 iterations;
+    test_psnr_parity_pipeline_*).  Training cannot run inside a timed bench step, so the newest
+    figures are quoted: those the GPU suite wrote in this tree (gpurun_out/, the same box) if
+    present, else the newest committed profiles/rNN_psnr_*.json."""
     import glob
     root = os.path.dirname(os.path.abspath(__file__))
-    name = f"psnr_pipeline_{args.gs}gs.json"
-    files = [os.path.join(root, "gpurun_out", name)]
-    files = [f for f in files if os.path.exists(f)] or sorted(glob.glob(os.path.join(root, "profiles", "r*_" + name)))
-    if not files:
+    out = {}
+    for key, name, test in (("at_scale", f"psnr_scale_{args.gs}gs.json", "test_psnr_parity_at_scale"),
+                            ("pipeline", f"psnr_pipeline_{args.gs}gs.json", "test_psnr_parity_pipeline")):
+        files = [os.path.join(root, "gpurun_out", name)]
+        files = [f for f in files if os.path.exists(f)] or sorted(glob.glob(os.path.join(root, "profiles", "r*_" + name)))
+        if not files:
+            continue
+        d = json.load(open(files[-1]))
+        src = os.path.relpath(files[-1], root)
+        out[key] = {"psnr_delta_db": d["psnr_delta_db"], "psnr_hip_db": d["psnr_hip_db"],
+                    "psnr_ref_db": d["psnr_ref_db"], "iterations": d["iterations"], "anchors": d.get("anchors"),
+                    "width": d.get("width"), "height": d.get("height"), "lr_scale": d.get("lr_scale"),
+                    "noise_floor_window_db": d.get("noise_floor_window_db"),
+                    "source": f"{src} (tests/test_gpu_training_parity.py::{test}_{args.gs}dgs)"}
+    if not out:
         return None
-    d = json.load(open(files[-1]))
-    src = os.path.relpath(files[-1], root)
-    return {"psnr_delta_db": d["psnr_delta_db"], "psnr_hip_db": d["psnr_hip_db"], "psnr_ref_db": d["psnr_ref_db"],
-            "iterations": d["iterations"], "anchors": d.get("anchors"),
-            "source": src + " (tests/test_gpu_training_parity.py::test_psnr_parity_pipeline_*)"}
+    head = out.get("at_scale") or out["pipeline"]
+    return dict({k: head[k] for k in ("psnr_delta_db", "psnr_hip_db", "psnr_ref_db", "iterations", "anchors",
+                                      "source")}, **out)
 
 
 def _cpu_model():
@@ -523,12 +533,13 @@ def measure(args, rank, world, dev):
 
 
 def roofline(args, res):
-    """Dominant-kernel roofline: the raster backward is fp32-VALU bound (no MFMA, no HBM
-    limit), so achieved = algorithmic FLOP / kernel time against the fp32 vector peak.
-    Algorithmic FLOP = gsplat's visit count (every Gaussian up to each tile's latest
-    contributor x 256 pixels, counted on the device over the timed launches) x FLOP per
-    pair; frac_executed prices the lane-pairs the kernel actually stepped
-    (compacted per-quadrant lists x 64 lanes) the same way."""
+    """Dominant-kernel roofline: the raster backward is bound by fp32 work on
+    (pixel, Gaussian) pairs, so achieved = pairs_evaluated x FLOP per pair / kernel time
+    against the fp32 peak (vector = f32 MFMA rate, 157.3 TF).  pairs_evaluated = the
+    lane-pairs the kernel actually stepped (every entry of each wave's compacted per-quadrant
+    list x 64 lanes), counted on the device over exactly the timed launches.  gsplat's visit
+    count (every Gaussian up to each tile's latest contributor x 256 pixels, which includes
+    pairs the quadrant culling never evaluates) is kept beside it as a note only."""
     live = res["live"]
     if not live:
         return None
@@ -541,15 +552,17 @@ def roofline(args, res):
     fpp = FLOP_PER_PAIR[dom]
     ach = pairs * fpp / avg_s / 1e12
     ach_x = epairs * fpp / avg_s / 1e12
-    roof = {"bound": "valu", "achieved": round(ach, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": traffic.get(dom), "kernel": dom,
-            "pairs_per_launch": pairs, "executed_pairs_per_launch": epairs,
-            "achieved_executed": round(ach_x, 3), "frac_executed": round(ach_x / FP32_PEAK_TFLOPS, 4),
-            "note": (f"fp32 VALU-bound compositing (no MFMA, far below the HBM roof): peak = fp32 vector rate; "
-                     f"frac = {pairs} gsplat (pixel, Gaussian) pairs x {fpp:.0f} FLOP/pair (SURVEY 8(d)) / "
-                     f"kernel time; frac_executed = {epairs} lane-pairs actually stepped after the per-quadrant "
-                     f"compaction x the same FLOP/pair; both counted on the device over the timed launches; "
-                     f"{n_isects} intersections; VALU counters in profiles/r02_pmc_valu_mfma.txt")}
+    roof = {"bound": "valu", "achieved": round(ach_x, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach_x / FP32_PEAK_TFLOPS, 4), "traffic": traffic.get(dom), "kernel": dom,
+            "pairs_evaluated_per_launch": epairs, "flop_per_pair": fpp,
+            "gsplat_visited_pairs_per_launch": pairs, "frac_on_gsplat_visited_pairs": round(ach / FP32_PEAK_TFLOPS, 4),
+            "note": (f"fp32-bound compositing (far below the HBM roof): peak = the fp32 rate (vector = f32 MFMA); "
+                     f"achieved = {epairs} (pixel, Gaussian) pairs evaluated per launch (each wave's compacted "
+                     f"per-quadrant list x 64 lanes, counted on the device over the timed launches) x {fpp:.0f} "
+                     f"FLOP/pair (SURVEY 8(d)) / kernel time; frac_on_gsplat_visited_pairs prices gsplat's visit "
+                     f"count ({pairs}: every Gaussian up to each tile's latest contributor x 256 pixels, pairs the "
+                     f"culling skips included) -- a note, not the roofline; {n_isects} intersections; limiter "
+                     f"counters in profiles/r04_pmc_raster3d_bwd_limiters.txt")}
     # aggregate compulsory-bytes figure of SURVEY 8(d): B_step = 384 N + 132 I + 52 P
     b_step = 384 * wl.last_colors.shape[0] + 132 * n_isects + 52 * args.width * args.height
     if roof.get("traffic") is not None:
@@ -606,11 +619,11 @@ def secondary(args, rank, world, dev):
                         "ms_per_step": round(r["dt"] / a.steps * 1e3, 3), "steps": a.steps, "warmup": a.warmup,
                         "gaussians": int(r["wl"].last_colors.shape[0]), "n_isects": r["isects_after"],
                         "roofline": None if roof is None else dict(
-                            {k: roof[k] for k in ("bound", "kernel", "achieved", "frac", "frac_executed",
-                                                  "kernel_avg_ms", "pairs_per_launch", "executed_pairs_per_launch")},
-                            note=("frac prices gsplat's visited (pixel, Gaussian) pairs, including those the "
-                                  "per-quadrant culling skips, so it exceeds 1 where culling removes most of them "
-                                  "(clustered neural Gaussians); frac_executed prices the work actually executed")),
+                            {k: roof[k] for k in ("bound", "kernel", "achieved", "frac", "kernel_avg_ms",
+                                                  "pairs_evaluated_per_launch", "gsplat_visited_pairs_per_launch",
+                                                  "frac_on_gsplat_visited_pairs")},
+                            note=("frac prices the (pixel, Gaussian) pairs the kernel evaluated; the gsplat-visited "
+                                  "figure (pairs the per-quadrant culling skips included) is a note only")),
                         "decode_mfma": decode_mfma(r["wl"], r["kernels"]) if a.anchors else None,
                         "kernels": r["kernels"]})
         del r
