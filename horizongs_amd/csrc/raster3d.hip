@@ -694,7 +694,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
 #endif
 typedef float f32x4m __attribute__((ext_vector_type(4)));
 
-template <int D>
+template <int D, int NB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HGSR_BWD3_MFMA_WAVES_N, 8))) void
 raster3d_bwd_mfma_kernel(int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec,
                          const float* __restrict__ backgrounds, int bg_ch, int ed_ch,
@@ -704,7 +704,7 @@ raster3d_bwd_mfma_kernel(int C, int W, int H, int tw, int th, const Rec3* __rest
                          const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
                          float* __restrict__ acc_rows, unsigned long long* __restrict__ pair_counter,
                          const uint64_t* __restrict__ qmask, int64_t qstride) {
-    constexpr int NB = kBwdBatch;
+    static_assert(NB == 64 || NB == 128, "record batch of 64 or 128");
     constexpr int FVP = 68;  // staging row pitch: 64 pixels + 4 (row r starts at bank 4r: conflict-free b128 reads)
     __shared__ struct {
         float4 g0[2][NB + 1], g1[2][NB + 1], col[2][NB + 1];
@@ -796,6 +796,7 @@ raster3d_bwd_mfma_kernel(int C, int W, int H, int tw, int th, const Rec3* __rest
     uint32_t stepped = 0;
     // output role of this lane in a flushed tile: column col of rows 4 g4 + i
     const int koff = col < 4 ? 6 + col : col == 4 ? 5 : col < 10 ? col - 5 : -1;
+    constexpr int NW = NB / 64 + 1;  // quadrant-mask words covering one batch's window
     uint64_t qw[3] = {0, 0, 0};
     auto qfetch = [&](int bb) {
         const int64_t lo = (end - 1 - (int64_t)bb * NB - tc.start) - (NB - 1);
@@ -803,9 +804,8 @@ raster3d_bwd_mfma_kernel(int C, int W, int H, int tw, int th, const Rec3* __rest
         const int idx = __builtin_amdgcn_readfirstlane(
             (int)(__builtin_amdgcn_readfirstlane(wave) * qstride + qmask_word0(tc.start, bin) + (lo >> 6)));
         const uint64_t* qp = qmask + idx;
-        qw[0] = qp[0];
-        qw[1] = qp[1];
-        qw[2] = qp[2];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) qw[k] = qp[k];
     };
     if (qmask && nb > 0) qfetch(0);
     for (int b = 0; b < nb; ++b) {
@@ -823,15 +823,18 @@ raster3d_bwd_mfma_kernel(int C, int W, int H, int tw, int th, const Rec3* __rest
         const int t0 = max(0, batch_end - wave_final);
         int n_mine = 0;
         if (qmask) {
+            // record t <-> tile-relative bit R - t: the NB-bit window [R - NB + 1, R], realigned
+            // and bit-reversed (word k of mk holds records 64 k .. 64 k + 63)
             const int64_t R = batch_end - tc.start, lo = R - (NB - 1);
             const uint64_t w0 = qw[0], w1 = qw[1], w2 = qw[2];
             if (b + 1 < nb) qfetch(b + 1);
             const int sh = (int)(lo & 63);
             const uint64_t wlo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
             const uint64_t whi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
-            uint64_t mk[2] = {__builtin_bitreverse64(whi), __builtin_bitreverse64(wlo)};
+            uint64_t mk[2] = {NB == 128 ? __builtin_bitreverse64(whi) : __builtin_bitreverse64(wlo),
+                              __builtin_bitreverse64(wlo)};
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < NB / 64; ++k) {
                 const int a = min(max(t0 - 64 * k, 0), 64), z = min(max(bsz - 64 * k, 0), 64);
                 const uint64_t below_z = z >= 64 ? ~0ull : ((1ull << z) - 1);
                 const uint64_t below_a = a >= 64 ? ~0ull : ((1ull << a) - 1);
@@ -1215,22 +1218,33 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     const int64_t qstride = qmask_stride_of(qmask_bytes);
     const bool abs = v_means2d_abs != nullptr;
     // pass 2 on the matrix pipe (raster3d_bwd_mfma_kernel); HGSR_BWD3_MFMA=0 selects the VALU kernel
-    static const bool mfma = [] {
+    // (1: 128-record batches, 2: 64-record batches -- less LDS, one more workgroup per CU)
+    static const int mfma = [] {
         const char* e = getenv("HGSR_BWD3_MFMA");
-        return e ? atoi(e) != 0 : false;
+        return e ? atoi(e) : 0;
     }();
     if (mfma && !abs) {
         {
             KernelTimer kt("raster3d_bwd", s);
-#define LAUNCH_M(DD)                                                                                            \
-    hipLaunchKernelGGL((raster3d_bwd_mfma_kernel<DD>), grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, \
-                       rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects, flatten_ids,      \
-                       render_alphas, last_ids, v_render_colors, v_render_alphas, rows, pairs, qmask, qstride)
-            switch (D) {
-                case 1: LAUNCH_M(1); break;
-                case 2: LAUNCH_M(2); break;
-                case 3: LAUNCH_M(3); break;
-                default: LAUNCH_M(4); break;
+#define LAUNCH_M(DD, NBB)                                                                                       \
+    hipLaunchKernelGGL((raster3d_bwd_mfma_kernel<DD, NBB>), grid, dim3(256), 0, s, C, width, height, tile_w,    \
+                       tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,           \
+                       flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, pairs, qmask, \
+                       qstride)
+            if (mfma == 2) {
+                switch (D) {
+                    case 1: LAUNCH_M(1, 64); break;
+                    case 2: LAUNCH_M(2, 64); break;
+                    case 3: LAUNCH_M(3, 64); break;
+                    default: LAUNCH_M(4, 64); break;
+                }
+            } else {
+                switch (D) {
+                    case 1: LAUNCH_M(1, 128); break;
+                    case 2: LAUNCH_M(2, 128); break;
+                    case 3: LAUNCH_M(3, 128); break;
+                    default: LAUNCH_M(4, 128); break;
+                }
             }
 #undef LAUNCH_M
         }

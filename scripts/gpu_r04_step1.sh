@@ -14,5 +14,10 @@ HGSR_BWD3_MFMA=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity_den
   -k "3dgs and not c2 or raster3d or rasterization" --timeout 240 --timeout-method thread > $O/tests_mfma.log 2>&1 \
   || { tail -60 $O/tests_mfma.log; exit 1; }
 tail -2 $O/tests_mfma.log
+HGSR_BWD3_MFMA=2 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity_dense.py -m gpu -x -q \
+  -k "3dgs and not c2" --timeout 240 --timeout-method thread > $O/tests_mfma2.log 2>&1 \
+  || { tail -60 $O/tests_mfma2.log; exit 1; }
+tail -2 $O/tests_mfma2.log
 TAG=r04s1/ab_defer ENV_A="HGSR_DEFER_ISECT=0" ENV_B="HGSR_DEFER_ISECT=1" CONFIGS="c2 c3" bash scripts/gpu_r04_ab.sh || exit $?
-TAG=r04s1/ab_mfma ENV_A="HGSR_BWD3_MFMA=0" ENV_B="HGSR_BWD3_MFMA=1" CONFIGS="c2" bash scripts/gpu_r04_ab.sh || exit $?
+TAG=r04s1/ab_mfma1 ENV_A="HGSR_BWD3_MFMA=0" ENV_B="HGSR_BWD3_MFMA=1" CONFIGS="c2" bash scripts/gpu_r04_ab.sh || exit $?
+TAG=r04s1/ab_mfma2 ENV_A="HGSR_BWD3_MFMA=0" ENV_B="HGSR_BWD3_MFMA=2" CONFIGS="c2" bash scripts/gpu_r04_ab.sh || exit $?
