@@ -8,8 +8,6 @@
 // Per pair: h_u = px*w - u, h_v = py*w - v (rows u,v,w of the ray transform),
 // x = h_u x h_v, s = x.xy / x.z, G = min(|s|^2, 2|mean2d - p|^2), alpha =
 // min(0.999, o*exp(-G/2)).  The last colour channel is the depth (RGB+ED).
-#include <stdlib.h>
-
 #include "common.h"
 
 namespace hgsr {
@@ -651,288 +649,6 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
         atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
 }
 
-// ---------------------------------------------------------------- backward, reduction on MFMA
-// The 2DGS backward with its per-step 19-value wave reduction (TransposeReduce: permlane swaps +
-// DPP, ~50 VALU and 15 swaps a step) moved to the matrix pipe.  Per pair of steps the 16 x 64
-// matrix A of per-pixel values (rows 8 s + {v_x, v_y, v_c0, v_c1, v_c2, v_opacity, fac, 0} of
-// step s; staged in LDS by pass 1) times the 64 x 16 matrix B of per-pixel constants
-// [1, u, v, vo_0..3, vn_0..2] ((u, v) = pixel offset from the quadrant centre) gives every sum
-// the accumulator row needs: sum v_x, sum v_y, sum v_c_k (x 1), sum u v_c_k and sum v v_c_k ->
-// sum (p - m)_x v_c_k = Su - Gx S (Gx = mean - quadrant centre), sum fac vo_k, sum fac vn_k;
-// sixteen v_mfma_f32_16x16x4_f32 per two steps.  The sums go into the same LDS partial rows
-// (s_part, LDS float atomics) and per-batch global flush as raster2d_bwd_kernel.
-#ifndef HGSR_BWD2_MFMA_WAVES_N
-#define HGSR_BWD2_MFMA_WAVES_N 4
-#endif
-typedef float f32x4m2 __attribute__((ext_vector_type(4)));
-
-template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HGSR_BWD2_MFMA_WAVES_N, 8))) void
-raster2d_bwd_mfma_kernel(int C, int W, int H, int tw, int th, const Rec2* __restrict__ rec,
-                         const float* __restrict__ backgrounds, int bg_ch, int ed_ch,
-                         const float* __restrict__ render_colors, const int32_t* __restrict__ offsets,
-                         int64_t n_isects, const int32_t* __restrict__ flatten_ids,
-                         const float* __restrict__ render_alphas, const int32_t* __restrict__ last_ids,
-                         const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
-                         const float* __restrict__ v_render_normals, float* __restrict__ acc_rows,
-                         unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask,
-                         int64_t qstride, const float* __restrict__ normal_rot,
-                         const float* __restrict__ v_depth_extra) {
-    constexpr int KV = 15 + D;
-    constexpr int KVP = KV + 1;
-    constexpr int NB = kBwd2Batch;
-    constexpr int FVP = 68;  // staging row pitch (row r starts at bank 4 r: conflict-free b128 reads)
-    __shared__ struct {
-        float4 r0[2][NB], r1[2][NB], r2[2][NB], col[2][NB], r4[2][NB], box[2][NB];
-    } sr;
-    __shared__ int32_t s_id[2][NB];
-    __shared__ float s_part[NB * KVP];
-    __shared__ __attribute__((aligned(16))) uint8_t s_list[4][NB + 8];
-    __shared__ int32_t s_last[4];
-    __shared__ __attribute__((aligned(16))) float s_fv[4][16 * FVP];
-    const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
-    const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
-    const float T_final = tc.inside ? 1.0f - render_alphas[tc.pix] : 1.0f;
-    float T = T_final;
-    float Bsum = 0.f, vo[4] = {0.f, 0.f, 0.f, 0.f}, vn[3];
-#pragma unroll
-    for (int k = 0; k < D; ++k) vo[k] = tc.inside ? v_render_colors[tc.pix * D + k] : 0.f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) vn[k] = tc.inside ? v_render_normals[tc.pix * 3 + k] : 0.f;
-    if (normal_rot) {
-        const float* R = normal_rot + tc.cam * 16;
-        float vc[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) vc[j] = R[4 * j] * vn[0] + R[4 * j + 1] * vn[1] + R[4 * j + 2] * vn[2];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) vn[j] = vc[j];
-    }
-    if (v_depth_extra && tc.inside) vo[D - 1] += v_depth_extra[tc.pix];
-    float va = tc.inside ? v_render_alphas[tc.pix] : 0.f;
-    if (ed_ch >= 0 && tc.inside) {
-        const float alpha = 1.0f - T_final, ac = fmaxf(alpha, 1e-10f);
-        float v_ed = 0.f;
-#pragma unroll
-        for (int k = 0; k < D; ++k)
-            if (k == ed_ch) {
-                v_ed = vo[k];
-                vo[k] = v_ed / ac;
-            }
-        if (alpha >= 1e-10f) va -= v_ed * render_colors[tc.pix * D + ed_ch] / ac;
-    }
-    float bg_dot = 0.f;
-#pragma unroll
-    for (int k = 0; k < D; ++k)
-        if (backgrounds && k < bg_ch) bg_dot += backgrounds[tc.cam * bg_ch + k] * vo[k];
-    const float va_term = T_final * (va - bg_dot);
-    float* const fv = s_fv[wave];
-    const int g4 = lane >> 4, col = lane & 15;
-    // B columns at pixels 16 g4 + j (this wave's staging rows 0..6 as scratch: its LDS operations
-    // complete in order): [1, u, v, vo_0..3, vn_0..2, 0...]
-    float bm[16];
-    {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) fv[k * FVP + lane] = vo[k];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) fv[(4 + k) * FVP + lane] = vn[k];
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-            const int p = 16 * g4 + jj;
-            const float u = (float)(p & 7) - 3.5f, v = (float)(p >> 3) - 3.5f;
-            const float cv = (col >= 3 && col < 10) ? fv[(col - 3) * FVP + p] : 0.f;
-            bm[jj] = col == 0 ? 1.0f : col == 1 ? u : col == 2 ? v : cv;
-        }
-        fv[7 * FVP + lane] = 0.f;  // the zero rows 7 and 15 of every group
-        fv[15 * FVP + lane] = 0.f;
-    }
-    // output slot of this lane's four accumulator registers (rows 4 g4 + i, column col): step
-    // g4 >> 1, row type 4 (g4 & 1) + i; -1 = not a sum of the row layout (split2 kernel)
-    int koff[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int ty = 4 * (g4 & 1) + i;
-        int k = -1;
-        if (ty == 0 && col == 0) k = 0;
-        else if (ty == 1 && col == 0) k = 1;
-        else if (ty >= 2 && ty <= 4 && col < 3) k = col == 0 ? 8 + (ty - 2) : col == 1 ? 2 + (ty - 2) : 5 + (ty - 2);
-        else if (ty == 5 && col == 0) k = 11;
-        else if (ty == 6 && col >= 3 && col < 3 + D) k = 15 + (col - 3);
-        else if (ty == 6 && col >= 7 && col < 10) k = 12 + (col - 7);
-        koff[i] = k;
-    }
-    const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
-    const int32_t wave_final = wave_max2(bin_final);
-    if (lane == 0) s_last[wave] = wave_final;
-    for (int e = tid; e < NB * KVP; e += 256) s_part[e] = 0.f;
-    lds_barrier();
-    const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
-    const int32_t end = min(tc.end, blk_final + 1);
-    const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
-    if (pair_counter && threadIdx.x == 0 && end > tc.start)
-        atomicAdd(pair_slot(pair_counter, 0), (unsigned long long)(end - tc.start) * kTilePixels);
-    float4* const stage_arr[6] = {&sr.r0[0][0], &sr.r1[0][0], &sr.r2[0][0], &sr.col[0][0], &sr.r4[0][0], &sr.box[0][0]};
-    int32_t cid = 0, nid = 0;
-    const bool loader = tid < NB;
-    auto dma_batch = [&](int buf, int32_t id) {
-        const float4* r = reinterpret_cast<const float4*>(rec + id);
-#pragma unroll
-        for (int q = 0; q < 6; ++q)
-            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + q),
-                                             (void __attribute__((address_space(3)))*)(stage_arr[q] + buf * NB), 16,
-                                             0, 0);
-    };
-    if (nb > 0 && loader) {
-        cid = flatten_ids[max(end - 1 - tid, tc.start)];
-        dma_batch(0, cid);
-        nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
-    }
-    uint8_t* my_list = s_list[wave];
-    int prev_bsz = 0;
-    uint32_t stepped = 0;
-    uint64_t qw[2] = {0, 0};
-    auto qfetch = [&](int bb) {
-        const int64_t lo = (end - 1 - (int64_t)bb * NB - tc.start) - (NB - 1);
-        const int64_t bin = (int64_t)tc.cam * (tw * th) + tc.tile;
-        const int idx = __builtin_amdgcn_readfirstlane(
-            (int)(__builtin_amdgcn_readfirstlane(wave) * qstride + qmask_word0(tc.start, bin) + (lo >> 6)));
-        const uint64_t* qp = qmask + idx;
-        qw[0] = qp[0];
-        qw[1] = qp[1];
-    };
-    if (qmask && nb > 0) qfetch(0);
-    for (int b = 0; b <= nb; ++b) {
-        const int cur = b & 1, prv = cur ^ 1;
-        const int32_t batch_end = end - 1 - b * NB;
-        const int bsz = b < nb ? min(NB, batch_end + 1 - tc.start) : 0;
-        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-        if (tid < bsz) s_id[cur][tid] = cid;
-        if (b + 1 < nb && loader) {
-            cid = nid;
-            dma_batch(prv, cid);
-            nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
-        }
-        if (b > 0) {
-            for (int e = tid; e < prev_bsz * KV; e += 256) {
-                const int t = e / KV, k = e - t * KV;
-                const float sv = s_part[t * KVP + k];
-                s_part[t * KVP + k] = 0.f;
-                if (sv != 0.f) atomicAdd(acc_rows + (int64_t)s_id[prv][t] * kRec2 + k, sv);
-            }
-        }
-        if (b == nb) break;
-        lds_barrier();
-        const int t0 = max(0, batch_end - wave_final);
-        uint64_t m;
-        bool rel;
-        if (qmask) {
-            const int64_t R = batch_end - tc.start, lo = R - (NB - 1);
-            const uint64_t w0 = qw[0], w1 = qw[1];
-            if (b + 1 < nb) qfetch(b + 1);
-            const int sh = (int)(lo & 63);
-            const uint64_t win = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
-            const uint64_t below_z = bsz >= 64 ? ~0ull : ((1ull << bsz) - 1);
-            const uint64_t below_a = t0 >= 64 ? ~0ull : ((1ull << t0) - 1);
-            const uint64_t mk = __builtin_bitreverse64(win) & below_z & ~below_a;
-            m = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mk) |
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mk >> 32)) << 32);
-            rel = (m >> lane) & 1;
-        } else {
-            rel = lane < bsz && lane >= t0 &&
-                  reaches2_exact(sr.r0[cur][lane], sr.r1[cur][lane], sr.r2[cur][lane], sr.r4[cur][lane],
-                                 sr.box[cur][lane], qx, qy);
-            m = __ballot(rel);
-        }
-        if (rel) my_list[lanes_below2(m)] = (uint8_t)lane;
-        const int n_mine = __popcll(m);
-        if (lane < 2) my_list[n_mine + lane] = (uint8_t)NB;  // padded with the dummy to a multiple of 2
-        stepped += (uint32_t)n_mine;
-        if (n_mine > 0) {
-            const uint32_t lstp = reinterpret_cast<const uint32_t*>(my_list)[lane < (NB + 8) / 4 ? lane : 0];
-            for (int i = 0; i < n_mine; i += 2) {
-                const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)lstp, i >> 2);
-                const int sub = (i & 3) * 8;  // this pair's two entries start at byte (i & 3)
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const int t = (int)((pk >> (sub + 8 * q)) & 0xffu);
-                    const bool dummy = t >= NB;
-                    const int tt = dummy ? 0 : t;
-                    const float4 r0 = sr.r0[cur][tt], r1 = sr.r1[cur][tt], r2 = sr.r2[cur][tt],
-                                 c = sr.col[cur][tt], r4 = sr.r4[cur][tt];
-                    const Hit2 h = hit2(r0, r1, r2, tc.px, tc.py);
-                    const float vis = __builtin_amdgcn_exp2f(-h.sigma);
-                    const float araw = r2.w * vis;
-                    const float alpha = fminf(0.999f, araw);
-                    const bool valid = !dummy & (batch_end - t <= bin_final) & h.ok & (h.sigma >= 0.f) &
-                                       (alpha >= 1.0f / 255.0f);
-                    const float al = valid ? alpha : 0.f;
-                    const float ra = __builtin_amdgcn_rcpf(1.0f - al);
-                    const float Tn = T * ra;
-                    const float fac = al * Tn;
-                    const float ck[4] = {c.x, c.y, c.z, c.w};
-                    float cv = r4.x * vn[0] + r4.y * vn[1] + r4.z * vn[2];
-#pragma unroll
-                    for (int k = 0; k < D; ++k) cv += ck[k] * vo[k];
-                    const float v_alpha = Tn * cv + ra * (va_term - Bsum);
-                    Bsum += fac * cv;
-                    const float va2 = (valid & (araw <= 0.999f)) ? v_alpha : 0.f;
-                    const float v_sigma = -araw * va2;
-                    const bool ell = h.g3 <= h.g2;
-                    const float ve = ell ? v_sigma : 0.f, vp = ell ? 0.f : v_sigma;
-                    const float vs0 = ve * h.sx, vs1 = ve * h.sy;
-                    T = Tn;
-                    float* row = fv + (8 * q) * FVP + lane;
-                    row[0 * FVP] = 2.0f * vp * h.dx;  // v_x
-                    row[1 * FVP] = 2.0f * vp * h.dy;  // v_y
-                    row[2 * FVP] = vs0 * h.iz;         // v_c0
-                    row[3 * FVP] = vs1 * h.iz;         // v_c1
-                    row[4 * FVP] = -(vs0 * h.sx + vs1 * h.sy) * h.iz;  // v_c2
-                    row[5 * FVP] = vis * va2;          // v_opacity
-                    row[6 * FVP] = fac;
-                }
-                // the pair's 16 x 64 x 16 product (inline-asm A reads: see raster3d_bwd_mfma_kernel)
-                f32x4m2 a0, a1, a2, a3;
-                {
-                    const uint32_t adr = (uint32_t)reinterpret_cast<uintptr_t>(&s_fv[wave][col * FVP + 16 * g4]);
-                    asm volatile(
-                        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
-                        "ds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48\n\ts_waitcnt lgkmcnt(0)"
-                        : "=v"(a0), "=v"(a1), "=v"(a2), "=v"(a3)
-                        : "v"(adr)
-                        : "memory");
-                }
-                const float av[16] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3],
-                                      a2[0], a2[1], a2[2], a2[3], a3[0], a3[1], a3[2], a3[3]};
-                f32x4m2 e = {0.f, 0.f, 0.f, 0.f}, o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int jj = 0; jj < 16; jj += 2) {
-                    e = __builtin_amdgcn_mfma_f32_16x16x4f32(av[jj], bm[jj], e, 0, 0, 0);
-                    o = __builtin_amdgcn_mfma_f32_16x16x4f32(av[jj + 1], bm[jj + 1], o, 0, 0, 0);
-                }
-                const f32x4m2 acc = e + o;
-                // this lane's step (rows 4 g4 + i all belong to step g4 >> 1) and its surfel
-                const int t = (int)__builtin_amdgcn_ubfe(pk, sub + 8 * (g4 >> 1), 8);
-                const float2 mxy = *reinterpret_cast<const float2*>(&sr.r2[cur][t < NB ? t : 0].y);
-                const float Gx = mxy.x - qx, Gy = mxy.y - qy;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    // column 0 of the same row (S = sum v_c), 32-lane swizzle from lane 16 g4
-                    const float S = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(acc[i]), 0x10));
-                    float v = acc[i];
-                    v = col == 1 ? v - Gx * S : v;  // sum (p - m)_x v_c = Su - Gx S
-                    v = col == 2 ? v - Gy * S : v;
-                    if (koff[i] >= 0 && t < NB && v != 0.f) atomicAdd(&s_part[t * KVP + koff[i]], v);
-                }
-            }
-        }
-        prev_bsz = bsz;
-        lds_barrier();
-    }
-    if (pair_counter && lane == 0 && stepped)
-        atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
-}
-
 // Per surfel: fold the accumulated sums into gsplat's gradient tensors (overwrite), in f64.
 // gA = sum p_x v_c = gA' + m_x gC (gA' = sum (p-m)_x v_c), gB likewise, gC = sum v_c; with
 // d(a x b).g = da.(b x g) + db.(g x a):
@@ -1242,24 +958,13 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     const dim3 grid(C * tile_w * tile_h);
     unsigned long long* const pairs = timing_pair_counter("raster2d_bwd");
     const int64_t qstride = qmask_stride_of(qmask_bytes);
-    // the reduction on the matrix pipe (raster2d_bwd_mfma_kernel): HGSR_BWD2_MFMA=1
-    static const bool mfma = [] {
-        const char* e = getenv("HGSR_BWD2_MFMA");
-        return e ? atoi(e) != 0 : false;
-    }();
 #define LAUNCH_B2(DD)                                                                                             \
     {                                                                                                             \
         KernelTimer kt("raster2d_bwd", s);                                                                        \
-        if (mfma)                                                                                                 \
-            hipLaunchKernelGGL((raster2d_bwd_mfma_kernel<DD>), grid, dim3(256), 0, s, C, width, height, tile_w,    \
-                               tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,    \
-                               flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,            \
-                               v_render_normals, rows, pairs, qmask, qstride, normal_rot, v_depth_extra);        \
-        else                                                                                                      \
-            hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w,  \
-                               tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,    \
-                               flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,            \
-                               v_render_normals, rows, pairs, qmask, qstride, normal_rot, v_depth_extra);        \
+        hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
+                           tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,        \
+                           flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,                \
+                           v_render_normals, rows, pairs, qmask, qstride, normal_rot, v_depth_extra);            \
     }                                                                                                             \
     hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s,   \
                        C, N, rows, rt, m2, reinterpret_cast<float2*>(v_means2d), v_rt, cd, v_normals,             \

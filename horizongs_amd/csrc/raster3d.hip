@@ -18,8 +18,6 @@
 //    reduced across the wave together (step-major DPP, no hazard stalls), and
 //    each wave's sums go straight to the Gaussian's 48-byte accumulator row as
 //    one float-atomic instruction per 4 steps (the waves' partials meet in L2).
-#include <stdlib.h>
-
 #include "rec3.h"
 
 namespace hgsr {
@@ -673,286 +671,6 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
 }
 
-// ---------------------------------------------------------------- backward, pass 2 on MFMA
-// The same pass 1 as raster3d_bwd_kernel (one Gaussian per step over the wave's 8x8 quadrant,
-// two values per pixel: fac = alpha T and v_sigma), but the per-Gaussian reduction over the 64
-// pixels runs on the matrix pipe, which the VALU-bound pass 1 leaves idle.  Per group of 8 steps
-// the 16 x 64 matrix A (rows 2s + {0: fac, 1: v_sigma} of step s, one column per pixel; staged
-// in LDS by pass 1) times the 64 x 16 matrix B of per-pixel constants gives in one 16x16 tile
-//   fac rows x B[:, 0..3] = sum_p fac vo_k        (the colour gradients),
-//   v_sigma rows x B[:, 4..9] = sum_p v_sigma (1, u, v, u^2, uv, v^2)
-// with (u, v) the pixel's offset from the quadrant centre; sixteen v_mfma_f32_16x16x4_f32 (K =
-// 4 pixels each).  The sigma moments about the Gaussian (dx = Gx - u, Gx = mean - quadrant
-// centre) follow per wave from the central ones: Sx = Gx S0 - Su, Sxx = Gx^2 S0 - 2 Gx Su + Suu,
-// Sxy = Gx Gy S0 - Gx Sv - Gy Su + Suv, ... -- |u|, |v| <= 3.5, so the expansion adds at most a
-// few ulps of the terms -- and go to the 48-B accumulator rows exactly like the VALU kernel's.
-// A: lane l reads row l & 15 of the staging at pixels 16 (l >> 4) + j (4 x ds_read_b128); B: lane
-// l holds column l & 15 at those pixels (16 registers for the whole kernel); C: lane l holds
-// rows 4 (l >> 4) + i, column l & 15.
-#ifndef HGSR_BWD3_MFMA_WAVES_N
-#define HGSR_BWD3_MFMA_WAVES_N 5
-#endif
-typedef float f32x4m __attribute__((ext_vector_type(4)));
-
-template <int D, int NB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HGSR_BWD3_MFMA_WAVES_N, 8))) void
-raster3d_bwd_mfma_kernel(int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec,
-                         const float* __restrict__ backgrounds, int bg_ch, int ed_ch,
-                         const float* __restrict__ render_colors, const int32_t* __restrict__ offsets,
-                         int64_t n_isects, const int32_t* __restrict__ flatten_ids,
-                         const float* __restrict__ render_alphas, const int32_t* __restrict__ last_ids,
-                         const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
-                         float* __restrict__ acc_rows, unsigned long long* __restrict__ pair_counter,
-                         const uint64_t* __restrict__ qmask, int64_t qstride) {
-    static_assert(NB == 64 || NB == 128, "record batch of 64 or 128");
-    constexpr int FVP = 68;  // staging row pitch: 64 pixels + 4 (row r starts at bank 4r: conflict-free b128 reads)
-    __shared__ struct {
-        float4 g0[2][NB + 1], g1[2][NB + 1], col[2][NB + 1];
-    } sr;
-    __shared__ int32_t s_id[2][NB];
-    __shared__ __attribute__((aligned(16))) uint8_t s_list[4][NB + 16];  // read back as 32-bit words
-    __shared__ int32_t s_last[4];
-    __shared__ __attribute__((aligned(16))) float s_fv[4][16 * FVP];
-    const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const float qx = (float)(tc.j - (lane & 7)) + 4.0f;  // quadrant centre (wave-uniform)
-    const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
-    float vo[4], va_term, T_final;
-    {
-        const bool in = tc.inside;
-        const int64_t pix = tc.pix;
-        T_final = in ? 1.0f - render_alphas[pix] : 1.0f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) vo[k] = (in && k < D) ? v_render_colors[pix * D + k] : 0.f;
-        float va = in ? v_render_alphas[pix] : 0.f;
-        if (ed_ch >= 0 && in) {
-            const float alpha = 1.0f - T_final, ac = fmaxf(alpha, 1e-10f);
-            float v_ed = 0.f;
-#pragma unroll
-            for (int k = 0; k < D; ++k)
-                if (k == ed_ch) {
-                    v_ed = vo[k];
-                    vo[k] = v_ed / ac;
-                }
-            if (alpha >= 1e-10f) va -= v_ed * render_colors[pix * D + ed_ch] / ac;
-        }
-        float bg_dot = 0.f;
-#pragma unroll
-        for (int k = 0; k < D; ++k)
-            if (backgrounds && k < bg_ch) bg_dot += backgrounds[tc.cam * bg_ch + k] * vo[k];
-        va_term = T_final * (va - bg_dot);
-    }
-    float* const fv = s_fv[wave];
-    const int g4 = lane >> 4, col = lane & 15;
-    // B columns at pixels 16 g4 + j: colour gradients (via the staging buffer, this wave only:
-    // its LDS operations complete in order) or the pixel's offset moments
-    float bm[16];
-    {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) fv[k * FVP + lane] = vo[k];
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-            const int p = 16 * g4 + jj;
-            const float u = (float)(p & 7) - 3.5f, v = (float)(p >> 3) - 3.5f;
-            const float cv = fv[(col & 3) * FVP + p];
-            bm[jj] = col < 4 ? cv : col == 4 ? 1.0f : col == 5 ? u : col == 6 ? v : col == 7 ? u * u
-                   : col == 8 ? u * v : col == 9 ? v * v : 0.f;
-        }
-    }
-    float T = T_final, B = 0.f;
-    const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
-    const int32_t wave_final = wave_max_i32(bin_final);
-    if (lane == 0) s_last[wave] = wave_final;
-    if (tid < 6) {
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        sr.g0[tid >> 1][NB] = z;
-        sr.g1[tid >> 1][NB] = z;
-        sr.col[tid >> 1][NB] = z;
-    }
-    lds_barrier();
-    const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
-    const int32_t end = min(tc.end, blk_final + 1);
-    const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
-    if (pair_counter && threadIdx.x == 0 && end > tc.start)
-        atomicAdd(pair_slot(pair_counter, 0), (unsigned long long)(end - tc.start) * kTilePixels);
-    int32_t cid = 0, nid = 0;
-    const bool loader = tid < NB;
-    auto dma_batch = [&](int buf, int32_t id) {
-        const float4* r = reinterpret_cast<const float4*>(rec + id);
-        const int w0 = tid & ~63;
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r),
-                                         (void __attribute__((address_space(3)))*)(&sr.g0[buf][w0]), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + 1),
-                                         (void __attribute__((address_space(3)))*)(&sr.g1[buf][w0]), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + 2),
-                                         (void __attribute__((address_space(3)))*)(&sr.col[buf][w0]), 16, 0, 0);
-    };
-    if (nb > 0 && loader) {
-        cid = flatten_ids[max(end - 1 - tid, tc.start)];
-        dma_batch(0, cid);
-        nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
-    }
-    uint8_t* my_list = s_list[wave];
-    uint32_t stepped = 0;
-    // output role of this lane in a flushed tile: column col of rows 4 g4 + i
-    const int koff = col < 4 ? 6 + col : col == 4 ? 5 : col < 10 ? col - 5 : -1;
-    constexpr int NW = NB / 64 + 1;  // quadrant-mask words covering one batch's window
-    uint64_t qw[3] = {0, 0, 0};
-    auto qfetch = [&](int bb) {
-        const int64_t lo = (end - 1 - (int64_t)bb * NB - tc.start) - (NB - 1);
-        const int64_t bin = (int64_t)tc.cam * (tw * th) + tc.tile;
-        const int idx = __builtin_amdgcn_readfirstlane(
-            (int)(__builtin_amdgcn_readfirstlane(wave) * qstride + qmask_word0(tc.start, bin) + (lo >> 6)));
-        const uint64_t* qp = qmask + idx;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) qw[k] = qp[k];
-    };
-    if (qmask && nb > 0) qfetch(0);
-    for (int b = 0; b < nb; ++b) {
-        const int cur = b & 1, prv = cur ^ 1;
-        const int32_t batch_end = end - 1 - b * NB;
-        const int bsz = min(NB, batch_end + 1 - tc.start);
-        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-        if (tid < bsz) s_id[cur][tid] = cid;
-        if (b + 1 < nb && loader) {
-            cid = nid;
-            dma_batch(prv, cid);
-            nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
-        }
-        lds_barrier();
-        const int t0 = max(0, batch_end - wave_final);
-        int n_mine = 0;
-        if (qmask) {
-            // record t <-> tile-relative bit R - t: the NB-bit window [R - NB + 1, R], realigned
-            // and bit-reversed (word k of mk holds records 64 k .. 64 k + 63)
-            const int64_t R = batch_end - tc.start, lo = R - (NB - 1);
-            const uint64_t w0 = qw[0], w1 = qw[1], w2 = qw[2];
-            if (b + 1 < nb) qfetch(b + 1);
-            const int sh = (int)(lo & 63);
-            const uint64_t wlo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
-            const uint64_t whi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
-            uint64_t mk[2] = {NB == 128 ? __builtin_bitreverse64(whi) : __builtin_bitreverse64(wlo),
-                              __builtin_bitreverse64(wlo)};
-#pragma unroll
-            for (int k = 0; k < NB / 64; ++k) {
-                const int a = min(max(t0 - 64 * k, 0), 64), z = min(max(bsz - 64 * k, 0), 64);
-                const uint64_t below_z = z >= 64 ? ~0ull : ((1ull << z) - 1);
-                const uint64_t below_a = a >= 64 ? ~0ull : ((1ull << a) - 1);
-                mk[k] &= below_z & ~below_a;
-                const uint64_t m = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mk[k]) |
-                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mk[k] >> 32)) << 32);
-                if ((m >> lane) & 1) my_list[n_mine + lanes_below(m)] = (uint8_t)(k * 64 + lane);
-                n_mine += __popcll(m);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < NB / 64; ++k) {
-                const int t = k * 64 + lane;
-                const bool rel = t < bsz && t >= t0 && reaches(sr.g0[cur][t], sr.g1[cur][t], qx, qy) &&
-                                 ellipse_reaches(sr.g0[cur][t], sr.g1[cur][t], qx, qy);
-                const uint64_t m = __ballot(rel);
-                if (rel) my_list[n_mine + lanes_below(m)] = (uint8_t)t;
-                n_mine += __popcll(m);
-            }
-        }
-        // padded with the dummy to a multiple of 8
-        if (lane < 8) my_list[n_mine + lane] = (uint8_t)NB;
-        stepped += (uint32_t)n_mine;
-        if (n_mine > 0) {
-            const uint32_t lstp = reinterpret_cast<const uint32_t*>(my_list)[lane < (NB + 16) / 4 ? lane : 0];
-            for (int i = 0; i < n_mine; i += 8) {
-                const uint32_t pk0 = (uint32_t)__builtin_amdgcn_readlane((int)lstp, i >> 2);
-                const uint32_t pk1 = (uint32_t)__builtin_amdgcn_readlane((int)lstp, (i >> 2) + 1);
-                // pass 1: 8 steps, fac and v_sigma of this lane's pixel into staging rows 2s, 2s + 1
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int t = (int)(((q < 4 ? pk0 : pk1) >> (8 * (q & 3))) & 0xffu);
-                    const float4 g0 = sr.g0[cur][t], g1 = sr.g1[cur][t], c = sr.col[cur][t];
-                    const float dx = g0.x - tc.px, dy = g0.y - tc.py;
-                    const float sigma = sigma2(g0, g1, dx, dy);
-                    const float vis = __builtin_amdgcn_exp2f(-sigma);
-                    const float araw = g1.y * vis;
-                    const float alpha = fminf(0.999f, araw);
-                    const bool valid = (batch_end - t <= bin_final) & (sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
-                    const float ck[4] = {c.x, c.y, c.z, c.w};
-                    const float al = valid ? alpha : 0.f;
-                    const float ra = __builtin_amdgcn_rcpf(1.0f - al);
-                    const float Tn = T * ra;
-                    const float fac = al * Tn;
-                    float cv = ck[0] * vo[0];
-#pragma unroll
-                    for (int k = 1; k < D; ++k) cv += ck[k] * vo[k];
-                    const float v_alpha = Tn * cv + ra * (va_term - B);
-                    B += fac * cv;
-                    const float va2 = (valid & (araw <= 0.999f)) ? v_alpha : 0.f;
-                    T = Tn;
-                    s_fv[wave][(2 * q) * FVP + lane] = fac;
-                    s_fv[wave][(2 * q + 1) * FVP + lane] = -araw * va2;
-                }
-                // pass 2: the 16 x 64 x 16 product on the matrix pipe (two accumulators: the
-                // dependent-accumulator latency exceeds the issue interval)
-                // (inline asm: the compiler cannot tell these reads from the LDS-DMA destination and
-                // would wait vmcnt(0) -- on the next batch's record prefetch -- before them; a wave's
-                // LDS operations complete in order, so the staging writes above are visible)
-                f32x4m a0, a1, a2, a3;
-                {
-                    const uint32_t adr = (uint32_t)reinterpret_cast<uintptr_t>(&s_fv[wave][col * FVP + 16 * g4]);
-                    asm volatile(
-                        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
-                        "ds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48\n\ts_waitcnt lgkmcnt(0)"
-                        : "=v"(a0), "=v"(a1), "=v"(a2), "=v"(a3)
-                        : "v"(adr)
-                        : "memory");
-                }
-                const float av[16] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3],
-                                      a2[0], a2[1], a2[2], a2[3], a3[0], a3[1], a3[2], a3[3]};
-                f32x4m e = {0.f, 0.f, 0.f, 0.f}, o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int jj = 0; jj < 16; jj += 2) {
-                    e = __builtin_amdgcn_mfma_f32_16x16x4f32(av[jj], bm[jj], e, 0, 0, 0);
-                    o = __builtin_amdgcn_mfma_f32_16x16x4f32(av[jj + 1], bm[jj + 1], o, 0, 0, 0);
-                }
-                const f32x4m acc = e + o;
-                // rows 4 g4 + i: i = 0 / 2 fac rows of steps 2 g4 / 2 g4 + 1, i = 1 / 3 their v_sigma rows
-                // central moments of the v_sigma rows, from lanes 16 g4 + 4, 5, 6 (ds_swizzle, 32-lane groups)
-                const float s0a = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(acc[1]), 0x90));
-                const float sua = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(acc[1]), 0xB0));
-                const float sva = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(acc[1]), 0xD0));
-                const float s0b = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(acc[3]), 0x90));
-                const float sub = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(acc[3]), 0xB0));
-                const float svb = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(acc[3]), 0xD0));
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int q = 2 * g4 + h;  // the step of this lane's rows 4 g4 + 2h, + 2h + 1
-                    const uint32_t pk = q < 4 ? pk0 : pk1;
-                    const int t = (int)__builtin_amdgcn_ubfe(pk, 8 * (q & 3), 8);
-                    const float2 xy = *reinterpret_cast<const float2*>(&sr.g0[cur][t]);
-                    const int sid = s_id[cur][t < NB ? t : 0];
-                    const float Gx = xy.x - qx, Gy = xy.y - qy;
-                    const float s0 = h ? s0b : s0a, su = h ? sub : sua, sv = h ? svb : sva;
-                    const float mine = h ? acc[3] : acc[1], cf = h ? acc[2] : acc[0];
-                    float sx = Gx * s0 - su, sy = Gy * s0 - sv;
-                    float mxx = __builtin_fmaf(Gx, sx - su, mine);              // Gx^2 S0 - 2 Gx Su + Suu
-                    float mxy = __builtin_fmaf(Gx, sy, mine) - Gy * su;        // Gx Gy S0 - Gx Sv - Gy Su + Suv
-                    float myy = __builtin_fmaf(Gy, sy - sv, mine);              // Gy^2 S0 - 2 Gy Sv + Svv
-                    // materialised in every lane: selects, not exec-mask branches
-                    asm volatile("" : "+v"(sx), "+v"(sy), "+v"(mxx), "+v"(mxy), "+v"(myy));
-                    float v = col < 4 ? cf : s0;
-                    v = col == 5 ? sx : v;
-                    v = col == 6 ? sy : v;
-                    v = col == 7 ? mxx : v;
-                    v = col == 8 ? mxy : v;
-                    v = col == 9 ? myy : v;
-                    if (koff >= 0 && t < NB && v != 0.f) atomicAdd(acc_rows + (int64_t)sid * kRec3 + koff, v);
-                }
-            }
-        }
-        lds_barrier();
-    }
-    if (pair_counter && lane == 0 && stepped)
-        atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
-}
-
 // scatter accumulator rows into gsplat's separate gradient tensors (overwrite);
 // one lane per Gaussian, looping cameras in order (deterministic sums).  The rows
 // hold sigma moments (Sx, Sy, Sxx, Sxy, Syy) = sum_p v_sigma (dx, dy, dx^2, dx dy, dy^2):
@@ -1217,49 +935,6 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     unsigned long long* const pairs = timing_pair_counter("raster3d_bwd");
     const int64_t qstride = qmask_stride_of(qmask_bytes);
     const bool abs = v_means2d_abs != nullptr;
-    // pass 2 on the matrix pipe (raster3d_bwd_mfma_kernel); HGSR_BWD3_MFMA=0 selects the VALU kernel
-    // (1: 128-record batches, 2: 64-record batches -- less LDS, one more workgroup per CU)
-    static const int mfma = [] {
-        const char* e = getenv("HGSR_BWD3_MFMA");
-        return e ? atoi(e) : 0;
-    }();
-    if (mfma && !abs) {
-        {
-            KernelTimer kt("raster3d_bwd", s);
-#define LAUNCH_M(DD, NBB)                                                                                       \
-    hipLaunchKernelGGL((raster3d_bwd_mfma_kernel<DD, NBB>), grid, dim3(256), 0, s, C, width, height, tile_w,    \
-                       tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,           \
-                       flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, pairs, qmask, \
-                       qstride)
-            if (mfma == 2) {
-                switch (D) {
-                    case 1: LAUNCH_M(1, 64); break;
-                    case 2: LAUNCH_M(2, 64); break;
-                    case 3: LAUNCH_M(3, 64); break;
-                    default: LAUNCH_M(4, 64); break;
-                }
-            } else {
-                switch (D) {
-                    case 1: LAUNCH_M(1, 128); break;
-                    case 2: LAUNCH_M(2, 128); break;
-                    case 3: LAUNCH_M(3, 128); break;
-                    default: LAUNCH_M(4, 128); break;
-                }
-            }
-#undef LAUNCH_M
-        }
-#define LAUNCH_S(DD)                                                                                              \
-    hipLaunchKernelGGL((split3_kernel<DD, false>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, \
-                       N, rows, rec, conics, reinterpret_cast<float2*>(v_means2d), v_conics, cd, nullptr)
-        switch (D) {
-            case 1: LAUNCH_S(1); break;
-            case 2: LAUNCH_S(2); break;
-            case 3: LAUNCH_S(3); break;
-            default: LAUNCH_S(4); break;
-        }
-#undef LAUNCH_S
-        return check_launch("raster3d_bwd");
-    }
 #define LAUNCH_B(DD, AA)                                                                                       \
     {                                                                                                          \
         KernelTimer kt("raster3d_bwd", s);                                                                     \

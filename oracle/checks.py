@@ -39,7 +39,7 @@ def strict_rate(a, b, atol=ATOL, rtol=RTOL):
 
 
 def cond_close(a, b32, b64, name, rel_floor=1e-4, factor=3.0, min_strict=None, dilate_axes=None, env=None,
-               alt32=None, env_k=1.0):
+               alt32=None, env_k=1.0, dilate=3):
     """fp32-conditioning-aware check (expected-depth normalisation, x depth channel, 2DGS,
     deep tiles).  Per element: the GPU value must be within 1e-5 abs / 1e-4 rel (relative
     part against max(|b32|, rel_floor * max|b32|)) of the f32 oracle PLUS twice that
@@ -51,7 +51,9 @@ def cond_close(a, b32, b64, name, rel_floor=1e-4, factor=3.0, min_strict=None, d
     dilate_axes (image-shaped tensors only, e.g. the (H, W) axes of a depth-derived normal
     map): the per-element error is max-filtered over the 3-neighbourhood along those axes,
     since a pixel's conditioning is shared with the neighbours it is differenced against and
-    one particular f32 operation order can be accidentally exact at a single pixel.
+    one particular f32 operation order can be accidentally exact at a single pixel.  dilate:
+    the neighbourhood width (3; 5 for a quantity whose stencil reaches two pixels, e.g. the
+    depth gradient of K13, which sums the vjps of the normals at +-1, each differencing +-1).
 
     env (raster gradients): the element's rounding envelope E (oracle Raster*.envelope: sum
     of |terms| weighted by compositing depth); u * E (u = 2^-24) is added to its slack, so a
@@ -59,7 +61,7 @@ def cond_close(a, b32, b64, name, rel_floor=1e-4, factor=3.0, min_strict=None, d
     f32 evaluation order could meet.  Used with rel_floor=0: nothing tensor-wide remains.
 
     alt32: a second correct f32 evaluation of the same quantity (e.g. the 2DGS plane-form
-    hit, oracle set_hitform); the element's f32 error is the larger of the two.
+    hit, oracle set_hitform), or a list of them; the element's f32 error is the largest.
 
     env_k: multiple of u * E allowed (E is a first-order bound; the resolved-branch re-check
     of tests/raster_parity.py, which keeps the near-threshold pixels' gradients, uses 2)."""
@@ -71,10 +73,11 @@ def cond_close(a, b32, b64, name, rel_floor=1e-4, factor=3.0, min_strict=None, d
         return 1.0
     e32 = np.abs(b - c)
     if alt32 is not None:
-        e32 = np.maximum(e32, np.abs(np.asarray(alt32, np.float64) - c))
+        for alt in (alt32 if isinstance(alt32, (list, tuple)) else [alt32]):
+            e32 = np.maximum(e32, np.abs(np.asarray(alt, np.float64) - c))
     if dilate_axes:
         from scipy.ndimage import maximum_filter
-        size = [3 if ax in [d % e32.ndim for d in dilate_axes] else 1 for ax in range(e32.ndim)]
+        size = [dilate if ax in [d % e32.ndim for d in dilate_axes] else 1 for ax in range(e32.ndim)]
         e32 = maximum_filter(e32, size=size, mode="nearest")
     scale = np.maximum(np.abs(b), rel_floor * np.abs(b).max()) if rel_floor else np.abs(b)
     bar = ATOL + RTOL * scale

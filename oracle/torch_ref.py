@@ -186,10 +186,16 @@ def raster2d(means2d, rt, colors, opacities, normals, depths, radius, W, H, bg=N
     return img.reshape(H, W, -1), (1 - T).reshape(H, W, 1), nrm.reshape(H, W, 3)
 
 
-def depth_to_normal(depths, camtoworlds, Ks, z_depth=True):
+def depth_to_normal(depths, camtoworlds, Ks, z_depth=True, origin=True, jitter=None):
     """The gsplat fork's depth_to_normal restated in torch (any device / dtype; autograd):
     unproject the depth map [C,H,W,1] through the pinhole rays, central differences along
-    y (dx) and x (dy), normalize(cross(dx, dy)), zero one-pixel border -> [C,H,W,3]."""
+    y (dx) and x (dy), normalize(cross(dx, dy)), zero one-pixel border -> [C,H,W,3].
+    origin=False: the points without the camera origin, which cancels from every difference in
+    exact arithmetic -- a second correct f32 evaluation order (the HIP kernel's), used by the
+    parity tests as the element's other f32 error sample (checks.cond_close alt32).
+    jitter ([C,H,W,3], f64 runs): relative perturbation of every unprojected point coordinate,
+    e.g. uniform +-u -- the two roundings (ray direction, depth product) of an f32 unprojection -- so that f64 runs with
+    several jitters sample the spread of correct f32 evaluations (k13_error_samples)."""
     import torch.nn.functional as F
     height, width = depths.shape[-3:-1]
     dev, dt = depths.device, depths.dtype
@@ -203,8 +209,35 @@ def depth_to_normal(depths, camtoworlds, Ks, z_depth=True):
     origins = camtoworlds[..., :3, -1]
     if not z_depth:
         directions = F.normalize(directions, dim=-1)
-    points = origins[..., None, None, :] + depths * directions
+    points = origins[..., None, None, :] + depths * directions if origin else depths * directions
+    if jitter is not None:
+        points = points * (1 + jitter)
     dx = points[..., 2:, 1:-1, :] - points[..., :-2, 1:-1, :]
     dy = points[..., 1:-1, 2:, :] - points[..., 1:-1, :-2, :]
     normals = F.normalize(torch.cross(dx, dy, dim=-1), dim=-1)
     return F.pad(normals, (0, 0, 1, 1, 1, 1), value=0.0)
+
+
+def k13_error_samples(depth, c2w, Ks, gup, z_depth=True, n_jitter=4, seed=0):
+    """K13 (depth_to_normal) forward / backward error samples for the conditioning-aware checks.
+    Returns (n64, g64, [(n, g), ...]): the f64 normals and depth gradient (loss sum(n * gup)),
+    then correct f32-level evaluations of the same quantities -- the fork's f32 order, the f32
+    order without the camera origin (the HIP kernel's), and n_jitter f64 runs whose unprojected
+    points carry a random relative perturbation of +-u (u = 2^-24).  The per-element spread of
+    these samples around f64 is what any correct f32 evaluation may show at that element."""
+    import torch
+
+    def run(dt, origin=True, jitter=None):
+        d = depth.detach().cpu().to(dt).requires_grad_(True)
+        n = depth_to_normal(d, c2w.cpu().to(dt), Ks.cpu().to(dt), z_depth=z_depth, origin=origin, jitter=jitter)
+        (n * gup.cpu().to(dt)).sum().backward()
+        return n.detach().double().numpy(), d.grad.double().numpy()
+
+    n64, g64 = run(torch.float64)
+    samples = [run(torch.float32), run(torch.float32, origin=False)]
+    g = torch.Generator().manual_seed(seed)
+    shape = tuple(depth.shape[:-1]) + (3,)
+    for _ in range(n_jitter):
+        j = (torch.rand(shape, generator=g, dtype=torch.float64) * 2 - 1) * 2.0 ** -24
+        samples.append(run(torch.float64, jitter=j))
+    return n64, g64, samples

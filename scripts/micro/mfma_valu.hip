@@ -19,13 +19,19 @@ __global__ __launch_bounds__(256) void k(float* out, float a, float b) {
     f32x4 acc[4];
     for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float ma = x[1], mb = x[2];
-    for (int it = 0; it < ITER; ++it) {
+    // unrolled by 4 so every accumulator index is static (a dynamic one turns into indexed
+    // moves that read the MFMA result -- a dependency -- every iteration)
+    for (int it = 0; it < ITER; it += 4) {
 #pragma unroll
-        for (int m = 0; m < NM; ++m) acc[(it * NM + m) & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(ma, mb, acc[(it * NM + m) & 3], 0, 0, 0);
+        for (int u = 0; u < 4; ++u) {
 #pragma unroll
-        for (int r = 0; r < NV / 8; ++r) {
+            for (int m = 0; m < NM; ++m)
+                acc[(u * NM + m) & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(ma, mb, acc[(u * NM + m) & 3], 0, 0, 0);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(x[i]) : "v"(a), "v"(b));
+            for (int r = 0; r < NV / 8; ++r) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(x[i]) : "v"(a), "v"(b));
+            }
         }
     }
     float s = 0;

@@ -71,7 +71,9 @@ def test_deferred_count_matches_synchronous(gs, monkeypatch):
         # the capacity predicted from this very view: the deferred path proper
         "deferred": lambda: G._pred.__setitem__(_key(sc), (n, mb)),
         # predicted from a smaller view: more keys than the capacity -> redone synchronously
-        "overflow_keys": lambda: G._pred.__setitem__(_key(sc), (n // 4, mb)),
+        # (capacities come in 256K-key grains, above this scene's count: the headroom is patched)
+        "overflow_keys": lambda: (G._pred.__setitem__(_key(sc), (n // 4, mb)),
+                                  monkeypatch.setattr(G, "_capacity", lambda a, b: (a + 1024, capacity(a, b)[1]))),
         # a bin over the predicted sort class (capacity 16 keys per bin) -> redone
         "overflow_bin": lambda: (G._pred.__setitem__(_key(sc), (n, mb)),
                                  monkeypatch.setattr(G, "_capacity", lambda a, b: (n + 1024, 16))),

@@ -52,20 +52,17 @@ def test_depth_to_normal_fwd_bwd(C, H, W, z_depth):
     depth = _depth(C, H, W, seed=W)
     gup = torch.randn(C, H, W, 3, generator=torch.Generator().manual_seed(7))
 
-    def ref(dt):
-        d = depth.to(dt).clone().requires_grad_(True)
-        n = TR.depth_to_normal(d, c2w.to(dt), Ks.to(dt), z_depth=z_depth)
-        (n * gup.to(dt)).sum().backward()
-        return n.detach().numpy(), d.grad.numpy()
-
-    n32, g32 = ref(torch.float32)
-    n64, g64 = ref(torch.float64)
+    # f64, then correct f32-level samples: the fork's f32 order, the kernel's (no camera origin),
+    # f64 runs with +-u jittered points
+    n64, g64, S = TR.k13_error_samples(depth, c2w, Ks, gup, z_depth=z_depth)
+    n32, g32 = S[0]
     d = depth.to(DEV).requires_grad_(True)
     n = G.depth_to_normal(d, c2w.to(DEV), Ks.to(DEV), z_depth=z_depth)
     (n * gup.to(DEV)).sum().backward()
     # [C,H,W,*]: conditioning is shared with the differenced neighbours (axes 1, 2)
-    cond_close(n.detach().cpu().numpy(), n32, n64, "normals_from_depth", dilate_axes=(1, 2))
-    cond_close(d.grad.cpu().numpy(), g32, g64, "v_depth", dilate_axes=(1, 2))
+    cond_close(n.detach().cpu().numpy(), n32, n64, "normals_from_depth", dilate_axes=(1, 2),
+               alt32=[x[0] for x in S[1:]])
+    cond_close(d.grad.cpu().numpy(), g32, g64, "v_depth", dilate_axes=(1, 2), dilate=5, alt32=[x[1] for x in S[1:]])
 
 
 def test_depth_to_normal_strided_render_channel():
