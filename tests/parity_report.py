@@ -11,7 +11,12 @@ row with, against the bare north-star bar |x - ref| <= 1e-5 + 1e-4 |ref|:
   worse_g32 / worse_k32         fraction of elements where the GPU is further from f64 than the
                                 gsplat-form (kernel-form) f32 oracle is, by more than the bar:
                                 |gpu - f64| > |o32 - f64| + 1e-5 + 1e-4 |f64|;
-  worse_best                    ... further than the closer of the two f32 oracles.
+  worse_best                    ... further than the closer of the two f32 oracles;
+  better_g32 / better_k32       the mirror image: fraction where that f32 oracle is further from
+                                f64 than the GPU is, by more than the bar.  worse ~ better means
+                                the GPU and that oracle are two equally accurate f32 evaluations
+                                whose errors fall on different elements (gradient sums in another
+                                order); worse >> better would mean a systematically worse GPU.
 
 Rows are kept in RECORDS (printed by tests/conftest.py's terminal summary, so the suite's own
 log carries them) and appended as JSON lines to $HGSR_PARITY_REPORT (default
@@ -54,7 +59,9 @@ def tensor(name, gpu, g32, k32, f64, mask=None):
            "g32~f64": _rate(b, c), "k32~f64": _rate(k, c),
            "worse_g32": float((e > eg + bar).mean()) if a.size else 0.0,
            "worse_k32": float((e > ek + bar).mean()) if a.size else 0.0,
-           "worse_best": float((e > np.minimum(eg, ek) + bar).mean()) if a.size else 0.0}
+           "worse_best": float((e > np.minimum(eg, ek) + bar).mean()) if a.size else 0.0,
+           "better_g32": float((eg > e + bar).mean()) if a.size else 0.0,
+           "better_k32": float((ek > e + bar).mean()) if a.size else 0.0}
     RECORDS.append(row)
     path = os.environ.get("HGSR_PARITY_REPORT") or os.path.join(_ROOT, "gpurun_out", "parity_strict.jsonl")
     try:
@@ -66,7 +73,8 @@ def tensor(name, gpu, g32, k32, f64, mask=None):
     return row
 
 
-COLS = ("gpu~g32", "gpu~k32", "gpu~f64", "g32~f64", "k32~f64", "worse_g32", "worse_k32", "worse_best")
+COLS = ("gpu~g32", "gpu~k32", "gpu~f64", "g32~f64", "k32~f64", "worse_g32", "worse_k32", "worse_best", "better_g32",
+        "better_k32")
 
 
 def table(rows=None):
@@ -75,5 +83,5 @@ def table(rows=None):
            f"{'test':40s} {'tensor':16s} {'n':>9s} " + " ".join(f"{c:>10s}" for c in COLS)]
     for r in rows:
         out.append(f"{r['test'][:40]:40s} {r['tensor'][:16]:16s} {r['n']:9d} "
-                   + " ".join(f"{r[c]:10.6f}" for c in COLS))
+                   + " ".join(f"{r[c]:10.6f}" if c in r else f"{'-':>10s}" for c in COLS))
     return "\n".join(out)
