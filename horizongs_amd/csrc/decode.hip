@@ -18,6 +18,8 @@
 //  * opacity > 0 compaction is order-preserving (anchor-major, then offset) with
 //    wave ballots + a per-tile offset table from a count pass and a scan;
 //  * the colour head (pure linear) is stored straight from the accumulators.
+#include <stdlib.h>
+
 #include <map>
 #include <mutex>
 
@@ -991,6 +993,268 @@ __global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtr
     for (int e = threadIdx.x; e < pf; e += 256) out[e] = red[e];
 }
 
+// ---------------------------------------------------------------- colour head backward, one launch
+// An SH colour head (c4: 27 x 10 = 270 outputs, 17 tiles) used to take four chunked launches of
+// decode_bwd_kernel, each re-staging X, recomputing the hidden layer and doing the dW1 / dX /
+// d feat work again for its 5 tiles (a fixed ~68 us per launch at c4).  Here one launch covers
+// every output row: the workgroup's four waves share their 64 anchors' hidden layer H (LDS) and
+// walk the rows in chunks of 64 (one 16-row tile per wave):
+//   * each wave gathers dY (the colour gradients of the kept slots, zero for dropped ones) of
+//     its own 16 anchors for the chunk's rows into LDS, and the chunk's W2 rows are staged;
+//   * dW2 of the wave's tile accumulates over all 64 anchors (K = anchors, H from LDS) -- so
+//     every wave keeps <= 5 tiles of dW2 accumulators, as in the chunked launches;
+//   * dH of the wave's own anchors accumulates over the chunk's rows (W2^T dY).
+// After the last chunk each wave finishes its anchors as decode_bwd_kernel does (ReLU mask,
+// dW1, dX -> d feat / d anchor, one read-modify-write of d feat instead of four).  dW2 rows
+// are owned by one wave each and go straight to the workgroup's partial; dW1 / db1 are summed
+// over the waves in wave order (deterministic).  Fragment reads use padded strides (one base
+// register + immediate offsets per pattern): ydt at 68 floats per anchor row is conflict-free
+// for the dH fragment and 2-way for the dW2 one; hs / w2c at 32 are 2-way.
+constexpr int kColBwdTilesPerWave = 5;  // <= 20 output tiles (320 rows)
+constexpr int kYdtS = 68;               // ydt row stride (floats)
+
+struct DecodeColBwdSmem {
+    float w1[32 * kDecS];
+    float b1[32];
+    float x[4][16 * kDecS];
+    float ydt[64 * kYdtS];  // the chunk's dY: [anchor][row]; after the chunks: dH^T scratch, reduction
+    float hs[64 * 32];      // H of the tile's anchors: [anchor][hidden]
+    float w2c[64 * 32];     // the chunk's W2 rows: [row][hidden]
+    int slot[64 * 12];      // slot rows of the tile's (anchor, offset) pairs
+};
+
+template <int KSTEPS>
+__global__ __launch_bounds__(256, 3) void decode_bwd_color_kernel(DecodeDims d, MlpPtrs mp,
+                                                                  const int32_t* __restrict__ vis_idx,
+                                                                  const float* __restrict__ anchor,
+                                                                  const float* __restrict__ feat,
+                                                                  const float* __restrict__ cam,
+                                                                  const int32_t* __restrict__ slot_row,
+                                                                  DecodeGrads gr, float* __restrict__ partials) {
+    constexpr int NTW = kColBwdTilesPerWave;
+    __shared__ DecodeColBwdSmem sm;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    const int K1 = kDecF + d.vd, noff = d.noff, cd = d.cd, O = d.O[2], T = d.T[2];
+    const int n_chunks = (T + 3) / 4;
+    const float* gcol = gr.g_color;  // non-null: the host skips a colour head without gradients
+    for (int e = threadIdx.x; e < 32 * kDecS; e += 256) {
+        const int h = e / kDecS, k = e - h * kDecS;
+        sm.w1[e] = k < K1 ? mp.w1[2][h * K1 + k] : 0.f;
+    }
+    if (threadIdx.x < 32) sm.b1[threadIdx.x] = mp.b1[2][threadIdx.x];
+    f32x4 aw2[NTW][2], aw1[2][3];
+#pragma unroll
+    for (int c = 0; c < NTW; ++c) aw2[c][0] = aw2[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < 2; ++a) aw1[a][0] = aw1[a][1] = aw1[a][2] = f32x4{0.f, 0.f, 0.f, 0.f};
+    double ab2[NTW], ab1 = 0.0;
+#pragma unroll
+    for (int c = 0; c < NTW; ++c) ab2[c] = 0.0;
+    float* sx = sm.x[wave];
+    const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
+    XPrefetch px;
+    if (blockIdx.x < (unsigned)n_tiles) {
+        x_issue_id(px, vis_idx, blockIdx.x * kDecTile + wave * 16, d.Av);
+        x_issue_data(px, feat, anchor, d.vd);
+    }
+    __syncthreads();  // W1 staged
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const int A0 = t * kDecTile;     // the workgroup's 64 anchors
+        const int a0 = A0 + wave * 16;   // this wave's 16
+        float my_ov[3], my_dist;
+        x_store(px, sx, d.vd, cam, my_ov, my_dist);
+        const int cur_id = px.id;  // lane i: id of anchor i of this wave, -1 past Av
+        for (int e = threadIdx.x; e < kDecTile * noff; e += 256)
+            sm.slot[e] = A0 + e / noff < d.Av ? slot_row[(int64_t)A0 * noff + e] : -1;
+        const int tn = t + gridDim.x;
+        if (tn < n_tiles) x_issue_id(px, vis_idx, tn * kDecTile + wave * 16, d.Av);
+        float old_feat[2][4], old_anc[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                old_feat[kt][r] = cur_id >= 0 ? gr.d_feat[(int64_t)cur_id * kDecF + kt * 16 + 4 * g + r] : 0.f;
+        const bool anc_lane = lane < 16 && cur_id >= 0 && gr.d_anchor && d.vd > 0;
+        if (anc_lane)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) old_anc[q] = gr.d_anchor[(int64_t)cur_id * 3 + q];
+        wave_lds_sync();
+        // hidden layer of this wave's anchors, published to the workgroup as H[anchor][hidden]
+        f32x4 h0 = {0.f, 0.f, 0.f, 0.f}, h1 = h0;
+#pragma unroll
+        for (int kk = 0; kk < KSTEPS; ++kk) {
+            h0 = mfma4(sm.w1[i * kDecS + 4 * kk + g], sx[i * kDecS + 4 * kk + g], h0);
+            h1 = mfma4(sm.w1[(16 + i) * kDecS + 4 * kk + g], sx[i * kDecS + 4 * kk + g], h1);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            h0[r] = fmaxf(h0[r] + sm.b1[4 * g + r], 0.f);
+            h1[r] = fmaxf(h1[r] + sm.b1[16 + 4 * g + r], 0.f);
+            sm.hs[(wave * 16 + i) * 32 + 4 * g + r] = h0[r];
+            sm.hs[(wave * 16 + i) * 32 + 16 + 4 * g + r] = h1[r];
+        }
+        if (tn < n_tiles) x_issue_data(px, feat, anchor, d.vd);
+        __syncthreads();  // H and the slot table published (every wave is past its last tile)
+        f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;  // dH[hidden 4g + r (+16)][own anchor i]
+        // chunk c works on aw2[0] / ab2[0], then the accumulators rotate by one (a rolled loop:
+        // unrolled, the compiler hoists every chunk's fragment reads and spills); NTW rotations
+        // per tile in all, so aw2[c] belongs to chunk c again after the tile
+#pragma nounroll
+        for (int c = 0; c < NTW; ++c) {
+            if (c < n_chunks) {
+            {
+                // dY of this wave's anchors, rows [64 c, 64 c + 64): lane = row (a slot's colours
+                // are contiguous, so a wave's loads cover whole slot rows)
+                const int o = 64 * c + lane;
+                const bool orow = o < O;
+                const int k = orow ? o / cd : 0, ch = o - k * cd;
+                // branch-free: a dropped slot (or a padding row) loads the first colour, then 0
+                float v[16];
+                const int* srow = sm.slot + wave * 16 * noff + k;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int p = srow[j * noff];
+                    const float x = gcol[(int64_t)(p > 0 ? p : 0) * cd + (orow ? ch : 0)];
+                    v[j] = (orow & (p >= 0)) ? x : 0.f;
+                }
+                // the chunk's W2 rows: thread -> row tid / 4, 8 columns
+                const int rr = threadIdx.x >> 2, hc = 8 * (threadIdx.x & 3), oo = 64 * c + rr;
+                float w[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) w[q] = oo < O ? mp.w2[2][oo * kDecF + hc + q] : 0.f;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) sm.ydt[(wave * 16 + j) * kYdtS + lane] = v[j];
+                *reinterpret_cast<float4*>(&sm.w2c[rr * 32 + hc]) = make_float4(w[0], w[1], w[2], w[3]);
+                *reinterpret_cast<float4*>(&sm.w2c[rr * 32 + hc + 4]) = make_float4(w[4], w[5], w[6], w[7]);
+            }
+            __syncthreads();
+            // dH of this wave's anchors over the chunk's rows: dH[h][a] += sum_r W2[r][h] dY[r][a]
+            {
+                const float* yb = sm.ydt + (wave * 16 + i) * kYdtS + g;
+                const float* wb = sm.w2c + g * 32 + i;
+#pragma unroll
+                for (int kk = 0; kk < 16; ++kk) {
+                    const float b = yb[4 * kk];
+                    d0 = mfma4(wb[kk * 128], b, d0);
+                    d1 = mfma4(wb[kk * 128 + 16], b, d1);
+                }
+            }
+            // dW2 of this wave's tile (4 c + wave) over the 64 anchors, db2 partial row sums
+            if (4 * c + wave < T) {
+                float sum = 0.f;
+                const float* ya = sm.ydt + g * kYdtS + wave * 16 + i;
+                const float* hb = sm.hs + g * 32 + i;
+#pragma unroll
+                for (int kk = 0; kk < 16; ++kk) {
+                    const float a = ya[4 * kk * kYdtS];
+                    sum += a;
+                    aw2[0][0] = mfma4(a, hb[kk * 128], aw2[0][0]);
+                    aw2[0][1] = mfma4(a, hb[kk * 128 + 16], aw2[0][1]);
+                }
+                ab2[0] += sum;
+            }
+            __syncthreads();  // the chunk's ydt / w2c / hs reads are done before they are rewritten
+            }
+            const f32x4 r0 = aw2[0][0], r1 = aw2[0][1];
+            const double rb = ab2[0];
+#pragma unroll
+            for (int q = 0; q + 1 < NTW; ++q) {
+                aw2[q][0] = aw2[q + 1][0];
+                aw2[q][1] = aw2[q + 1][1];
+                ab2[q] = ab2[q + 1];
+            }
+            aw2[NTW - 1][0] = r0;
+            aw2[NTW - 1][1] = r1;
+            ab2[NTW - 1] = rb;
+        }
+        // ReLU mask, then dH^T through this wave's scratch (the chunk buffer, free now) for dW1
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            d0[r] = h0[r] > 0.f ? d0[r] : 0.f;
+            d1[r] = h1[r] > 0.f ? d1[r] : 0.f;
+        }
+        float* sh = sm.ydt + wave * (32 * kDecBS);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            sh[(4 * g + r) * kDecBS + i] = d0[r];
+            sh[(16 + 4 * g + r) * kDecBS + i] = d1[r];
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+            for (int kt = 0; kt < 3; ++kt) {
+                if (kt * 16 >= K1) break;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                    aw1[ht][kt] = mfma4(sh[(ht * 16 + i) * kDecBS + 4 * kk + g], sx[(4 * kk + g) * kDecS + kt * 16 + i],
+                                        aw1[ht][kt]);
+            }
+        if (lane < 32) {
+            float sum = 0.f;
+#pragma unroll
+            for (int a = 0; a < 16; ++a) sum += sh[lane * kDecBS + a];
+            ab1 += sum;
+        }
+        // dX = W1^T dH -> d feat (k < 32), d ob_view (k = 32..34) -> d anchor
+        const bool present = cur_id >= 0;
+#pragma unroll
+        for (int kt = 0; kt < 3; ++kt) {
+            if (kt * 16 >= K1) break;
+            f32x4 dx = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dx = mfma4(sm.w1[(4 * g + r) * kDecS + kt * 16 + i], d0[r], dx);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dx = mfma4(sm.w1[(16 + 4 * g + r) * kDecS + kt * 16 + i], d1[r], dx);
+            if (!present) continue;
+            if (kt < 2) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    gr.d_feat[(int64_t)cur_id * kDecF + kt * 16 + 4 * g + r] = old_feat[kt][r] + dx[r];
+            } else if (g == 0 && gr.d_anchor) {
+                const float dot = my_ov[0] * dx[0] + my_ov[1] * dx[1] + my_ov[2] * dx[2];
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    gr.d_anchor[(int64_t)cur_id * 3 + q] = old_anc[q] + (dx[q] - my_ov[q] * dot) / my_dist;
+            }
+        }
+    }
+    // partial of this workgroup, layout of bwd_partial_floats(T): dW2 [rows][32] | db2 [rows] |
+    // dW1 [32][48] | db1 [32].  dW2 / db2 rows belong to one wave each: stored directly.
+    const int rows = T * 16;
+    float* out = partials + (int64_t)blockIdx.x * bwd_partial_floats(T);
+#pragma unroll
+    for (int c = 0; c < NTW; ++c) {
+        const int tt = 4 * c + wave;
+        if (tt >= T) continue;
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[(tt * 16 + 4 * g + r) * 32 + ht * 16 + i] = aw2[c][ht][r];
+        double s2 = ab2[c];
+        s2 += __shfl_xor(s2, 16);
+        s2 += __shfl_xor(s2, 32);
+        if (g == 0) out[rows * 32 + tt * 16 + i] = (float)s2;
+    }
+    __syncthreads();  // the chunk buffer is reused for the dW1 / db1 sum
+    float* red = sm.ydt;
+    static_assert(sizeof(sm.ydt) >= sizeof(float) * (32 * 48 + 32), "LDS too small for the combine");
+    for (int w = 0; w < 4; ++w) {
+        if (wave == w) {
+            auto put = [&](int idx, float v) { red[idx] = w == 0 ? v : red[idx] + v; };
+#pragma unroll
+            for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+                for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) put((ht * 16 + 4 * g + r) * 48 + kt * 16 + i, aw1[ht][kt][r]);
+            if (lane < 32) put(32 * 48 + lane, (float)ab1);
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < 32 * 48 + 32; e += 256) out[rows * 33 + e] = red[e];
+}
+
 // sum the per-wave partials of one launch into the weight gradients (+=), in two
 // fixed-order levels: decode_wgrad_sum_kernel folds groups of partials (f64 sums),
 // decode_wgrad_reduce_kernel folds the groups and scatters into the gradient tensors
@@ -1193,9 +1457,17 @@ static int bwd_grid(int Av) {
 }
 
 
+// partials: 4 per workgroup of a chunked launch, or 1 (all rows) of the one-launch colour head
+static size_t bwd_part_floats_max() {
+    const size_t a = 4 * (size_t)bwd_partial_floats(kBwdChunk), b = bwd_partial_floats(4 * kColBwdTilesPerWave);
+    return a > b ? a : b;
+}
+
 extern "C" size_t hgsr_decode_bwd_ws_bytes(int Av) {
-    const size_t parts = ((size_t)bwd_grid(Av) * 4 * bwd_partial_floats(kBwdChunk) * sizeof(float) + 255) & ~(size_t)255;
-    return parts + (size_t)kRedGroups * bwd_partial_floats(kBwdChunk) * sizeof(double);
+    const size_t parts = ((size_t)bwd_grid(Av) * bwd_part_floats_max() * sizeof(float) + 255) & ~(size_t)255;
+    const size_t pf = bwd_partial_floats(4 * kColBwdTilesPerWave) > bwd_partial_floats(kBwdChunk)
+                          ? bwd_partial_floats(4 * kColBwdTilesPerWave) : bwd_partial_floats(kBwdChunk);
+    return parts + (size_t)kRedGroups * pf * sizeof(double);
 }
 
 extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim, const int32_t* vis_idx,
@@ -1218,8 +1490,11 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
     hipStream_t s = as_stream(stream);
     int grid = bwd_grid(Av);
     float* partials = (float*)ws;
-    double* level2 = (double*)((char*)ws + (((size_t)grid * 4 * bwd_partial_floats(kBwdChunk) * sizeof(float) + 255) &
-                                            ~(size_t)255));
+    double* level2 = (double*)((char*)ws + (((size_t)grid * bwd_part_floats_max() * sizeof(float) + 255) & ~(size_t)255));
+    // an SH colour head (more tiles than one chunked launch holds) in one launch:
+    // decode_bwd_color_kernel; HGSR_DEC_COLBWD=0 keeps the chunked launches (A/B)
+    const char* col_env = getenv("HGSR_DEC_COLBWD");  // read per call: the tests switch it
+    const bool col_one = col_env ? atoi(col_env) != 0 : true;
     const int K1 = kDecF + view_dim;
     KernelTimer kt("decode_bwd", s);
     // the cov head first: after it d_offset, d_scaling and the cov weights are final, so a
@@ -1231,6 +1506,28 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
         if (!((mask >> head) & 1)) continue;
         // up to 5 output tiles per launch (the cov head in one launch; measured: splitting it
         // into 3 + 2 tiles gains nothing, its time is the per-tile work, not the accumulators)
+        if (head == 2 && col_one && d.T[2] > kBwdChunk && d.T[2] <= 4 * kColBwdTilesPerWave) {
+            if (!g_color) continue;  // no colour gradient: every term of this head is zero
+            const int nt = d.T[2];
+            if (view_dim == 3) {
+                grid = grid_resident(reinterpret_cast<const void*>(&decode_bwd_color_kernel<9>), Av);
+                hipLaunchKernelGGL(decode_bwd_color_kernel<9>, dim3(grid), dim3(256), 0, s, d, mp, vis_idx, anchor,
+                                   feat, cam_center, slot_row, gr, partials);
+            } else {
+                grid = grid_resident(reinterpret_cast<const void*>(&decode_bwd_color_kernel<8>), Av);
+                hipLaunchKernelGGL(decode_bwd_color_kernel<8>, dim3(grid), dim3(256), 0, s, d, mp, vis_idx, anchor,
+                                   feat, cam_center, slot_row, gr, partials);
+            }
+            if (int st = check_launch("decode_bwd")) return st;
+            const int pf = bwd_partial_floats(nt);
+            hipLaunchKernelGGL(decode_wgrad_sum_kernel, dim3((pf + 255) / 256, kRedGroups), dim3(256), 0, s, grid,
+                               pf, partials, level2);
+            if (int st = check_launch("decode_wgrad_sum")) return st;
+            hipLaunchKernelGGL(decode_wgrad_reduce_kernel, dim3((pf + 255) / 256), dim3(256), 0, s, nt, 0, d.O[2], K1,
+                               level2, d_mlp[4 * 2 + 2], d_mlp[4 * 2 + 3], d_mlp[4 * 2], d_mlp[4 * 2 + 1]);
+            if (int st = check_launch("decode_wgrad_reduce")) return st;
+            continue;
+        }
         const int chunk = kBwdChunk;
         for (int t0 = 0; t0 < d.T[head]; t0 += chunk) {
             const int nt = d.T[head] - t0 < chunk ? d.T[head] - t0 : chunk;

@@ -356,8 +356,11 @@ def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
     rates["alpha"], _ = image_close(alpha.detach()[:, :rr].cpu().numpy(), ra, r64.ra, amb, "2dgs alphas",
                                     alt32=r32b.ra)
     # viewmat = I: the world-frame normals are the camera-frame ones
+    # normals keep factor 3: at c3 one element of 6.2M (an edge-on surfel, where the normal's
+    # direction is the cross product of two nearly parallel tangent axes) sits 2.2e-3 further
+    # from f64 than either f32 hit form (profiles/r04_parity_strict.txt)
     rates["normals"], _ = image_close(normals.detach()[:, :rr].cpu().numpy(), rn, r64.rn, amb, "2dgs normals",
-                                      alt32=r32b.rn)
+                                      alt32=r32b.rn, factor=3.0)
     rates["ambiguous_px"] = n_amb
     rates["grad_ambiguous_px"] = int(gamb.sum())
     assert gamb.mean() <= MAX_GRAD_AMBIGUOUS, gamb.mean()
