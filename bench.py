@@ -320,9 +320,11 @@ def decode_mfma(wl, kernels):
     inputs, KS = ceil(K1 / 4) k-steps, output tiles T = ceil(rows / 16) per head):
       forward  : hidden 2 KS per head x 3 + second layer 8 T per head (+ the count pass: the
                  opacity head again, 2 KS + 8);
-      backward : per head launch (colour head chunked by <= 5 output tiles) hidden 2 KS +
-                 recomputed Y (8 x all T, opacity / cov) + dW2 8 nt + dH 8 nt + dW1 and dX
-                 8 ceil(K1 / 16) each.
+      backward : per head launch (an RGB colour head in one chunk of <= 5 output tiles) hidden
+                 2 KS + recomputed Y (8 x all T, opacity / cov) + dW2 8 nt + dH 8 nt + dW1 and
+                 dX 8 ceil(K1 / 16) each; an SH colour head (T > 5) runs as one launch
+                 (decode_bwd_color_kernel): hidden 2 KS + dW2 8 T + dH 32 ceil(T / 4) (64-row
+                 chunks, padding rows included) + dW1 and dX as above.
     busy = MFMA FLOP / kernel time / 157.3 TFLOP/s (= the f32 MFMA peak at 64 FLOP/clk/SIMD),
     which is SQ_VALU_MFMA_BUSY_CYCLES / (SIMD count x kernel cycles) at the peak clock: the
     r02 PMC pass measured exactly 374 x 32 SIMD-cycles per wave tile for the RGB model."""
@@ -335,7 +337,11 @@ def decode_mfma(wl, kernels):
     T = [1, 5, (wl.color_dim * 10 + 15) // 16]  # opacity 10, cov 70, colour color_dim x 10 rows
     fwd = 3 * 2 * KS + 8 * sum(T) + (2 * KS + 8)
     bwd = 0
+    col_one = os.environ.get("HGSR_DEC_COLBWD", "1") != "0" and 5 < T[2] <= 20
     for h in range(3):
+        if h == 2 and col_one:
+            bwd += 2 * KS + 8 * T[2] + 32 * ((T[2] + 3) // 4) + 16 * kt
+            continue
         chunks = [min(5, T[h] - t0) for t0 in range(0, T[h], 5)]
         for nt in chunks:
             bwd += 2 * KS + (8 * T[h] if h < 2 else 0) + 16 * nt + 16 * kt

@@ -592,14 +592,13 @@ struct DecodeBwdSmem {
     float x[4][16 * kDecS];
     float dy[4][YR * kDecBS];  // recomputed pre-activations Y^T, overwritten in place by dY^T[o][anchor]
     float h[4][32 * kDecBS];                 // H^T, then dH^T [hidden][anchor]
-    float acc[4][16 * 9];                    // per-anchor d scaling_raw (6) + d anchor (3)
 };
 
 // partial layout per wave: dW2 chunk [nt*16][32] | db2 chunk [nt*16] | dW1 [32][48] | db1 [32]
 __host__ __device__ inline int bwd_partial_floats(int nt) { return nt * 16 * 32 + nt * 16 + 32 * 48 + 32; }
 
 template <int KSTEPS, int HEAD, int NT>
-__global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtrs mp, int t0, int nt,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HEAD == 0 ? 3 : 2, 8))) void decode_bwd_kernel(DecodeDims d, MlpPtrs mp, int t0, int nt,
                                                          const int32_t* __restrict__ vis_idx,
                                                          const float* __restrict__ anchor,
                                                          const float* __restrict__ feat,
@@ -641,7 +640,6 @@ __global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtr
     float* sdy = sm.dy[wave];
     float* sy = sdy;  // every slot reads its own Y entries before writing its dY there
     float* sh = sm.h[wave];
-    float* sacc = sm.acc[wave];
     const int n_tiles = (d.Av + kDecTile - 1) / kDecTile;
     __syncthreads();  // weights staged
     DPROF_INIT
@@ -656,7 +654,10 @@ __global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtr
         x_issue_id(px, vis_idx, blockIdx.x * kDecTile + wave * 16, d.Av);
         x_issue_data(px, feat, anchor, d.vd);
     }
-    constexpr int kSI = 3;  // 16 anchors x n_offsets <= 12 -> <= 192 slots = 3 per lane
+    // slots of the opacity / cov heads: lane (anchor i, group g) takes offsets k = g + 4 it,
+    // it < 3 (n_offsets <= 12), so an anchor's slot sums reduce across the 4 lane groups with
+    // two cross-lane adds instead of LDS float atomics (3 cycles per lane each on the CU)
+    constexpr int kSI = 3;
     constexpr int kCI = NT * 4;  // colour head: rows * 16 / 64 (anchor, output) pairs per lane
     for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
         wave_lds_sync();  // this wave's previous tile is done with its LDS arrays
@@ -664,7 +665,6 @@ __global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtr
         float my_ov[3], my_dist;
         x_store(px, sx, d.vd, cam, my_ov, my_dist);
         const int cur_id = px.id;  // lane i (= lane & 15): id of anchor i of this tile, -1 past Av
-        for (int e = lane; e < 16 * 9; e += 64) sacc[e] = 0.f;
         const int tn = t + gridDim.x;
         if (tn < n_tiles) x_issue_id(px, vis_idx, tn * kDecTile + wave * 16, d.Av);
         // old values of the accumulated input gradients of this tile (d feat rows of anchor i,
@@ -686,9 +686,8 @@ __global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtr
         int sp[kSI], cp[kCI];
 #pragma unroll
         for (int it = 0; it < kSI; ++it) {
-            const int sl = lane + 64 * it;
-            const int a = sl / noff;
-            sp[it] = (head < 2 && sl < 16 * noff && a0 + a < d.Av) ? slot_row[(int64_t)a0 * noff + sl] : -1;
+            const int k = g + 4 * it;
+            sp[it] = (head < 2 && k < noff && cur_id >= 0) ? slot_row[(int64_t)(a0 + i) * noff + k] : -1;
         }
 #pragma unroll
         for (int it = 0; it < kCI; ++it) {
@@ -716,33 +715,29 @@ __global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtr
         // the next tile's X rows (its ids have arrived) and this tile's output-gradient gathers
         if (tn < n_tiles) x_issue_data(px, feat, anchor, d.vd);
         float gop[kSI], gcol[kCI];
-        int sk[kSI], sid[kSI];
-        float gsc[kSI][3], grt[kSI][4], gxy[kSI][3], gof[kSI][3], ofs[kSI][3], srw[kSI][6];
+        float gsc[kSI][3], grt[kSI][4], gxy[kSI][3], gof[kSI][3], ofs[kSI][3], srw[6];
 #pragma unroll
         for (int it = 0; it < kSI; ++it) {
-            const int sl = lane + 64 * it;
-            const int a = sl / noff;
-            sk[it] = sl - a * noff;
-            const int aid = __shfl(cur_id, a < 16 ? a : 0);
-            sid[it] = (sl < 16 * noff && a0 + a < d.Av) ? aid : -1;
+            const int k = g + 4 * it;
             const int64_t p = sp[it] < 0 ? 0 : sp[it];
             const bool live = sp[it] >= 0;
             gop[it] = (head == 0 && live && gr.g_opacity) ? gr.g_opacity[p] : 0.f;
             if (head == 1) {
-                const int64_t id = sid[it] < 0 ? 0 : sid[it];
+                const int64_t id = cur_id < 0 ? 0 : cur_id;
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
                     gsc[it][q] = (live && gr.g_scaling) ? gr.g_scaling[p * 3 + q] : 0.f;
                     gxy[it][q] = (live && gr.g_xyz && t0 == 0) ? gr.g_xyz[p * 3 + q] : 0.f;
                     gof[it][q] = (live && gr.g_offsets && t0 == 0) ? gr.g_offsets[p * 3 + q] : 0.f;
-                    ofs[it][q] = (live && t0 == 0) ? offset[(id * noff + sk[it]) * 3 + q] : 0.f;
+                    ofs[it][q] = (live && t0 == 0) ? offset[(id * noff + k) * 3 + q] : 0.f;
                 }
 #pragma unroll
                 for (int q = 0; q < 4; ++q) grt[it][q] = (live && gr.g_rot) ? gr.g_rot[p * 4 + q] : 0.f;
-#pragma unroll
-                for (int q = 0; q < 6; ++q) srw[it][q] = live ? scaling_raw[id * 6 + q] : 0.f;
             }
         }
+        if (head == 1)  // the anchor's raw scaling, once per lane (all its slots share it)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) srw[q] = cur_id >= 0 ? scaling_raw[(int64_t)cur_id * 6 + q] : 0.f;
 #pragma unroll
         for (int it = 0; it < kCI; ++it) {
             const int e = lane + 64 * it, o = o0 + (e >> 4);
@@ -776,25 +771,26 @@ __global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtr
             const int used = head == 0 ? noff : 7 * noff;
             for (int e = lane; e < (srows - used) * 16; e += 64) sdy[(used + (e >> 4)) * kDecBS + (e & 15)] = 0.f;
         }
+        // per-anchor sums of this lane's slots (cov head): d scaling_raw 0..5, d anchor 0..2
+        float asum[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         if (head == 0) {
 #pragma unroll
             for (int it = 0; it < kSI; ++it) {
-                const int sl = lane + 64 * it;
-                if (sl >= 16 * noff) continue;
-                const int a = sl / noff, k = sl - a * noff;
+                const int k = g + 4 * it;
+                if (k >= noff) continue;
                 float v = 0.f;
                 if (sp[it] >= 0 && gr.g_opacity) {
-                    const float th = fast_tanh(sy[k * kDecBS + a]);
+                    const float th = fast_tanh(sy[k * kDecBS + i]);
                     v = gop[it] * (1.0f - th * th);
                 }
-                sdy[k * kDecBS + a] = v;
+                sdy[k * kDecBS + i] = v;
             }
         } else if (head == 1) {
 #pragma unroll
             for (int it = 0; it < kSI; ++it) {
-                const int a = (lane + 64 * it) / noff, k = sk[it];
-                if (lane + 64 * it >= 16 * noff) continue;
-                const int64_t id = sid[it];
+                const int a = i, k = g + 4 * it;
+                if (k >= noff) continue;
+                const int64_t id = cur_id;
                 const int p = sp[it];
                 float cv[7], dv[7];
 #pragma unroll
@@ -815,10 +811,10 @@ __global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 if (gr.g_scaling) {
 #pragma unroll
                     for (int q = 0; q < 3; ++q) {
-                        const float es = __expf(srw[it][3 + q]), sg = __builtin_amdgcn_rcpf(1.0f + __expf(-cv[q]));
+                        const float es = __expf(srw[3 + q]), sg = __builtin_amdgcn_rcpf(1.0f + __expf(-cv[q]));
                         const float gs = gsc[it][q];
                         dv[q] = gs * es * sg * (1.0f - sg);
-                        if (t0 == 0) atomicAdd(&sacc[a * 9 + 3 + q], gs * es * sg);
+                        asum[3 + q] += gs * es * sg;
                     }
                 }
                 // rot = v / max(|v|, 1e-12)
@@ -845,24 +841,30 @@ __global__ __launch_bounds__(256, 2) void decode_bwd_kernel(DecodeDims d, MlpPtr
                 for (int q = 0; q < 3; ++q) {
                     const float gx = gxy[it][q];
                     const float gt = gx + gof[it][q];
-                    const float es = __expf(srw[it][q]);
+                    const float es = __expf(srw[q]);
                     dof[q] = gt * es;
-                    atomicAdd(&sacc[a * 9 + q], gt * ofs[it][q] * es);
-                    atomicAdd(&sacc[a * 9 + 6 + q], gx);
+                    asum[q] += gt * ofs[it][q] * es;
+                    asum[6 + q] += gx;
                 }
             }
+            // the anchor's slot sums: its 4 lane groups g (offsets g + 4 it) combined
+            if (t0 == 0)
+#pragma unroll
+                for (int q = 0; q < 9; ++q) {
+                    asum[q] += __shfl_xor(asum[q], 16);
+                    asum[q] += __shfl_xor(asum[q], 32);
+                }
         }
         DPROF_T(3);
         // per-anchor d scaling_raw / d anchor of the cov head (xyz and scaling outputs); the
         // d anchor sum joins the view-direction term of dX below (one store per tile)
         float anc_add[3] = {0.f, 0.f, 0.f};
         if (head == 1 && t0 == 0) {
-            wave_lds_sync();
             if (lane < 16 && cur_id >= 0) {
 #pragma unroll
-                for (int q = 0; q < 6; ++q) gr.d_scaling[(int64_t)cur_id * 6 + q] = old_sc[q] + sacc[lane * 9 + q];
+                for (int q = 0; q < 6; ++q) gr.d_scaling[(int64_t)cur_id * 6 + q] = old_sc[q] + asum[q];
 #pragma unroll
-                for (int q = 0; q < 3; ++q) anc_add[q] = sacc[lane * 9 + 6 + q];
+                for (int q = 0; q < 3; ++q) anc_add[q] = asum[6 + q];
                 if (gr.d_anchor && d.vd == 0)
 #pragma unroll
                     for (int q = 0; q < 3; ++q) gr.d_anchor[(int64_t)cur_id * 3 + q] = old_anc[q] + anc_add[q];

@@ -211,10 +211,13 @@ def test_pipeline_step_gradients(gs):
 
 
 # ----------------------------------------------------------------------------- at scale
-def _parity_at_scale(gs):
+def _parity_at_scale(gs, fixture=None):
     """PSNR parity at scale: 50k anchors at 480x270, 500 iterations of the whole train step at
-    the fine-stage learning rates (unscaled).  The CPU reference chain takes ~1 s per iteration,
-    so its result is a committed fixture (tests/golden/psnr_scale_{gs}.json, generated by
+    the fixture's multiple of the fine-stage learning rates (3DGS 0.1x, 2DGS 0.3x: there the
+    reference chain's own 1e-6 perturbation moves its window PSNR by 0.002 / 0.023 dB, under
+    the 0.05 dB bar; 3DGS at 0.3x and 1x below, where that floor is 0.11 / 0.43 dB).  The CPU
+    reference chain takes ~3 s per iteration, so its result is a committed fixture
+    (tests/golden/psnr_scale_{gs}[_lrNN].json, generated by
     scripts/psnr_at_scale.py with the same seeds: its own run and a run from a 1e-6-perturbed
     initialisation, the chain's noise floor).  The HIP chain runs here from the same
     initialisation; its window PSNR (last 50 iterations' renders) must be within 0.05 dB of the
@@ -222,7 +225,8 @@ def _parity_at_scale(gs):
     floor is what is stated, reference train.py:150-277)."""
     from scripts import psnr_at_scale as PS
     from tests import pipeline_fit as PF
-    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", f"psnr_scale_{gs}.json")))
+    fixture = fixture or f"psnr_scale_{gs}"
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", f"{fixture}.json")))
     A, W, H, iters = gold["anchors"], gold["width"], gold["height"], gold["iterations"]
     assert gold["seeds"] == PS.SEEDS
     gt, p0, cfg, _ = PS.problem(A, W, H, gs)
@@ -241,10 +245,10 @@ def _parity_at_scale(gs):
                iterations=iters, anchors=A, width=W, height=H, lr_scale=gold["lr_scale"],
                loss_first=[round(ref["loss_first"], 6), round(loss_gpu[0], 6)],
                loss_last=[round(ref["loss_last"], 6), round(loss_gpu[-1], 6)],
-               reference=f"tests/golden/psnr_scale_{gs}.json (scripts/psnr_at_scale.py: the CPU chain of "
+               reference=f"tests/golden/{fixture}.json (scripts/psnr_at_scale.py: the CPU chain of "
                          "tests/pipeline_fit.py, reference-pinned decode + loss, C-oracle rasterizer, torch Adam)")
     os.makedirs("gpurun_out", exist_ok=True)
-    with open(os.path.join("gpurun_out", f"psnr_scale_{gs}gs.json"), "w") as f:
+    with open(os.path.join("gpurun_out", f"{fixture}_{gs}gs.json".replace(f"psnr_scale_{gs}_", "psnr_scale_")), "w") as f:
         json.dump(res, f)
     print(res)
     # identical parameters at the first step: the chains agree before any divergence
@@ -261,3 +265,12 @@ def test_psnr_parity_at_scale_3dgs():
 @pytest.mark.slow
 def test_psnr_parity_at_scale_2dgs():
     _parity_at_scale("2d")
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("fixture", ["psnr_scale_3d_lr03", "psnr_scale_3d_lr1"])
+def test_psnr_parity_at_scale_3dgs_higher_lr(fixture):
+    """The 3DGS chain at 0.3x and at the unscaled fine-stage learning rates: the reference
+    chain's own 1e-6 perturbation moves its window PSNR by 0.11 / 0.43 dB there (the chain is
+    chaotic at these rates), so the bar is that floor; the 0.1x fixture above is the tight one."""
+    _parity_at_scale("3d", fixture)
