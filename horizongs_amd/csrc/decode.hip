@@ -1025,8 +1025,11 @@ struct DecodeColBwdSmem {
     int slot[64 * 12];      // slot rows of the tile's (anchor, offset) pairs
 };
 
+#ifndef HGSR_COLBWD_WAVES
+#define HGSR_COLBWD_WAVES 2  // waves / SIMD: 234 VGPRs, no spills (at 3 it spills ~170: 0.864 vs 0.803 ms at c4)
+#endif
 template <int KSTEPS>
-__global__ __launch_bounds__(256, 3) void decode_bwd_color_kernel(DecodeDims d, MlpPtrs mp,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HGSR_COLBWD_WAVES, 8))) void decode_bwd_color_kernel(DecodeDims d, MlpPtrs mp,
                                                                   const int32_t* __restrict__ vis_idx,
                                                                   const float* __restrict__ anchor,
                                                                   const float* __restrict__ feat,
