@@ -313,10 +313,18 @@ def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None
             if k == "colors" and not Dc:
                 continue
             rates["v2_" + k] = cond_close(v.cpu().numpy(), gv32[k], gv64[k], "v2_" + k + " (resolved branches)",
-                                          rel_floor=0, env=genv2[k], env_k=2.0)
+                                          rel_floor=0, env=genv2[k], env_k=ENV_K_RESOLVED)
     print("strict 1e-5/1e-4 pass rates:", {k: (round(float(v), 6) if not isinstance(v, dict) else v)
                                            for k, v in rates.items()}, "stats", stats)
     return stats, rates, dict(out=out, alpha=alpha, meta=meta, r32=r32, r64=r64, grads=got, gr32=gr32, gr64=gr64)
+
+
+# Envelope multiple of the resolved-branch re-check (gradients with the near-threshold pixels'
+# upstream kept, the oracle forced onto the GPU's branches).  E sums the per-step roundings in
+# quadrature (an RMS estimate, oracle Raster*.envelope), so its tail grows with the element
+# count: over the 6M colour gradients of the full c3 frame the worst element needs 5.9 u E
+# (profiles/r04_parity_strict.txt), the 1080-row band of round 3 needed < 2.
+ENV_K_RESOLVED = 8.0
 
 
 def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
@@ -445,7 +453,7 @@ def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
         got2 = {"densify": meta["gradient_2dgs"].grad, **{k: v.grad for k, v in leaves.items()}}
         for k, v in got2.items():
             rates["v2_" + k] = cond_close(v.cpu().numpy(), gv["32"][k], gv["64"][k], "v2_" + k + " (resolved branches)",
-                                          rel_floor=0, env=genv2[k], env_k=2.0, alt32=gv["32b"][k])
+                                          rel_floor=0, env=genv2[k], env_k=ENV_K_RESOLVED, alt32=gv["32b"][k])
     print("strict 1e-5/1e-4 pass rates:", {k: (round(float(v), 6) if not isinstance(v, dict) else v)
                                            for k, v in rates.items()}, "stats", stats)
     return stats, rates, dict(out=out, alpha=alpha, normals=normals, nfd=nfd, distort=distort, median=median,
