@@ -8,6 +8,8 @@
 // Per pair: h_u = px*w - u, h_v = py*w - v (rows u,v,w of the ray transform),
 // x = h_u x h_v, s = x.xy / x.z, G = min(|s|^2, 2|mean2d - p|^2), alpha =
 // min(0.999, o*exp(-G/2)).  The last colour channel is the depth (RGB+ED).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace hgsr {
@@ -649,6 +651,292 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
         atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
 }
 
+// ---------------------------------------------------------------- backward, transposed inputs
+// The 2DGS backward without its per-step 19-value wave reduction (TransposeReduce: 15
+// permlane swaps, 15 adds and 20 DPP adds a step, ~60 % of the kernel's issue).  As in the 3DGS
+// backward, pass 1 composites 4 steps per lane (pixel) and keeps two numbers per pixel and step:
+// F = fac = alpha T with the sigma branch in its sign bit (set: the low-pass disk, clear: the
+// ray-plane hit) and V = dL/dsigma.  They are transposed through LDS so that lane 16 s + r holds
+// step s's values for the 4 pixels of one column (rows y0, y0 + 2, y0 + 4, y0 + 6); pass 2
+// re-evaluates the hit of that step's surfel at those 4 pixels (the same float operations as
+// pass 1: identical values), forms the 19 accumulator terms (v_xy, (p - m) x v_c, v_c, the
+// opacity sum, fac x normal / colour upstream) summed over its 4 pixels, and a 16-lane
+// transpose-reduce (4 DPP levels, the value set halved at each) leaves 2 of the 19 sums per lane
+// for two global float atomics per 4 steps into the surfel's accumulator row (no LDS partials).
+#ifndef HGSR_BWD2TP_WAVES
+#define HGSR_BWD2TP_WAVES 5
+#endif
+// one transpose-reduce level over a 16-lane row: N values -> N / 2, lanes with `bit` set keep the
+// upper half; the partner (DPP control CTRL, an involution with the opposite bit) sends the rest
+template <int CTRL, int N>
+__device__ __forceinline__ void tr_level(const float (&v)[N], float (&w)[N / 2], bool bit) {
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) {
+        const float keep = bit ? v[i + N / 2] : v[i];
+        const float give = bit ? v[i] : v[i + N / 2];
+        w[i] = keep + dpp<CTRL>(give);
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HGSR_BWD2TP_WAVES, 8))) void
+raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restrict__ rec,
+                       const float* __restrict__ backgrounds, int bg_ch, int ed_ch,
+                       const float* __restrict__ render_colors, const int32_t* __restrict__ offsets,
+                       int64_t n_isects, const int32_t* __restrict__ flatten_ids,
+                       const float* __restrict__ render_alphas, const int32_t* __restrict__ last_ids,
+                       const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
+                       const float* __restrict__ v_render_normals, float* __restrict__ acc_rows,
+                       unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask,
+                       int64_t qstride, const float* __restrict__ normal_rot,
+                       const float* __restrict__ v_depth_extra) {
+    constexpr int KV = 15 + D;
+    constexpr int NB = kBwd2Batch;
+    __shared__ struct {
+        float4 r0[2][NB], r1[2][NB], r2[2][NB], col[2][NB], r4[2][NB], box[2][NB];
+    } sr;
+    __shared__ int32_t s_id[2][NB];
+    __shared__ __attribute__((aligned(16))) uint8_t s_list[4][NB + 4];
+    __shared__ int32_t s_last[4];
+    __shared__ __attribute__((aligned(16))) float s_tp[4][4 * 16 * 4 * 2];
+    __shared__ __attribute__((aligned(16))) float s_pv[4][64 * 8];  // per pixel: vo[4], vn[3], 0
+    const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
+    const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
+    // per-pixel upstream terms of pixel (i, j), as raster2d_bwd_kernel: colour (ED divided, the
+    // depth channel plus the depth->normal gradient), normal (back to the camera frame), the
+    // alpha / background term; returns T_final
+    auto pixel_terms = [&](int i, int j, float (&vo)[4], float (&vn)[3], float& va_term) {
+        const bool in = i < H && j < W;
+        const int64_t pix = ((int64_t)tc.cam * H + i) * W + j;
+        const float Tf = in ? 1.0f - render_alphas[pix] : 1.0f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vo[k] = (in && k < D) ? v_render_colors[pix * D + k] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) vn[k] = in ? v_render_normals[pix * 3 + k] : 0.f;
+        if (normal_rot) {
+            const float* R = normal_rot + tc.cam * 16;
+            float vc[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) vc[q] = R[4 * q] * vn[0] + R[4 * q + 1] * vn[1] + R[4 * q + 2] * vn[2];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) vn[q] = vc[q];
+        }
+        if (v_depth_extra && in) vo[D - 1] += v_depth_extra[pix];
+        float va = in ? v_render_alphas[pix] : 0.f;
+        if (ed_ch >= 0 && in) {
+            const float alpha = 1.0f - Tf, ac = fmaxf(alpha, 1e-10f);
+            float v_ed = 0.f;
+#pragma unroll
+            for (int k = 0; k < D; ++k)
+                if (k == ed_ch) {
+                    v_ed = vo[k];
+                    vo[k] = v_ed / ac;
+                }
+            if (alpha >= 1e-10f) va -= v_ed * render_colors[pix * D + ed_ch] / ac;
+        }
+        float bg_dot = 0.f;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+            if (backgrounds && k < bg_ch) bg_dot += backgrounds[tc.cam * bg_ch + k] * vo[k];
+        va_term = Tf * (va - bg_dot);
+        return Tf;
+    };
+    float vo[4], vn[3], va_term;
+    const float T_final = pixel_terms(tc.i, tc.j, vo, vn, va_term);
+    float T = T_final, Bsum = 0.f;
+    // pass-2 role: step lane >> 4, column cx, rows y0 + 2 m of the quadrant; the pixels'
+    // upstream colour / normal terms come from the wave's LDS table (pixel = lane of pass 1)
+    const int r16 = lane & 15, cx = r16 & 7, y0 = r16 >> 3;
+    const int qi0 = tc.i - (lane >> 3), qj0 = tc.j - (lane & 7);
+    const float p2x = (float)(qj0 + cx) + 0.5f, p2y0 = (float)(qi0 + y0) + 0.5f;
+    float* const pv = s_pv[wave];
+    *reinterpret_cast<float4*>(pv + lane * 8) = make_float4(vo[0], vo[1], vo[2], vo[3]);
+    *reinterpret_cast<float4*>(pv + lane * 8 + 4) = make_float4(vn[0], vn[1], vn[2], 0.f);
+    // this lane's two output sums after the transpose-reduce: index b3 10 + b2 5 + b1 3 + b0 2 + q
+    int koff[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int b3 = (r16 >> 3) & 1, b2 = (r16 >> 2) & 1, b1 = (r16 >> 1) & 1, b0 = r16 & 1;
+        const int l = b0 * 2 + q, k = b1 * 3 + l, idx = b3 * 10 + b2 * 5 + k;
+        koff[q] = (l < 3 && k < 5 && idx < KV) ? idx : -1;
+    }
+    const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
+    const int32_t wave_final = wave_max2(bin_final);
+    if (lane == 0) s_last[wave] = wave_final;
+    lds_barrier();
+    const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
+    const int32_t end = min(tc.end, blk_final + 1);
+    const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
+    if (pair_counter && threadIdx.x == 0 && end > tc.start)
+        atomicAdd(pair_slot(pair_counter, 0), (unsigned long long)(end - tc.start) * kTilePixels);
+    float4* const stage_arr[6] = {&sr.r0[0][0], &sr.r1[0][0], &sr.r2[0][0], &sr.col[0][0], &sr.r4[0][0], &sr.box[0][0]};
+    int32_t cid = 0, nid = 0;
+    const bool loader = tid < NB;
+    auto dma_batch = [&](int buf, int32_t id) {
+        const float4* r = reinterpret_cast<const float4*>(rec + id);
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + q),
+                                             (void __attribute__((address_space(3)))*)(stage_arr[q] + buf * NB), 16,
+                                             0, 0);
+    };
+    if (nb > 0 && loader) {
+        cid = flatten_ids[max(end - 1 - tid, tc.start)];
+        dma_batch(0, cid);
+        nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
+    }
+    uint8_t* my_list = s_list[wave];
+    uint32_t stepped = 0;
+    uint64_t qw[2] = {0, 0};
+    auto qfetch = [&](int bb) {
+        const int64_t lo = (end - 1 - (int64_t)bb * NB - tc.start) - (NB - 1);
+        const int64_t bin = (int64_t)tc.cam * (tw * th) + tc.tile;
+        const int idx = __builtin_amdgcn_readfirstlane(
+            (int)(__builtin_amdgcn_readfirstlane(wave) * qstride + qmask_word0(tc.start, bin) + (lo >> 6)));
+        const uint64_t* qp = qmask + idx;
+        qw[0] = qp[0];
+        qw[1] = qp[1];
+    };
+    if (qmask && nb > 0) qfetch(0);
+    const int slot = lane >> 4;
+    for (int b = 0; b < nb; ++b) {
+        const int cur = b & 1, prv = cur ^ 1;
+        const int32_t batch_end = end - 1 - b * NB;
+        const int bsz = min(NB, batch_end + 1 - tc.start);
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): batch b's DMA has landed
+        if (tid < bsz) s_id[cur][tid] = cid;
+        if (b + 1 < nb && loader) {
+            cid = nid;
+            dma_batch(prv, cid);
+            nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
+        }
+        lds_barrier();
+        const int t0 = max(0, batch_end - wave_final);
+        uint64_t m;
+        bool rel;
+        if (qmask) {
+            const int64_t R = batch_end - tc.start, lo = R - (NB - 1);
+            const uint64_t w0 = qw[0], w1 = qw[1];
+            if (b + 1 < nb) qfetch(b + 1);
+            const int sh = (int)(lo & 63);
+            const uint64_t win = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+            const uint64_t below_z = bsz >= 64 ? ~0ull : ((1ull << bsz) - 1);
+            const uint64_t below_a = t0 >= 64 ? ~0ull : ((1ull << t0) - 1);
+            const uint64_t mk = __builtin_bitreverse64(win) & below_z & ~below_a;
+            m = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mk) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mk >> 32)) << 32);
+            rel = (m >> lane) & 1;
+        } else {
+            rel = lane < bsz && lane >= t0 &&
+                  reaches2_exact(sr.r0[cur][lane], sr.r1[cur][lane], sr.r2[cur][lane], sr.r4[cur][lane],
+                                 sr.box[cur][lane], qx, qy);
+            m = __ballot(rel);
+        }
+        if (rel) my_list[lanes_below2(m)] = (uint8_t)lane;
+        const int n_mine = __popcll(m);
+        if (lane < 4) my_list[n_mine + lane] = (uint8_t)NB;  // padded with the dummy to a multiple of 4
+        stepped += (uint32_t)n_mine;
+        if (n_mine > 0) {
+            const uint32_t lstp = reinterpret_cast<const uint32_t*>(my_list)[lane < (NB + 4) / 4 ? lane : 0];
+            for (int i = 0; i < n_mine; i += 4) {
+                const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)lstp, i >> 2);
+                // pass 1: composite the group's 4 records for this lane's pixel; (F, V) of step q go
+                // to [q][r][m] of the wave's transpose buffer (lane L = pixel r + 16 m), lane 16 s + r
+                // reads its step's column back in pass 2 (a wave's LDS operations complete in order)
+                float* const tp = s_tp[wave];
+#pragma nounroll
+                for (int q = 0; q < 4; ++q) {
+                    const int t = (int)((pk >> (8 * q)) & 0xffu);
+                    const bool dummy = t >= NB;
+                    const int tt = dummy ? 0 : t;
+                    const float4 r0 = sr.r0[cur][tt], r1 = sr.r1[cur][tt], r2 = sr.r2[cur][tt],
+                                 c = sr.col[cur][tt], r4 = sr.r4[cur][tt];
+                    const Hit2 h = hit2(r0, r1, r2, tc.px, tc.py);
+                    const float vis = __builtin_amdgcn_exp2f(-h.sigma);
+                    const float araw = r2.w * vis;
+                    const float alpha = fminf(0.999f, araw);
+                    const bool valid = !dummy & (batch_end - t <= bin_final) & h.ok & (h.sigma >= 0.f) &
+                                       (alpha >= 1.0f / 255.0f);
+                    const float al = valid ? alpha : 0.f;
+                    const float ra = __builtin_amdgcn_rcpf(1.0f - al);
+                    const float Tn = T * ra;
+                    const float fac = al * Tn;
+                    const float ck[4] = {c.x, c.y, c.z, c.w};
+                    float cv = r4.x * vn[0] + r4.y * vn[1] + r4.z * vn[2];
+#pragma unroll
+                    for (int k = 0; k < D; ++k) cv += ck[k] * vo[k];
+                    const float v_alpha = Tn * cv + ra * (va_term - Bsum);
+                    Bsum += fac * cv;
+                    const float va2 = (valid & (araw <= 0.999f)) ? v_alpha : 0.f;
+                    T = Tn;
+                    // sigma = min(g3, g2) / 2: the sign bit of F carries the branch (set: low-pass)
+                    const float Fq = (h.g3 <= h.g2) ? fac : -fac;
+                    *reinterpret_cast<float2*>(tp + ((q * 16 + r16) * 4 + (lane >> 4)) * 2) =
+                        make_float2(Fq, -araw * va2);
+                }
+                // pass 2: step `slot`'s surfel at this lane's 4 pixels
+                const int t = (int)__builtin_amdgcn_ubfe(pk, 8 * slot, 8);
+                const int tt = t < NB ? t : 0;
+                const float4 r0 = sr.r0[cur][tt], r1 = sr.r1[cur][tt], r2 = sr.r2[cur][tt];
+                const int sid = s_id[cur][tt];
+                float g[20];
+#pragma unroll
+                for (int k = 0; k < 20; ++k) g[k] = 0.f;
+#pragma nounroll
+                for (int mq = 0; mq < 4; ++mq) {
+                    const float2 fv = *reinterpret_cast<const float2*>(tp + ((slot * 16 + r16) * 4 + mq) * 2);
+                    const float4 po = *reinterpret_cast<const float4*>(pv + ((y0 + 2 * mq) * 8 + cx) * 8);
+                    const float4 pn = *reinterpret_cast<const float4*>(pv + ((y0 + 2 * mq) * 8 + cx) * 8 + 4);
+                    const float pvo[4] = {po.x, po.y, po.z, po.w}, pvn[3] = {pn.x, pn.y, pn.z};
+                    const Hit2 h = hit2(r0, r1, r2, p2x, p2y0 + (float)(2 * mq));
+                    const float fac = fabsf(fv.x);
+                    const bool ell = !__builtin_signbit(fv.x);
+                    const float v_sigma = fv.y;
+                    const float ve = ell ? v_sigma : 0.f, vp = ell ? 0.f : v_sigma;
+                    const float vs0 = ve * h.sx, vs1 = ve * h.sy;
+                    const float vc0 = vs0 * h.iz, vc1 = vs1 * h.iz, vc2 = -(vs0 * h.sx + vs1 * h.sy) * h.iz;
+                    g[0] += 2.0f * vp * h.dx;
+                    g[1] += 2.0f * vp * h.dy;
+                    g[2] -= h.dx * vc0; g[3] -= h.dx * vc1; g[4] -= h.dx * vc2;
+                    g[5] -= h.dy * vc0; g[6] -= h.dy * vc1; g[7] -= h.dy * vc2;
+                    g[8] += vc0; g[9] += vc1; g[10] += vc2;
+                    g[11] += v_sigma;  // -> the opacity sum below
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) g[12 + k] += fac * pvn[k];
+#pragma unroll
+                    for (int k = 0; k < D; ++k) g[15 + k] += fac * pvo[k];
+                }
+                // opacity: sum vis va2 = -sum v_sigma / opacity
+                g[11] = r2.w != 0.f ? -g[11] / r2.w : 0.f;
+                // 16-lane transpose-reduce: 20 -> 10 -> 5 -> 3 -> 2 values per lane
+                float w1[10], w2[5], w3[3], w4[2];
+                tr_level<0x128, 20>(g, w1, (r16 >> 3) & 1);  // row_ror:8, partner r ^ 8
+                tr_level<0x141, 10>(w1, w2, (r16 >> 2) & 1);  // row_half_mirror, partner 7 - r
+                {
+                    const float w2p[6] = {w2[0], w2[1], w2[2], w2[3], w2[4], 0.f};
+                    tr_level<0x4E, 6>(w2p, w3, (r16 >> 1) & 1);  // quad_perm [2,3,0,1]
+                }
+                {
+                    const float w3p[4] = {w3[0], w3[1], w3[2], 0.f};
+                    tr_level<0xB1, 4>(w3p, w4, r16 & 1);  // quad_perm [1,0,3,2]
+                }
+#pragma unroll
+                for (int q = 0; q < 2; ++q) asm volatile("" : "+v"(w4[q]));
+                if (t < NB) {
+#pragma unroll
+                    for (int q = 0; q < 2; ++q)
+                        if (koff[q] >= 0 && w4[q] != 0.f) atomicAdd(acc_rows + (int64_t)sid * kRec2 + koff[q], w4[q]);
+                }
+            }
+        }
+        lds_barrier();
+    }
+    if (pair_counter && lane == 0 && stepped)
+        atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
+}
+
 // Per surfel: fold the accumulated sums into gsplat's gradient tensors (overwrite), in f64.
 // gA = sum p_x v_c = gA' + m_x gC (gA' = sum (p-m)_x v_c), gB likewise, gC = sum v_c; with
 // d(a x b).g = da.(b x g) + db.(g x a):
@@ -958,13 +1246,22 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     const dim3 grid(C * tile_w * tile_h);
     unsigned long long* const pairs = timing_pair_counter("raster2d_bwd");
     const int64_t qstride = qmask_stride_of(qmask_bytes);
+    // the transposed-input backward (raster2d_bwd_tp_kernel) unless HGSR_BWD2_TP=0 (read per call)
+    const char* tp_env = getenv("HGSR_BWD2_TP");
+    const bool tp = tp_env ? atoi(tp_env) != 0 : false;
 #define LAUNCH_B2(DD)                                                                                             \
     {                                                                                                             \
         KernelTimer kt("raster2d_bwd", s);                                                                        \
-        hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
-                           tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,        \
-                           flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,                \
-                           v_render_normals, rows, pairs, qmask, qstride, normal_rot, v_depth_extra);            \
+        if (tp)                                                                                                   \
+            hipLaunchKernelGGL((raster2d_bwd_tp_kernel<DD>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
+                               tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,    \
+                               flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,            \
+                               v_render_normals, rows, pairs, qmask, qstride, normal_rot, v_depth_extra);        \
+        else                                                                                                      \
+            hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w,  \
+                               tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,    \
+                               flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,            \
+                               v_render_normals, rows, pairs, qmask, qstride, normal_rot, v_depth_extra);        \
     }                                                                                                             \
     hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s,   \
                        C, N, rows, rt, m2, reinterpret_cast<float2*>(v_means2d), v_rt, cd, v_normals,             \
