@@ -653,8 +653,8 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
 
 // ---------------------------------------------------------------- backward, transposed inputs
 // The 2DGS backward without its per-step 19-value wave reduction (TransposeReduce: 15
-// permlane swaps, 15 adds and 20 DPP adds a step, ~60 % of the kernel's issue).  As in the 3DGS
-// backward, pass 1 composites 4 steps per lane (pixel) and keeps two numbers per pixel and step:
+// permlane swaps, 15 adds and 20 DPP adds a step).  As in the 3DGS backward, pass 1 composites
+// the steps per lane (pixel) and queues the ones some pixel composites, two numbers per pixel:
 // F = fac = alpha T with the sigma branch in its sign bit (set: the low-pass disk, clear: the
 // ray-plane hit) and V = dL/dsigma.  They are transposed through LDS so that lane 16 s + r holds
 // step s's values for the 4 pixels of one column (rows y0, y0 + 2, y0 + 4, y0 + 6); pass 2
@@ -665,6 +665,12 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
 // for two global float atomics per 4 steps into the surfel's accumulator row (no LDS partials).
 #ifndef HGSR_BWD2TP_WAVES
 #define HGSR_BWD2TP_WAVES 5
+#endif
+#ifndef HGSR_BWD2TP_U1  // unroll of the pass-1 step loop (1: rolled)
+#define HGSR_BWD2TP_U1 1
+#endif
+#ifndef HGSR_BWD2TP_U2  // unroll of the pass-2 pixel loop
+#define HGSR_BWD2TP_U2 1
 #endif
 // one transpose-reduce level over a 16-lane row: N values -> N / 2, lanes with `bit` set keep the
 // upper half; the partner (DPP control CTRL, an involution with the opposite bit) sends the rest
@@ -696,7 +702,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
         float4 r0[2][NB], r1[2][NB], r2[2][NB], col[2][NB], r4[2][NB], box[2][NB];
     } sr;
     __shared__ int32_t s_id[2][NB];
-    __shared__ __attribute__((aligned(16))) uint8_t s_list[4][NB + 4];
+    __shared__ __attribute__((aligned(16))) uint8_t s_list[4][NB];
     __shared__ int32_t s_last[4];
     __shared__ __attribute__((aligned(16))) float s_tp[4][4 * 16 * 4 * 2];
     __shared__ __attribute__((aligned(16))) float s_pv[4][64 * 8];  // per pixel: vo[4], vn[3], 0
@@ -836,55 +842,21 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
         }
         if (rel) my_list[lanes_below2(m)] = (uint8_t)lane;
         const int n_mine = __popcll(m);
-        if (lane < 4) my_list[n_mine + lane] = (uint8_t)NB;  // padded with the dummy to a multiple of 4
         stepped += (uint32_t)n_mine;
         if (n_mine > 0) {
-            const uint32_t lstp = reinterpret_cast<const uint32_t*>(my_list)[lane < (NB + 4) / 4 ? lane : 0];
-            for (int i = 0; i < n_mine; i += 4) {
-                const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)lstp, i >> 2);
-                // pass 1: composite the group's 4 records for this lane's pixel; (F, V) of step q go
-                // to [q][r][m] of the wave's transpose buffer (lane L = pixel r + 16 m), lane 16 s + r
-                // reads its step's column back in pass 2 (a wave's LDS operations complete in order)
-                float* const tp = s_tp[wave];
-#pragma nounroll
-                for (int q = 0; q < 4; ++q) {
-                    const int t = (int)((pk >> (8 * q)) & 0xffu);
-                    const bool dummy = t >= NB;
-                    const int tt = dummy ? 0 : t;
-                    const float4 r0 = sr.r0[cur][tt], r1 = sr.r1[cur][tt], r2 = sr.r2[cur][tt],
-                                 c = sr.col[cur][tt], r4 = sr.r4[cur][tt];
-                    const Hit2 h = hit2(r0, r1, r2, tc.px, tc.py);
-                    const float vis = __builtin_amdgcn_exp2f(-h.sigma);
-                    const float araw = r2.w * vis;
-                    const float alpha = fminf(0.999f, araw);
-                    const bool valid = !dummy & (batch_end - t <= bin_final) & h.ok & (h.sigma >= 0.f) &
-                                       (alpha >= 1.0f / 255.0f);
-                    const float al = valid ? alpha : 0.f;
-                    const float ra = __builtin_amdgcn_rcpf(1.0f - al);
-                    const float Tn = T * ra;
-                    const float fac = al * Tn;
-                    const float ck[4] = {c.x, c.y, c.z, c.w};
-                    float cv = r4.x * vn[0] + r4.y * vn[1] + r4.z * vn[2];
-#pragma unroll
-                    for (int k = 0; k < D; ++k) cv += ck[k] * vo[k];
-                    const float v_alpha = Tn * cv + ra * (va_term - Bsum);
-                    Bsum += fac * cv;
-                    const float va2 = (valid & (araw <= 0.999f)) ? v_alpha : 0.f;
-                    T = Tn;
-                    // sigma = min(g3, g2) / 2: the sign bit of F carries the branch (set: low-pass)
-                    const float Fq = (h.g3 <= h.g2) ? fac : -fac;
-                    *reinterpret_cast<float2*>(tp + ((q * 16 + r16) * 4 + (lane >> 4)) * 2) =
-                        make_float2(Fq, -araw * va2);
-                }
-                // pass 2: step `slot`'s surfel at this lane's 4 pixels
-                const int t = (int)__builtin_amdgcn_ubfe(pk, 8 * slot, 8);
+            const uint32_t lstp = reinterpret_cast<const uint32_t*>(my_list)[lane < NB / 4 ? lane : 0];
+            float* const tp = s_tp[wave];
+            // pass 2 over the 4 queued steps (packed record indices, NB = empty slot): step `slot`'s
+            // surfel at this lane's 4 pixels, the 16-lane transpose-reduce, two float atomics
+            auto pass2 = [&](const uint32_t qpk) {
+                const int t = (int)__builtin_amdgcn_ubfe(qpk, 8 * slot, 8);
                 const int tt = t < NB ? t : 0;
                 const float4 r0 = sr.r0[cur][tt], r1 = sr.r1[cur][tt], r2 = sr.r2[cur][tt];
                 const int sid = s_id[cur][tt];
                 float g[20];
 #pragma unroll
                 for (int k = 0; k < 20; ++k) g[k] = 0.f;
-#pragma nounroll
+#pragma unroll HGSR_BWD2TP_U2
                 for (int mq = 0; mq < 4; ++mq) {
                     const float2 fv = *reinterpret_cast<const float2*>(tp + ((slot * 16 + r16) * 4 + mq) * 2);
                     const float4 po = *reinterpret_cast<const float4*>(pv + ((y0 + 2 * mq) * 8 + cx) * 8);
@@ -929,6 +901,51 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
                     for (int q = 0; q < 2; ++q)
                         if (koff[q] >= 0 && w4[q] != 0.f) atomicAdd(acc_rows + (int64_t)sid * kRec2 + koff[q], w4[q]);
                 }
+            };
+            // pass 1, one step at a time; a step with a valid pixel is queued -- its (F, V) go to
+            // queue slot qn of the wave's transpose buffer ([qn][r][m], lane L = pixel r + 16 m) --
+            // and a full queue runs pass 2 (a step nobody composites contributes nothing: skipped)
+            int qn = 0;
+            uint32_t qpk = 0;
+            for (int i = 0; i < n_mine; ++i) {
+                const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)lstp, i >> 2);
+                const int t = (int)((word >> (8 * (i & 3))) & 0xffu);
+                const float4 r0 = sr.r0[cur][t], r1 = sr.r1[cur][t], r2 = sr.r2[cur][t], c = sr.col[cur][t],
+                             r4 = sr.r4[cur][t];
+                const Hit2 h = hit2(r0, r1, r2, tc.px, tc.py);
+                const float vis = __builtin_amdgcn_exp2f(-h.sigma);
+                const float araw = r2.w * vis;
+                const float alpha = fminf(0.999f, araw);
+                const bool valid = (batch_end - t <= bin_final) & h.ok & (h.sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
+                if (!__any(valid)) continue;
+                const float al = valid ? alpha : 0.f;
+                const float ra = __builtin_amdgcn_rcpf(1.0f - al);
+                const float Tn = T * ra;
+                const float fac = al * Tn;
+                const float ck[4] = {c.x, c.y, c.z, c.w};
+                float cv = r4.x * vn[0] + r4.y * vn[1] + r4.z * vn[2];
+#pragma unroll
+                for (int k = 0; k < D; ++k) cv += ck[k] * vo[k];
+                const float v_alpha = Tn * cv + ra * (va_term - Bsum);
+                Bsum += fac * cv;
+                const float va2 = (valid & (araw <= 0.999f)) ? v_alpha : 0.f;
+                T = Tn;
+                // sigma = min(g3, g2) / 2: the sign bit of F carries the branch (set: low-pass)
+                const float Fq = (h.g3 <= h.g2) ? fac : -fac;
+                *reinterpret_cast<float2*>(tp + ((qn * 16 + r16) * 4 + (lane >> 4)) * 2) = make_float2(Fq, -araw * va2);
+                qpk |= (uint32_t)t << (8 * qn);
+                if (++qn == 4) {
+                    pass2(qpk);
+                    qn = 0;
+                    qpk = 0;
+                }
+            }
+            if (qn > 0) {  // the partial queue: empty slots composite nothing
+                for (int q = qn; q < 4; ++q) {
+                    *reinterpret_cast<float2*>(tp + ((q * 16 + r16) * 4 + (lane >> 4)) * 2) = make_float2(0.f, 0.f);
+                    qpk |= (uint32_t)NB << (8 * q);
+                }
+                pass2(qpk);
             }
         }
         lds_barrier();
@@ -1248,7 +1265,7 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     const int64_t qstride = qmask_stride_of(qmask_bytes);
     // the transposed-input backward (raster2d_bwd_tp_kernel) unless HGSR_BWD2_TP=0 (read per call)
     const char* tp_env = getenv("HGSR_BWD2_TP");
-    const bool tp = tp_env ? atoi(tp_env) != 0 : false;
+    const bool tp = tp_env ? atoi(tp_env) != 0 : true;
 #define LAUNCH_B2(DD)                                                                                             \
     {                                                                                                             \
         KernelTimer kt("raster2d_bwd", s);                                                                        \

@@ -545,4 +545,5 @@ def test_2dgs_unused_outputs_get_no_grad_tensors(fused):
         loss.backward()
         grads.append([p.grad.clone() for p in ps])
     for a, b in zip(*grads):
-        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+        # two launches sum the per-pixel terms with float atomics in a run-dependent order
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max()) + 1e-7)
