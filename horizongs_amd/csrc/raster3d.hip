@@ -18,8 +18,6 @@
 //    reduced across the wave together (step-major DPP, no hazard stalls), and
 //    each wave's sums go straight to the Gaussian's 48-byte accumulator row as
 //    one float-atomic instruction per 4 steps (the waves' partials meet in L2).
-#include <stdlib.h>
-
 #include "rec3.h"
 
 namespace hgsr {
@@ -315,7 +313,7 @@ struct Pass2Lane {
     float vo[4][4];          // [m][slot]: upstream colour gradient of pixel m, lane-permuted channels
 };
 
-template <int D, bool ABS, bool Q = false>
+template <int D, bool ABS>
 __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
     int bg_ch, int ed_ch, const float* __restrict__ render_colors, const int32_t* __restrict__ offsets,
@@ -548,7 +546,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                 V = -araw * va2;  // dL/dsigma (unscaled sigma)
             };
             // pass 2 over 4 composited steps (records ts[0..3], values F/V in pass-1 layout)
-            auto pass2 = [&](const uint32_t packed, float (&F)[4], float (&V)[4], const bool fv_written) {
+            auto pass2 = [&](const uint32_t packed, float (&F)[4], float (&V)[4]) {
                 // this lane's Gaussian (step `slot`), extracted from the group's packed list
                 // entries: its position and id reads are independent and go out before the
                 // transpose
@@ -567,10 +565,9 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                     // its step's column [s][r][0..3] (a wave's LDS operations complete in order)
                     float* tp = s_tp[wave];
                     const int rr = lane & 15, mm = lane >> 4;
-                    if (!fv_written)
 #pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            *reinterpret_cast<float2*>(tp + ((q * 16 + rr) * 4 + mm) * 2) = make_float2(F[q], V[q]);
+                    for (int q = 0; q < 4; ++q)
+                        *reinterpret_cast<float2*>(tp + ((q * 16 + rr) * 4 + mm) * 2) = make_float2(F[q], V[q]);
                     const float4 lo = *reinterpret_cast<const float4*>(tp + ((slot * 16 + rr) * 4) * 2);
                     const float4 hi = *reinterpret_cast<const float4*>(tp + ((slot * 16 + rr) * 4) * 2 + 4);
                     F[0] = lo.x; V[0] = lo.y; F[1] = lo.z; V[1] = lo.w;
@@ -659,62 +656,13 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                         atomicAdd(acc_rows + (int64_t)sid * kRec3 + koff, v);
                 }
             };
-            if (!Q) {
-                for (int i = 0; i < n_mine; i += 4) {
-                    // the group's four list entries in one scalar register
-                    const uint32_t packed = (uint32_t)__builtin_amdgcn_readlane((int)lstp, i >> 2);
-                    float F[4], V[4];
+            for (int i = 0; i < n_mine; i += 4) {
+                // the group's four list entries in one scalar register
+                const uint32_t packed = (uint32_t)__builtin_amdgcn_readlane((int)lstp, i >> 2);
+                float F[4], V[4];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) step((int)((packed >> (8 * q)) & 0xffu), F[q], V[q]);
-                    pass2(packed, F, V, false);
-                }
-            } else {
-                // live-step queue: a step no pixel of the quadrant composites is skipped after its
-                // validity test; the others queue their (F, V) at [qn][r][m] of the transpose buffer
-                // and every 4 queued steps run pass 2
-                float* const tpq = s_tp[wave];
-                const int rr = lane & 15, mm = lane >> 4;
-                float Fd[4], Vd[4];  // unused: pass 2 reads the queued values from the buffer
-                int qn = 0;
-                uint32_t qpk = 0;
-                for (int i = 0; i < n_mine; ++i) {
-                    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)lstp, i >> 2);
-                    const int t = (int)((word >> (8 * (i & 3))) & 0xffu);
-                    const float4 g0 = sr.g0[cur][t], g1 = sr.g1[cur][t], c = sr.col[cur][t];
-                    const float dx = g0.x - tc.px, dy = g0.y - tc.py;
-                    const float sigma = sigma2(g0, g1, dx, dy);
-                    const float vis = __builtin_amdgcn_exp2f(-sigma);
-                    const float araw = g1.y * vis;
-                    const float alpha = fminf(0.999f, araw);
-                    const bool valid = (batch_end - t <= bin_final) & (sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
-                    if (!__any(valid)) continue;
-                    const float ck[4] = {c.x, c.y, c.z, c.w};
-                    const float al = valid ? alpha : 0.f;
-                    const float ra = __builtin_amdgcn_rcpf(1.0f - al);
-                    const float Tn = T * ra;
-                    const float fac = al * Tn;
-                    float cv = ck[0] * vo[0];
-#pragma unroll
-                    for (int k = 1; k < D; ++k) cv += ck[k] * vo[k];
-                    const float v_alpha = Tn * cv + ra * (va_term - B);
-                    B += fac * cv;
-                    const float va2 = (valid & (araw <= 0.999f)) ? v_alpha : 0.f;
-                    T = Tn;
-                    *reinterpret_cast<float2*>(tpq + ((qn * 16 + rr) * 4 + mm) * 2) = make_float2(fac, -araw * va2);
-                    qpk |= (uint32_t)t << (8 * qn);
-                    if (++qn == 4) {
-                        pass2(qpk, Fd, Vd, true);
-                        qn = 0;
-                        qpk = 0;
-                    }
-                }
-                if (qn > 0) {  // the partial queue: empty slots are the zero-opacity dummy
-                    for (int q = qn; q < 4; ++q) {
-                        *reinterpret_cast<float2*>(tpq + ((q * 16 + rr) * 4 + mm) * 2) = make_float2(0.f, 0.f);
-                        qpk |= (uint32_t)NB << (8 * q);
-                    }
-                    pass2(qpk, Fd, Vd, true);
-                }
+                for (int q = 0; q < 4; ++q) step((int)((packed >> (8 * q)) & 0xffu), F[q], V[q]);
+                pass2(packed, F, V);
             }
         }
         lds_barrier();
@@ -987,22 +935,13 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     unsigned long long* const pairs = timing_pair_counter("raster3d_bwd");
     const int64_t qstride = qmask_stride_of(qmask_bytes);
     const bool abs = v_means2d_abs != nullptr;
-    // live-step queue variant of the backward (HGSR_BWD3_Q=1, read per call; non-abs only)
-    const char* q_env = getenv("HGSR_BWD3_Q");
-    const bool qmode = q_env ? atoi(q_env) != 0 : false;
 #define LAUNCH_B(DD, AA)                                                                                       \
     {                                                                                                          \
         KernelTimer kt("raster3d_bwd", s);                                                                     \
-        if (qmode && !AA)                                                                                      \
-            hipLaunchKernelGGL((raster3d_bwd_kernel<DD, false, true>), grid, dim3(256), 0, s, C, width, height, \
-                               tile_w, tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets,     \
-                               n_isects, flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, \
-                               rows, pairs, qmask, qstride);                                                   \
-        else                                                                                                   \
-            hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w,  \
-                               tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,   \
-                               flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows,     \
-                               pairs, qmask, qstride);                                                         \
+        hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
+                           tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,       \
+                           flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, pairs,  \
+                           qmask, qstride);                                                                    \
     }                                                                                                          \
     hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, \
                        N, rows, rec, conics, reinterpret_cast<float2*>(v_means2d), v_conics, cd,                     \
