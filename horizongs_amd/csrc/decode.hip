@@ -437,18 +437,23 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
             }
         }
         if (!COLOR) continue;
-        // colour head straight from the accumulators (linear output)
+        // colour head (linear output), each tile transposed through the wave's (now free)
+        // pre-activation buffer so a store covers 16 consecutive rows of 4 anchors (see
+        // decode_color_kernel)
         const f32x4 hl0 = layer1_tile<KSTEPS>(sm, sx, 4), hl1 = layer1_tile<KSTEPS>(sm, sx, 5);
         for (int ot = 0; ot < d.T[2]; ++ot) {
             const f32x4 y = layer2_tile(sm, d.row0[2] + ot * 16, hl0, hl1);
-            if (a0 + i >= d.Av) continue;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int o = ot * 16 + 4 * g + r;
-                if (o >= cd * noff) continue;
-                const int k = o / cd;
-                const int p = pos[i * noff + k];
-                if (p >= 0) out.color[(int64_t)p * cd + (o - k * cd)] = y[r];
+            for (int r = 0; r < 4; ++r) syw[(4 * g + r) * kDecYS + i] = y[r];
+            const int row = lane & 15, o = ot * 16 + row;
+            const int k = o / cd;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int a = 4 * j + (lane >> 4);
+                const float v = syw[row * kDecYS + a];
+                if (o >= cd * noff || a0 + a >= d.Av) continue;
+                const int p = pos[a * noff + k];
+                if (p >= 0) out.color[(int64_t)p * cd + (o - k * cd)] = v;
             }
         }
     }
@@ -471,6 +476,7 @@ struct DecodeColorSmem {
     float b2[kDecColRows];
     float x[4][16 * kDecS];
     int pos[4][16 * 16];
+    float ty[4][16 * 20];  // per wave: one output tile transposed for the stores (pitch 20: conflict-free)
 };
 
 template <int KSTEPS>
@@ -518,16 +524,23 @@ __global__ __launch_bounds__(256) void decode_color_kernel(DecodeDims d, MlpPtrs
         wave_lds_sync();
         const f32x4 h0 = layer1_tile<KSTEPS>(sm, sx, 0), h1 = layer1_tile<KSTEPS>(sm, sx, 1);
         if (tn < n_tiles) x_issue_data(px, feat, anchor, d.vd);
+        // each tile goes out through the wave's transpose buffer: a store instruction then covers
+        // 16 consecutive rows (a slot's consecutive colour values) of 4 anchors -- 64-B runs --
+        // instead of 4 rows of 16 anchors (64 scattered words)
+        float* const ty = sm.ty[wave];
         for (int ot = 0; ot < d.T[2]; ++ot) {
             const f32x4 y = layer2_tile(sm, ot * 16, h0, h1);
-            if (a0 + i >= d.Av) continue;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int o = ot * 16 + 4 * g + r;
-                if (o >= cd * noff) continue;
-                const int k = o / cd;
-                const int p = pos[i * noff + k];
-                if (p >= 0) color[(int64_t)p * cd + (o - k * cd)] = y[r];
+            for (int r = 0; r < 4; ++r) ty[(4 * g + r) * 20 + i] = y[r];
+            const int row = lane & 15, o = ot * 16 + row;
+            const int k = o / cd;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int a = 4 * j + (lane >> 4);
+                const float v = ty[row * 20 + a];
+                if (o >= cd * noff || a0 + a >= d.Av) continue;
+                const int p = pos[a * noff + k];
+                if (p >= 0) color[(int64_t)p * cd + (o - k * cd)] = v;
             }
         }
     }
