@@ -402,7 +402,7 @@ def psnr_parity(args):
                     "psnr_ref_db": d["psnr_ref_db"], "iterations": d["iterations"], "anchors": d.get("anchors"),
                     "width": d.get("width"), "height": d.get("height"), "lr_scale": d.get("lr_scale"),
                     "noise_floor_window_db": d.get("noise_floor_window_db"), "bar_db": d.get("bar_db"),
-                    "source": f"{src} (tests/test_gpu_training_parity.py::{test}_{args.gs}dgs)"}
+                    "source": f"{src} (tests/test_gpu_training_parity.py::{test}_{args.gs}gs)"}
     if not out:
         return None
     head = out.get("at_scale") or out["pipeline"]

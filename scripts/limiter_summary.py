@@ -1,0 +1,66 @@
+"""Limiter breakdown of the raster backwards from a gpu_r04_prof.sh run (developer tool).
+
+usage: python scripts/limiter_summary.py gpurun_out/r04prof gpurun_out/<suite>/bench.json > profiles/r04_pmc_raster3d_bwd_limiters.txt
+Reads the l3 / l2 PMC summaries (scripts/pmc_summary.py output), profiles/r04_pmc_traffic.json and
+the bench line's evaluated-pair counter.  SQ_WAVE_CYCLES / SQ_WAIT_* count quad-cycles
+(MI355X_MICROARCH.md, PMC table); kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs.
+"""
+import json
+import os
+import subprocess
+import sys
+
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src, bench = sys.argv[1], sys.argv[2]
+b = json.loads(open(bench).read().strip().splitlines()[-1])
+roof = b["roofline"]
+steps = roof["pairs_evaluated_per_launch"] / 64
+nis = roof["n_isects"]
+
+
+def counters(d):
+    out = subprocess.run([sys.executable, os.path.join(root, "scripts", "pmc_summary.py"), d], capture_output=True,
+                         text=True).stdout
+    L = {}
+    for line in out.splitlines():
+        p = line.split()
+        if len(p) == 2:
+            L[p[0]] = float(p[1])
+    return L, out
+
+
+pm = json.load(open(os.path.join(root, "profiles", "r04_pmc_traffic.json")))["kernels"]
+lines = ["Round-4 limiter breakdown of the raster backwards (scripts/gpu_r04_prof.sh: rocprofv3 --pmc SQ_WAVES "
+         "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS "
+         "GRBM_GUI_ACTIVE, one pass per config; FETCH_SIZE / WRITE_SIZE from separate passes, "
+         "profiles/r04_pmc_traffic.json).  SQ_WAVE_CYCLES / SQ_WAIT_* count quad-cycles; kernel cycles = "
+         "GRBM_GUI_ACTIVE / 8 XCDs.", ""]
+raw = ["", "raw counters (per launch):"]
+P = 1920 * 1080
+for tag, gs, name, occ, rows_mb, alg in (
+        ("l3", "3dgs", "raster3d_bwd, c2 (2M Gaussians, 1080p)", "7 (72 VGPRs, 22 KB LDS)", 2e6 * 48 / 1e6,
+         (44 * nis + 28 * P) / 1e6),
+        ("l2", "2dgs", "raster2d_bwd (transposed inputs), c3", "5 (96 VGPRs, 29 KB LDS)", 2e6 * 96 / 1e6, None)):
+    L, txt = counters(os.path.join(src, tag))
+    raw += txt.splitlines()
+    kname = [k for k in pm[gs] if k.startswith(name.split(",")[0].split(" ")[0])]
+    kname = [k for k in kname if "bwd" in k][0]
+    k = pm[gs][kname]
+    t_us = k["avg_us"]
+    cyc = L["GRBM_GUI_ACTIVE"] / 8
+    wc = L["SQ_WAVE_CYCLES"]
+    lines.append(f"== {name} [{kname}]: {t_us:.1f} us under rocprofv3, effective clock {cyc / (t_us * 1e-6) / 1e9:.2f} GHz")
+    lines.append(f"   waves / SIMD: compiled occupancy {occ}; resident on average {wc * 4 / (1024 * cyc):.2f}")
+    lines.append(f"   SQ_INSTS_VALU {L['SQ_INSTS_VALU']:.4g} per launch = {L['SQ_INSTS_VALU'] / t_us / 1e3:.0f} G "
+                 f"wave-instr/s ({L['SQ_INSTS_VALU'] / t_us / 1e3 / 935:.2f} of the 935 G/s v_fma_f32 issue ceiling)")
+    if gs == "3dgs":
+        lines.append(f"   per wave-step: {L['SQ_INSTS_VALU'] / steps:.1f} VALU, {L['SQ_INSTS_LDS'] / steps:.2f} LDS "
+                     f"instructions ({steps / 1e6:.2f}M wave-steps = evaluated pairs / 64)")
+    lines.append(f"   wave time: parked on s_waitcnt / barrier (SQ_WAIT_ANY) {L['SQ_WAIT_ANY'] / wc:.1%}, issue-stalled "
+                 f"(SQ_WAIT_INST_ANY) {L['SQ_WAIT_INST_ANY'] / wc:.1%}, issuing {1 - (L['SQ_WAIT_ANY'] + L['SQ_WAIT_INST_ANY']) / wc:.1%}")
+    lines.append(f"   HBM: 2 x FETCH_SIZE {2 * k['fetch_size_raw_bytes'] / 1e6:.1f} MB + WRITE_SIZE {k['write_size_bytes'] / 1e6:.1f} MB"
+                 f" = {k['hbm_bytes_corrected'] / 1e6:.1f} MB / launch"
+                 + (f" against {alg:.0f} MB algorithmic ({k['hbm_bytes_corrected'] / 1e6 / alg:.2f}x)" if alg else ""))
+    lines.append(f"   WRITE_SIZE {k['write_size_bytes'] / 1e6:.1f} MB vs {rows_mb:.0f} MB of accumulator rows "
+                 f"({k['write_size_bytes'] / 1e6 / rows_mb:.1f}x: float atomics of every (wave, Gaussian) group meet in L2)")
+print("\n".join(lines + raw))
