@@ -666,9 +666,6 @@ __global__ __launch_bounds__(256) void raster2d_bwd_kernel(
 #ifndef HGSR_BWD2TP_WAVES
 #define HGSR_BWD2TP_WAVES 5
 #endif
-#ifndef HGSR_BWD2TP_LDS  // 1: merge the waves' sums in LDS per batch (LDS atomics + one flush)
-#define HGSR_BWD2TP_LDS 0
-#endif
 #ifndef HGSR_BWD2TP_U1  // unroll of the pass-1 step loop (1: rolled)
 #define HGSR_BWD2TP_U1 1
 #endif
@@ -709,12 +706,6 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
     __shared__ int32_t s_last[4];
     __shared__ __attribute__((aligned(16))) float s_tp[4][4 * 16 * 4 * 2];
     __shared__ __attribute__((aligned(16))) float s_pv[4][64 * 8];  // per pixel: vo[4], vn[3], 0
-#if HGSR_BWD2TP_LDS
-    // the four waves' sums merged in LDS per batch (LDS float atomics), one global atomic per
-    // (record, value) at the batch's flush
-    constexpr int KVP = KV + 1;
-    __shared__ float s_part[NB * KVP];
-#endif
     const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
@@ -780,9 +771,6 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
     const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
     const int32_t wave_final = wave_max2(bin_final);
     if (lane == 0) s_last[wave] = wave_final;
-#if HGSR_BWD2TP_LDS
-    for (int e = tid; e < NB * KVP; e += 256) s_part[e] = 0.f;
-#endif
     lds_barrier();
     const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
     const int32_t end = min(tc.end, blk_final + 1);
@@ -819,15 +807,10 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
     };
     if (qmask && nb > 0) qfetch(0);
     const int slot = lane >> 4;
-#if HGSR_BWD2TP_LDS
-    int prev_bsz = 0;
-    for (int b = 0; b <= nb; ++b) {
-#else
     for (int b = 0; b < nb; ++b) {
-#endif
         const int cur = b & 1, prv = cur ^ 1;
         const int32_t batch_end = end - 1 - b * NB;
-        const int bsz = b < nb ? min(NB, batch_end + 1 - tc.start) : 0;
+        const int bsz = min(NB, batch_end + 1 - tc.start);
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): batch b's DMA has landed
         if (tid < bsz) s_id[cur][tid] = cid;
         if (b + 1 < nb && loader) {
@@ -835,18 +818,6 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
             dma_batch(prv, cid);
             nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
-#if HGSR_BWD2TP_LDS
-        if (b > 0) {  // batch b-1's merged sums (its records' ids in s_id[prv])
-            for (int e = tid; e < prev_bsz * KV; e += 256) {
-                const int tq = e / KV, k = e - tq * KV;
-                const float sv = s_part[tq * KVP + k];
-                s_part[tq * KVP + k] = 0.f;
-                if (sv != 0.f) atomicAdd(acc_rows + (int64_t)s_id[prv][tq] * kRec2 + k, sv);
-            }
-        }
-        if (b == nb) break;
-        prev_bsz = bsz;
-#endif
         lds_barrier();
         const int t0 = max(0, batch_end - wave_final);
         uint64_t m;
@@ -928,13 +899,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
                 if (t < NB) {
 #pragma unroll
                     for (int q = 0; q < 2; ++q)
-                        if (koff[q] >= 0 && w4[q] != 0.f) {
-#if HGSR_BWD2TP_LDS
-                            atomicAdd(&s_part[t * KVP + koff[q]], w4[q]);
-#else
-                            atomicAdd(acc_rows + (int64_t)sid * kRec2 + koff[q], w4[q]);
-#endif
-                        }
+                        if (koff[q] >= 0 && w4[q] != 0.f) atomicAdd(acc_rows + (int64_t)sid * kRec2 + koff[q], w4[q]);
                 }
             };
             // pass 1, one step at a time; a step with a valid pixel is queued -- its (F, V) go to
