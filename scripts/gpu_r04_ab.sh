@@ -35,6 +35,6 @@ for f in sorted(glob.glob(f"gpurun_out/{tag}/*.json")):
     k = d["kernels"]
     r = d.get("roofline") or {}
     print(os.path.basename(f), d["value"], d["ms_per_step"],
-          {x: k[x]["avg_ms"] for x in k if "raster" in x or x in ("tile_sort", "isect_emit", "decode_bwd")},
+          {x: k[x]["avg_ms"] for x in k if "raster" in x or x in ("tile_sort", "isect_emit", "isect_count", "decode_bwd")},
           {x: r.get(x) for x in ("kernel_avg_ms", "frac")})
 PY
