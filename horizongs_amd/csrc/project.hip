@@ -289,9 +289,12 @@ __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
 #define HGSR_CAM_READY asm volatile("" ::"v"(rad), "v"(cn.x), "v"(cn.y), "v"(cn.z), "v"(vcn.x), "v"(vcn.y), \
                                     "v"(vcn.z), "v"(vm2.x), "v"(vm2.y), "v"(vdep))
     load_cam(g);
+    // the other consumer's scale gradient travels with the first round trip (loaded after the
+    // camera loop it costs one more exposed memory latency per lane at 3 waves / SIMD)
+    const float3 vsi = v_scales_in ? ld3(v_scales_in + (int64_t)g * 3) : make_float3(0.f, 0.f, 0.f);
     HGSR_CAM_READY;
     asm volatile("" ::"v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w), "v"(s3.x),
-                 "v"(s3.y), "v"(s3.z));
+                 "v"(s3.y), "v"(s3.z), "v"(vsi.x), "v"(vsi.y), "v"(vsi.z));
     Mat3 Rq;
     const Mat3 cov = covar_from_qs(q, s3, Rq);
     for (int c = 0; c < C; ++c) {
@@ -401,7 +404,7 @@ __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         v_means[(int64_t)g * 3 + j] = vm_acc[j];
-        v_scales[(int64_t)g * 3 + j] = v_scales_in ? vs_acc[j] + v_scales_in[(int64_t)g * 3 + j] : vs_acc[j];
+        v_scales[(int64_t)g * 3 + j] = v_scales_in ? vs_acc[j] + (j == 0 ? vsi.x : (j == 1 ? vsi.y : vsi.z)) : vs_acc[j];
     }
     v_quats[g] = vq_acc;
 }
@@ -526,6 +529,7 @@ __global__ __launch_bounds__(256) void project2d_bwd_kernel(
     const float m[3] = {means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2]};
     const float4 q = quats[g];
     const float3 s = ld3(scales + (int64_t)g * 3);
+    const float3 vsi = v_scales_in ? ld3(v_scales_in + (int64_t)g * 3) : make_float3(0.f, 0.f, 0.f);  // (issued early)
     float vm_acc[3] = {0.f, 0.f, 0.f};
     float vs0 = 0.f, vs1 = 0.f;
     float4 vq_acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -583,9 +587,9 @@ __global__ __launch_bounds__(256) void project2d_bwd_kernel(
 #pragma unroll
     for (int j = 0; j < 3; ++j) v_means[(int64_t)g * 3 + j] = vm_acc[j];
     if (v_scales_in) {
-        v_scales[(int64_t)g * 3 + 0] = vs0 + v_scales_in[(int64_t)g * 3 + 0];
-        v_scales[(int64_t)g * 3 + 1] = vs1 + v_scales_in[(int64_t)g * 3 + 1];
-        v_scales[(int64_t)g * 3 + 2] = 0.f + v_scales_in[(int64_t)g * 3 + 2];
+        v_scales[(int64_t)g * 3 + 0] = vs0 + vsi.x;
+        v_scales[(int64_t)g * 3 + 1] = vs1 + vsi.y;
+        v_scales[(int64_t)g * 3 + 2] = 0.f + vsi.z;
     } else {
         v_scales[(int64_t)g * 3 + 0] = vs0;
         v_scales[(int64_t)g * 3 + 1] = vs1;
