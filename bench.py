@@ -642,7 +642,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     args = resolve(parse(), world)
-    if world > 1:
+    if world > 1 or (os.environ.get("HGSR_DDP_FORCE", "0") != "0" and "WORLD_SIZE" in os.environ):
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)

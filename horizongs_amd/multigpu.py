@@ -15,6 +15,7 @@ is RCCL over xGMI on MI355X):
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Iterable, List, Sequence
 
 import torch
@@ -26,6 +27,9 @@ def chunks_for_rank(chunks: Sequence[str], rank: int, world: int) -> List[str]:
     if world < 1 or not (0 <= rank < world):
         raise ValueError(f"bad rank/world {rank}/{world}")
     return [c for i, c in enumerate(chunks) if i % world == rank]
+
+
+_FORCE = os.environ.get("HGSR_DDP_FORCE", "0") != "0"
 
 
 class GradientAllReduce:
@@ -89,7 +93,9 @@ class GradientAllReduce:
         return [p for p in ps if p.requires_grad]
 
     def _active(self) -> bool:
-        return dist.is_initialized() and dist.get_world_size(self.group) > 1
+        # HGSR_DDP_FORCE=1: a one-rank group runs the whole bucket / hook / RCCL path anyway (a
+        # single-GPU rehearsal of the multi-GPU step; the all-reduce of one rank is the identity)
+        return dist.is_initialized() and (dist.get_world_size(self.group) > 1 or _FORCE)
 
     def _bind(self) -> None:
         """(Re)build the buckets when the parameter objects changed.  Buckets follow the
@@ -168,7 +174,6 @@ class GradientAllReduce:
                 continue
             dst = b["flat"][b["offs"][k]:b["offs"][k] + p.numel()].view_as(p)
             torch.mul(g.reshape(p.shape), 1.0 / self.world, out=dst)
-            b["flat"][b["n"] + k] = 1.0
             b["ready"][k] = b["early"][k] = True
         self._launch_ready()
 
@@ -190,17 +195,21 @@ class GradientAllReduce:
         n = p.numel()
         dst = b["flat"][b["offs"][k]:b["offs"][k] + n].view_as(p)
         torch.mul(p.grad, 1.0 / self.world, out=dst)
-        b["flat"][b["n"] + k] = 1.0
         p.grad = dst  # the bucket slice is the gradient: no copy back after the collective
         b["ready"][k] = True
         self._launch_ready()
 
     def _launch(self, b) -> None:
-        for k, p in enumerate(b["params"]):  # parameters this rank never reached: zeros, absent
-            if not b["ready"][k]:
+        # presence slots written once per bucket on the device (a per-parameter Python scalar
+        # store is a host-to-device copy, issued from inside the backward's hooks)
+        if all(b["ready"]):
+            b["flat"][b["n"]:].fill_(1.0)
+        else:
+            for k, p in enumerate(b["params"]):  # parameters this rank never reached: zeros, absent
                 n = p.numel()
-                b["flat"][b["offs"][k]:b["offs"][k] + n].zero_()
-                b["flat"][b["n"] + k] = 0.0
+                if not b["ready"][k]:
+                    b["flat"][b["offs"][k]:b["offs"][k] + n].zero_()
+                b["flat"][b["n"] + k:b["n"] + k + 1].fill_(1.0 if b["ready"][k] else 0.0)
         b["work"] = dist.all_reduce(b["flat"], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         b["launched"] = True
 
