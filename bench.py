@@ -84,7 +84,7 @@ from horizongs_amd.activations import activate  # noqa: E402
 from horizongs_amd.loss import fused_loss  # noqa: E402
 from horizongs_amd.multigpu import GradientAllReduce  # noqa: E402
 from horizongs_amd.optim import Adam  # noqa: E402
-from horizongs_amd.synthetic import make_scene  # noqa: E402
+from horizongs_amd.synthetic import camera_set, make_scene  # noqa: E402
 
 METRIC = "train-step views/sec (fwd+bwd raster) @2M Gaussians/1080p; PSNR delta vs ref"
 FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
@@ -97,8 +97,10 @@ KERNELS = ["project3d_fwd", "isect_count", "isect_emit", "tile_sort", "raster3d_
 
 
 CONFIGS = {
-    "c2": dict(label="headline: 2M explicit Gaussians (the metric's own size), 1080p, 3DGS", gs="3d", anchors=0,
-               sh_degree=None, mode=None),
+    "c2": dict(label=("headline: 2M explicit Gaussians (the metric's own size), 1080p, 3DGS, a seeded 16-view "
+                      "camera set cycled per step"), gs="3d", anchors=0, sh_degree=None, mode=None),
+    "c2-fixed": dict(label=("c2 on its single identity camera every step (the rounds 1-4 headline: the view with the "
+                            "most intersections)"), gs="3d", anchors=0, sh_degree=None, mode=None, cameras=1),
     "c2-anchors": dict(label="configs[1] Block_small coarse: 500k anchors (RGB, view_dim 3), 1080p, 3DGS", gs="3d",
                        anchors=500_000, sh_degree=None, view_dim=3, mode=None),
     "c3": dict(label="configs[2] Block_small fine: 2DGS surfels, depth + normal outputs, 1080p", gs="2d", anchors=0,
@@ -134,6 +136,9 @@ def parse(argv=None):
     ap.add_argument("--anchors", type=int, default=None,
                     help="decode-inclusive variant (SURVEY 8(d) c2): A anchors -> fused decode -> raster")
     ap.add_argument("--view-dim", type=int, default=None, choices=[0, 3])
+    ap.add_argument("--cameras", type=int, default=None,
+                    help="training views cycled per step (default 16, c2-fixed 1): the reference picks a camera per "
+                         "iteration (train.py:133-148); synthetic.camera_set")
     return ap.parse_args(argv)
 
 
@@ -147,25 +152,29 @@ def resolve(args, world):
     if args.sh_degree is None:
         args.sh_degree = c["sh_degree"]
     args.view_dim = c.get("view_dim", 3) if args.view_dim is None else args.view_dim
+    args.cameras = c.get("cameras", 16) if args.cameras is None else args.cameras
     if args.mode == "auto":
         args.mode = c["mode"] or ("ddp" if world > 1 else "chunk")
     return args
 
 
 class Workload:
-    def __init__(self, args, rank, dev):
+    def __init__(self, args, rank, dev, world=1):
         self.args = args
         self.dev = dev
         seed = rank if args.mode == "chunk" else 0
         # anchor workloads build their anchors in _init_anchors; the explicit scene needs only a camera
         sc = make_scene(2 if args.anchors else args.n, args.width, args.height, seed=seed, sh_degree=args.sh_degree)
         self.sc = sc
-        vm = sc.viewmats.clone()
-        if args.mode == "ddp" and rank > 0:  # a different view of the same scene per rank
-            th = 0.02 * rank
-            vm[0, :3, :3] = torch.tensor([[np.cos(th), 0, np.sin(th)], [0, 1, 0], [-np.sin(th), 0, np.cos(th)]],
-                                         dtype=torch.float32)
-        self.viewmats = vm.to(dev)
+        # the training cameras (train.py:133-148 picks one per iteration): view 0 is the scene's
+        # identity camera, the rest a seeded ring / elevation / distance set (synthetic.camera_set);
+        # step s of rank r renders view (s * world + r) mod V -- a rank-sharded viewpoint stack
+        self.cams = camera_set(args.cameras).to(dev)[:, None] if args.cameras > 1 else sc.viewmats.to(dev)[None]
+        self.cam_centers = torch.linalg.inv(self.cams[:, 0].double())[:, :3, 3].float().contiguous()
+        self.rank, self.world = rank, (world if args.mode == "ddp" else 1)
+        self.n_steps = 0
+        self.view_log = []  # (view, intersections, Gaussians in view) of every step
+        self.viewmats = self.cams[self.rank % len(self.cams)]
         self.Ks = sc.Ks.to(dev)
         self.bg = torch.zeros(1, 3, device=dev)
         g = torch.Generator().manual_seed(1000 + rank)
@@ -210,7 +219,7 @@ class Workload:
         nn = torch.nn
         self.mlps = [nn.Sequential(nn.Linear(32 + self.view_dim, 32), nn.ReLU(True), nn.Linear(32, o)).to(dev)
                      for o in (k, 7 * k, self.color_dim * k)]
-        self.cam_center = torch.zeros(3, device=dev)
+        self.cam_center = self.cam_centers[self.rank % len(self.cams)]
         self.params = [self.anchor, self.feat, self.offset, self.scaling_raw] + [
             p for m in self.mlps for p in m.parameters()]
         self.ddp_order = [self.offset, self.scaling_raw, *self.mlps[1].parameters(), self.feat, self.anchor]
@@ -235,6 +244,12 @@ class Workload:
         for p in self.params:
             p.grad = None
         W, H = self.args.width, self.args.height
+        view = (self.n_steps * self.world + self.rank) % len(self.cams)
+        self.n_steps += 1
+        self.viewmats = self.cams[view]
+        if self.args.anchors:
+            self.cam_center = self.cam_centers[view]
+            self.lod["cam_center"] = self.cam_center
         if self.args.anchors:
             # set_anchor_mask + prefilter_voxel (scene/lod_model.py:286-290, gaussian_renderer/render.py
             # :120-197) fused: LoD test AND radius > 0 of the anchors projected with their first three
@@ -288,6 +303,7 @@ class Workload:
         else:
             self.optimizer.step()  # train.py:274-277 (zero_grad(set_to_none) = the grad reset above)
         self.meta = meta
+        self.view_log.append((view, meta["flatten_ids"].numel()))
         return loss
 
 
@@ -469,7 +485,7 @@ def cpu_baseline(args, wl):
 def measure(args, rank, world, dev):
     """Warm up, time exactly args.steps steps (barrier + synchronize on both sides, max over
     ranks), then a per-kernel breakdown pass.  Returns the measurements of this workload."""
-    wl = Workload(args, rank, dev)
+    wl = Workload(args, rank, dev, world)
     timing = not args.no_timing
     # live HIP events inside the timed region on the dominant kernel only (the roofline);
     # the per-kernel breakdown comes from a separate pass after it
@@ -489,6 +505,7 @@ def measure(args, rank, world, dev):
     isects_before = wl.meta["flatten_ids"].numel() if args.warmup else None
     if timing:
         NAT.call("hgsr_timing_enable", 1)
+    stats0, log0 = dict(G.isect_stats), len(wl.view_log)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -514,8 +531,11 @@ def measure(args, rank, world, dev):
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+    timed = wl.view_log[log0:]
     res = {"wl": wl, "dt": dt, "kernels": {}, "live": None, "isects_before": isects_before,
-           "isects_after": wl.meta["flatten_ids"].numel(), "dominant": dominant}
+           "isects_after": wl.meta["flatten_ids"].numel(), "dominant": dominant,
+           "isects_timed": [n for _, n in timed], "views_timed": [v for v, _ in timed],
+           "isect_stats": {k: G.isect_stats[k] - stats0[k] for k in stats0}}
     if timing:
         pc, ec = ct.c_ulonglong(0), ct.c_ulonglong(0)
         NAT.call("hgsr_timing_exec_pairs", ct.byref(ec))
@@ -527,10 +547,12 @@ def measure(args, rank, world, dev):
         NAT.call("hgsr_timing_reset")
         NAT.call("hgsr_timing_only", None)
         NAT.call("hgsr_timing_enable", 1)
+        log1 = len(wl.view_log)
         for _ in range(min(args.steps, 10)):
             wl.step()
         torch.cuda.synchronize(dev)
         NAT.call("hgsr_timing_enable", 0)
+        res["isects_breakdown"] = float(np.mean([n for _, n in wl.view_log[log1:]]))
         for k in KERNELS:
             tot, cnt = NAT.kernel_time(k)
             if cnt:
@@ -551,7 +573,7 @@ def roofline(args, res):
         return None
     dom, wl = res["dominant"], res["wl"]
     traffic, traffic_src = pmc_traffic(args)
-    n_isects = res["isects_after"]
+    n_isects = float(np.mean(res["isects_timed"]))  # mean over the timed steps (the views differ)
     pairs = res["pairs_timed"] // args.steps  # mean over exactly the launches the events time
     epairs = res["exec_pairs_timed"] // args.steps
     avg_s = live["avg_ms"] * 1e-3
@@ -567,7 +589,8 @@ def roofline(args, res):
                      f"per-quadrant list x 64 lanes, counted on the device over the timed launches) x {fpp:.0f} "
                      f"FLOP/pair (SURVEY 8(d)) / kernel time; frac_on_gsplat_visited_pairs prices gsplat's visit "
                      f"count ({pairs}: every Gaussian up to each tile's latest contributor x 256 pixels, pairs the "
-                     f"culling skips included) -- a note, not the roofline; {n_isects} intersections; limiter "
+                     f"culling skips included) -- a note, not the roofline; {n_isects:.0f} intersections per view "
+                     f"(mean over the timed steps); limiter "
                      f"counters in profiles/r04_pmc_raster3d_bwd_limiters.txt")}
     # aggregate compulsory-bytes figure of SURVEY 8(d): B_step = 384 N + 132 I + 52 P
     b_step = 384 * wl.last_colors.shape[0] + 132 * n_isects + 52 * args.width * args.height
@@ -575,7 +598,7 @@ def roofline(args, res):
         roof["traffic_unit"] = "bytes/launch"
         roof["traffic_source"] = traffic_src
     roof["aggregate_hbm_frac"] = round(b_step / (res["dt"] / args.steps) / (HBM_PEAK_GBS * 1e9), 4)
-    roof["n_isects"] = n_isects
+    roof["n_isects"] = round(n_isects)
     roof["n_isects_before_timed"] = res["isects_before"]
     roof["kernel_avg_ms"] = live["avg_ms"]
     roof["timing"] = ("HIP events (no system fence) on the kernel's stream, recorded inside the timed region "
@@ -583,10 +606,27 @@ def roofline(args, res):
     return roof
 
 
+def camera_summary(args, res):
+    """The views of the timed steps: how many cameras the set cycles, their intersection counts
+    and the deferred-count outcome of every timed view (gsplat_api.isect_stats: deferred = the
+    count was read after the forward was queued; redo = the view overflowed the capacity and was
+    re-emitted at the exact size; sync = no history for the camera grid yet)."""
+    n = res["isects_timed"]
+    out = {"views_in_set": args.cameras, "views_timed": len(set(res["views_timed"])),
+           "n_isects_mean": round(float(np.mean(n))), "n_isects_min": int(min(n)), "n_isects_max": int(max(n)),
+           "isect_counts_timed": res["isect_stats"]}
+    if args.cameras > 1:
+        out["note"] = ("synthetic.camera_set: view 0 = the scene's identity camera (its most intersections), the "
+                       "others on a ring (yaw +-25 deg, elevation +-15 deg, 0.5-1.5x its distance); view (step * "
+                       "world + rank) mod V per step (reference train.py:133-148 picks a camera per iteration)")
+    return out
+
+
 def workload_name(args):
     anchors = (f"LoD mask + anchor prefilter + fused anchor decode ({args.anchors} anchors, view_dim {args.view_dim}, "
                + ("RGB" if args.sh_degree is None else f"SH{args.sh_degree} colour head") + ") + ")
-    return (f"{args.config} {'3DGS' if args.gs == '3d' else '2DGS'} train step: "
+    cams = (f"a {args.cameras}-view camera set cycled per step" if args.cameras > 1 else "one fixed camera")
+    return (f"{args.config} {'3DGS' if args.gs == '3d' else '2DGS'} train step on {cams}: "
             + (f"SH{args.sh_degree} colours + " if args.sh_degree is not None and not args.anchors else "")
             + (anchors if args.anchors else "")
             + "rasterization fwd" + (f" (SH degree {args.sh_degree})" if args.sh_degree is not None else "")
@@ -604,7 +644,7 @@ def parallelism(args, world):
 
 
 def secondary_names(args, world):
-    names = ["c4", "c5"] if world > 1 else ["c2-anchors", "c3", "c4", "c5"]
+    names = ["c4", "c5"] if world > 1 else ["c2-fixed", "c2-anchors", "c3", "c4", "c5"]
     return [n for n in names if n != args.config]
 
 
@@ -623,7 +663,7 @@ def secondary(args, rank, world, dev):
                         "parallelism": parallelism(a, world), "n_gpus": world,
                         "value": round(world * a.steps / r["dt"], 3), "unit": "views/s",
                         "ms_per_step": round(r["dt"] / a.steps * 1e3, 3), "steps": a.steps, "warmup": a.warmup,
-                        "gaussians": int(r["wl"].last_colors.shape[0]), "n_isects": r["isects_after"],
+                        "gaussians": int(r["wl"].last_colors.shape[0]), "cameras": camera_summary(a, r),
                         "roofline": None if roof is None else dict(
                             {k: roof[k] for k in ("bound", "kernel", "achieved", "frac", "kernel_avg_ms",
                                                   "pairs_evaluated_per_launch", "gsplat_visited_pairs_per_launch",
@@ -663,10 +703,10 @@ def main():
             "data": "synthetic (seeded scenes of SURVEY 8(d); no dataset in the environment)",
             "config": {"workload": workload_name(args), "config": args.config, "label": CONFIGS[args.config]["label"],
                        "gaussians": int(wl.last_colors.shape[0]), "width": args.width, "height": args.height,
-                       "parallelism": parallelism(args, world)},
+                       "parallelism": parallelism(args, world), "cameras": camera_summary(args, res)},
             "roofline": roof, "cpu_baseline": cpu, "quality": psnr_parity(args), "kernels": res["kernels"],
             "kernels_source": "HIP events of every kernel over a separate pass after the timed region",
-            "hbm_kernels": hbm_kernels(wl, res["kernels"], res["isects_after"]),
+            "hbm_kernels": hbm_kernels(wl, res["kernels"], res.get("isects_breakdown")),
         }
     del res, wl
     torch.cuda.empty_cache()

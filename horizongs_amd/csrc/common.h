@@ -136,81 +136,6 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Sum K values across the wave at once, step-major: every DPP step is applied to
-// all K values before the next, so no DPP read waits on the previous write
-// (no s_nop hazards) and the VALU stays busy; totals land in lane 63.
-template <int K>
-__device__ __forceinline__ void wave_sum_many_to_lane63(float (&v)[K]) {
-#define HGSR_DPP_STEP(CTRL, ROWMASK)                                                                    \
-    _Pragma("unroll") for (int k = 0; k < K; ++k) {                                                    \
-        const int x = __builtin_amdgcn_update_dpp(0, __float_as_int(v[k]), CTRL, ROWMASK, 0xF, false); \
-        v[k] += __int_as_float(x);                                                                      \
-    }
-    HGSR_DPP_STEP(0xB1, 0xF)   // quad_perm [1,0,3,2]
-    HGSR_DPP_STEP(0x4E, 0xF)   // quad_perm [2,3,0,1]
-    HGSR_DPP_STEP(0x124, 0xF)  // row_ror:4
-    HGSR_DPP_STEP(0x128, 0xF)  // row_ror:8
-    HGSR_DPP_STEP(0x142, 0xA)  // row_bcast:15 into rows 1,3
-    HGSR_DPP_STEP(0x143, 0xC)  // row_bcast:31 into rows 2,3
-#undef HGSR_DPP_STEP
-}
-
-// Transpose-reduction of K per-lane values across the wave (gfx950):
-//   step A: v_permlane32_swap pairs value i with value i+H (H = ceil(K/2)); one
-//           add leaves value i summed over lane pairs (l, l+32) in lanes 0-31 and
-//           value i+H in lanes 32-63;
-//   step B: v_permlane16_swap pairs those registers again; each 16-lane row now
-//           holds a different value summed over the 4 rows;
-//   step C: ROW_STEPS DPP row steps finish the 16-lane sums: with 4, every lane of
-//           row r holds the row total; with 3 (the last, row_ror:8, left out), lanes
-//           0 and 8 of each row hold two halves whose sum is the total, for callers
-//           that add both halves into memory anyway (LDS atomics from 2 lanes/row).
-// ~2.6 instructions per value instead of 6+ for independent full reductions.
-// Afterwards register u[j] holds, in row r, (a part of) the total of value
-// transpose_index<K>(j, r) (or -1 = padding).
-template <int K, int ROW_STEPS = 4>
-struct TransposeReduce {
-    static constexpr int H = (K + 1) / 2;  // registers after step A
-    static constexpr int G = (H + 1) / 2;  // registers after step B
-    __device__ static constexpr int index(int j, int r) {
-        // r0: 2j, r1: 2j+1 (both < H); r2: 2j+H, r3: 2j+1+H (both < K)
-        return r == 0 ? (2 * j < H ? 2 * j : -1)
-             : r == 1 ? (2 * j + 1 < H ? 2 * j + 1 : -1)
-             : r == 2 ? (2 * j < H && 2 * j + H < K ? 2 * j + H : -1)
-                      : (2 * j + 1 < H && 2 * j + 1 + H < K ? 2 * j + 1 + H : -1);
-    }
-    __device__ static __forceinline__ void run(const float (&v)[K], float (&u)[G]) {
-        float w[2 * G];
-#pragma unroll
-        for (int i = 0; i < H; ++i) {
-            const float hi = (i + H < K) ? v[i + H] : 0.f;
-            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(hi), false, false);
-            w[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-        }
-        if constexpr (H < 2 * G) w[H] = 0.f;
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[2 * j]), __float_as_uint(w[2 * j + 1]),
-                                                            false, false);
-            u[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-        }
-#define HGSR_ROW_STEP(CTRL)                                                                              \
-    _Pragma("unroll") for (int j = 0; j < G; ++j) {                                                     \
-        const int x = __builtin_amdgcn_update_dpp(0, __float_as_int(u[j]), CTRL, 0xF, 0xF, false);      \
-        u[j] += __int_as_float(x);                                                                       \
-    }
-        HGSR_ROW_STEP(0xB1)   // quad_perm [1,0,3,2]
-        HGSR_ROW_STEP(0x4E)   // quad_perm [2,3,0,1]
-        HGSR_ROW_STEP(0x124)  // row_ror:4
-        if constexpr (ROW_STEPS == 4) HGSR_ROW_STEP(0x128)  // row_ror:8
-#undef HGSR_ROW_STEP
-        // materialise the sums in every lane: otherwise the compiler sinks the last
-        // add into the caller's lane-predicated branch as mov 0 + mov_dpp + add
-#pragma unroll
-        for (int j = 0; j < G; ++j) asm volatile("" : "+v"(u[j]));
-    }
-};
-
 template <int CTRL>
 __device__ __forceinline__ float dpp(float x) {  // lane-shuffled copy of x (bound_ctrl: 0 for invalid)
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));

@@ -985,12 +985,10 @@ extern "C" int hgsr_isect_count(int C, int N, const float* means2d, const int32_
     return check_launch("isect_binscan");
 }
 
+// bands of tile rows emitted one after another (4 bands let each XCD's L2 merge
+// the key lines; more bands trade the write amplification against time, r03_emit_phase_sweep)
 static int emit_phases(int tile_h) {
-    static const int env = [] {
-        const char* e = getenv("HGSR_EMIT_PHASES");
-        return e ? atoi(e) : 0;
-    }();
-    int p = env > 0 ? env : 4;
+    constexpr int p = 4;
     return p < tile_h ? p : (tile_h > 0 ? tile_h : 1);
 }
 

@@ -8,8 +8,6 @@
 // Per pair: h_u = px*w - u, h_v = py*w - v (rows u,v,w of the ray transform),
 // x = h_u x h_v, s = x.xy / x.z, G = min(|s|^2, 2|mean2d - p|^2), alpha =
 // min(0.999, o*exp(-G/2)).  The last colour channel is the depth (RGB+ED).
-#include <stdlib.h>
-
 #include "common.h"
 
 namespace hgsr {
@@ -413,247 +411,9 @@ __device__ __forceinline__ int32_t wave_max2(int32_t v) {
     return v;
 }
 
-template <int D, bool ABS>
-__global__ __launch_bounds__(256) void raster2d_bwd_kernel(
-    int C, int W, int H, int tw, int th, const Rec2* __restrict__ rec, const float* __restrict__ backgrounds,
-    int bg_ch, int ed_ch, const float* __restrict__ render_colors, const int32_t* __restrict__ offsets,
-    int64_t n_isects, const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
-    const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
-    const float* __restrict__ v_render_alphas, const float* __restrict__ v_render_normals,
-    float* __restrict__ acc_rows, unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask,
-    int64_t qstride, const float* __restrict__ normal_rot, const float* __restrict__ v_depth_extra) {
-    // row layout: 0-1 xy, 2-4 sum (p-m)_x v_c, 5-7 sum (p-m)_y v_c, 8-10 sum v_c (v_c = dL/d(h_u x h_v)),
-    // 11 opac, 12-14 normal, 15.. colour, then abs xy; split2 maps v_c sums to u, v, w and densify
-    constexpr int KV = 15 + D + (ABS ? 2 : 0);
-    constexpr int NB = kBwd2Batch;
-    // one LDS object: every component of record t sits at a compile-time offset from one address
-    __shared__ struct {
-        float4 r0[2][NB], r1[2][NB], r2[2][NB], col[2][NB], r4[2][NB], box[2][NB];
-    } sr;
-    auto& s_r0 = sr.r0;
-    auto& s_r1 = sr.r1;
-    auto& s_r2 = sr.r2;
-    auto& s_col = sr.col;
-    auto& s_r4 = sr.r4;
-    auto& s_box = sr.box;
-    __shared__ int32_t s_id[2][NB];
-    // row j of a lane row r lands in slot slot0(r) + 2j (TransposeReduce's pattern); the
-    // pattern's positions past KV are never read, and a padding position inside [0, KV) only
-    // ever receives an exact 0 (the padded values), so one base address serves every j
-    constexpr int KVP = (KV + 1) > (2 * TransposeReduce<KV>::G + TransposeReduce<KV>::H)
-                            ? (KV + 1) : (2 * TransposeReduce<KV>::G + TransposeReduce<KV>::H);
-    __shared__ float s_part[NB * KVP];  // the four waves' partials merged with LDS float atomics
-    __shared__ uint8_t s_list[4][NB];
-    __shared__ int32_t s_last[4];
-    const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
-    const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
-    const float T_final = tc.inside ? 1.0f - render_alphas[tc.pix] : 1.0f;
-    float T = T_final;
-    // Bsum = sum_k buf_k vo_k + sum_k nbuf_k vn_k: the only form in which the
-    // colour/normal composited behind the current surfel enters v_alpha
-    float Bsum = 0.f, vo[4] = {0.f, 0.f, 0.f, 0.f}, vn[3];
-#pragma unroll
-    for (int k = 0; k < D; ++k) vo[k] = tc.inside ? v_render_colors[tc.pix * D + k] : 0.f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) vn[k] = tc.inside ? v_render_normals[tc.pix * 3 + k] : 0.f;
-    if (normal_rot) {  // world-frame normal gradients back to the camera frame: R v
-        const float* R = normal_rot + tc.cam * 16;
-        float vc[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) vc[j] = R[4 * j] * vn[0] + R[4 * j + 1] * vn[1] + R[4 * j + 2] * vn[2];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) vn[j] = vc[j];
-    }
-    // the depth channel's second consumer (normals from depth, K13), added here instead of by a
-    // separate sum: the gradient w.r.t. the rendered (expected) depth value
-    if (v_depth_extra && tc.inside) vo[D - 1] += v_depth_extra[tc.pix];
-    float va = tc.inside ? v_render_alphas[tc.pix] : 0.f;
-    if (ed_ch >= 0 && tc.inside) {
-        // ED = raw / max(alpha, 1e-10): d/d raw = 1/ac, d/d alpha = -ED/ac (alpha >= 1e-10)
-        const float alpha = 1.0f - T_final, ac = fmaxf(alpha, 1e-10f);
-        float v_ed = 0.f;
-#pragma unroll
-        for (int k = 0; k < D; ++k)
-            if (k == ed_ch) {
-                v_ed = vo[k];
-                vo[k] = v_ed / ac;
-            }
-        if (alpha >= 1e-10f) va -= v_ed * render_colors[tc.pix * D + ed_ch] / ac;
-    }
-    float bg_dot = 0.f;
-#pragma unroll
-    for (int k = 0; k < D; ++k)
-        if (backgrounds && k < bg_ch) bg_dot += backgrounds[tc.cam * bg_ch + k] * vo[k];
-    const float va_term = T_final * (va - bg_dot);
-    const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
-    const int32_t wave_final = wave_max2(bin_final);
-    if (lane == 0) s_last[wave] = wave_final;
-    for (int e = tid; e < NB * KVP; e += 256) s_part[e] = 0.f;
-    lds_barrier();
-    const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
-    const int32_t end = min(tc.end, blk_final + 1);
-    const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
-    if (pair_counter && threadIdx.x == 0 && end > tc.start)  // measurement only (bench roofline)
-        atomicAdd(pair_slot(pair_counter, 0), (unsigned long long)(end - tc.start) * kTilePixels);
-    // records are staged with LDS-DMA (global_load_lds_dwordx4: per-lane source, LDS
-    // destination base + 16 B x lane), one batch ahead, so they cost no VGPRs (89 -> 59);
-    // the 64 loader lanes are exactly wave 0
-    float4* const stage_arr[6] = {&s_r0[0][0], &s_r1[0][0], &s_r2[0][0], &s_col[0][0], &s_r4[0][0], &s_box[0][0]};
-    int32_t cid = 0, nid = 0;
-    const bool loader = tid < NB;
-    auto dma_batch = [&](int buf, int32_t id) {
-        const float4* r = reinterpret_cast<const float4*>(rec + id);
-#pragma unroll
-        for (int q = 0; q < 6; ++q)
-            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + q),
-                                             (void __attribute__((address_space(3)))*)(stage_arr[q] + buf * NB), 16,
-                                             0, 0);
-    };
-    if (nb > 0 && loader) {
-        cid = flatten_ids[max(end - 1 - tid, tc.start)];
-        dma_batch(0, cid);
-        nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
-    }
-    using TR = TransposeReduce<KV>;
-    const int row = lane >> 4;
-    // first accumulator slot of this lane row's reduced values (slot0 + 2j for value j)
-    const int slot0 = row == 0 ? 0 : row == 1 ? 1 : row == 2 ? TR::H : TR::H + 1;
-    uint8_t* my_list = s_list[wave];
-    int prev_bsz = 0;
-    uint32_t stepped = 0;  // compacted list entries this wave stepped (bench roofline only)
-    // quadrant-mask words of batch bb (the forward's culling bits): wave-uniform index, so
-    // they are scalar loads, issued one batch ahead
-    uint64_t qw[2] = {0, 0};
-    auto qfetch = [&](int bb) {
-        const int64_t lo = (end - 1 - (int64_t)bb * NB - tc.start) - (NB - 1);
-        const int64_t bin = (int64_t)tc.cam * (tw * th) + tc.tile;
-        const int idx = __builtin_amdgcn_readfirstlane(
-            (int)(__builtin_amdgcn_readfirstlane(wave) * qstride + qmask_word0(tc.start, bin) + (lo >> 6)));
-        const uint64_t* qp = qmask + idx;
-        qw[0] = qp[0];
-        qw[1] = qp[1];
-    };
-    if (qmask && nb > 0) qfetch(0);
-    for (int b = 0; b <= nb; ++b) {
-        const int cur = b & 1, prv = cur ^ 1;
-        const int32_t batch_end = end - 1 - b * NB;
-        const int bsz = b < nb ? min(NB, batch_end + 1 - tc.start) : 0;
-        // batch b's DMA (issued one iteration ago, together with one batch-old atomics) lands
-        // before the barrier below publishes it; then DMA batch b+1 into the other buffer
-        // (its previous records were last read before the previous barrier) and combine b-1
-        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-        if (tid < bsz) s_id[cur][tid] = cid;
-        if (b + 1 < nb && loader) {
-            cid = nid;
-            dma_batch(prv, cid);
-            nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
-        }
-        if (b > 0) {
-            for (int e = tid; e < prev_bsz * KV; e += 256) {
-                const int t = e / KV, k = e - t * KV;
-                const float sv = s_part[t * KVP + k];
-                s_part[t * KVP + k] = 0.f;
-                if (sv != 0.f) atomicAdd(acc_rows + (int64_t)s_id[prv][t] * kRec2 + k, sv);
-            }
-        }
-        if (b == nb) break;
-        lds_barrier();
-        const int t0 = max(0, batch_end - wave_final);
-        const int t = lane;
-        uint64_t m;
-        bool rel;
-        if (qmask) {
-            // record t <-> tile-relative bit R - t (R = batch_end - start): the 64-bit window
-            // [R - 63, R] realigned from two words and bit-reversed, then limited to [t0, bsz)
-            const int64_t R = batch_end - tc.start, lo = R - (NB - 1);
-            const uint64_t w0 = qw[0], w1 = qw[1];
-            if (b + 1 < nb) qfetch(b + 1);
-            const int sh = (int)(lo & 63);
-            const uint64_t win = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
-            const uint64_t below_z = bsz >= 64 ? ~0ull : ((1ull << bsz) - 1);
-            const uint64_t below_a = t0 >= 64 ? ~0ull : ((1ull << t0) - 1);
-            const uint64_t mk = __builtin_bitreverse64(win) & below_z & ~below_a;
-            // (uint32_t casts: readfirstlane returns int, which would sign-extend)
-            m = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mk) |
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mk >> 32)) << 32);
-            rel = (m >> lane) & 1;
-        } else {
-            rel = t < bsz && t >= t0 &&
-                  reaches2_exact(s_r0[cur][t], s_r1[cur][t], s_r2[cur][t], s_r4[cur][t], s_box[cur][t], qx, qy);
-            m = __ballot(rel);
-        }
-        if (rel) my_list[lanes_below2(m)] = (uint8_t)t;
-        const int n_mine = __popcll(m);
-        stepped += (uint32_t)n_mine;
-        if (n_mine > 0) {
-            const int lst = my_list[lane];
-            for (int i = 0; i < n_mine; ++i) {
-                const int t = __builtin_amdgcn_readlane(lst, i);
-                const float4 r0 = s_r0[cur][t], r1 = s_r1[cur][t], r2 = s_r2[cur][t], c = s_col[cur][t],
-                             r4 = s_r4[cur][t];
-                const Hit2 h = hit2(r0, r1, r2, tc.px, tc.py);
-                const float vis = __builtin_amdgcn_exp2f(-h.sigma);
-                const float araw = r2.w * vis;
-                const float alpha = fminf(0.999f, araw);
-                const bool valid = (batch_end - t <= bin_final) & h.ok & (h.sigma >= 0.f) & (alpha >= 1.0f / 255.0f);
-                if (!__any(valid)) continue;
-                // an invalid lane composites alpha = 0: T, fac and Bsum come out unchanged
-                const float al = valid ? alpha : 0.f;
-                const float ra = __builtin_amdgcn_rcpf(1.0f - al);
-                const float Tn = T * ra;
-                const float fac = al * Tn;
-                const float ck[4] = {c.x, c.y, c.z, c.w};
-                float gv[KV];
-                float cv = r4.x * vn[0] + r4.y * vn[1] + r4.z * vn[2];
-#pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    cv += ck[k] * vo[k];
-                    gv[15 + k] = fac * vo[k];
-                }
-#pragma unroll
-                for (int k = 0; k < 3; ++k) gv[12 + k] = fac * vn[k];
-                const float v_alpha = Tn * cv + ra * (va_term - Bsum);
-                Bsum += fac * cv;
-                const float va2 = (valid & (araw <= 0.999f)) ? v_alpha : 0.f;  // clamped: no gradient
-                const float v_sigma = -araw * va2;
-                // sigma = |s|^2/2 (ray-plane hit) or |m - p|^2 (low-pass), whichever is smaller
-                const bool ell = h.g3 <= h.g2;
-                const float ve = ell ? v_sigma : 0.f, vp = ell ? 0.f : v_sigma;
-                const float vs0 = ve * h.sx, vs1 = ve * h.sy;
-                const float vc0 = vs0 * h.iz, vc1 = vs1 * h.iz, vc2 = -(vs0 * h.sx + vs1 * h.sy) * h.iz;
-                const float vx = 2.0f * vp * h.dx, vy = 2.0f * vp * h.dy;
-                gv[0] = vx;
-                gv[1] = vy;
-                gv[2] = -h.dx * vc0; gv[3] = -h.dx * vc1; gv[4] = -h.dx * vc2;
-                gv[5] = -h.dy * vc0; gv[6] = -h.dy * vc1; gv[7] = -h.dy * vc2;
-                gv[8] = vc0; gv[9] = vc1; gv[10] = vc2;
-                gv[11] = vis * va2;
-                if constexpr (ABS) {
-                    gv[15 + D] = fabsf(vx);
-                    gv[16 + D] = fabsf(vy);
-                }
-                T = Tn;
-                float u[TR::G];
-                TR::run(gv, u);
-                if ((lane & 15) == 0) {
-                    float* dst = s_part + t * KVP;
-#pragma unroll
-                    for (int j = 0; j < TR::G; ++j) atomicAdd(dst + slot0 + 2 * j, u[j]);  // ds_add_f32
-                }
-            }
-        }
-        prev_bsz = bsz;
-        lds_barrier();
-    }
-    if (pair_counter && lane == 0 && stepped)  // measurement only: lane-pairs stepped
-        atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
-}
-
 // ---------------------------------------------------------------- backward, transposed inputs
-// The 2DGS backward without its per-step 19-value wave reduction (TransposeReduce: 15
-// permlane swaps, 15 adds and 20 DPP adds a step).  As in the 3DGS backward, pass 1 composites
+// The 2DGS backward without a per-step 19-value wave reduction (round 2's kernel spent 15
+// permlane swaps, 15 adds and 20 DPP adds a step on it).  As in the 3DGS backward, pass 1 composites
 // the steps per lane (pixel) and queues the ones some pixel composites, two numbers per pixel:
 // F = fac = alpha T with the sigma branch in its sign bit (set: the low-pass disk, clear: the
 // ray-plane hit) and V = dL/dsigma.  They are transposed through LDS so that lane 16 s + r holds
@@ -1263,22 +1023,13 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     const dim3 grid(C * tile_w * tile_h);
     unsigned long long* const pairs = timing_pair_counter("raster2d_bwd");
     const int64_t qstride = qmask_stride_of(qmask_bytes);
-    // the transposed-input backward (raster2d_bwd_tp_kernel) unless HGSR_BWD2_TP=0 (read per call)
-    const char* tp_env = getenv("HGSR_BWD2_TP");
-    const bool tp = tp_env ? atoi(tp_env) != 0 : true;
 #define LAUNCH_B2(DD)                                                                                             \
     {                                                                                                             \
         KernelTimer kt("raster2d_bwd", s);                                                                        \
-        if (tp)                                                                                                   \
-            hipLaunchKernelGGL((raster2d_bwd_tp_kernel<DD>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
-                               tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,    \
-                               flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,            \
-                               v_render_normals, rows, pairs, qmask, qstride, normal_rot, v_depth_extra);        \
-        else                                                                                                      \
-            hipLaunchKernelGGL((raster2d_bwd_kernel<DD, false>), grid, dim3(256), 0, s, C, width, height, tile_w,  \
-                               tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,    \
-                               flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas,            \
-                               v_render_normals, rows, pairs, qmask, qstride, normal_rot, v_depth_extra);        \
+        hipLaunchKernelGGL((raster2d_bwd_tp_kernel<DD>), grid, dim3(256), 0, s, C, width, height, tile_w, tile_h,  \
+                           rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects, flatten_ids,    \
+                           render_alphas, last_ids, v_render_colors, v_render_alphas, v_render_normals, rows,      \
+                           pairs, qmask, qstride, normal_rot, v_depth_extra);                                     \
     }                                                                                                             \
     hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s,   \
                        C, N, rows, rt, m2, reinterpret_cast<float2*>(v_means2d), v_rt, cd, v_normals,             \

@@ -19,12 +19,12 @@ RuntimeError, as gsplat's TORCH_CHECKs do.
 """
 from __future__ import annotations
 
+import collections
 import ctypes as ct
 import math
 import threading
 from typing import Optional, Tuple
 
-import os
 
 import torch
 import torch.nn.functional as F
@@ -92,16 +92,30 @@ class GradSink:
         return v
 
 
-_GRAD_SINK = os.environ.get("HGSR_GRAD_SINK", "1") != "0"  # (A/B knob)
-# rasterization_2dgs: world-frame normals and K13 inside the fused raster Function (A/B knob)
-_FUSE_FRAME = os.environ.get("HGSR_FUSE_FRAME", "1") != "0"
+# The folded glue (DESIGN.md §8 "Round 4: the deferred intersection count and the folded glue"):
+# the loss's scale gradient through a GradSink, and rasterization_2dgs' world-frame normals + K13
+# inside the fused raster Function.  Module constants, not knobs: tests/test_gpu_glue.py flips
+# them to compare against the unfolded composition they replace.
+_GRAD_SINK = True
+_FUSE_FRAME = True
 
 
 def _attach_sink(ctx, scales, grad_mode, idx):
+    """Hang a fresh sink on `scales` for this projection.  If the tensor still carries an OPEN
+    sink -- a second projection of the same scales before the first one's backward ran, e.g. a
+    render whose graph is never backpropagated -- the loss could not tell which projection's
+    backward will take its gradient: both sinks are closed (a put is refused, so the loss
+    returns its gradient through autograd) and this projection gets none."""
     ctx.sink = None
-    if _GRAD_SINK and grad_mode and ctx.needs_input_grad[idx]:
-        ctx.sink = GradSink()
-        scales._hgsr_grad_sink = ctx.sink
+    if not (_GRAD_SINK and grad_mode and ctx.needs_input_grad[idx]):
+        return
+    prev = getattr(scales, "_hgsr_grad_sink", None)
+    if prev is not None and not prev.closed:
+        prev.closed = True
+        scales._hgsr_grad_sink = None
+        return
+    ctx.sink = GradSink()
+    scales._hgsr_grad_sink = ctx.sink
 
 
 def _sink_grad(ctx, like):
@@ -308,12 +322,17 @@ _pinned = threading.local()
 # Deferred intersection count: rasterization() enqueues the emission, the sort
 # and the raster forward into capacity-sized buffers BEFORE it reads the count, so the one
 # host wait of a view lands behind queued work instead of draining the queue.  The capacity
-# comes from the previous view of the same camera grid; an overflow (device-detected, the
-# kernels then write nothing) is redone at the exact size.  HGSR_DEFER_ISECT=0: the
-# synchronous order (count -> host -> emit), as gsplat does it.
-_DEFER = os.environ.get("HGSR_DEFER_ISECT", "1") != "0"
-_pred = {}  # (device, C, tile_w, tile_h) -> (n_isects, largest bin) of the last view
+# is the largest count of the last _PRED_VIEWS views of the same camera grid (+ headroom): a
+# training loop cycles cameras (train.py:133-148) whose intersection counts differ widely, and
+# the previous view alone under-predicts every view busier than it.  An overflow (detected on
+# the device: the kernels then write nothing) is redone at the exact size; the first view of a
+# grid takes the synchronous order (count -> host -> emit), as gsplat does it.
+_PRED_VIEWS = 64
+_pred = {}  # (device, C, tile_w, tile_h) -> deque of (n_isects, largest bin) of the last views
 _CAP_GRAIN = 1 << 18  # capacities in steps of 256K keys: stable sizes for the caching allocator
+# views through the binned intersection: deferred (count read after the forward was queued),
+# redone (deferred over capacity, re-emitted at the exact size), synchronous (no prediction yet)
+isect_stats = {"deferred": 0, "redo": 0, "sync": 0}
 
 
 def _capacity(n, max_bin):
@@ -364,7 +383,10 @@ def _isect_count_host(st):
     m2, radii, host, ev, tw, th = st[0], st[2], st[7], st[8], st[11], st[12]
     ev.synchronize()
     n_isects, max_bin = int(host[0]), int(host[1])
-    _pred[(m2.device.index, radii.shape[0], tw, th)] = (n_isects, max_bin)
+    key = (m2.device.index, radii.shape[0], tw, th)
+    if key not in _pred:
+        _pred[key] = collections.deque(maxlen=_PRED_VIEWS)
+    _pred[key].append((n_isects, max_bin))
     return n_isects, max_bin
 
 
@@ -397,16 +419,15 @@ class _Deferred:
 def _isect_emit_deferred(st):
     """Stage 2 enqueued before the count is read (None without a prediction for this camera
     grid: the first view takes the synchronous path)."""
-    if not _DEFER:
-        return None
     m2, dep, radii, tpg, offsets, ws1, ws1_b, host, ev, info, tile_size, tile_width, tile_height = st
     C, Ng = radii.shape
-    p = _pred.get((m2.device.index, C, tile_width, tile_height))
-    if p is None:
+    hist = _pred.get((m2.device.index, C, tile_width, tile_height))
+    if not hist:
+        isect_stats["sync"] += 1
         return None
     dev = m2.device
     d = _Deferred()
-    d.cap, d.mbcap = _capacity(*p)
+    d.cap, d.mbcap = _capacity(max(h[0] for h in hist), max(h[1] for h in hist))
     d.ids = torch.empty(d.cap, dtype=torch.int64, device=dev)
     d.flat = torch.empty(d.cap, dtype=torch.int32, device=dev)
     ws2_b = N.size_query("hgsr_isect_ws2_bytes", d.cap, d.mbcap)
@@ -422,8 +443,11 @@ def _isect_resolve(st, d):
     """After the raster forward is enqueued: read the count (its copy finished long ago, so the
     host does not drain the queue).  True when it fit the capacities; d.n = n_isects."""
     n_isects, max_bin = _isect_count_host(st)
+    d.ws2 = d.info = None  # the sort scratch and the count are the queued kernels' alone now
     if n_isects > d.cap or max_bin > d.mbcap:
+        isect_stats["redo"] += 1
         return False  # the kernels wrote nothing: the caller redoes it at the exact size
+    isect_stats["deferred"] += 1
     d.n = n_isects
     return True
 
@@ -532,8 +556,7 @@ def _bwd_ws(size_fn, ctx, C, Ng, D, dev, grad_mode):
     needs_input_grad follows requires_grad only): an evaluation render under no_grad()
     allocates and clears nothing."""
     ctx.bwd_ws = None
-    if (not grad_mode or not any(ctx.needs_input_grad)
-            or os.environ.get("HGSR_RASTER_PREZERO", "1") == "0"):  # (A/B knob)
+    if not grad_mode or not any(ctx.needs_input_grad):
         return None
     ws_b = N.size_query(size_fn, C, Ng, D, 1)
     ctx.bwd_ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)

@@ -76,3 +76,42 @@ def c1(seed: int = 0) -> Scene:
 def c2(seed: int = 0, n: int = 2_000_000) -> Scene:
     """c2 north-star: 2M Gaussians at 1920x1080."""
     return make_scene(n, 1920, 1080, seed)
+
+
+def look_at(eye, target, up=(0.0, -1.0, 0.0)) -> torch.Tensor:
+    """world -> camera viewmat [4,4] (OpenCV axes as the synthetic scenes: x right, y down, z forward)
+    of a camera at `eye` looking at `target`."""
+    eye, target, up = (torch.tensor(v, dtype=torch.float64) for v in (eye, target, up))
+    z = target - eye
+    z = z / z.norm()
+    x = torch.linalg.cross(-up, z)
+    x = x / x.norm()
+    y = torch.linalg.cross(z, x)
+    R = torch.stack([x, y, z])  # rows: camera axes in world coordinates
+    vm = torch.eye(4, dtype=torch.float64)
+    vm[:3, :3] = R
+    vm[:3, 3] = -R @ eye
+    return vm.float()
+
+
+def camera_set(n_views: int = 16, seed: int = 0, centre=(0.0, 0.0, 6.0), radius: float = 6.0) -> torch.Tensor:
+    """A seeded training-camera set around a synthetic scene: [n_views, 4, 4] viewmats.
+
+    Horizon-GS trains one camera per iteration, picked at random from aerial and street views
+    (reference train.py:133-148), whose intersection counts differ widely.  View 0 is the scene's
+    own identity camera; the others sit on a ring around the scene centre (yaw within +-25 deg),
+    at elevations within +-15 deg, at 0.5-1.5x the identity camera's distance -- close "street"
+    views (fewer Gaussians in view, larger footprints) to far "aerial" ones (everything in view,
+    small footprints)."""
+    g = torch.Generator().manual_seed(1000 + seed)
+    c = torch.tensor(centre, dtype=torch.float64)
+    views = [torch.eye(4)]
+    for i in range(1, n_views):
+        yaw = math.radians(float(torch.rand(1, generator=g)) * 50.0 - 25.0)
+        pitch = math.radians(float(torch.rand(1, generator=g)) * 30.0 - 15.0)
+        dist = radius * (0.5 + 1.0 * (i - 1) / max(n_views - 2, 1))  # spread over the range, shuffled below
+        d = torch.tensor([math.sin(yaw) * math.cos(pitch), math.sin(pitch), -math.cos(yaw) * math.cos(pitch)],
+                         dtype=torch.float64)
+        views.append(look_at((c + dist * d).tolist(), c.tolist()))
+    perm = [0] + (1 + torch.randperm(n_views - 1, generator=g)).tolist()
+    return torch.stack([views[i] for i in perm])

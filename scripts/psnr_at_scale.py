@@ -43,8 +43,8 @@ def problem(A, W, H, gs):
     return gt, p0, cfg, n_target
 
 
-def perturbed(p0):
-    g = torch.Generator().manual_seed(SEEDS["perturb"])
+def perturbed(p0, seed=None):
+    g = torch.Generator().manual_seed(SEEDS["perturb"] if seed is None else seed)
     return {k: (v * (1 + 1e-6 * torch.randn(v.shape, generator=g)) if k != "anchor" else v) for k, v in p0.items()}
 
 
@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--lr-scale", type=float, default=1.0)
     ap.add_argument("--window", type=int, default=50)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--perturb-seed", type=int, default=None,
+                    help="ensemble member: run ONLY the chain from the initialisation perturbed with this seed "
+                         "and write it to --out (merged into the fixture by scripts/psnr_ensemble.py)")
     a = ap.parse_args()
     gt, p0, cfg, n_target = problem(a.anchors, a.width, a.height, a.gs)
     with torch.no_grad():
@@ -65,14 +68,17 @@ def main():
     res = dict(gs=a.gs, anchors=a.anchors, width=a.width, height=a.height, iterations=a.iters, lr_scale=a.lr_scale,
                window=a.window, target_gaussians=n_target, seeds=SEEDS, psnr_init_db=round(psnr_init, 4),
                threads=torch.get_num_threads(), omp_num_threads=os.environ.get("OMP_NUM_THREADS"))
-    for name, p in (("ref", p0), ("ref_perturbed_1e-6", perturbed(p0))):
+    runs = ((("ref", p0), ("ref_perturbed_1e-6", perturbed(p0))) if a.perturb_seed is None
+            else ((f"ref_perturbed_1e-6_seed{a.perturb_seed}", perturbed(p0, a.perturb_seed)),))
+    for name, p in runs:
         t0 = time.time()
         fin, win, losses = PF.fit(p, cfg, gt, a.iters, gs=a.gs, window=a.window, lr_scale=a.lr_scale)
         res[name] = dict(final_db=round(fin, 4), window_db=round(win, 4), seconds=round(time.time() - t0, 1),
                          loss_first=losses[0], loss_last=losses[-1], losses_every_10=[round(x, 6) for x in losses[::10]])
         print(name, res[name]["final_db"], res[name]["window_db"], res[name]["seconds"], "s", flush=True)
-    res["noise_floor_window_db"] = round(res["ref_perturbed_1e-6"]["window_db"] - res["ref"]["window_db"], 4)
-    res["noise_floor_final_db"] = round(res["ref_perturbed_1e-6"]["final_db"] - res["ref"]["final_db"], 4)
+    if a.perturb_seed is None:
+        res["noise_floor_window_db"] = round(res["ref_perturbed_1e-6"]["window_db"] - res["ref"]["window_db"], 4)
+        res["noise_floor_final_db"] = round(res["ref_perturbed_1e-6"]["final_db"] - res["ref"]["final_db"], 4)
     out = a.out or os.path.join(ROOT, "tests", "golden", f"psnr_scale_{a.gs}.json")
     with open(out, "w") as f:
         json.dump(res, f, indent=1)

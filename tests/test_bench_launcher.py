@@ -86,6 +86,24 @@ def test_configs_resolve(bench, argv, world, expect):
 
 def test_secondary_lines_per_world(bench):
     a = bench.resolve(bench.parse([]), 1)
-    assert bench.secondary_names(a, 1) == ["c2-anchors", "c3", "c4", "c5"]
+    assert bench.secondary_names(a, 1) == ["c2-fixed", "c2-anchors", "c3", "c4", "c5"]
+    assert a.cameras == 16 and bench.resolve(bench.parse(["--config", "c2-fixed"]), 1).cameras == 1
     assert bench.secondary_names(bench.resolve(bench.parse([]), 8), 8) == ["c4", "c5"]
     assert "c4" not in bench.secondary_names(bench.resolve(bench.parse(["--config", "c4"]), 2), 2)
+
+
+def test_camera_set_views():
+    """The bench's training cameras (reference train.py:133-148 picks one per iteration): view 0
+    is the scene's identity camera, the others valid rigid transforms looking at the scene
+    centre, seeded (the same set on every rank and run)."""
+    import torch
+    from horizongs_amd.synthetic import camera_set
+    cams = camera_set(16)
+    assert cams.shape == (16, 4, 4) and torch.equal(cams[0], torch.eye(4))
+    assert torch.equal(cams, camera_set(16))
+    R = cams[:, :3, :3].double()
+    assert torch.allclose(R @ R.transpose(1, 2), torch.eye(3, dtype=torch.float64).expand(16, 3, 3), atol=1e-6)
+    assert torch.allclose(torch.linalg.det(R), torch.ones(16, dtype=torch.float64), atol=1e-6)
+    centre = torch.tensor([0.0, 0.0, 6.0, 1.0])
+    zc = (cams @ centre)[:, 2]  # the scene centre lies straight ahead of every camera
+    assert torch.all(zc > 2.5) and len({round(float(z), 3) for z in zc}) > 8

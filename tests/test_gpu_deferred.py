@@ -2,11 +2,13 @@
 
 gsplat reads the intersection count on the host between the count pass and the emission
 (reference call: gaussian_renderer/render.py:40-76).  gsplat_api instead enqueues the
-emission, the per-tile sort and the raster forward into buffers sized from the previous
-view's count, and reads the count afterwards.  These tests check that this is
+emission, the per-tile sort and the raster forward into buffers sized from the largest count
+of the last views of the same camera grid, and reads the count afterwards.  These tests check that this is
 invisible: intersection arrays bit-identical to the synchronous order, renders bit-identical,
 gradients equal up to the backward's float-atomic order, and both overflow kinds (more keys
 than the capacity, a bin larger than the sort class launched) redone at the exact size."""
+import collections
+
 import numpy as np
 import pytest
 import torch
@@ -60,29 +62,30 @@ def _key(sc):
 @pytest.mark.parametrize("gs", ["3d", "2d"])
 def test_deferred_count_matches_synchronous(gs, monkeypatch):
     sc = _scene(30000, 256, 192, seed=11)
-    monkeypatch.setattr(G, "_DEFER", False)
+    G._pred.pop(_key(sc), None)  # no prediction for the grid: the synchronous order
     ref_imgs, ref_arr, ref_grads, ref_def = _run(sc, gs)
     assert not ref_def and ref_arr["isect_ids"].size > 50000
-    monkeypatch.setattr(G, "_DEFER", True)
     n = ref_arr["isect_ids"].size
     capacity = G._capacity
     mb = int(np.diff(np.append(ref_arr["isect_offsets"].reshape(-1), n)).max())
     cases = {
         # the capacity predicted from this very view: the deferred path proper
-        "deferred": lambda: G._pred.__setitem__(_key(sc), (n, mb)),
+        "deferred": lambda: _predict(sc, (n, mb)),
         # predicted from a smaller view: more keys than the capacity -> redone synchronously
         # (capacities come in 256K-key grains, above this scene's count: the headroom is patched)
-        "overflow_keys": lambda: (G._pred.__setitem__(_key(sc), (n // 4, mb)),
+        "overflow_keys": lambda: (_predict(sc, (n // 4, mb)),
                                   monkeypatch.setattr(G, "_capacity", lambda a, b: (a + 1024, capacity(a, b)[1]))),
         # a bin over the predicted sort class (capacity 16 keys per bin) -> redone
-        "overflow_bin": lambda: (G._pred.__setitem__(_key(sc), (n, mb)),
+        "overflow_bin": lambda: (_predict(sc, (n, mb)),
                                  monkeypatch.setattr(G, "_capacity", lambda a, b: (n + 1024, 16))),
     }
     for name, setup in cases.items():
         setup()
+        redo0 = G.isect_stats["redo"]
         imgs, arr, grads, deferred = _run(sc, gs)
         assert deferred == (name == "deferred"), name
-        assert G._pred[_key(sc)] == (n, mb), name  # the count of this view is the next prediction
+        assert G.isect_stats["redo"] - redo0 == int(name != "deferred"), name  # counted
+        assert G._pred[_key(sc)][-1] == (n, mb), name  # the count of this view joins the history
         for k in ref_arr:
             np.testing.assert_array_equal(arr[k], ref_arr[k], err_msg=f"{name}: {k}")
         for i, (a, b) in enumerate(zip(imgs, ref_imgs)):
@@ -95,10 +98,13 @@ def test_deferred_count_matches_synchronous(gs, monkeypatch):
         monkeypatch.setattr(G, "_capacity", capacity)
 
 
-def test_deferred_count_first_view_and_empty(monkeypatch):
+def _predict(sc, nm):
+    G._pred[_key(sc)] = collections.deque([nm], maxlen=G._PRED_VIEWS)
+
+
+def test_deferred_count_first_view_and_empty():
     """No prediction for a camera grid -> synchronous; a view with no intersection after a
     predicted one composites nothing."""
-    monkeypatch.setattr(G, "_DEFER", True)
     sc = _scene(2000, 208, 176, seed=3)  # a grid size no other test uses
     G._pred.pop(_key(sc), None)
     _, arr0, _, d0 = _run(sc, "3d")
@@ -112,3 +118,23 @@ def test_deferred_count_first_view_and_empty(monkeypatch):
     imgs, arr, grads, d2 = _run(empty, "3d")
     assert d2 and arr["isect_ids"].size == 0
     assert np.all(imgs[1] == 0) and all(np.all(g == 0) for g in grads[:5])
+
+
+def test_deferred_capacity_covers_a_camera_cycle():
+    """A training loop cycles cameras (train.py:133-148): the capacity is the largest count of
+    the grid's recent views, so after one pass over a busy and a quiet view neither is redone
+    (with the previous view alone as the prediction, every quiet -> busy change overflowed)."""
+    busy = _scene(20000, 224, 160, seed=5)  # a grid size no other test uses
+    quiet = _scene(20000, 224, 160, seed=5)
+    quiet.means[:, 2] += 6.0  # twice as far: a quarter of the footprint
+    G._pred.pop(_key(busy), None)
+    counts = []
+    for sc in (busy, quiet):
+        counts.append(_run(sc, "3d")[1]["isect_ids"].size)
+    assert counts[0] > 2 * counts[1]
+    s0 = dict(G.isect_stats)
+    for _ in range(3):
+        for sc in (quiet, busy):
+            assert _run(sc, "3d")[3]
+    assert G.isect_stats["redo"] == s0["redo"] and G.isect_stats["deferred"] == s0["deferred"] + 6
+    assert max(h[0] for h in G._pred[_key(busy)]) == counts[0]

@@ -103,3 +103,28 @@ def test_2dgs_fused_frame_matches_separate_kernels(monkeypatch):
     assert np.abs(out[2]).max() > 0.1 and np.abs(out[3]).max() > 0.1
     for i, (a, b) in enumerate(zip(gr, ref_g)):
         np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5 * float(np.abs(b).max()), err_msg=f"grad {i}")
+
+
+def test_grad_sink_second_projection_falls_back_to_autograd():
+    """A second projection of the same scales before the first one's backward (a render whose
+    graph is never backpropagated) closes the open sink: the loss then returns its scale
+    gradient through autograd, so no gradient lands in an orphaned sink."""
+    sc = make_scene(6000, 160, 120, seed=21, scale_range=(0.01, 0.05), depth_range=(2.0, 6.0))
+    ref = _train_step(sc, "3d")
+    means, quats, cols = (t.to(DEV).clone().requires_grad_(True) for t in (sc.means, sc.quats, sc.colors))
+    log_s = torch.log(sc.scales).to(DEV).requires_grad_(True)
+    logit = torch.logit(sc.opacities).to(DEV).requires_grad_(True)
+    scales, opac = activate(log_s, logit)
+    W, H = sc.width, sc.height
+    vm, K = sc.viewmats.to(DEV), sc.Ks.to(DEV)
+    bg = torch.zeros(1, 3, device=DEV)
+    gt = torch.rand(3, H, W, generator=torch.Generator().manual_seed(3)).to(DEV)
+    out, alpha, _ = G.rasterization(means, quats, scales, opac, cols, vm, K, W, H, packed=False, backgrounds=bg,
+                                    render_mode="RGB+ED")
+    G.rasterization(means, quats, scales, opac, cols, vm, K, W, H, packed=False, backgrounds=bg,
+                    render_mode="RGB+ED")  # an orphaned render of the same scales, never backpropagated
+    img = out.reshape(H, W, -1).permute(2, 0, 1)
+    fused_loss(img, gt, None, 0.2, alpha.reshape(H, W), 0.05, 0.05, scales, 0.01)[0].backward()
+    got = [t.grad.cpu().numpy() for t in (means, quats, log_s, logit, cols)]
+    for i, (a, b) in enumerate(zip(got, ref)):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5 * float(np.abs(b).max()), err_msg=f"grad {i}")
