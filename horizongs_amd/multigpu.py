@@ -142,7 +142,7 @@ class GradientAllReduce:
         # flat = [grads of every parameter | one presence slot per parameter]
         flat = torch.empty(o + len(params), dtype=torch.float32, device=dev)
         return {"params": params, "offs": offs, "n": o, "flat": flat, "ready": [False] * len(params),
-                "early": [False] * len(params), "work": None, "launched": False}
+                "early": [None] * len(params), "work": None, "launched": False}
 
     # ---------------------------------------------------------------- per step
     def begin(self) -> None:
@@ -153,7 +153,7 @@ class GradientAllReduce:
         self._next = 0
         for b in self.buckets:
             b["ready"] = [False] * len(b["params"])
-            b["early"] = [False] * len(b["params"])
+            b["early"] = [None] * len(b["params"])
             b["work"], b["launched"] = None, False
         self._in_step = True
         from . import decode
@@ -161,7 +161,12 @@ class GradientAllReduce:
 
     def early(self, pairs) -> None:
         """Gradients final before the backward ends ([(parameter, gradient)], decode backward):
-        copied into their buckets now, and the buckets that became complete are launched."""
+        copied into their buckets now, and the buckets that became complete are launched.
+
+        The handed-over tensor must be the very gradient the caller's backward then returns
+        for the parameter, and the only one: _on_grad checks that autograd's accumulated
+        gradient IS that tensor (a second consumer of the parameter would have made autograd
+        sum a new one, whose extra part the early collective never saw) and raises otherwise."""
         if not self._in_step:
             return
         for p, g in pairs:
@@ -171,10 +176,15 @@ class GradientAllReduce:
             b = self.buckets[loc[0]]
             k = loc[1]
             if b["launched"] or b["ready"][k]:
-                continue
+                raise RuntimeError("hgsr GradientAllReduce: an early gradient arrived for a parameter whose gradient "
+                                   "is already in its bucket this step (exactly one backward, and one hand-off, "
+                                   "between begin() and finish())")
             dst = b["flat"][b["offs"][k]:b["offs"][k] + p.numel()].view_as(p)
             torch.mul(g.reshape(p.shape), 1.0 / self.world, out=dst)
-            b["ready"][k] = b["early"][k] = True
+            b["ready"][k] = True
+            # the storage address only: holding the tensor would make autograd copy it instead of
+            # adopting it as .grad, and the check below relies on the adoption
+            b["early"][k] = g.data_ptr()
         self._launch_ready()
 
     def _on_grad(self, p) -> None:
@@ -184,8 +194,14 @@ class GradientAllReduce:
             return
         bi, k = self._where[id(p)]
         b = self.buckets[bi]
-        if b["early"][k]:  # handed over by early(): autograd's copy of the same gradient arrives now
-            b["early"][k] = False
+        if b["early"][k] is not None:  # handed over by early(): autograd's adoption of it arrives now
+            handed, b["early"][k] = b["early"][k], None
+            if p.grad.data_ptr() != handed:
+                raise RuntimeError(
+                    "hgsr GradientAllReduce: the gradient autograd accumulated for a parameter differs from the one "
+                    "the decode backward handed over early (another consumer of the parameter in this graph, or a "
+                    "create_graph backward): its all-reduce already left with the decode's part only.  Train such "
+                    "graphs without the early hand-off (decode.set_early_grad_hook(None) after begin()).")
             p.grad = b["flat"][b["offs"][k]:b["offs"][k] + p.numel()].view_as(p)
             return
         if b["launched"] or b["ready"][k]:

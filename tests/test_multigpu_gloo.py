@@ -298,6 +298,26 @@ def test_sync_reduce_across_steps_and_bucket_identity():
 # early gradients (the decode backward's cov head hands over _offset / _scaling / cov MLP
 # gradients before the backward ends) and the bucket order that launches them first
 # ---------------------------------------------------------------------------------------
+class _EarlyStandIn(torch.autograd.Function):
+    """CPU stand-in of the decode backward's hand-off: the identity on b whose backward passes
+    the gradient it returns to the early hook first (decode.py _Decode.backward, head_mask 2),
+    while the rest of the backward has not run yet."""
+
+    @staticmethod
+    def forward(ctx, b, red):
+        ctx.b, ctx.red = b, red
+        return b.view_as(b)
+
+    @staticmethod
+    def backward(ctx, g):
+        from horizongs_amd import decode as HD
+        gb = g.clone()
+        HD._EARLY_GRAD[0]([(ctx.b, gb)])
+        first = ctx.red.buckets[0]
+        _EarlyStandIn.launched = first["launched"] and [id(p) for p in first["params"]] == [id(ctx.b)]
+        return gb, None
+
+
 def _early_worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -313,19 +333,26 @@ def _early_worker(rank, world, port, q):
             opt.zero_grad(set_to_none=True)
             red.begin()
             assert HD._EARLY_GRAD[0] is not None  # installed for the step
-            loss = _view_loss(params, rank)
-            # the CPU stand-in of the decode backward: b's gradient is final "early" and handed
-            # over before the rest of the backward runs
-            gb, = torch.autograd.grad(loss, [b], retain_graph=True)
-            HD._EARLY_GRAD[0]([(b, gb)])
-            first = red.buckets[0]
-            launched_early = first["launched"] and [id(p) for p in first["params"]] == [id(b)]
+            # b reaches the loss only through the stand-in, whose backward runs before a's
+            _EarlyStandIn.launched = None
+            loss = _view_loss([a, _EarlyStandIn.apply(b, red), c, d], rank)
             loss.backward()
             red.finish()
             assert HD._EARLY_GRAD[0] is None  # removed after the step
-            out.append((launched_early, [None if p.grad is None else p.grad.detach().numpy().copy() for p in params]))
+            out.append((_EarlyStandIn.launched,
+                        [None if p.grad is None else p.grad.detach().numpy().copy() for p in params]))
             opt.step()
-        q.put((rank, out))
+        # a second consumer of b besides the hand-off: autograd sums a new gradient, which the
+        # early collective never saw -- refused
+        opt.zero_grad(set_to_none=True)
+        red.begin()
+        err = None
+        try:
+            (_view_loss([a, _EarlyStandIn.apply(b, red), c, d], rank) + (3 * b).sum()).backward()
+        except RuntimeError as e:
+            err = str(e)
+        red.finish()
+        q.put((rank, out, err))
     finally:
         dist.destroy_process_group()
 
@@ -350,7 +377,8 @@ def test_early_gradients_launch_first_and_match():
         (sum(_view_loss(params, v) for v in (0, 1)) / 2).backward()
         ref_grads.append([None if p.grad is None else p.grad.clone() for p in params])
         opt.step()
-    for rank, out in res:
+    for rank, out, err in res:
+        assert err and "handed over early" in err, err
         for step, (launched_early, grads) in enumerate(out):
             assert launched_early, (rank, step)  # the early bucket's collective was in flight before backward
             for g, r in zip(grads, ref_grads[step]):
