@@ -111,7 +111,7 @@ def load_stage(d, device):
     return p, w
 
 
-def train(p, weights, cid, iters, width, height, views, seed):
+def train(p, weights, cid, iters, width, height, views, seed, lr_scale=1.0):
     """`iters` reference train steps (train.py:150-277) of the chunk model on the device: fused
     LoD-free prefilter -> fused decode -> rasterization(SH2) -> fused loss -> backward -> Adam."""
     from . import decode as HD
@@ -137,8 +137,8 @@ def train(p, weights, cid, iters, width, height, views, seed):
     P = {k: v.to(dev).clone().requires_grad_(k != "anchor") for k, v in p.items()}
     W = {k: v.to(dev).clone().requires_grad_(True) for k, v in weights.items()}
     lr = dict(feat=0.0075, offset=0.01, scaling=0.007, opacity=0.002, cov=0.004, color=0.008)
-    groups = [{"params": [P[k]], "lr": lr[k]} for k in ("feat", "offset", "scaling")]
-    groups += [{"params": [W[k]], "lr": lr[k.split("_")[0]]} for k in W]
+    groups = [{"params": [P[k]], "lr": lr_scale * lr[k]} for k in ("feat", "offset", "scaling")]
+    groups += [{"params": [W[k]], "lr": lr_scale * lr[k.split("_")[0]]} for k in W]
     opt = Adam(groups, lr=0.0, eps=1e-15)
     quats = torch.zeros(P["anchor"].shape[0], 4, device=dev)
     quats[:, 0] = 1
@@ -171,6 +171,7 @@ def main(argv=None):
     ap.add_argument("--width", type=int, default=320)
     ap.add_argument("--height", type=int, default=180)
     ap.add_argument("--views", type=int, default=8)
+    ap.add_argument("--lr-scale", type=float, default=1.0, help="every learning rate times this")
     ap.add_argument("--dry", action="store_true", help="plumbing only: no device work")
     a = ap.parse_args(argv)
     d = _paths(a.out, a.chunk, a.stage)
@@ -203,7 +204,7 @@ def main(argv=None):
         p, weights = load_stage(_paths(a.out, a.chunk, "coarse"), "cpu")
         weights = {k: v.cpu() for k, v in weights.items()}
         seed = 3
-    p, weights = train(p, weights, a.chunk, a.iters, a.width, a.height, a.views, seed)
+    p, weights = train(p, weights, a.chunk, a.iters, a.width, a.height, a.views, seed, a.lr_scale)
     mlps = []
     for h in ("opacity", "cov", "color"):
         lin1 = torch.nn.Linear(32, 32)

@@ -69,6 +69,13 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
     return xcd * q + (xcd < r ? xcd : r) + idx;
 }
 
+// the raster kernels' tile of workgroup blockIdx.x: its XCD band's slot, through the
+// heaviest-first order when one was computed (order == nullptr: band order)
+__device__ __forceinline__ int raster_bin(const int32_t* __restrict__ order) {
+    const int slot = xcd_remap(blockIdx.x, gridDim.x);
+    return order ? order[slot] : slot;
+}
+
 // Full 64-lane sum with DPP row ops; the total lands in lane 63.
 __device__ __forceinline__ float wave_sum_to_lane63(float v) {
     int x;
@@ -105,9 +112,32 @@ __host__ __device__ __forceinline__ int64_t qmask_word0(int64_t start, int64_t b
 __host__ __device__ __forceinline__ int64_t qmask_stride(int64_t n_isects, int64_t n_bins) {
     return (n_isects + 63) / 64 + n_bins + 4;
 }
-// the stride of a caller-sized quadrant-mask buffer (4 arrays of 64-bit words): forward and
-// backward derive it from the same buffer, which may be sized for a capacity above n_isects
-inline int64_t qmask_stride_of(size_t qmask_bytes) { return (int64_t)(qmask_bytes / (4 * sizeof(uint64_t))); }
+// The caller-sized quadrant-mask buffer (hgsr_raster3d_qmask_bytes) starts with the tiles'
+// dispatch order (tile_order_kernel, one int32 per (camera, tile) bin, 256-B aligned), then
+// the 4 arrays of 64-bit words.  Forward and backward derive both from the same buffer,
+// which may be sized for a capacity above n_isects.
+inline size_t tile_order_bytes(int64_t n_bins) { return ((size_t)n_bins * sizeof(int32_t) + 255) & ~(size_t)255; }
+inline int64_t qmask_stride_of(size_t qmask_bytes, int64_t n_bins) {
+    const size_t ob = tile_order_bytes(n_bins);
+    return qmask_bytes > ob ? (int64_t)((qmask_bytes - ob) / (4 * sizeof(uint64_t))) : 0;
+}
+inline uint64_t* qmask_words(void* buf, int64_t n_bins) {
+    return buf ? reinterpret_cast<uint64_t*>(static_cast<char*>(buf) + tile_order_bytes(n_bins)) : nullptr;
+}
+inline const uint64_t* qmask_words(const void* buf, int64_t n_bins) {
+    return buf ? reinterpret_cast<const uint64_t*>(static_cast<const char*>(buf) + tile_order_bytes(n_bins)) : nullptr;
+}
+inline int32_t* tile_order_of(void* buf) { return static_cast<int32_t*>(buf); }
+inline const int32_t* tile_order_of(const void* buf) { return static_cast<const int32_t*>(buf); }
+
+// Heaviest-first dispatch order of the raster tiles (core.hip): within each XCD's contiguous
+// band of bins (xcd_remap), the bins sorted by intersection count, largest first, so the
+// long tiles start early and the grid does not end on a few stragglers.  order[slot] = bin.
+#ifndef HGSR_TILE_ORDER
+#define HGSR_TILE_ORDER 1
+#endif
+int launch_tile_order(int64_t n_bins, const int32_t* offsets, int64_t n_isects, const int64_t* info, int32_t* order,
+                      hipStream_t s);
 
 // count floats from src to LDS dst (16-B aligned) as float4 runs when src allows
 __device__ __forceinline__ void stage_floats(const float* __restrict__ src, int count, float* dst) {

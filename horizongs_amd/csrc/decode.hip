@@ -1078,7 +1078,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HGSR_COLBWD
     __syncthreads();  // W1 staged
     for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
         const int A0 = t * kDecTile;     // the workgroup's 64 anchors
-        const int a0 = A0 + wave * 16;   // this wave's 16
         float my_ov[3], my_dist;
         x_store(px, sx, d.vd, cam, my_ov, my_dist);
         const int cur_id = px.id;  // lane i: id of anchor i of this wave, -1 past Av

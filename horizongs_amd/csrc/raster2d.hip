@@ -33,10 +33,10 @@ struct Tile2 {
 // in raster3d.hip tile_ctx
 __device__ __forceinline__ Tile2 tile2_ctx(int C, int W, int H, int tw, int th,
                                            const int32_t* __restrict__ offsets, int64_t n_isects,
-                                           const int64_t* __restrict__ info = nullptr) {
+                                           const int64_t* __restrict__ info, const int32_t* __restrict__ order) {
     Tile2 t;
     const int n_tiles = tw * th;
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bid = raster_bin(order);
     t.cam = bid / n_tiles;
     t.tile = bid - t.cam * n_tiles;
     const int ty = t.tile / tw, tx = t.tile - ty * tw;
@@ -264,7 +264,8 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     float* __restrict__ render_normals,
     float* __restrict__ render_distort, float* __restrict__ render_median, int32_t* __restrict__ last_ids,
     int32_t* __restrict__ median_ids, uint64_t* __restrict__ qmask, int64_t qstride, float4* __restrict__ zero_rows,
-    int64_t zero_n4, const int64_t* __restrict__ isect_info, const float* __restrict__ normal_rot) {
+    int64_t zero_n4, const int64_t* __restrict__ isect_info, const float* __restrict__ normal_rot,
+    const int32_t* __restrict__ order) {
     constexpr int NB = kFwd2Batch;
     // one LDS object: every component of record t sits at a compile-time offset from one address;
     // double-buffered and filled by LDS-DMA one batch ahead (no staging VGPRs: 96 -> 72 VGPRs)
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     } sr;
     __shared__ uint8_t s_list[4][NB];
     __shared__ int s_vote[2][4];
-    const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects, isect_info);
+    const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects, isect_info, order);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
@@ -455,7 +456,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
                        const float* __restrict__ v_render_normals, float* __restrict__ acc_rows,
                        unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask,
                        int64_t qstride, const float* __restrict__ normal_rot,
-                       const float* __restrict__ v_depth_extra) {
+                       const float* __restrict__ v_depth_extra, const int32_t* __restrict__ order) {
     constexpr int KV = 15 + D;
     constexpr int NB = kBwd2Batch;
     __shared__ struct {
@@ -466,7 +467,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
     __shared__ int32_t s_last[4];
     __shared__ __attribute__((aligned(16))) float s_tp[4][4 * 16 * 4 * 2];
     __shared__ __attribute__((aligned(16))) float s_pv[4][64 * 8];  // per pixel: vo[4], vn[3], 0
-    const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects);
+    const Tile2 tc = tile2_ctx(C, W, H, tw, th, offsets, n_isects, nullptr, order);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
@@ -832,7 +833,7 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
                                float* render_alphas, float* render_normals, float* render_distort,
                                float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s,
-                               uint64_t* qmask = nullptr, int64_t qstride = 0, float* zero_rows = nullptr,
+                               void* qbuf = nullptr, size_t qbytes = 0, float* zero_rows = nullptr,
                                size_t zero_bytes = 0, const int64_t* isect_info = nullptr,
                                const float* normal_rot = nullptr);
 
@@ -865,17 +866,23 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
                                float* render_alphas, float* render_normals, float* render_distort,
                                float* render_median, int32_t* last_ids, int32_t* median_ids, hipStream_t s,
-                               uint64_t* qmask, int64_t qstride, float* zero_rows, size_t zero_bytes,
+                               void* qbuf, size_t qbytes, float* zero_rows, size_t zero_bytes,
                                const int64_t* isect_info, const float* normal_rot) {
-    const dim3 grid(C * tile_w * tile_h);
+    const int64_t n_bins = (int64_t)C * tile_w * tile_h;
+    const dim3 grid((unsigned)n_bins);
     float4* const z4 = reinterpret_cast<float4*>(zero_rows);
     const int64_t zn4 = (int64_t)(zero_bytes / sizeof(float4));
+    uint64_t* const qmask = qmask_words(qbuf, n_bins);
+    const int64_t qstride = qbuf ? qmask_stride_of(qbytes, n_bins) : 0;
+    int32_t* order = (qbuf && HGSR_TILE_ORDER && n_isects > 0) ? tile_order_of(qbuf) : nullptr;
+    if (order)
+        if (int st = launch_tile_order(n_bins, isect_offsets, n_isects, isect_info, order, s)) return st;
     KernelTimer kt("raster2d_fwd", s);
 #define LAUNCH_F2(DD)                                                                                            \
     hipLaunchKernelGGL(raster2d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,     \
                        backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,           \
                        render_alphas, render_normals, render_distort, render_median, last_ids, median_ids, qmask,   \
-                       qstride, z4, zn4, isect_info, normal_rot)
+                       qstride, z4, zn4, isect_info, normal_rot, order)
     switch (D) {
         case 1: LAUNCH_F2(1); break;
         case 2: LAUNCH_F2(2); break;
@@ -955,7 +962,7 @@ extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, in
                      render_median && last_ids && median_ids,
                  "null pointer");
     HGSR_REQUIRE(n_isects == 0 || (flatten_ids && records), "null pointer");
-    HGSR_REQUIRE(!qmask || qmask_bytes >= (size_t)(4 * qmask_stride(n_isects, (int64_t)C * tile_w * tile_h)) * 8,
+    HGSR_REQUIRE(!qmask || qmask_bytes >= hgsr_raster3d_qmask_bytes(C, tile_w, tile_h, n_isects),
                  "raster2d_fwd_packed: quadrant-mask buffer too small");
     // bwd_ws (nullable): the backward's workspace, whose accumulator rows this launch clears
     const size_t rows_b = (size_t)C * N * kRec2 * sizeof(float);
@@ -964,8 +971,8 @@ extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, in
     return raster2d_fwd_launch(C, D, (const Rec2*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
                                tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
                                render_normals, render_distort, render_median, last_ids, median_ids,
-                               as_stream(stream), (uint64_t*)qmask, qmask_stride_of(qmask_bytes), (float*)bwd_ws,
-                               bwd_ws ? rows_b : 0, isect_info, normal_rot);
+                               as_stream(stream), qmask, qmask_bytes, (float*)bwd_ws, bwd_ws ? rows_b : 0, isect_info,
+                               normal_rot);
 }
 
 extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
@@ -981,7 +988,7 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* render_alphas, const int32_t* last_ids, const float* v_render_colors,
                              const float* v_render_alphas, const float* v_render_normals, float* v_means2d,
                              float* v_rt, const ChanDst& cd, float* v_normals, float* v_densify,
-                             const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream, const uint64_t* qmask = nullptr,
+                             const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream, const void* qbuf = nullptr,
                              size_t qmask_bytes = 0, bool rows_zeroed = false, const float* normal_rot = nullptr,
                              const float* v_depth_extra = nullptr) {
     if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
@@ -1020,16 +1027,19 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         if (int st = pack2(C, N, D, means2d, rt, cs, normals, own, s)) return st;
         rec = own;
     }
-    const dim3 grid(C * tile_w * tile_h);
+    const int64_t n_bins = (int64_t)C * tile_w * tile_h;
+    const dim3 grid((unsigned)n_bins);
     unsigned long long* const pairs = timing_pair_counter("raster2d_bwd");
-    const int64_t qstride = qmask_stride_of(qmask_bytes);
+    const uint64_t* const qmask = qmask_words(qbuf, n_bins);
+    const int64_t qstride = qbuf ? qmask_stride_of(qmask_bytes, n_bins) : 0;
+    const int32_t* const order = (qbuf && HGSR_TILE_ORDER) ? tile_order_of(qbuf) : nullptr;
 #define LAUNCH_B2(DD)                                                                                             \
     {                                                                                                             \
         KernelTimer kt("raster2d_bwd", s);                                                                        \
         hipLaunchKernelGGL((raster2d_bwd_tp_kernel<DD>), grid, dim3(256), 0, s, C, width, height, tile_w, tile_h,  \
                            rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects, flatten_ids,    \
                            render_alphas, last_ids, v_render_colors, v_render_alphas, v_render_normals, rows,      \
-                           pairs, qmask, qstride, normal_rot, v_depth_extra);                                     \
+                           pairs, qmask, qstride, normal_rot, v_depth_extra, order);                              \
     }                                                                                                             \
     hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s,   \
                        C, N, rows, rt, m2, reinterpret_cast<float2*>(v_means2d), v_rt, cd, v_normals,             \
@@ -1079,7 +1089,7 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
     HGSR_REQUIRE(!(expected_depth && !depths), "expected_depth needs depths");
     HGSR_REQUIRE(!depths || v_depths, "null pointer");
     HGSR_REQUIRE(!v_depth_extra || depths, "v_depth_extra needs the depth channel");
-    HGSR_REQUIRE(!qmask || qmask_bytes >= (size_t)(4 * qmask_stride(n_isects, (int64_t)C * tile_w * tile_h)) * 8,
+    HGSR_REQUIRE(!qmask || qmask_bytes >= hgsr_raster3d_qmask_bytes(C, tile_w, tile_h, n_isects),
                  "raster2d_bwd_fused: quadrant-mask buffer too small");
     const int D = Dc + (depths ? 1 : 0);
     const ChanSrc cs{colors, colors_shared ? 0 : (int64_t)N * Dc, Dc, depths, opacities,
@@ -1090,6 +1100,6 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                              expected_depth ? Dc : -1, render_colors, width, height, tile_size, tile_w, tile_h,
                              isect_offsets, n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
                              v_render_alphas, v_render_normals, v_means2d, v_ray_transforms, cd, v_normals,
-                             v_densify, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask, qmask_bytes,
+                             v_densify, fwd_ws, ws, ws_bytes, stream, qmask, qmask_bytes,
                              ws_zeroed != 0, normal_rot, v_depth_extra);
 }

@@ -39,10 +39,10 @@ struct TileCtx {
 // and an overflowed emission (capacity exceeded; the host re-runs it) leaves every tile empty
 __device__ __forceinline__ TileCtx tile_ctx(int C, int W, int H, int tw, int th,
                                             const int32_t* __restrict__ offsets, int64_t n_isects,
-                                            const int64_t* __restrict__ info = nullptr) {
+                                            const int64_t* __restrict__ info, const int32_t* __restrict__ order) {
     TileCtx t;
     const int n_tiles = tw * th;
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bid = raster_bin(order);
     t.cam = bid / n_tiles;
     t.tile = bid - t.cam * n_tiles;
     const int ty = t.tile / tw, tx = t.tile - ty * tw;
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     int bg_ch, int ed_ch, const int32_t* __restrict__ offsets, int64_t n_isects,
     const int32_t* __restrict__ flatten_ids, float* __restrict__ render_colors, float* __restrict__ render_alphas,
     int32_t* __restrict__ last_ids, uint64_t* __restrict__ qmask, int64_t qstride, float4* __restrict__ zero_rows,
-    int64_t zero_n4, const int64_t* __restrict__ isect_info) {
+    int64_t zero_n4, const int64_t* __restrict__ isect_info, const int32_t* __restrict__ order) {
     // slot kFwdBatch is a zero-opacity dummy used to pad the per-wave lists
     __shared__ float4 s_g0[kFwdBatch + 1];
     __shared__ float4 s_g1[kFwdBatch + 1];
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     // keeps the offset, rebased once per batch
     __shared__ uint32_t s_list[4][kFwdBatch + 4];
     __shared__ int s_vote[2][4];
-    const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects, isect_info);
+    const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects, isect_info, order);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;   // centre of this wave's quadrant
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
@@ -320,7 +320,8 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     int64_t n_isects, const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
     const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
     const float* __restrict__ v_render_alphas, float* __restrict__ acc_rows,
-    unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask, int64_t qstride) {
+    unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask, int64_t qstride,
+    const int32_t* __restrict__ order) {
     constexpr int NB = kBwdBatch;
     // double-buffered staging: batch b+1 is loaded while batch b is composited (two
     // barriers per batch); slot NB is a zero-opacity dummy
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     __shared__ int32_t s_last[4];
     // pass-1 -> pass-2 transpose through LDS: [step s][column lane r][pixel m][F, V]
     __shared__ __attribute__((aligned(16))) float s_tp[4][4 * 16 * 4 * 2];
-    const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects);
+    const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects, nullptr, order);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
@@ -752,8 +753,10 @@ static int pack3(int C, int N, int D, const float* means2d, const float* conics,
     return check_launch("raster3d_pack");
 }
 
+// the tiles' dispatch order, then the 4 quadrant-mask arrays (common.h qmask_words)
 extern "C" size_t hgsr_raster3d_qmask_bytes(int C, int tile_w, int tile_h, int64_t n_isects) {
-    return (size_t)(4 * qmask_stride(n_isects, (int64_t)C * tile_w * tile_h)) * sizeof(uint64_t);
+    const int64_t n_bins = (int64_t)C * tile_w * tile_h;
+    return tile_order_bytes(n_bins) + (size_t)(4 * qmask_stride(n_isects, n_bins)) * sizeof(uint64_t);
 }
 
 extern "C" size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D) {
@@ -764,8 +767,8 @@ extern "C" size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D) {
 static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backgrounds, int bg_ch, int ed_ch,
                                int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
-                               float* render_alphas, int32_t* last_ids, hipStream_t s, uint64_t* qmask = nullptr,
-                               int64_t qstride = 0, float* zero_rows = nullptr, size_t zero_bytes = 0,
+                               float* render_alphas, int32_t* last_ids, hipStream_t s, void* qbuf = nullptr,
+                               size_t qbytes = 0, float* zero_rows = nullptr, size_t zero_bytes = 0,
                                const int64_t* isect_info = nullptr);
 
 static int raster3d_fwd_impl(int C, int N, int D, const float* means2d, const float* conics, const ChanSrc& cs,
@@ -789,16 +792,23 @@ static int raster3d_fwd_impl(int C, int N, int D, const float* means2d, const fl
 static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backgrounds, int bg_ch, int ed_ch,
                                int width, int height, int tile_w, int tile_h, const int32_t* isect_offsets,
                                int64_t n_isects, const int32_t* flatten_ids, float* render_colors,
-                               float* render_alphas, int32_t* last_ids, hipStream_t s, uint64_t* qmask,
-                               int64_t qstride, float* zero_rows, size_t zero_bytes, const int64_t* isect_info) {
-    const dim3 grid(C * tile_w * tile_h);
+                               float* render_alphas, int32_t* last_ids, hipStream_t s, void* qbuf,
+                               size_t qbytes, float* zero_rows, size_t zero_bytes, const int64_t* isect_info) {
+    const int64_t n_bins = (int64_t)C * tile_w * tile_h;
+    const dim3 grid((unsigned)n_bins);
     float4* const z4 = reinterpret_cast<float4*>(zero_rows);
     const int64_t zn4 = (int64_t)(zero_bytes / sizeof(float4));
+    uint64_t* const qmask = qmask_words(qbuf, n_bins);
+    const int64_t qstride = qbuf ? qmask_stride_of(qbytes, n_bins) : 0;
+    // heaviest-first tile order, kept in the mask buffer for the backward
+    int32_t* const order = (qbuf && HGSR_TILE_ORDER) ? tile_order_of(qbuf) : nullptr;
+    if (order && n_isects > 0)
+        if (int st = launch_tile_order(n_bins, isect_offsets, n_isects, isect_info, order, s)) return st;
     KernelTimer kt("raster3d_fwd", s);
 #define LAUNCH_F(DD)                                                                                           \
     hipLaunchKernelGGL(raster3d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,    \
                        backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,          \
-                       render_alphas, last_ids, qmask, qstride, z4, zn4, isect_info)
+                       render_alphas, last_ids, qmask, qstride, z4, zn4, isect_info, n_isects > 0 ? order : nullptr)
     switch (D) {
         case 1: LAUNCH_F(1); break;
         case 2: LAUNCH_F(2); break;
@@ -877,8 +887,8 @@ extern "C" int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, in
     // the backward, given the same buffer, derives the same stride)
     return raster3d_fwd_launch(C, D, (const Rec3*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
                                tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
-                               last_ids, as_stream(stream), (uint64_t*)qmask, qmask_stride_of(qmask_bytes),
-                               (float*)bwd_ws, bwd_ws ? rows_b : 0, isect_info);
+                               last_ids, as_stream(stream), qmask, qmask_bytes, (float*)bwd_ws, bwd_ws ? rows_b : 0,
+                               isect_info);
 }
 
 extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
@@ -894,7 +904,7 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* render_alphas, const int32_t* last_ids, const float* v_render_colors,
                              const float* v_render_alphas, float* v_means2d, float* v_conics, const ChanDst& cd,
                              float* v_means2d_abs, const void* fwd_ws, void* ws, size_t ws_bytes,
-                             hgsr_stream_t stream, const uint64_t* qmask = nullptr, size_t qmask_bytes = 0,
+                             hgsr_stream_t stream, const void* qbuf = nullptr, size_t qmask_bytes = 0,
                              bool rows_zeroed = false) {
     if (int st = check_raster(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
@@ -931,9 +941,13 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         if (int st = pack3(C, N, D, means2d, conics, cs, own, s)) return st;
         rec = own;
     }
-    const dim3 grid(C * tile_w * tile_h);
+    const int64_t n_bins = (int64_t)C * tile_w * tile_h;
+    const dim3 grid((unsigned)n_bins);
     unsigned long long* const pairs = timing_pair_counter("raster3d_bwd");
-    const int64_t qstride = qmask_stride_of(qmask_bytes);
+    // the mask buffer of the forward: its quadrant bits and its heaviest-first tile order
+    const uint64_t* const qmask = qmask_words(qbuf, n_bins);
+    const int64_t qstride = qbuf ? qmask_stride_of(qmask_bytes, n_bins) : 0;
+    const int32_t* const order = (qbuf && HGSR_TILE_ORDER) ? tile_order_of(qbuf) : nullptr;
     const bool abs = v_means2d_abs != nullptr;
 #define LAUNCH_B(DD, AA)                                                                                       \
     {                                                                                                          \
@@ -941,7 +955,7 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
                            tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,       \
                            flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, pairs,  \
-                           qmask, qstride);                                                                    \
+                           qmask, qstride, order);                                                             \
     }                                                                                                          \
     hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, \
                        N, rows, rec, conics, reinterpret_cast<float2*>(v_means2d), v_conics, cd,                     \
@@ -1001,6 +1015,6 @@ extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2
     return raster3d_bwd_impl(C, N, D, means2d, conics, cs, backgrounds, Dc, expected_depth ? Dc : -1,
                              render_colors, width, height, tile_size, tile_w, tile_h, isect_offsets, n_isects,
                              flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, v_means2d,
-                             v_conics, cd, v_means2d_abs, fwd_ws, ws, ws_bytes, stream, (const uint64_t*)qmask,
-                             qmask_bytes, ws_zeroed != 0);
+                             v_conics, cd, v_means2d_abs, fwd_ws, ws, ws_bytes, stream, qmask, qmask_bytes,
+                             ws_zeroed != 0);
 }

@@ -276,6 +276,195 @@ class GradientAllReduce:
         self.finish()
 
 
+def _hip_adam(descs, betas, eps, device):
+    """One fused HIP Adam launch over (param, grad, exp_avg, exp_avg_sq, numel, lr, step)
+    segments (csrc/optim.hip, the kernel horizongs_amd.optim.Adam launches)."""
+    import ctypes as ct
+
+    from . import _native as NAT
+    from .optim import _AdamTensor
+    if not descs:
+        return
+    arr = (_AdamTensor * len(descs))(*[_AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
+                                                   lr, step) for p, g, m, v, lr, step in descs])
+    NAT.call("hgsr_adam_step", len(descs), ct.cast(arr, ct.c_void_p), betas[0], betas[1], eps, NAT.stream(device))
+
+
+class ShardedAdamDDP:
+    """DDP over views with the optimizer state and step sharded across ranks (ZeRO stage 1),
+    for the explicit-Gaussian step (bench c2 at N > 1).
+
+    GradientAllReduce all-reduces every gradient and then every rank runs Adam over all of the
+    parameters: 2 (N-1)/N S bytes per GPU on the links, then 28 B per parameter of HBM on every
+    rank.  Here each bucket's gradients are reduce-scattered (each rank receives the sum over
+    ranks of its 1/N shard), each rank runs Adam on its shard only (its exp_avg / exp_avg_sq
+    shards live here, 1/N of the optimizer state), and the updated parameter shards are
+    all-gathered back into every rank's parameters: the same link bytes as the all-reduce
+    ((N-1)/N S each way), Adam's HBM traffic and state memory divided by N, and the all-gather of
+    bucket b overlaps the optimizer step and collectives of the later buckets.
+
+    * Buckets (~bucket_mb MiB) follow the optimizer's param_groups in reverse registration order
+      (the order a backward produces gradients); every parameter of a bucket becomes a view into
+      the bucket's flat parameter buffer (its values copied in), so the all-gather writes the
+      parameters in place.  Bucket data is padded to a multiple of the world size.
+    * A post-accumulate-grad hook copies each gradient, pre-scaled by 1/world, into its bucket
+      and drops it; a complete bucket's reduce-scatter is launched during the backward, buckets in
+      bucket order on every rank.
+    * Every rank must produce a gradient for every parameter in every step (the explicit
+      Gaussians' step always does): a missing one raises instead of desynchronising the
+      collectives.  Densification (new Parameter objects) is not supported under the sharded
+      state and raises; use GradientAllReduce for the anchor model.
+    * Adam: torch's single-tensor order of operations per element (the HIP kernel of
+      optim.Adam), per-parameter learning rates from the groups, one step counter per
+      parameter kept here (state that exists in the optimizer when the buckets are built --
+      exp_avg / exp_avg_sq / step -- is taken over shard by shard).
+    adam_fn(descs, betas, eps, device): the optimizer kernel over segments (default: the HIP
+    launch); tests pass a CPU restatement."""
+
+    def __init__(self, optimizer, bucket_mb: float = 64.0, group=None, adam_fn=None):
+        self.opt = optimizer
+        self.group = group
+        self.cap = max(1, int(bucket_mb * (1 << 20) // 4))
+        self.adam_fn = adam_fn or _hip_adam
+        self._key = None
+        self._hooks = []
+        self.buckets: List[dict] = []
+        self._in_step = False
+
+    def _active(self) -> bool:
+        return dist.is_initialized() and (dist.get_world_size(self.group) > 1 or _FORCE)
+
+    @property
+    def active(self) -> bool:
+        return self._active()
+
+    def _bind(self) -> None:
+        entries = [(p, g) for g in self.opt.param_groups for p in g["params"] if p.requires_grad]
+        key = tuple(id(p) for p, _ in entries) + tuple(p.numel() for p, _ in entries)
+        if key == self._key:
+            return
+        if self._key is not None:
+            raise NotImplementedError("hgsr ShardedAdamDDP: the parameter set changed (densification); the sharded "
+                                      "optimizer state cannot follow it -- use GradientAllReduce")
+        world = dist.get_world_size(self.group)
+        rank = dist.get_rank(self.group)
+        cur, size, groups = [], 0, []
+        for p, g in reversed(entries):
+            if cur and size + p.numel() > self.cap:
+                groups.append(cur)
+                cur, size = [], 0
+            cur.append((p, g))
+            size += p.numel()
+        if cur:
+            groups.append(cur)
+        self.buckets, self._where = [], {}
+        for bi, members in enumerate(groups):
+            n = sum(p.numel() for p, _ in members)
+            L = (n + world - 1) // world
+            dev, dt = members[0][0].device, members[0][0].dtype
+            pflat = torch.zeros(world * L, dtype=dt, device=dev)
+            offs, o = [], 0
+            lo, hi = rank * L, rank * L + L
+            m = torch.zeros(L, dtype=dt, device=dev)
+            v = torch.zeros(L, dtype=dt, device=dev)
+            steps = []
+            for k, (p, g) in enumerate(members):
+                nk = p.numel()
+                with torch.no_grad():
+                    pflat[o:o + nk].copy_(p.detach().reshape(-1))
+                    p.data = pflat[o:o + nk].view_as(p)
+                st = self.opt.state.get(p, {})
+                steps.append(int(float(st["step"])) if "step" in st else 0)
+                a, z = max(o, lo), min(o + nk, hi)
+                if a < z and "exp_avg" in st:  # take the existing state's shard over
+                    m[a - lo:z - lo].copy_(st["exp_avg"].reshape(-1)[a - o:z - o])
+                    v[a - lo:z - lo].copy_(st["exp_avg_sq"].reshape(-1)[a - o:z - o])
+                self.opt.state.pop(p, None)
+                self._where[id(p)] = (bi, k)
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                offs.append(o)
+                o += nk
+            self.buckets.append({"members": members, "offs": offs, "n": n, "L": L, "pflat": pflat,
+                                 "gflat": torch.zeros(world * L, dtype=dt, device=dev),
+                                 "gshard": torch.empty(L, dtype=dt, device=dev), "m": m, "v": v, "steps": steps,
+                                 "ready": [False] * len(members), "work": None, "launched": False})
+        self.rank, self.world = rank, world
+        self._key = key
+
+    def begin(self) -> None:
+        if not self._active():
+            return
+        self._bind()
+        self._next = 0
+        for b in self.buckets:
+            b["ready"] = [False] * len(b["members"])
+            b["work"], b["launched"] = None, False
+        self._in_step = True
+
+    def _on_grad(self, p) -> None:
+        if not self._in_step or p.grad is None:
+            return
+        bi, k = self._where[id(p)]
+        b = self.buckets[bi]
+        if b["launched"] or b["ready"][k]:
+            raise RuntimeError("hgsr ShardedAdamDDP: a second gradient arrived for a parameter in this step; "
+                               "exactly one backward is allowed between begin() and finish()")
+        o, n = b["offs"][k], p.numel()
+        torch.mul(p.grad.reshape(-1), 1.0 / self.world, out=b["gflat"][o:o + n])
+        p.grad = None  # the reduced gradient exists only as this rank's shard
+        b["ready"][k] = True
+        while self._next < len(self.buckets) and all(self.buckets[self._next]["ready"]):
+            self._launch(self.buckets[self._next])
+            self._next += 1
+
+    def _launch(self, b) -> None:
+        if not all(b["ready"]):
+            miss = [tuple(p.shape) for (p, _), r in zip(b["members"], b["ready"]) if not r]
+            raise RuntimeError(f"hgsr ShardedAdamDDP: no gradient this step for parameters {miss}; every rank must "
+                               "produce every gradient (use GradientAllReduce for partial graphs)")
+        b["work"] = dist.reduce_scatter_tensor(b["gshard"], b["gflat"], op=dist.ReduceOp.SUM, group=self.group,
+                                               async_op=True)
+        b["launched"] = True
+
+    def finish(self) -> None:
+        """Launch what the backward left, then per bucket: wait for its reduce-scatter, Adam on
+        this rank's shard, launch the all-gather of the updated shard (which overlaps the later
+        buckets); finally the current stream waits for every all-gather."""
+        if not self._active():
+            self.opt.step()
+            return
+        self._in_step = False
+        while self._next < len(self.buckets):
+            self._launch(self.buckets[self._next])
+            self._next += 1
+        gathers = []
+        lo = self.rank
+        for b in self.buckets:
+            b["work"].wait()
+            L = b["L"]
+            s0, s1 = lo * L, lo * L + L
+            descs = {}
+            for k, ((p, g), o) in enumerate(zip(b["members"], b["offs"])):
+                b["steps"][k] += 1
+                a, z = max(o, s0), min(o + p.numel(), s1)
+                if a >= z:
+                    continue
+                key = (tuple(g["betas"]), float(g["eps"]))
+                descs.setdefault(key, []).append((b["pflat"][a:z], b["gshard"][a - s0:z - s0], b["m"][a - s0:z - s0],
+                                                  b["v"][a - s0:z - s0], float(g["lr"]), b["steps"][k]))
+            for (betas, eps), dl in descs.items():
+                self.adam_fn(dl, betas, eps, b["pflat"].device)
+            gathers.append(dist.all_gather_into_tensor(b["pflat"], b["pflat"][s0:s1], group=self.group,
+                                                       async_op=True))
+        for w in gathers:
+            w.wait()
+
+    def state_shard(self):
+        """This rank's optimizer state: [(bucket, shard range, exp_avg, exp_avg_sq, steps)]."""
+        return [(i, (self.rank * b["L"], self.rank * b["L"] + b["L"]), b["m"], b["v"], list(b["steps"]))
+                for i, b in enumerate(self.buckets)]
+
+
 MAX_FIELDS = ("max_radii2D",)
 
 

@@ -22,7 +22,7 @@ for cfg in ${CONFIGS:-c2}; do
     for v in a b; do
       if [ $v = a ]; then L=$A; E=$ENV_A; else L=$B; E=$ENV_B; fi
       env HGSR_LIB=$L $E timeout -k 10 300 python bench.py --config $cfg --steps ${STEPS:-30} --warmup 5 \
-        --no-cpu-baseline --no-secondary $BENCH_EXTRA > gpurun_out/$TAG/${cfg}_${v}$r.json \
+        --no-cpu-baseline --no-secondary --no-quality $BENCH_EXTRA > gpurun_out/$TAG/${cfg}_${v}$r.json \
         2> gpurun_out/$TAG/${cfg}_${v}$r.err || { tail -20 gpurun_out/$TAG/${cfg}_${v}$r.err; exit 1; }
     done
   done

@@ -6,9 +6,9 @@ set -o pipefail
 O=gpurun_out/r04prof
 rm -rf $O && mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-B3="python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --no-timing"
-B2="python bench.py --gs 2d --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --no-timing"
-B4="python bench.py --config c4 --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --no-timing"
+B3="python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --no-timing --no-quality"
+B2="python bench.py --gs 2d --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --no-timing --no-quality"
+B4="python bench.py --config c4 --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --no-timing --no-quality"
 K="raster3d|raster2d|tile_sort|isect|project|pack|split|adam|loss|normal|rotate"
 L="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS GRBM_GUI_ACTIVE"
 R() { local name=$1; shift; timeout -k 10 300 rocprofv3 "$@" > $O/$name.log 2>&1 || { tail -20 $O/$name.log; return 1; }; echo "$name ok"; }

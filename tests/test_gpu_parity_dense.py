@@ -52,7 +52,7 @@ def _dense_scene(n=20000, W=128, H=96, seed=5, scale_range=(0.03, 0.18), C=1, op
 def test_dense_3dgs_multibatch(mode):
     sc = _dense_scene()
     bg = torch.tensor([[0.1, 0.3, 0.2]])
-    (max_tile, replay, sat), _, _ = run_3dgs(sc, mode, bg)
+    (max_tile, replay, sat), _, _ = run_3dgs(sc, mode, bg, count_pairs=True)
     assert max_tile >= 1024, max_tile          # >= 4 forward batches of 256
     assert replay >= 1024, replay              # >= 8 backward batches of 128
     assert sat >= 0.10, sat                    # exclusive T <= 1e-4 stop exercised
@@ -70,7 +70,8 @@ def test_c2_fullsize_3dgs_vs_oracle():
     every output and gradient vs the oracle (about 1,070 intersections per tile)."""
     sc = c2()
     bg = torch.tensor([[0.2, 0.1, 0.3]])
-    (max_tile, replay, sat), _, _ = run_3dgs(sc, "RGB+ED", bg, seed=2)
+    # count_pairs: bench.py's roofline numerator (the executed-pair counter) pinned at c2
+    (max_tile, replay, sat), _, _ = run_3dgs(sc, "RGB+ED", bg, seed=2, count_pairs=True)
     assert max_tile >= 1024 and replay >= 1024 and sat >= 0.10, (max_tile, replay, sat)
 
 

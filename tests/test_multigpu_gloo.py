@@ -386,3 +386,90 @@ def test_early_gradients_launch_first_and_match():
                     assert g is None
                 else:
                     torch.testing.assert_close(torch.from_numpy(g), r, rtol=1e-6, atol=1e-7)
+
+
+# ---------------------------------------------------------------------------------------
+# the sharded optimizer (ZeRO-1): reduce-scatter -> Adam on each rank's shard -> all-gather
+# ---------------------------------------------------------------------------------------
+def _cpu_adam(descs, betas, eps, device):
+    """CPU restatement of the fused HIP Adam on segments: torch's single-tensor Adam order
+    (lerp, mul + addcmul, sqrt / sqrt(bc2) + eps, addcdiv; torch/optim/adam.py)."""
+    import math
+    b1, b2 = betas
+    for p, g, m, v, lr, step in descs:
+        m.lerp_(g, 1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+        denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+        p.addcdiv_(m, denom, value=-lr / bc1)
+
+
+def _sharded_params():
+    g = torch.Generator().manual_seed(0)
+    return [torch.nn.Parameter(torch.randn(301, 3, generator=g)), torch.nn.Parameter(torch.randn(53, generator=g)),
+            torch.nn.Parameter(torch.randn(7, 2, generator=g))]
+
+
+def _sharded_loss(params, view):
+    a, b, c = params
+    w = torch.linspace(0.5, 1.5, a.numel()).reshape(a.shape) * (view + 1)
+    return (torch.sin(a * w) ** 2).sum() + ((b * (view + 1)) ** 2).sum() + (c ** 3).sum() * (view + 1)
+
+
+def _sharded_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from horizongs_amd.multigpu import ShardedAdamDDP
+        params = _sharded_params()
+        opt = torch.optim.Adam([{"params": [p], "lr": 0.01 * (i + 1)} for i, p in enumerate(params)], eps=1e-15)
+        red = ShardedAdamDDP(opt, bucket_mb=0.0012, adam_fn=_cpu_adam)  # ~300 floats: several buckets
+        for _ in range(3):
+            red.begin()
+            _sharded_loss(params, rank).backward()
+            red.finish()
+        errs = []
+        red.begin()  # a parameter without a gradient on this rank: refused, not a desynchronised collective
+        try:
+            (params[0].sum() + params[1].sum()).backward()
+            red.finish()
+        except RuntimeError as e:
+            errs.append(str(e))
+        q.put((rank, [p.detach().numpy().copy() for p in params], len(red.buckets), errs,
+               sum(int(s[2].numel()) for s in red.state_shard())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_adam_matches_one_rank_two_views():
+    """2 ranks x 1 view with the sharded optimizer == 1 process x 2 views averaged with
+    torch.optim.Adam (reference train.py:274-277 over the batch), parameters identical on
+    both ranks, each rank holding half of the Adam state; a parameter missing its gradient
+    on a rank raises."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    params = _sharded_params()
+    opt = torch.optim.Adam([{"params": [p], "lr": 0.01 * (i + 1)} for i, p in enumerate(params)], eps=1e-15,
+                           foreach=False)
+    for _ in range(3):
+        opt.zero_grad(set_to_none=True)
+        (sum(_sharded_loss(params, v) for v in (0, 1)) / 2).backward()
+        opt.step()
+    (r0, p0, nb, e0, s0), (r1, p1, _, e1, s1) = res
+    assert nb >= 2
+    total = sum(p.numel() for p in params)
+    assert s0 + s1 >= total and max(s0, s1) <= total // 2 + nb  # each rank holds about half of the state
+    for a, b, ref in zip(p0, p1, params):
+        assert (a == b).all()  # the all-gather leaves every rank with the same parameters
+        torch.testing.assert_close(torch.from_numpy(a), ref.detach(), rtol=1e-6, atol=1e-7)
+    assert e0 and e1 and "no gradient this step" in e0[0]
