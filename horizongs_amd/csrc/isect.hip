@@ -25,7 +25,7 @@
 
 namespace hgsr {
 
-constexpr int kLdsBins = 16384;   // <= 64 KiB of LDS per block for the histogram / cursors
+constexpr int kLdsBins = 15360;   // <= 60 KiB of LDS per block for the histogram / cursors (+ the 4-KiB BigQ)
 constexpr int kSortCap = 2048;    // keys sorted entirely in LDS by one 256-lane workgroup
 constexpr int kIsectBatch = 8;    // Gaussians per lane whose loads are issued together (count / emit)
 
@@ -65,6 +65,63 @@ __device__ __forceinline__ int cam_of(int64_t o, int N) {
     return o < N ? 0 : (int)((uint32_t)o / (uint32_t)N);
 }
 
+// Large footprints (close street views put Gaussians hundreds of pixels wide on screen): a lane
+// walking a 30 x 30-tile rectangle alone keeps its whole wave for 900 iterations while the other
+// lanes' rectangles hold a few tiles.  Rectangles above kBigRect tiles are therefore queued in
+// LDS (kBigQ per block; a full queue falls back to the lane) and walked by the whole block after
+// the per-lane pass: key j of the block's queued keys goes to thread j mod 256, its entry found
+// by binary search over the entries' key prefixes.  Count and emit do this identically, so a
+// block's (bin, key count) pairs -- all the emission needs to agree on -- are unchanged.
+#ifndef HGSR_BIGRECT
+#define HGSR_BIGRECT 12
+#endif
+constexpr int kBigRect = HGSR_BIGRECT;
+constexpr int kBigQ = 256;
+struct BigQ {
+    unsigned long long ctr;  // (entries << 32) | keys, one 64-bit LDS atomic per push
+    int o[kBigQ];            // flattened (camera, Gaussian) index
+    int start[kBigQ];        // first key of the entry in the block's queued-key order
+    int x0y0[kBigQ];         // x0 | y0 << 16
+    int wh[kBigQ];           // width | height << 16
+};
+// the dynamic LDS of count / emit: n_bins int counters, then the queue (16-B aligned)
+__host__ __device__ inline size_t isect_lds_bytes(int n_bins) {
+    return (((size_t)n_bins * 4 + 15) & ~(size_t)15) + sizeof(BigQ);
+}
+__device__ __forceinline__ BigQ* bigq_of(int* s, int n_bins) {
+    return reinterpret_cast<BigQ*>(reinterpret_cast<char*>(s) + (((size_t)n_bins * 4 + 15) & ~(size_t)15));
+}
+// queue a rectangle; false when the queue is full (the caller walks it itself)
+__device__ __forceinline__ bool bigq_push(BigQ* q, int o, int x0, int y0, int w, int h) {
+    const unsigned long long old = atomicAdd(&q->ctr, (1ull << 32) | (unsigned long long)(w * h));
+    const int e = (int)(old >> 32);
+    if (e >= kBigQ) return false;  // (the counter keeps counting; entries past kBigQ are ignored)
+    q->o[e] = o;
+    q->start[e] = (int)(old & 0xffffffffu);
+    q->x0y0[e] = x0 | (y0 << 16);
+    q->wh[e] = w | (h << 16);
+    return true;
+}
+// after a barrier: call f(o, x, y) for every tile of every queued rectangle, keys spread evenly
+// over the block's threads
+template <typename F>
+__device__ __forceinline__ void bigq_walk(const BigQ* q, F&& f) {
+    const int n = min((int)(q->ctr >> 32), kBigQ);
+    if (n == 0) return;
+    const int total = q->start[n - 1] + (q->wh[n - 1] & 0xffff) * (q->wh[n - 1] >> 16);
+    for (int j = threadIdx.x; j < total; j += blockDim.x) {
+        int lo = 0, hi = n - 1;  // the last entry starting at or before j
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (q->start[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        const int t = j - q->start[lo], w = q->wh[lo] & 0xffff;
+        const int dy = t / w;
+        f(q->o[lo], (q->x0y0[lo] & 0xffff) + (t - dy * w), (q->x0y0[lo] >> 16) + dy);
+    }
+}
+
 struct IsectGeom {
     int64_t CN;
     int n_tiles, n_bins;
@@ -97,7 +154,9 @@ __global__ __launch_bounds__(256) void isect_count_lds_kernel(
     const int32_t* __restrict__ radii, int tile_size, int tw, int th, int n_tiles, int n_bins,
     int32_t* __restrict__ tiles_per_gauss, int32_t* __restrict__ blockhist) {
     extern __shared__ __attribute__((aligned(16))) int s_hist[];
+    BigQ* const bq = bigq_of(s_hist, n_bins);
     for (int i = threadIdx.x; i < n_bins; i += 256) s_hist[i] = 0;
+    if (threadIdx.x == 0) bq->ctr = 0;
     __syncthreads();
     const int blk = xcd_remap(blockIdx.x, gridDim.x);  // the same block <-> Gaussian range map as the emit
     const int64_t g0 = (int64_t)blk * per_block;
@@ -122,12 +181,16 @@ __global__ __launch_bounds__(256) void isect_count_lds_kernel(
             }
             int x0, y0, x1, y1;
             tile_rect(m[k].x, m[k].y, r[k], tile_size, tw, th, x0, y0, x1, y1);
-            tiles_per_gauss[o] = (y1 - y0) * (x1 - x0);
+            const int area = (y1 - y0) * (x1 - x0);
+            tiles_per_gauss[o] = area;
+            if (area > kBigRect && bigq_push(bq, (int)o, x0, y0, x1 - x0, y1 - y0)) continue;
             const int base = cam_of(o, N) * n_tiles;
             for (int y = y0; y < y1; ++y)
                 for (int x = x0; x < x1; ++x) atomicAdd(&s_hist[base + y * tw + x], 1);
         }
     }
+    __syncthreads();
+    bigq_walk(bq, [&](int o, int x, int y) { atomicAdd(&s_hist[cam_of(o, N) * n_tiles + y * tw + x], 1); });
     __syncthreads();
     int32_t* row = blockhist + (int64_t)blk * n_bins;
     for (int i = threadIdx.x; i < n_bins; i += 256) row[i] = s_hist[i];
@@ -276,6 +339,8 @@ __global__ __launch_bounds__(256) void isect_emit_lds_kernel(
     int phases, int64_t* __restrict__ info, int64_t cap, int64_t mb_cap) {
     extern __shared__ __attribute__((aligned(16))) int s_cur[];
     if (emit_overflow(info, cap, mb_cap)) return;
+    BigQ* const bq = bigq_of(s_cur, n_bins);
+    if (threadIdx.x == 0) bq->ctr = 0;
     // Logical block = XCD-contiguous remap of the dispatch index: the blocks resident on one
     // XCD hold consecutive slices of every bin, so their scattered 8-B key writes to a bin
     // land in adjacent addresses of the same L2 and leave it as whole lines.
@@ -308,6 +373,9 @@ __global__ __launch_bounds__(256) void isect_emit_lds_kernel(
             const int64_t o = ob + 256 * k;
             if (o < g1 && r[k] > 0) {
                 tile_rect(m[k].x, m[k].y, r[k], tile_size, tw, th, rx0[k], ry0[k], rx1[k], ry1[k]);
+                const int w = rx1[k] - rx0[k], h = ry1[k] - ry0[k];
+                // a large rectangle goes to the block's queue (walked by every thread below)
+                if (w * h > kBigRect && bigq_push(bq, (int)o, rx0[k], ry0[k], w, h)) rx0[k] = rx1[k] = 0;
             } else {
                 rx0[k] = ry0[k] = rx1[k] = ry1[k] = 0;
             }
@@ -336,6 +404,11 @@ __global__ __launch_bounds__(256) void isect_emit_lds_kernel(
             }
         }
     }
+    __syncthreads();
+    bigq_walk(bq, [&](int o, int x, int y) {
+        const uint64_t key = ((uint64_t)__float_as_uint(depths[o]) << 32) | (uint32_t)o;
+        keys[atomicAdd(&s_cur[cam_of(o, N) * n_tiles + y * tw + x], 1)] = key;
+    });
 }
 
 __global__ __launch_bounds__(256) void isect_emit_global_kernel(
@@ -961,7 +1034,7 @@ extern "C" int hgsr_isect_count(int C, int N, const float* means2d, const int32_
     if (g.lds) {
         if (g.CN > 0) {
             KernelTimer kt("isect_count", s);
-            hipLaunchKernelGGL(isect_count_lds_kernel, dim3(g.n_blocks), dim3(256), g.n_bins * 4, s, g.CN, N,
+            hipLaunchKernelGGL(isect_count_lds_kernel, dim3(g.n_blocks), dim3(256), isect_lds_bytes(g.n_bins), s, g.CN, N,
                                g.per_block, reinterpret_cast<const float2*>(means2d), radii, tile_size, tile_w,
                                tile_h, g.n_tiles, g.n_bins, tiles_per_gauss, w.blockhist);
             if (int st = check_launch("isect_count")) return st;
@@ -1012,7 +1085,7 @@ extern "C" int hgsr_isect_emit_sorted(int C, int N, const float* means2d, const 
     hipStream_t s = as_stream(stream);
     if (g.lds) {
         KernelTimer kt("isect_emit", s);
-        hipLaunchKernelGGL(isect_emit_lds_kernel, dim3(g.n_blocks), dim3(256), g.n_bins * 4, s, g.CN, N,
+        hipLaunchKernelGGL(isect_emit_lds_kernel, dim3(g.n_blocks), dim3(256), isect_lds_bytes(g.n_bins), s, g.CN, N,
                            g.per_block, reinterpret_cast<const float2*>(means2d), radii, depths, tile_size,
                            tile_w, tile_h, g.n_tiles, g.n_bins, isect_offsets, w.blockhist, w.chunk_pre, keys,
                            emit_phases(tile_h), isect_info, n_isects, max_bin);

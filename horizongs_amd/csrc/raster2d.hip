@@ -660,7 +660,11 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
                 if (t < NB) {
 #pragma unroll
                     for (int q = 0; q < 2; ++q)
+#if HGSR_PROBE_NOATOM2  // (probe build: the sums are formed but never added -- wrong results)
+                        if (koff[q] >= 0 && w4[q] == 1234.5f) atomicAdd(acc_rows + (int64_t)sid * kRec2 + koff[q], w4[q]);
+#else
                         if (koff[q] >= 0 && w4[q] != 0.f) atomicAdd(acc_rows + (int64_t)sid * kRec2 + koff[q], w4[q]);
+#endif
                 }
             };
             // pass 1, one step at a time; a step with a valid pixel is queued -- its (F, V) go to

@@ -211,6 +211,36 @@ def test_isect_sorted_bitexact(C):
     np.testing.assert_array_equal(o2.cpu().numpy(), offs)
 
 
+@pytest.mark.parametrize("n_big", [300, 5000])
+def test_isect_large_footprints_bitexact(n_big):
+    """Close views put Gaussians hundreds of pixels wide on screen: rectangles above kBigRect
+    tiles are walked by the whole block from an LDS queue (csrc/isect.hip BigQ) in count and
+    emit alike, and a block with more than kBigQ of them walks the rest per lane.  Mixed with
+    small footprints, with depth ties; bit-exact against the oracle (n_big = 5000: blocks of
+    2048 Gaussians overflow the 256-entry queue)."""
+    rng = np.random.default_rng(13 + n_big)
+    W, H, n_small = 320, 240, 20000
+    tw, th = (W + 15) // 16, (H + 15) // 16
+    n = n_small + n_big
+    m2 = np.stack([rng.uniform(-40, W + 40, n), rng.uniform(-40, H + 40, n)], 1).astype(np.float32)
+    r = np.concatenate([rng.integers(1, 14, n_small), rng.integers(30, 200, n_big)]).astype(np.int32)
+    perm = rng.permutation(n)
+    m2, r = m2[perm][None], r[perm][None]
+    r[0, ::97] = 0  # culled ones in between
+    d = rng.uniform(0.5, 40.0, n).astype(np.float32)
+    d[::5] = d[1::5][: d[::5].shape[0]]
+    d = d[None]
+    tpg, ids, fl = O.isect_tiles(m2, r, d, 16, tw, th)
+    offs = O.isect_offsets(ids, 1, tw, th)
+    assert (tpg > 12).sum() > min(n_big, 256)
+    gr, gm2, gd = to_dev(torch.from_numpy(r), torch.from_numpy(m2), torch.from_numpy(d))
+    gtpg, gids, gfl, goffs = G._isect_binned(gm2, gr, 16, tw, th, gd)
+    np.testing.assert_array_equal(gtpg.cpu().numpy(), tpg)
+    np.testing.assert_array_equal(goffs.cpu().numpy(), offs)
+    np.testing.assert_array_equal(gids.cpu().numpy(), ids)
+    np.testing.assert_array_equal(gfl.cpu().numpy(), fl)
+
+
 def test_isect_unsorted_bitexact():
     sc = scene(n=3000, seed=8)
     r, m2, d, _ = O.proj3d_fwd(sc.means.numpy(), sc.quats.numpy(), sc.scales.numpy(), sc.viewmats.numpy(),
