@@ -132,6 +132,9 @@ def parse(argv=None):
                     help="skip the secondary config lines (N = 1: c2-anchors, c3, c4, c5; N > 1: c4, c5)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events (rocprof runs)")
     ap.add_argument("--no-quality", action="store_true", help="skip the live PSNR-parity measurement (N = 1)")
+    ap.add_argument("--freeze", action="store_true",
+                    help="diagnostic A/Bs of kernel builds that change the gradients: skip the optimizer step so every "
+                         "build sees the same scene (the line is then not the metric)")
     ap.add_argument("--sh-degree", type=int, default=None, choices=[0, 1, 2, 3],
                     help="SH colours: [N,(d+1)^2,3] ~ N(0, 0.3) (explicit), or an SH colour head (anchors)")
     ap.add_argument("--anchors", type=int, default=None,
@@ -308,7 +311,7 @@ class Workload:
             # train.py:274-277 per bucket: each bucket's Adam launch follows its own all-reduce and
             # overlaps the later buckets' collectives
             self.allreduce.finish(step=self.optimizer.step_params)
-        else:
+        elif not self.args.freeze:
             self.optimizer.step()  # train.py:274-277 (zero_grad(set_to_none) = the grad reset above)
         self.meta = meta
         self.view_log.append((view, meta["flatten_ids"].numel()))
@@ -725,7 +728,8 @@ def main():
     if rank == 0:
         ms = dt / args.steps * 1e3
         line = {
-            "metric": METRIC, "value": round(world * args.steps / dt, 3), "unit": "views/s", "n_gpus": world,
+            "metric": METRIC if not args.freeze else "DIAGNOSTIC (--freeze: no optimizer step) " + METRIC,
+            "value": round(world * args.steps / dt, 3), "unit": "views/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (seeded scenes of SURVEY 8(d); no dataset in the environment)",

@@ -308,9 +308,6 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
 #else
 #define HGSR_BWD_WAVES
 #endif
-#ifndef HGSR_BWD3_ONEBAR
-#define HGSR_BWD3_ONEBAR 0
-#endif
 struct Pass2Lane {
     float pxc, py0c;         // pixel-centre x of this lane's column, y of its first row
     float vo[4][4];          // [m][slot]: upstream colour gradient of pixel m, lane-permuted channels
@@ -468,23 +465,12 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         // (its previous records were last read before the previous barrier)
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
         if (tid < bsz) s_id[cur][tid] = cid;
-#if !HGSR_BWD3_ONEBAR
         if (b + 1 < nb && loader) {
             cid = nid;
             dma_batch(prv, cid);
             nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
-#endif
         lds_barrier();
-#if HGSR_BWD3_ONEBAR
-        // one barrier per batch: every wave has passed the barrier above, i.e. finished batch b-1,
-        // whose buffer the DMA of batch b+1 refills -- no end-of-batch barrier needed
-        if (b + 1 < nb && loader) {
-            cid = nid;
-            dma_batch(prv, cid);
-            nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
-        }
-#endif
         // phase 2: composite batch b, first the per-wave list of its records that reach this
         // quadrant and are not behind every pixel's last contributor (order-preserving)
         const int t0 = max(0, batch_end - wave_final);
@@ -680,9 +666,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                 pass2(packed, F, V);
             }
         }
-#if !HGSR_BWD3_ONEBAR
         lds_barrier();
-#endif
     }
     if (pair_counter && lane == 0 && stepped)  // measurement only: lane-pairs stepped
         atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
