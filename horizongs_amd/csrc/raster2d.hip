@@ -19,7 +19,12 @@ namespace hgsr {
 // raster2d_fwd 0.682 -> 0.633 ms at c3 against 128 (25 KB, 6 waves)
 constexpr int kFwd2Batch = HGSR_FWD2_BATCH;
 constexpr int kBwd2Batch = 64;
-constexpr int kRec2 = 24;  // floats per accumulator row (96 B): 15 + D colour + 2 abs xy <= 21 used
+#ifndef HGSR_REC2
+#define HGSR_REC2 24
+#endif
+// floats per accumulator row (96 B): 15 + D colour + 2 abs xy <= 21 used; HGSR_REC2 = 32 aligns
+// every row to one 128-B line (A/B build)
+constexpr int kRec2 = HGSR_REC2;
 
 struct Tile2 {
     int cam, tile, i, j;
@@ -736,7 +741,7 @@ __global__ __launch_bounds__(256) void split2_kernel(int C, int N, const float* 
     for (int c = 0; c < C; ++c) {
         const int64_t i = (int64_t)c * N + g;
         const float4* r4 = reinterpret_cast<const float4*>(rows + i * kRec2);
-        float r[kRec2];
+        float r[24];
 #pragma unroll
         for (int q = 0; q < (15 + D + 2 + 3) / 4; ++q) {
             const float4 v = r4[q];

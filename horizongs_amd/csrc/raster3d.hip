@@ -24,7 +24,13 @@ namespace hgsr {
 
 constexpr int kFwdBatch = 256;
 constexpr int kBwdBatch = 128;
-constexpr int kRec3 = 12;  // floats per accumulator row (48 B): sigma moments(5) S0(1) color(D<=4) absxy(2)
+#ifndef HGSR_REC3
+#define HGSR_REC3 12
+#endif
+// floats per accumulator row (48 B): sigma moments(5) S0(1) color(D<=4) absxy(2); HGSR_REC3 = 16
+// pads the row to 64 B so no row straddles a cache line (A/B build)
+constexpr int kRec3 = HGSR_REC3;
+constexpr int kRec3Used = 12;
 
 struct TileCtx {
     int cam, tile, i, j;
@@ -653,7 +659,11 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                     v = qsel2 ? c : v;
                     v = qcol ? g[6] : v;
                     if (ABS) v = r16 == 8 ? kLn2 * A0 : r16 == 9 ? kLn2 * A1 : v;
+#if HGSR_PROBE_NOATOM3  // (probe build: the sums are formed but never added -- wrong results)
+                    if (koff >= 0 && t < NB && v == 1234.5f)
+#else
                     if (koff >= 0 && t < NB && v != 0.f)
+#endif
                         atomicAdd(acc_rows + (int64_t)sid * kRec3 + koff, v);
                 }
             };
@@ -688,9 +698,9 @@ __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* 
     for (int c = 0; c < C; ++c) {
         const int64_t i = (int64_t)c * N + g;
         const float4* r4 = reinterpret_cast<const float4*>(rows + i * kRec3);
-        float r[kRec3];
+        float r[kRec3Used];
 #pragma unroll
-        for (int q = 0; q < kRec3 / 4; ++q) {
+        for (int q = 0; q < kRec3Used / 4; ++q) {
             const float4 v = r4[q];
             r[q * 4] = v.x; r[q * 4 + 1] = v.y; r[q * 4 + 2] = v.z; r[q * 4 + 3] = v.w;
         }
