@@ -162,6 +162,27 @@ __device__ __forceinline__ void zero_share(float4* __restrict__ p, int64_t n4) {
     for (int64_t q = a + threadIdx.x; q < z; q += blockDim.x) p[q] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// LDS-DMA of 16 B per lane (global_load_lds_dwordx4): per-lane source, LDS destination = the
+// wave-uniform base + 16 B x lane.  HGSR_ASM_DMA issues it as inline asm, so the compiler's wait
+// insertion does not know an LDS-DMA is outstanding: with the builtin it puts s_waitcnt vmcnt(0)
+// in front of LDS reads it cannot prove disjoint from the destination, which waits for the
+// prefetch itself and for every outstanding gradient atomic of the wave.  Callers order the
+// DMA themselves (s_waitcnt vmcnt(0) and a barrier before the destination is read, and before
+// the workgroup ends).
+#ifndef HGSR_ASM_DMA
+#define HGSR_ASM_DMA 1
+#endif
+__device__ __forceinline__ void lds_dma16(const void* src, void* lds_dst) {
+#if HGSR_ASM_DMA
+    const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_dst);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(base) : "memory", "m0");
+#else
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)lds_dst, 16, 0, 0);
+#endif
+}
+
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }

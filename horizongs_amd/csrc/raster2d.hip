@@ -297,9 +297,7 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
         float4* const dst[6] = {&sr.r0[buf][w0], &sr.r1[buf][w0], &sr.r2[buf][w0],
                                 &sr.col[buf][w0], &sr.r4[buf][w0], &sr.box[buf][w0]};
 #pragma unroll
-        for (int q = 0; q < 6; ++q)
-            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + q),
-                                             (void __attribute__((address_space(3)))*)(dst[q]), 16, 0, 0);
+        for (int q = 0; q < 6; ++q) lds_dma16(r + q, dst[q]);
     };
     int32_t nid = 0;
     if (nb > 0 && loader) {
@@ -549,10 +547,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
     auto dma_batch = [&](int buf, int32_t id) {
         const float4* r = reinterpret_cast<const float4*>(rec + id);
 #pragma unroll
-        for (int q = 0; q < 6; ++q)
-            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + q),
-                                             (void __attribute__((address_space(3)))*)(stage_arr[q] + buf * NB), 16,
-                                             0, 0);
+        for (int q = 0; q < 6; ++q) lds_dma16(r + q, stage_arr[q] + buf * NB);
     };
     if (nb > 0 && loader) {
         cid = flatten_ids[max(end - 1 - tid, tc.start)];

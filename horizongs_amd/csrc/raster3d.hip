@@ -25,10 +25,11 @@ namespace hgsr {
 constexpr int kFwdBatch = 256;
 constexpr int kBwdBatch = 128;
 #ifndef HGSR_REC3
-#define HGSR_REC3 12
+#define HGSR_REC3 16
 #endif
-// floats per accumulator row (48 B): sigma moments(5) S0(1) color(D<=4) absxy(2); HGSR_REC3 = 16
-// pads the row to 64 B so no row straddles a cache line (A/B build)
+// floats per accumulator row: sigma moments(5) S0(1) color(D<=4) absxy(2) = 12 used, padded to
+// 64 B so no row's atomics straddle two cache lines (raster3d_bwd 0.556 -> 0.542 ms at c2,
+// gpurun_out/r05s8/ab_rec; 2DGS's 96-B rows padded to 128 B gained nothing and stay)
 constexpr int kRec3 = HGSR_REC3;
 constexpr int kRec3Used = 12;
 
@@ -424,12 +425,9 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     auto dma_batch = [&](int buf, int32_t id) {
         const float4* r = reinterpret_cast<const float4*>(rec + id);
         const int w0 = tid & ~63;
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r),
-                                         (void __attribute__((address_space(3)))*)(&sr.g0[buf][w0]), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + 1),
-                                         (void __attribute__((address_space(3)))*)(&sr.g1[buf][w0]), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(r + 2),
-                                         (void __attribute__((address_space(3)))*)(&sr.col[buf][w0]), 16, 0, 0);
+        lds_dma16(r, &sr.g0[buf][w0]);
+        lds_dma16(r + 1, &sr.g1[buf][w0]);
+        lds_dma16(r + 2, &sr.col[buf][w0]);
     };
     if (nb > 0 && loader) {
         cid = flatten_ids[max(end - 1 - tid, tc.start)];
@@ -660,11 +658,10 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                     v = qcol ? g[6] : v;
                     if (ABS) v = r16 == 8 ? kLn2 * A0 : r16 == 9 ? kLn2 * A1 : v;
 #if HGSR_PROBE_NOATOM3  // (probe build: the sums are formed but never added -- wrong results)
-                    if (koff >= 0 && t < NB && v == 1234.5f)
+                    if (koff >= 0 && t < NB && v == 1234.5f) atomicAdd(acc_rows + (int64_t)sid * kRec3 + koff, v);
 #else
-                    if (koff >= 0 && t < NB && v != 0.f)
+                    if (koff >= 0 && t < NB && v != 0.f) atomicAdd(acc_rows + (int64_t)sid * kRec3 + koff, v);
 #endif
-                        atomicAdd(acc_rows + (int64_t)sid * kRec3 + koff, v);
                 }
             };
             for (int i = 0; i < n_mine; i += 4) {
