@@ -176,7 +176,9 @@ __device__ __forceinline__ void lds_dma16(const void* src, void* lds_dst) {
 #if HGSR_ASM_DMA
     const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane(
         (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_dst);
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(base) : "memory", "m0");
+    // m0 is a reserved register the compiler does not let a clobber list name; none of the kernels
+    // that call this reads m0 anywhere else (their listings hold no other m0 access)
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(base) : "memory");
 #else
     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                      (void __attribute__((address_space(3)))*)lds_dst, 16, 0, 0);
