@@ -34,7 +34,7 @@ def _launch(gs, ts, W, H, wts):
     means, quats, scales, opac, cols, vm, K = ts
     ps = [t.clone().requires_grad_(True) for t in (means, quats, scales, opac, cols)]
     if gs == "3d":
-        rc, ra, _ = G.rasterization(*ps, vm, K, W, H, render_mode="RGB+ED")
+        rc, ra, _ = G.rasterization(*ps, vm, K, W, H, packed=False, render_mode="RGB+ED")
         outs = [rc, ra]
     else:
         (rc, ra, rn, _nfd, _rd, _rm), _ = G.rasterization_2dgs(*ps, vm, K, W, H, render_mode="RGB+ED")
