@@ -331,6 +331,10 @@ def hbm_kernels(wl, kernels, n_isects):
         "tile_sort": 20 * n_isects, "isect_emit": 8 * n_isects + 16 * N,
         "loss_fwd": 60 * 3 * P, "loss_bwd": 72 * 3 * P, "adam": 28 * n_par,
     }
+    if wl.args.sh_degree:  # rasterization()'s SH colours (csrc/sh.hip): K coefficient triples per Gaussian
+        K = (wl.args.sh_degree + 1) ** 2
+        per["sh_fwd"] = (12 + 12 * K + 4 + 12) * N  # means, coefficients, radii in; colours out
+        per["sh_bwd"] = (12 + 12 * K + 4 + 12 + 12 * K + 12) * N  # + v_colours in; v_coeffs, v_means out
     out = {}
     for k, nbytes in per.items():
         if k in kernels:

@@ -151,6 +151,18 @@ __device__ __forceinline__ void stage_floats(const float* __restrict__ src, int 
     for (int e = done + threadIdx.x; e < count; e += 256) dst[e] = src[e];
 }
 
+// count floats from LDS src (16-B aligned) to dst as float4 runs when dst allows
+__device__ __forceinline__ void unstage_floats(const float* src, int count, float* __restrict__ dst) {
+    int done = 0;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        const int n4 = count >> 2;
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        for (int q = threadIdx.x; q < n4; q += 256) d4[q] = *reinterpret_cast<const float4*>(src + 4 * q);
+        done = n4 << 2;
+    }
+    for (int e = done + threadIdx.x; e < count; e += 256) dst[e] = src[e];
+}
+
 // A grid-wide memset folded into a kernel that is not HBM-bound (the raster forwards clear
 // the backward's accumulator rows): workgroup b of the grid clears its share
 // [b n4 / nwg, (b+1) n4 / nwg) of the n4 float4s.  Called after the kernel's last load, so

@@ -315,16 +315,6 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
 #else
 #define HGSR_BWD_WAVES
 #endif
-// HGSR_PROBE_NOBAR3 (timing probe, wrong results): the batch loop without its two workgroup
-// barriers -- an upper bound on what a barrier-free backward could gain
-#ifndef HGSR_PROBE_NOBAR3
-#define HGSR_PROBE_NOBAR3 0
-#endif
-#if HGSR_PROBE_NOBAR3
-#define HGSR_BWD3_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
-#else
-#define HGSR_BWD3_BARRIER() lds_barrier()
-#endif
 struct Pass2Lane {
     float pxc, py0c;         // pixel-centre x of this lane's column, y of its first row
     float vo[4][4];          // [m][slot]: upstream colour gradient of pixel m, lane-permuted channels
@@ -420,9 +410,6 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         sr.g1[tid >> 1][NB] = z;
         sr.col[tid >> 1][NB] = z;
     }
-#if HGSR_PROBE_NOBAR3
-    for (int i = tid; i < 2 * NB; i += 256) (&s_id[0][0])[i] = 0;
-#endif
     lds_barrier();
     const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
     // Gaussians after the block's last contributor are never reached
@@ -487,7 +474,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
             dma_batch(prv, cid);
             nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
-        HGSR_BWD3_BARRIER();
+        lds_barrier();
         // phase 2: composite batch b, first the per-wave list of its records that reach this
         // quadrant and are not behind every pixel's last contributor (order-preserving)
         const int t0 = max(0, batch_end - wave_final);
@@ -686,7 +673,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                 pass2(packed, F, V);
             }
         }
-        HGSR_BWD3_BARRIER();
+        lds_barrier();
     }
     if (pair_counter && lane == 0 && stepped)  // measurement only: lane-pairs stepped
         atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);

@@ -140,10 +140,15 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int K, int64_t n, const flo
 // colors = spherical_harmonics(dirs, coeffs, masks = radii > 0), clamp_min(colors + 0.5, 0)):
 // no dirs tensor, no elementwise offset / clamp kernels and no clamp mask in the backward,
 // whose v_means (= v_dirs) is written directly.  Lane per Gaussian, cameras in a loop
-// (deterministic sums over cameras for shared coefficients).
+// (deterministic sums over cameras for shared coefficients).  A workgroup's 256 coefficient
+// rows (K x 3 floats each, contiguous in HBM) come in -- and the backward's gradient rows go
+// out -- as contiguous float4 runs through LDS: lane-strided 108-B rows made every load and
+// store instruction touch 64 cache lines.
+constexpr int kShMaxK = 16;  // (degree 3 + 1)^2: at most 48 KB of dynamic LDS per workgroup
+
 template <int DEG>
 __device__ __forceinline__ bool sh_rgb_eval(int K, const float* __restrict__ m, const float* __restrict__ cp,
-                                            const float* __restrict__ c, bool on, float (&u)[3], float& inv,
+                                            const float* c, bool on, float (&u)[3], float& inv,
                                             float (&b)[(DEG + 1) * (DEG + 1)], float (&r)[3]) {
     constexpr int NB = (DEG + 1) * (DEG + 1);
     r[0] = r[1] = r[2] = 0.f;
@@ -167,6 +172,7 @@ __global__ __launch_bounds__(256) void sh_rgb_fwd_kernel(int C, int N, int K, co
                                                          const float* __restrict__ coeffs, int shared,
                                                          const int32_t* __restrict__ radii,
                                                          float* __restrict__ colors) {
+    // (the forward only reads its rows: staging them through LDS measured slower, 83 -> 90 us at c4)
     constexpr int NB = (DEG + 1) * (DEG + 1);
     const int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= N) return;
@@ -188,57 +194,73 @@ __global__ __launch_bounds__(256) void sh_rgb_bwd_kernel(int C, int N, int K, co
                                                          const float* __restrict__ v_colors,
                                                          float* __restrict__ v_coeffs, float* __restrict__ v_means) {
     constexpr int NB = (DEG + 1) * (DEG + 1);
-    const int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= N) return;
+    extern __shared__ __attribute__((aligned(16))) float s_cf[];  // [256][K x 3], sized at launch
+    const int g0 = blockIdx.x * 256, nloc = min(256, N - g0), t = threadIdx.x, g = g0 + t;
+    const int row = K * 3;
+    float* const my = s_cf + t * row;  // this lane's row: coefficients in, their gradient out
     float vm[3] = {0.f, 0.f, 0.f};
     float vsum[NB * 3];  // shared coefficients: summed over cameras
 #pragma unroll
     for (int k = 0; k < NB * 3; ++k) vsum[k] = 0.f;
     for (int c = 0; c < C; ++c) {
-        const int64_t i = (int64_t)c * N + g;
-        const float* cf = coeffs + (shared ? g : i) * K * 3;
-        float u[3], inv, b[NB], r[3];
-        const bool on = sh_rgb_eval<DEG>(K, means + (int64_t)g * 3, campos + c * 3, cf, radii[i] > 0, u, inv, b, r);
-        // clamp_min backward: the gradient passes where colour + 0.5 >= 0
-        float gq[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) gq[q] = (on && r[q] + 0.5f >= 0.0f) ? v_colors[i * 3 + q] : 0.f;
-        if (shared) {
-#pragma unroll
-            for (int k = 0; k < NB; ++k)
-#pragma unroll
-                for (int q = 0; q < 3; ++q) vsum[k * 3 + q] += b[k] * gq[q];
-        } else {
-            float* vc = v_coeffs + i * K * 3;
-#pragma unroll
-            for (int k = 0; k < NB; ++k)
-#pragma unroll
-                for (int q = 0; q < 3; ++q) vc[k * 3 + q] = on ? b[k] * gq[q] : 0.f;
-            for (int k = NB * 3; k < K * 3; ++k) vc[k] = 0.f;
+        const int64_t base = shared ? (int64_t)g0 : (int64_t)c * N + g0;
+        if (c == 0 || !shared) {
+            if (c > 0) __syncthreads();  // the previous camera's gradient rows have left
+            stage_floats(coeffs + base * row, nloc * row, s_cf);
+            __syncthreads();
         }
-        if (DEG < 1 || !on || !v_means) continue;
-        float bx[NB], by[NB], bz[NB];
-        sh_basis_grad<DEG>(u[0], u[1], u[2], bx, by, bz);
-        float gu0 = 0.f, gu1 = 0.f, gu2 = 0.f;
+        if (t < nloc) {
+            const int64_t i = (int64_t)c * N + g;
+            float u[3], inv, b[NB], r[3];
+            const bool on = sh_rgb_eval<DEG>(K, means + (int64_t)g * 3, campos + c * 3, my, radii[i] > 0, u, inv, b, r);
+            // clamp_min backward: the gradient passes where colour + 0.5 >= 0
+            float gq[3];
 #pragma unroll
-        for (int k = 0; k < NB; ++k) {
-            const float vb = cf[k * 3] * gq[0] + cf[k * 3 + 1] * gq[1] + cf[k * 3 + 2] * gq[2];
-            gu0 += vb * bx[k];
-            gu1 += vb * by[k];
-            gu2 += vb * bz[k];
+            for (int q = 0; q < 3; ++q) gq[q] = (on && r[q] + 0.5f >= 0.0f) ? v_colors[i * 3 + q] : 0.f;
+            if (DEG >= 1 && on && v_means) {
+                float bx[NB], by[NB], bz[NB];
+                sh_basis_grad<DEG>(u[0], u[1], u[2], bx, by, bz);
+                float gu0 = 0.f, gu1 = 0.f, gu2 = 0.f;
+#pragma unroll
+                for (int k = 0; k < NB; ++k) {
+                    const float vb = my[k * 3] * gq[0] + my[k * 3 + 1] * gq[1] + my[k * 3 + 2] * gq[2];
+                    gu0 += vb * bx[k];
+                    gu1 += vb * by[k];
+                    gu2 += vb * bz[k];
+                }
+                const float dot = gu0 * u[0] + gu1 * u[1] + gu2 * u[2];
+                vm[0] += (gu0 - dot * u[0]) * inv;
+                vm[1] += (gu1 - dot * u[1]) * inv;
+                vm[2] += (gu2 - dot * u[2]) * inv;
+            }
+            if (shared) {
+#pragma unroll
+                for (int k = 0; k < NB; ++k)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) vsum[k * 3 + q] += b[k] * gq[q];
+            } else {  // the row's coefficients are no longer needed: its gradient replaces them
+#pragma unroll
+                for (int k = 0; k < NB; ++k)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) my[k * 3 + q] = on ? b[k] * gq[q] : 0.f;
+                for (int k = NB * 3; k < row; ++k) my[k] = 0.f;
+            }
         }
-        const float dot = gu0 * u[0] + gu1 * u[1] + gu2 * u[2];
-        vm[0] += (gu0 - dot * u[0]) * inv;
-        vm[1] += (gu1 - dot * u[1]) * inv;
-        vm[2] += (gu2 - dot * u[2]) * inv;
+        if (!shared) {
+            __syncthreads();
+            unstage_floats(s_cf, nloc * row, v_coeffs + base * row);
+        }
     }
     if (shared) {
-        float* vc = v_coeffs + (int64_t)g * K * 3;
+        if (t < nloc) {
 #pragma unroll
-        for (int k = 0; k < NB * 3; ++k) vc[k] = vsum[k];
-        for (int k = NB * 3; k < K * 3; ++k) vc[k] = 0.f;
+            for (int k = 0; k < NB * 3; ++k) my[k] = vsum[k];
+            for (int k = NB * 3; k < row; ++k) my[k] = 0.f;
+        }
+        __syncthreads();
+        unstage_floats(s_cf, nloc * row, v_coeffs + (int64_t)g0 * row);
     }
-    if (v_means)
+    if (v_means && t < nloc)
 #pragma unroll
         for (int q = 0; q < 3; ++q) v_means[(int64_t)g * 3 + q] = vm[q];
 }
@@ -313,12 +335,14 @@ extern "C" int hgsr_sh_rgb_bwd(int degree, int C, int N, int K, const float* mea
     HGSR_REQUIRE(degree >= 0 && degree <= 3, "sh degree %d unsupported (0..3)", degree);
     HGSR_REQUIRE(K >= (degree + 1) * (degree + 1), "K=%d too small for degree %d", K, degree);
     HGSR_REQUIRE(C >= 1 && N >= 0, "bad dims C=%d N=%d", C, N);
+    HGSR_REQUIRE(K <= kShMaxK, "sh_rgb: K=%d coefficients per Gaussian (at most %d)", K, kShMaxK);
     if (N == 0) return HGSR_OK;
     HGSR_REQUIRE(means && campos && coeffs && radii && v_colors && v_coeffs, "null pointer");
     dim3 grid((unsigned)((N + 255) / 256));
     hipStream_t s = as_stream(stream);
     KernelTimer kt("sh_bwd", s);
-#define SH_RGB_B(D) hipLaunchKernelGGL(sh_rgb_bwd_kernel<D>, grid, dim3(256), 0, s, C, N, K, means, campos, coeffs, \
+    const size_t lds = (size_t)256 * K * 3 * sizeof(float);
+#define SH_RGB_B(D) hipLaunchKernelGGL(sh_rgb_bwd_kernel<D>, grid, dim3(256), lds, s, C, N, K, means, campos, coeffs, \
                                        shared, radii, v_colors, v_coeffs, v_means)
     switch (degree) {
         case 0: SH_RGB_B(0); break;

@@ -103,7 +103,8 @@ int hgsr_sh_bwd(int degree, int K, int64_t n, const float* dirs, const float* co
  * masks = radii > 0); colors = clamp_min(colors + 0.5, 0)).  means [N,3], campos [C,3],
  * coeffs [N,K,3] (shared = 1) or [C,N,K,3], radii [C,N] -> colors [C,N,3] (written).
  * The backward writes v_coeffs (summed over cameras when shared) and v_means [N,3]
- * (nullable; overwritten, = the gradient through dirs). */
+ * (nullable; overwritten, = the gradient through dirs).  The backward takes K <= 16
+ * (degree <= 3 coefficient rows, staged through LDS); HGSR_EINVAL otherwise. */
 int hgsr_sh_rgb_fwd(int degree, int C, int N, int K, const float* means, const float* campos,
                     const float* coeffs, int shared, const int32_t* radii, float* colors,
                     hgsr_stream_t stream);
