@@ -522,8 +522,10 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
     const int qi0 = tc.i - (lane >> 3), qj0 = tc.j - (lane & 7);
     const float p2x = (float)(qj0 + cx) + 0.5f, p2y0 = (float)(qi0 + y0) + 0.5f;
     float* const pv = s_pv[wave];
-    *reinterpret_cast<float4*>(pv + lane * 8) = make_float4(vo[0], vo[1], vo[2], vo[3]);
-    *reinterpret_cast<float4*>(pv + lane * 8 + 4) = make_float4(vn[0], vn[1], vn[2], 0.f);
+    // pixel p = lane: colour terms at float 128 (p >> 4) + 4 (p & 15), normal terms 64 further; pass 2
+    // reads 16 distinct pixels p = r + 16 m per 16-B read, conflict-free on CDNA4's banks
+    *reinterpret_cast<float4*>(pv + 128 * (lane >> 4) + 4 * (lane & 15)) = make_float4(vo[0], vo[1], vo[2], vo[3]);
+    *reinterpret_cast<float4*>(pv + 128 * (lane >> 4) + 64 + 4 * (lane & 15)) = make_float4(vn[0], vn[1], vn[2], 0.f);
     // this lane's two output sums after the transpose-reduce: index b3 10 + b2 5 + b1 3 + b0 2 + q
     int koff[2];
 #pragma unroll
@@ -619,9 +621,10 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
                 for (int k = 0; k < 20; ++k) g[k] = 0.f;
 #pragma unroll HGSR_BWD2TP_U2
                 for (int mq = 0; mq < 4; ++mq) {
-                    const float2 fv = *reinterpret_cast<const float2*>(tp + ((slot * 16 + r16) * 4 + mq) * 2);
-                    const float4 po = *reinterpret_cast<const float4*>(pv + ((y0 + 2 * mq) * 8 + cx) * 8);
-                    const float4 pn = *reinterpret_cast<const float4*>(pv + ((y0 + 2 * mq) * 8 + cx) * 8 + 4);
+                    const float2 fv = *reinterpret_cast<const float2*>(tp + 128 * mq + 32 * slot + 2 * r16);
+                    // pixel (y0 + 2 mq) * 8 + cx = r16 + 16 mq
+                    const float4 po = *reinterpret_cast<const float4*>(pv + 128 * mq + 4 * r16);
+                    const float4 pn = *reinterpret_cast<const float4*>(pv + 128 * mq + 64 + 4 * r16);
                     const float pvo[4] = {po.x, po.y, po.z, po.w}, pvn[3] = {pn.x, pn.y, pn.z};
                     const Hit2 h = hit2(r0, r1, r2, p2x, p2y0 + (float)(2 * mq));
                     const float fac = fabsf(fv.x);
@@ -668,7 +671,9 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
                 }
             };
             // pass 1, one step at a time; a step with a valid pixel is queued -- its (F, V) go to
-            // queue slot qn of the wave's transpose buffer ([qn][r][m], lane L = pixel r + 16 m) --
+            // queue slot qn of the wave's transpose buffer (float 128 m + 32 qn + 2 r for lane L =
+            // pixel r + 16 m: conflict-free 8-B writes, and 8-B reads by lane 16 s + r at 128 m + 32 s
+            // + 2 r conflict-free too; the [qn][r][m] layout read 4-way) --
             // and a full queue runs pass 2 (a step nobody composites contributes nothing: skipped)
             int qn = 0;
             uint32_t qpk = 0;
@@ -697,7 +702,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
                 T = Tn;
                 // sigma = min(g3, g2) / 2: the sign bit of F carries the branch (set: low-pass)
                 const float Fq = (h.g3 <= h.g2) ? fac : -fac;
-                *reinterpret_cast<float2*>(tp + ((qn * 16 + r16) * 4 + (lane >> 4)) * 2) = make_float2(Fq, -araw * va2);
+                *reinterpret_cast<float2*>(tp + 128 * (lane >> 4) + 32 * qn + 2 * r16) = make_float2(Fq, -araw * va2);
                 qpk |= (uint32_t)t << (8 * qn);
                 if (++qn == 4) {
                     pass2(qpk);
@@ -707,7 +712,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
             }
             if (qn > 0) {  // the partial queue: empty slots composite nothing
                 for (int q = qn; q < 4; ++q) {
-                    *reinterpret_cast<float2*>(tp + ((q * 16 + r16) * 4 + (lane >> 4)) * 2) = make_float2(0.f, 0.f);
+                    *reinterpret_cast<float2*>(tp + 128 * (lane >> 4) + 32 * q + 2 * r16) = make_float2(0.f, 0.f);
                     qpk |= (uint32_t)NB << (8 * q);
                 }
                 pass2(qpk);

@@ -566,15 +566,20 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                 const float g1x = ABS ? sr.g1[cur][t].x : 0.f;
                 const int sid = s_id[cur][t < NB ? t : 0];
                 {
-                    // lane L = pixel r + 16 m writes (F[s], V[s]) at [s][r][m]; lane 16 s + r reads
-                    // its step's column [s][r][0..3] (a wave's LDS operations complete in order)
+                    // lane L = pixel r + 16 m writes (F[s], V[s]) at float 128 s + 64 (m >> 1) + 4 r +
+                    // 2 (m & 1); lane 16 s + r reads its step's column as two 16-B chunks, pixels
+                    // 0-1 at 128 s + 4 r and 2-3 at + 64 (a wave's LDS operations complete in order).
+                    // On CDNA4's banking the reads are conflict-free and the writes 2-way (the
+                    // [s][r][m] layout read 2-way and wrote 4-way: 72M of raster3d_bwd's 161M LDS
+                    // cycles at c2 were conflict cycles, profiles/r05_pmc_lds.txt)
                     float* tp = s_tp[wave];
                     const int rr = lane & 15, mm = lane >> 4;
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
-                        *reinterpret_cast<float2*>(tp + ((q * 16 + rr) * 4 + mm) * 2) = make_float2(F[q], V[q]);
-                    const float4 lo = *reinterpret_cast<const float4*>(tp + ((slot * 16 + rr) * 4) * 2);
-                    const float4 hi = *reinterpret_cast<const float4*>(tp + ((slot * 16 + rr) * 4) * 2 + 4);
+                        *reinterpret_cast<float2*>(tp + 128 * q + 64 * (mm >> 1) + 4 * rr + 2 * (mm & 1)) =
+                            make_float2(F[q], V[q]);
+                    const float4 lo = *reinterpret_cast<const float4*>(tp + 128 * slot + 4 * rr);
+                    const float4 hi = *reinterpret_cast<const float4*>(tp + 128 * slot + 64 + 4 * rr);
                     F[0] = lo.x; V[0] = lo.y; F[1] = lo.z; V[1] = lo.w;
                     F[2] = hi.x; V[2] = hi.y; F[3] = hi.z; V[3] = hi.w;
                 }
