@@ -32,7 +32,8 @@ int check_launch(const char* what) {
 // independent of the order.
 __global__ __launch_bounds__(1024) void tile_order_kernel(int64_t n_bins, const int32_t* __restrict__ offsets,
                                                           int64_t n_isects, const int64_t* __restrict__ info,
-                                                          int32_t* __restrict__ order) {
+                                                          int32_t* __restrict__ order,
+                                                          const int32_t* __restrict__ tile_end) {
     constexpr int NBK = 1024;
     __shared__ int hist[NBK];
     __shared__ int s_max[16];
@@ -42,7 +43,8 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(int64_t n_bins, const 
     const int64_t n = info ? info[0] : n_isects;
     const bool ovf = info && info[2];
     auto cnt = [&](int64_t b) {
-        const int64_t e = b == n_bins - 1 ? n : offsets[b + 1];
+        int64_t e = b == n_bins - 1 ? n : offsets[b + 1];
+        if (tile_end) e = min(e, (int64_t)tile_end[b]);
         return (int)max((int64_t)0, e - (int64_t)offsets[b]);
     };
     int mx = 0;
@@ -83,9 +85,9 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(int64_t n_bins, const 
 }
 
 int launch_tile_order(int64_t n_bins, const int32_t* offsets, int64_t n_isects, const int64_t* info, int32_t* order,
-                      hipStream_t s) {
+                      hipStream_t s, const int32_t* tile_end) {
     if (n_bins <= 0 || !order) return HGSR_OK;
-    hipLaunchKernelGGL(tile_order_kernel, dim3(8), dim3(1024), 0, s, n_bins, offsets, n_isects, info, order);
+    hipLaunchKernelGGL(tile_order_kernel, dim3(8), dim3(1024), 0, s, n_bins, offsets, n_isects, info, order, tile_end);
     return check_launch("tile_order");
 }
 

@@ -270,7 +270,8 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
     float* __restrict__ render_distort, float* __restrict__ render_median, int32_t* __restrict__ last_ids,
     int32_t* __restrict__ median_ids, uint64_t* __restrict__ qmask, int64_t qstride, float4* __restrict__ zero_rows,
     int64_t zero_n4, const int64_t* __restrict__ isect_info, const float* __restrict__ normal_rot,
-    const int32_t* __restrict__ order) {
+    const int32_t* __restrict__ order,
+    int32_t* __restrict__ tile_end) {
     constexpr int NB = kFwd2Batch;
     // one LDS object: every component of record t sits at a compile-time offset from one address;
     // double-buffered and filled by LDS-DMA one batch ahead (no staging VGPRs: 96 -> 72 VGPRs)
@@ -403,6 +404,16 @@ __global__ __launch_bounds__(256) void raster2d_fwd_kernel(
         render_median[tc.pix] = median;
         last_ids[tc.pix] = cur;
         median_ids[tc.pix] = med_idx;
+    }
+    if (tile_end) {  // the tile's latest contributor + 1 (the backward's tile order), as raster3d_fwd
+        __shared__ int32_t s_end[4];
+        int32_t m = tc.inside ? cur : -1;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) m = max(m, __shfl_xor(m, d));
+        if (lane == 0) s_end[wave] = m;
+        __syncthreads();
+        if (tid == 0)
+            tile_end[(int64_t)tc.cam * (tw * th) + tc.tile] = max(max(s_end[0], s_end[1]), max(s_end[2], s_end[3])) + 1;
     }
     // the backward's accumulator rows, cleared here (after the last load) instead of by a
     // memset on the step's critical path
@@ -891,7 +902,8 @@ static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backg
     hipLaunchKernelGGL(raster2d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,     \
                        backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,           \
                        render_alphas, render_normals, render_distort, render_median, last_ids, median_ids, qmask,   \
-                       qstride, z4, zn4, isect_info, normal_rot, order)
+                       qstride, z4, zn4, isect_info, normal_rot, order,                                        \
+                       (HGSR_BWD_ORDER && order) ? tile_end_of(qbuf, n_bins) : nullptr)
     switch (D) {
         case 1: LAUNCH_F2(1); break;
         case 2: LAUNCH_F2(2); break;
@@ -1042,6 +1054,12 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     const uint64_t* const qmask = qmask_words(qbuf, n_bins);
     const int64_t qstride = qbuf ? qmask_stride_of(qmask_bytes, n_bins) : 0;
     const int32_t* const order = (qbuf && HGSR_TILE_ORDER) ? tile_order_of(qbuf) : nullptr;
+    if (HGSR_BWD_ORDER && order) {  // tiles by the ranges the backward walks (raster3d_bwd_impl)
+        void* const qb = const_cast<void*>(qbuf);
+        if (int st = launch_tile_order(n_bins, isect_offsets, n_isects, nullptr, tile_order_of(qb), s,
+                                       tile_end_of(qb, n_bins)))
+            return st;
+    }
 #define LAUNCH_B2(DD)                                                                                             \
     {                                                                                                             \
         KernelTimer kt("raster2d_bwd", s);                                                                        \

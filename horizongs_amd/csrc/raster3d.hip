@@ -167,13 +167,37 @@ __device__ __forceinline__ void fwd_step(const float4 g0, const float4 g1, const
     cur = ok ? idx : cur;
 }
 
+// HGSR_PROBE_WGTIME (diagnostic build): each workgroup of the raster kernels records its start /
+// end on the 100-MHz real-time counter and its bin (scripts/wg_time.py reads them)
+#ifndef HGSR_PROBE_WGTIME
+#define HGSR_PROBE_WGTIME 0
+#endif
+#if HGSR_PROBE_WGTIME
+constexpr int kWgtSlots = 16384;
+__device__ unsigned long long g_wgtime[2][kWgtSlots][3];
+#define WGT_START const unsigned long long wgt0 = __builtin_amdgcn_s_memrealtime()
+#define WGT_END(k, bin)                                                                   \
+    do {                                                                                  \
+        __syncthreads();                                                                  \
+        if (threadIdx.x == 0 && blockIdx.x < kWgtSlots) {                                 \
+            g_wgtime[k][blockIdx.x][0] = wgt0;                                            \
+            g_wgtime[k][blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();                \
+            g_wgtime[k][blockIdx.x][2] = (unsigned long long)(bin);                       \
+        }                                                                                 \
+    } while (0)
+#else
+#define WGT_START
+#define WGT_END(k, bin)
+#endif
+
 template <int D>
 __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
     int bg_ch, int ed_ch, const int32_t* __restrict__ offsets, int64_t n_isects,
     const int32_t* __restrict__ flatten_ids, float* __restrict__ render_colors, float* __restrict__ render_alphas,
     int32_t* __restrict__ last_ids, uint64_t* __restrict__ qmask, int64_t qstride, float4* __restrict__ zero_rows,
-    int64_t zero_n4, const int64_t* __restrict__ isect_info, const int32_t* __restrict__ order) {
+    int64_t zero_n4, const int64_t* __restrict__ isect_info, const int32_t* __restrict__ order,
+    int32_t* __restrict__ tile_end) {
     // slot kFwdBatch is a zero-opacity dummy used to pad the per-wave lists
     __shared__ float4 s_g0[kFwdBatch + 1];
     __shared__ float4 s_g1[kFwdBatch + 1];
@@ -183,6 +207,7 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     // keeps the offset, rebased once per batch
     __shared__ uint32_t s_list[4][kFwdBatch + 4];
     __shared__ int s_vote[2][4];
+    WGT_START;
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects, isect_info, order);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;   // centre of this wave's quadrant
@@ -278,9 +303,21 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
         }
         last_ids[tc.pix] = cur;
     }
+    if (tile_end) {
+        // the tile's latest contributor + 1 (the backward's trimmed range, for its tile order)
+        int32_t m = tc.inside ? cur : -1;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) m = max(m, __shfl_xor(m, d));
+        __shared__ int32_t s_end[4];
+        if (lane == 0) s_end[wave] = m;
+        __syncthreads();
+        if (tid == 0)
+            tile_end[(int64_t)tc.cam * (tw * th) + tc.tile] = max(max(s_end[0], s_end[1]), max(s_end[2], s_end[3])) + 1;
+    }
     // the backward's accumulator rows, cleared here (after the last load: no wait covers
     // these stores) instead of by a memset on the step's critical path
     zero_share(zero_rows, zero_n4);
+    WGT_END(0, (int64_t)tc.cam * (tw * th) + tc.tile);
 }
 
 __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
@@ -342,6 +379,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     __shared__ int32_t s_last[4];
     // pass-1 -> pass-2 transpose through LDS: [step s][column lane r][pixel m][F, V]
     __shared__ __attribute__((aligned(16))) float s_tp[4][4 * 16 * 4 * 2];
+    WGT_START;
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects, nullptr, order);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
@@ -682,6 +720,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     }
     if (pair_counter && lane == 0 && stepped)  // measurement only: lane-pairs stepped
         atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
+    WGT_END(1, (int64_t)tc.cam * (tw * th) + tc.tile);
 }
 
 // scatter accumulator rows into gsplat's separate gradient tensors (overwrite);
@@ -820,7 +859,8 @@ static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backg
 #define LAUNCH_F(DD)                                                                                           \
     hipLaunchKernelGGL(raster3d_fwd_kernel<DD>, grid, dim3(256), 0, s, C, width, height, tile_w, tile_h, rec,    \
                        backgrounds, bg_ch, ed_ch, isect_offsets, n_isects, flatten_ids, render_colors,          \
-                       render_alphas, last_ids, qmask, qstride, z4, zn4, isect_info, n_isects > 0 ? order : nullptr)
+                       render_alphas, last_ids, qmask, qstride, z4, zn4, isect_info, n_isects > 0 ? order : nullptr, \
+                       (HGSR_BWD_ORDER && order && n_isects > 0) ? tile_end_of(qbuf, n_bins) : nullptr)
     switch (D) {
         case 1: LAUNCH_F(1); break;
         case 2: LAUNCH_F(2); break;
@@ -960,6 +1000,14 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     const uint64_t* const qmask = qmask_words(qbuf, n_bins);
     const int64_t qstride = qbuf ? qmask_stride_of(qmask_bytes, n_bins) : 0;
     const int32_t* const order = (qbuf && HGSR_TILE_ORDER) ? tile_order_of(qbuf) : nullptr;
+    if (HGSR_BWD_ORDER && order) {
+        // re-sort the tiles by the ranges the backward walks (up to each tile's latest contributor,
+        // written by the forward) instead of by their whole bins
+        void* const qb = const_cast<void*>(qbuf);
+        if (int st = launch_tile_order(n_bins, isect_offsets, n_isects, nullptr, tile_order_of(qb), s,
+                                       tile_end_of(qb, n_bins)))
+            return st;
+    }
     const bool abs = v_means2d_abs != nullptr;
 #define LAUNCH_B(DD, AA)                                                                                       \
     {                                                                                                          \
@@ -1030,3 +1078,10 @@ extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2
                              v_conics, cd, v_means2d_abs, fwd_ws, ws, ws_bytes, stream, qmask, qmask_bytes,
                              ws_zeroed != 0);
 }
+
+#if HGSR_PROBE_WGTIME
+// diagnostic build only: [fwd, bwd][workgroup][start, end, bin] of the last launches
+extern "C" int hgsr_debug_wgtime(void* dst) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(hgsr::g_wgtime), sizeof(hgsr::g_wgtime)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -207,8 +207,9 @@ int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * the forward's per-quadrant culling bits of every tile list, which hgsr_raster3d_bwd_fused
  * (given the same buffer) reads instead of repeating the culling tests; caller-allocated,
  * OVERWRITTEN where the forward visits a tile (the backward reads only those bits).  The
- * buffer starts with the tiles' heaviest-first dispatch order, which the forward writes and
- * the backward reuses (placement only: no result depends on it).
+ * buffer starts with the tiles' heaviest-first dispatch order and each tile's latest
+ * contributor + 1, which the forward writes; the backward re-sorts the order by the ranges it
+ * walks (placement only: no result depends on it).
  * bwd_ws (nullable, 16-B aligned, >= hgsr_raster3d_bwd_ws_bytes(C, N, D, 1)): the workspace
  * the backward will get; the forward clears its accumulator rows while it composites (HBM
  * is idle there), so hgsr_raster3d_bwd_fused given it with ws_zeroed = 1 skips its memset.

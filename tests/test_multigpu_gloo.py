@@ -442,12 +442,12 @@ def _sharded_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sharded_adam_matches_one_rank_two_views():
-    """2 ranks x 1 view with the sharded optimizer == 1 process x 2 views averaged with
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_adam_matches_one_rank_two_views(world):
+    """N ranks x 1 view with the sharded optimizer == 1 process x N views averaged with
     torch.optim.Adam (reference train.py:274-277 over the batch), parameters identical on
-    both ranks, each rank holding half of the Adam state; a parameter missing its gradient
-    on a rank raises."""
-    world = 2
+    every rank, each rank holding 1/N of the Adam state (world 3: buckets padded to a multiple
+    of the world size); a parameter missing its gradient on a rank raises."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -463,13 +463,16 @@ def test_sharded_adam_matches_one_rank_two_views():
                            foreach=False)
     for _ in range(3):
         opt.zero_grad(set_to_none=True)
-        (sum(_sharded_loss(params, v) for v in (0, 1)) / 2).backward()
+        (sum(_sharded_loss(params, v) for v in range(world)) / world).backward()
         opt.step()
-    (r0, p0, nb, e0, s0), (r1, p1, _, e1, s1) = res
+    nb = res[0][2]
     assert nb >= 2
     total = sum(p.numel() for p in params)
-    assert s0 + s1 >= total and max(s0, s1) <= total // 2 + nb  # each rank holds about half of the state
-    for a, b, ref in zip(p0, p1, params):
-        assert (a == b).all()  # the all-gather leaves every rank with the same parameters
-        torch.testing.assert_close(torch.from_numpy(a), ref.detach(), rtol=1e-6, atol=1e-7)
-    assert e0 and e1 and "no gradient this step" in e0[0]
+    shards = [r[4] for r in res]
+    assert sum(shards) >= total and max(shards) <= total // world + nb  # each rank holds ~1/N of the state
+    for k, ref in enumerate(params):
+        for r in res[1:]:
+            assert (r[1][k] == res[0][1][k]).all()  # the all-gather leaves every rank with the same parameters
+        torch.testing.assert_close(torch.from_numpy(res[0][1][k]), ref.detach(), rtol=1e-6, atol=1e-7)
+    for r in res:
+        assert r[3] and "no gradient this step" in r[3][0]
