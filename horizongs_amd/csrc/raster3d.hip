@@ -44,14 +44,12 @@ struct TileCtx {
 // info (nullable): the device-resident {n_isects, largest bin, overflow} of a deferred
 // intersection count (hgsr_isect_emit_sorted with isect_info): the last bin ends at info[0],
 // and an overflowed emission (capacity exceeded; the host re-runs it) leaves every tile empty
-// slot (>= 0): this workgroup's dispatch slot when it walks several tiles (else blockIdx's)
 __device__ __forceinline__ TileCtx tile_ctx(int C, int W, int H, int tw, int th,
                                             const int32_t* __restrict__ offsets, int64_t n_isects,
-                                            const int64_t* __restrict__ info, const int32_t* __restrict__ order,
-                                            int slot = -1) {
+                                            const int64_t* __restrict__ info, const int32_t* __restrict__ order) {
     TileCtx t;
     const int n_tiles = tw * th;
-    const int bid = slot < 0 ? raster_bin(order) : (order ? order[slot] : slot);
+    const int bid = raster_bin(order);
     t.cam = bid / n_tiles;
     t.tile = bid - t.cam * n_tiles;
     const int ty = t.tile / tw, tx = t.tile - ty * tw;
@@ -192,9 +190,6 @@ __device__ unsigned long long g_wgtime[2][kWgtSlots][3];
 #define WGT_END(k, bin)
 #endif
 
-#ifndef HGSR_FWD_TPW  // tiles per forward workgroup (A/B)
-#define HGSR_FWD_TPW 1
-#endif
 template <int D>
 __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
@@ -214,13 +209,7 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     __shared__ int s_vote[2][4];
     WGT_START;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    // HGSR_FWD_TPW tiles per workgroup: consecutive slots of this XCD's band of the dispatch order
-    const int64_t n_bins = (int64_t)C * tw * th;
-    const int slot0 = HGSR_FWD_TPW > 1 ? xcd_remap(blockIdx.x, gridDim.x) * HGSR_FWD_TPW : -1;
-    for (int sub = 0; sub < HGSR_FWD_TPW; ++sub) {
-    if (HGSR_FWD_TPW > 1 && slot0 + sub >= n_bins) break;
-    const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects, isect_info, order,
-                                HGSR_FWD_TPW > 1 ? slot0 + sub : -1);
+    const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects, isect_info, order);
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;   // centre of this wave's quadrant
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
     if (tid == 0) {
@@ -325,12 +314,10 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
         if (tid == 0)
             tile_end[(int64_t)tc.cam * (tw * th) + tc.tile] = max(max(s_end[0], s_end[1]), max(s_end[2], s_end[3])) + 1;
     }
-    if (HGSR_FWD_TPW > 1) __syncthreads();  // the next tile refills the workgroup's LDS
-    WGT_END(0, (int64_t)tc.cam * (tw * th) + tc.tile);
-    }
     // the backward's accumulator rows, cleared here (after the last load: no wait covers
     // these stores) instead of by a memset on the step's critical path
     zero_share(zero_rows, zero_n4);
+    WGT_END(0, (int64_t)tc.cam * (tw * th) + tc.tile);
 }
 
 __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
@@ -859,7 +846,7 @@ static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backg
                                float* render_alphas, int32_t* last_ids, hipStream_t s, void* qbuf,
                                size_t qbytes, float* zero_rows, size_t zero_bytes, const int64_t* isect_info) {
     const int64_t n_bins = (int64_t)C * tile_w * tile_h;
-    const dim3 grid((unsigned)((n_bins + HGSR_FWD_TPW - 1) / HGSR_FWD_TPW));
+    const dim3 grid((unsigned)n_bins);
     float4* const z4 = reinterpret_cast<float4*>(zero_rows);
     const int64_t zn4 = (int64_t)(zero_bytes / sizeof(float4));
     uint64_t* const qmask = qmask_words(qbuf, n_bins);
