@@ -318,6 +318,13 @@ class Workload:
         return loss
 
 
+def _newest_profile(pattern):
+    """profiles/<the newest round's file matching pattern> (rNN-prefixed names sort by round)"""
+    import glob
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    return os.path.relpath(hits[-1], ROOT) if hits else None
+
+
 def hbm_kernels(wl, kernels, n_isects):
     """Algorithmic-bytes rate of the HBM-bound kernels of the step (DESIGN.md §4 per-unit
     bytes; unit counts of the last step) against the 8 TB/s HBM3E peak."""
@@ -624,7 +631,7 @@ def roofline(args, res):
                      f"count ({pairs}: every Gaussian up to each tile's latest contributor x 256 pixels, pairs the "
                      f"culling skips included) -- a note, not the roofline; {n_isects:.0f} intersections per view "
                      f"(mean over the timed steps); limiter "
-                     f"counters in profiles/r04_pmc_raster3d_bwd_limiters.txt")}
+                     f"counters in {_newest_profile('*_pmc_raster*limiters*.txt')}")}
     # aggregate compulsory-bytes figure of SURVEY 8(d): B_step = 384 N + 132 I + 52 P
     b_step = 384 * wl.last_colors.shape[0] + 132 * n_isects + 52 * args.width * args.height
     if roof.get("traffic") is not None:

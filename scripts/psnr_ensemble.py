@@ -24,11 +24,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gs", choices=["2d", "3d"], required=True)
     ap.add_argument("--fixture", default=None)
+    ap.add_argument("--prefix", default=None, help="ensemble file prefix (default: the --gs value)")
     a = ap.parse_args()
     path = os.path.join(ROOT, "tests", "golden", f"{a.fixture or 'psnr_scale_' + a.gs}.json")
     fx = json.load(open(path))
     ens = {5: fx["ref_perturbed_1e-6"]}
-    for f in sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "psnr_ensemble", f"{a.gs}_seed*.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "psnr_ensemble", f"{a.prefix or a.gs}_seed*.json"))):
         d = json.load(open(f))
         if d["lr_scale"] != fx["lr_scale"] or d["iterations"] != fx["iterations"] or d["anchors"] != fx["anchors"]:
             continue
