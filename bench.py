@@ -206,7 +206,15 @@ class Workload:
         # the explicit-Gaussian step (c2 / c3 at N > 1): every rank produces every gradient and
         # nothing is densified, so the optimizer is sharded instead (ZeRO-1: reduce-scatter ->
         # Adam on this rank's 1/N -> all-gather, multigpu.ShardedAdamDDP)
-        self.sharded = None if args.anchors else ShardedAdamDDP(self.optimizer, bucket_mb=64.0)
+        self.sharded = None
+        if not args.anchors:
+            # buckets in the order the backward finishes their gradients; the colours' all-gather is
+            # left in flight by finish() and waited for inside the next rasterization() just before
+            # it reads them (gsplat_api parameter-ready hook), under the projection and binning
+            self.sharded = ShardedAdamDDP(self.optimizer, order=[[self.means, self.quats],
+                                                                 [self.log_scales, self.opac_logit], [self.colors]],
+                                          defer=[self.colors])
+            G.register_param_ready_hook(self.sharded.wait_deferred)
 
     def _init_anchors(self, args, seed, dev):
         """SURVEY 8(d) decode-inclusive c2: anchors placed like the c2 Gaussians, feat ~ N(0, 0.1),

@@ -941,6 +941,24 @@ def _with_depth(colors, backgrounds, depths, render_mode, C):
     return colors, backgrounds
 
 
+# Parameter-ready hooks: called by rasterization() / rasterization_2dgs() with the colour
+# tensor right before the first kernel that reads it (after the projection and the intersection
+# count are queued).  multigpu.ShardedAdamDDP(defer=[colours]) registers its wait_deferred here,
+# so the colours' all-gather of the previous step lands under this step's first kernels.
+_READY_HOOKS = []
+
+
+def register_param_ready_hook(fn):
+    """fn(*tensors) before rasterization reads the colours; returns a remover."""
+    _READY_HOOKS.append(fn)
+    return lambda: _READY_HOOKS.remove(fn) if fn in _READY_HOOKS else None
+
+
+def _params_ready(*tensors):
+    for fn in tuple(_READY_HOOKS):
+        fn(*tensors)
+
+
 def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, height, near_plane=0.01,
                   far_plane=1e10, radius_clip=0.0, eps2d=0.3, sh_degree=None, packed=True, tile_size=16,
                   backgrounds=None, render_mode="RGB", sparse_grad=False, absgrad=False,
@@ -956,9 +974,10 @@ def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, 
         means, covars, quats, scales, viewmats, Ks, width, height, eps2d=eps2d, packed=False,
         near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip, sparse_grad=sparse_grad,
         calc_compensations=False, camera_model=camera_model)
-    cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
     tw, th = _tile_grid(width, height, tile_size)
     isect_state = _isect_count(means2d, radii, int(tile_size), tw, th, depths)
+    _params_ready(colors)
+    cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
     with_depth = render_mode in ("RGB+D", "RGB+ED", "D", "ED")
     rgb = render_mode in ("RGB", "RGB+D", "RGB+ED")
     Dc = cols.shape[-1] if rgb else 0
@@ -1095,9 +1114,10 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
     radii, means2d, depths, ray_transforms, normals = fully_fused_projection_2dgs(
         means, quats, scales, viewmats, densifications, Ks, width, height, eps2d=eps2d, packed=False,
         near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip, sparse_grad=sparse_grad)
-    cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
     tw, th = _tile_grid(width, height, tile_size)
     isect_state = _isect_count(means2d, radii, int(tile_size), tw, th, depths)
+    _params_ready(colors)
+    cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
     with_depth = render_mode in ("RGB+D", "RGB+ED", "D", "ED")
     rgb = render_mode in ("RGB", "RGB+D", "RGB+ED")
     Dc = cols.shape[-1] if rgb else 0

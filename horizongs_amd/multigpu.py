@@ -319,13 +319,24 @@ class ShardedAdamDDP:
       parameter kept here (state that exists in the optimizer when the buckets are built --
       exp_avg / exp_avg_sq / step -- is taken over shard by shard).
     adam_fn(descs, betas, eps, device): the optimizer kernel over segments (default: the HIP
-    launch); tests pass a CPU restatement."""
+    launch); tests pass a CPU restatement.
+    order (optional): the buckets themselves, a list of parameter lists in launch order (every
+    trainable parameter exactly once; bucket_mb is then unused) -- e.g. the gradients the
+    backward produces first in the first bucket.
+    defer (optional): parameters whose bucket's all-gather finish() leaves in flight.  The next
+    step may run kernels that do not read them (projection, binning) while it lands;
+    wait_deferred() -- which rasterization() calls through gsplat_api's parameter-ready hooks
+    before it first reads the colours, and begin() calls as a backstop -- makes the current
+    stream wait for it.  A deferred parameter must not be read between finish() and that wait."""
 
-    def __init__(self, optimizer, bucket_mb: float = 64.0, group=None, adam_fn=None):
+    def __init__(self, optimizer, bucket_mb: float = 64.0, group=None, adam_fn=None, order=None, defer=None):
         self.opt = optimizer
         self.group = group
         self.cap = max(1, int(bucket_mb * (1 << 20) // 4))
         self.adam_fn = adam_fn or _hip_adam
+        self.order = [list(b) for b in order] if order is not None else None
+        self.defer_ids = {id(p) for p in (defer or ())}
+        self._deferred = []
         self._key = None
         self._hooks = []
         self.buckets: List[dict] = []
@@ -348,15 +359,27 @@ class ShardedAdamDDP:
                                       "optimizer state cannot follow it -- use GradientAllReduce")
         world = dist.get_world_size(self.group)
         rank = dist.get_rank(self.group)
-        cur, size, groups = [], 0, []
-        for p, g in reversed(entries):
-            if cur and size + p.numel() > self.cap:
+        if self.order is not None:
+            gof = {id(p): g for p, g in entries}
+            listed = [id(p) for b in self.order for p in b]
+            if sorted(listed) != sorted(gof) or len(set(listed)) != len(listed):
+                raise ValueError("hgsr ShardedAdamDDP: order must list every trainable parameter exactly once")
+            groups = [[(p, gof[id(p)]) for p in b] for b in self.order if b]
+        else:
+            cur, size, groups = [], 0, []
+            for p, g in reversed(entries):
+                if cur and size + p.numel() > self.cap:
+                    groups.append(cur)
+                    cur, size = [], 0
+                cur.append((p, g))
+                size += p.numel()
+            if cur:
                 groups.append(cur)
-                cur, size = [], 0
-            cur.append((p, g))
-            size += p.numel()
-        if cur:
-            groups.append(cur)
+        for members in groups:
+            d = [id(p) in self.defer_ids for p, _ in members]
+            if any(d) and not all(d):
+                raise ValueError("hgsr ShardedAdamDDP: a deferred parameter must share its bucket only with "
+                                 "deferred parameters (pass order=)")
         self.buckets, self._where = [], {}
         for bi, members in enumerate(groups):
             n = sum(p.numel() for p, _ in members)
@@ -391,9 +414,16 @@ class ShardedAdamDDP:
         self.rank, self.world = rank, world
         self._key = key
 
+    def wait_deferred(self, *_tensors) -> None:
+        """The current stream waits for the all-gathers finish() left in flight."""
+        works, self._deferred = self._deferred, []
+        for w in works:
+            w.wait()
+
     def begin(self) -> None:
         if not self._active():
             return
+        self.wait_deferred()  # backstop: the next backward / Adam touch the deferred buffers
         self._bind()
         self._next = 0
         for b in self.buckets:
@@ -454,8 +484,8 @@ class ShardedAdamDDP:
                                                   b["v"][a - s0:z - s0], float(g["lr"]), b["steps"][k]))
             for (betas, eps), dl in descs.items():
                 self.adam_fn(dl, betas, eps, b["pflat"].device)
-            gathers.append(dist.all_gather_into_tensor(b["pflat"], b["pflat"][s0:s1], group=self.group,
-                                                       async_op=True))
+            w = dist.all_gather_into_tensor(b["pflat"], b["pflat"][s0:s1], group=self.group, async_op=True)
+            (self._deferred if id(b["members"][0][0]) in self.defer_ids else gathers).append(w)
         for w in gathers:
             w.wait()
 

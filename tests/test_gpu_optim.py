@@ -140,3 +140,44 @@ def test_adam_step_params_subsets_bit_identical():
             assert torch.equal(a, b)
             assert torch.equal(oa.state[a]["exp_avg_sq"], ob.state[b]["exp_avg_sq"])
             assert float(oa.state[a]["step"]) == float(ob.state[b]["step"]) == t + 1
+
+
+def test_sharded_adam_one_rank_rccl_matches_adam(monkeypatch):
+    """multigpu.ShardedAdamDDP through a one-rank RCCL group (the HGSR_DDP_FORCE rehearsal path:
+    hooks, explicit buckets, reduce-scatter, the HIP Adam over shard segments, all-gather, the
+    last bucket's all-gather deferred to the next use) gives the parameters of hgsr's Adam stepping
+    the same gradients, bit for bit."""
+    import socket
+    import torch.distributed as dist
+    from horizongs_amd import multigpu as MG
+    from horizongs_amd.optim import Adam
+    monkeypatch.setattr(MG, "_FORCE", True)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", world_size=1, rank=0)
+    try:
+        g = torch.Generator().manual_seed(3)
+        shapes = [(100_003, 3), (77_001, 4), (5, 3)]
+        base = [torch.randn(sh, generator=g) for sh in shapes]
+        pa = [b.to(DEV).clone().requires_grad_(True) for b in base]
+        pb = [b.to(DEV).clone().requires_grad_(True) for b in base]
+        oa = Adam([{"params": [p], "lr": 1e-3 * (i + 1)} for i, p in enumerate(pa)], lr=0.0, eps=1e-15)
+        ob = Adam([{"params": [p], "lr": 1e-3 * (i + 1)} for i, p in enumerate(pb)], lr=0.0, eps=1e-15)
+        red = MG.ShardedAdamDDP(ob, order=[[pb[0], pb[1]], [pb[2]]], defer=[pb[2]])
+        for _ in range(3):
+            w = [torch.randn(sh, generator=g).to(DEV) for sh in shapes]
+            oa.zero_grad(set_to_none=True)
+            sum((a * c).sin().sum() for a, c in zip(pa, w)).backward()
+            oa.step()
+            red.begin()
+            red.wait_deferred()
+            sum((b * c).sin().sum() for b, c in zip(pb, w)).backward()
+            red.finish()
+        red.wait_deferred()
+        torch.cuda.synchronize()
+        for a, b in zip(pa, pb):
+            assert torch.equal(a.detach(), b.detach())
+    finally:
+        dist.destroy_process_group()

@@ -416,7 +416,7 @@ def _sharded_loss(params, view):
     return (torch.sin(a * w) ** 2).sum() + ((b * (view + 1)) ** 2).sum() + (c ** 3).sum() * (view + 1)
 
 
-def _sharded_worker(rank, world, port, q):
+def _sharded_worker(rank, world, port, q, defer=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -424,11 +424,17 @@ def _sharded_worker(rank, world, port, q):
         from horizongs_amd.multigpu import ShardedAdamDDP
         params = _sharded_params()
         opt = torch.optim.Adam([{"params": [p], "lr": 0.01 * (i + 1)} for i, p in enumerate(params)], eps=1e-15)
-        red = ShardedAdamDDP(opt, bucket_mb=0.0012, adam_fn=_cpu_adam)  # ~300 floats: several buckets
+        if defer:  # explicit buckets, the last one's all-gather left in flight until the next use
+            red = ShardedAdamDDP(opt, adam_fn=_cpu_adam, order=[[params[0]], [params[1]], [params[2]]],
+                                 defer=[params[2]])
+        else:
+            red = ShardedAdamDDP(opt, bucket_mb=0.0012, adam_fn=_cpu_adam)  # ~300 floats: several buckets
         for _ in range(3):
             red.begin()
+            red.wait_deferred()  # what rasterization's parameter-ready hook does before reading them
             _sharded_loss(params, rank).backward()
             red.finish()
+        red.wait_deferred()
         errs = []
         red.begin()  # a parameter without a gradient on this rank: refused, not a desynchronised collective
         try:
@@ -442,8 +448,8 @@ def _sharded_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_adam_matches_one_rank_two_views(world):
+@pytest.mark.parametrize("world,defer", [(2, False), (3, False), (2, True)])
+def test_sharded_adam_matches_one_rank_two_views(world, defer):
     """N ranks x 1 view with the sharded optimizer == 1 process x N views averaged with
     torch.optim.Adam (reference train.py:274-277 over the batch), parameters identical on
     every rank, each rank holding 1/N of the Adam state (world 3: buckets padded to a multiple
@@ -451,7 +457,7 @@ def test_sharded_adam_matches_one_rank_two_views(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q, defer)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
@@ -466,7 +472,7 @@ def test_sharded_adam_matches_one_rank_two_views(world):
         (sum(_sharded_loss(params, v) for v in range(world)) / world).backward()
         opt.step()
     nb = res[0][2]
-    assert nb >= 2
+    assert nb >= 2 and (nb == 3 if defer else True)
     total = sum(p.numel() for p in params)
     shards = [r[4] for r in res]
     assert sum(shards) >= total and max(shards) <= total // world + nb  # each rank holds ~1/N of the state
