@@ -50,10 +50,14 @@ struct AdamArgs {
 
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float w1, float beta2, float w2,
                                           float eps, float step_size, float bc2_sqrt) {
-    m = m + w1 * (g - m);
-    v = v * beta2 + w2 * g * g;
+    // Contraction is spelled out: left to the compiler, the float4 and the scalar path
+    // fused different products, so a tensor's result depended on its alignment (a shard
+    // segment at an odd offset of a flat bucket stepped differently from the whole tensor).
+#pragma clang fp contract(off)
+    m = __builtin_fmaf(w1, g - m, m);
+    v = __builtin_fmaf(v, beta2, (w2 * g) * g);
     const float denom = sqrtf(v) / bc2_sqrt + eps;
-    p = p + (-step_size) * (m / denom);
+    p = __builtin_fmaf(-step_size, m / denom, p);
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {

@@ -142,6 +142,31 @@ def test_adam_step_params_subsets_bit_identical():
             assert float(oa.state[a]["step"]) == float(ob.state[b]["step"]) == t + 1
 
 
+def test_adam_alignment_bit_identical():
+    """A parameter whose storage is not 16-B aligned (the scalar path of csrc/optim.hip, e.g. a
+    shard segment at an odd offset of a flat bucket) steps bit-identically to an aligned copy
+    (the float4 path)."""
+    from horizongs_amd.optim import Adam
+    n = 3 * 4096 + 7
+    g = torch.Generator().manual_seed(4)
+    base = torch.randn(n, generator=g)
+    pa = base.to(DEV).clone().requires_grad_(True)
+    buf = torch.zeros(n + 1, device=DEV)
+    pb = buf[1:]
+    pb.copy_(base.to(DEV))
+    pb.requires_grad_(True)
+    assert pa.data_ptr() % 16 == 0 and pb.data_ptr() % 16 != 0
+    oa, ob = Adam([pa], lr=1e-2, eps=1e-15), Adam([pb], lr=1e-2, eps=1e-15)
+    for _ in range(4):
+        gr = torch.randn(n, generator=g).to(DEV)
+        pa.grad, pb.grad = gr.clone(), gr.clone()
+        oa.step()
+        ob.step()
+    torch.cuda.synchronize()
+    assert torch.equal(pa.detach(), pb.detach()), float((pa - pb).abs().max())
+    assert torch.equal(oa.state[pa]["exp_avg_sq"], ob.state[pb]["exp_avg_sq"])
+
+
 def test_sharded_adam_one_rank_rccl_matches_adam(monkeypatch):
     """multigpu.ShardedAdamDDP through a one-rank RCCL group (the HGSR_DDP_FORCE rehearsal path:
     hooks, explicit buckets, reduce-scatter, the HIP Adam over shard segments, all-gather, the
@@ -177,7 +202,7 @@ def test_sharded_adam_one_rank_rccl_matches_adam(monkeypatch):
             red.finish()
         red.wait_deferred()
         torch.cuda.synchronize()
-        for a, b in zip(pa, pb):
-            assert torch.equal(a.detach(), b.detach())
+        for i, (a, b) in enumerate(zip(pa, pb)):
+            assert torch.equal(a.detach(), b.detach()), (i, float((a - b).abs().max()))
     finally:
         dist.destroy_process_group()
