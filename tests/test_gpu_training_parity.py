@@ -219,7 +219,7 @@ def _hip_fit(p0, cfg, gt, iters, gs, gold):
     return PF.fit(p0, cfg, gt, iters, gs=gs, device="cuda", window=gold["window"], lr_scale=gold["lr_scale"])
 
 
-def _parity_at_scale(gs, fixture=None, statement_only=False):
+def _parity_at_scale(gs, fixture=None, chaotic=False):
     """PSNR parity at scale: 50k anchors at 480x270, 500 iterations of the whole train step
     (reference train.py:150-277; PSNR as utils/image_utils.py:18-20 over the renders of the last
     50 iterations) at the fixture's multiple of the fine-stage learning rates.  The CPU reference
@@ -241,7 +241,12 @@ def _parity_at_scale(gs, fixture=None, statement_only=False):
         (2DGS) a single draw sits outside 0.05 dB of another in a sizeable fraction of runs
         whichever implementation produced it.
     A fixture without a full ensemble (>= MIN_ENSEMBLE members) keeps the single-draw bar
-    (0.05 dB, or twice the reference chain's own 1e-6 floor when that is larger)."""
+    (0.05 dB, or twice the reference chain's own 1e-6 floor when that is larger).
+    chaotic (the unscaled learning rates, where a 1e-6 perturbation moves the reference chain's
+    window PSNR by ~1 dB): a fixed 0.05 dB bar on the means is below what 8 draws of either chain
+    can resolve, so the means must agree within 3 standard errors of the difference computed
+    from the REFERENCE ensemble's sd (3 sd_ref sqrt(1/n_ref + 1/n_hip)); the HIP spread bound
+    is the same as above."""
     import statistics
 
     from scripts import psnr_at_scale as PS
@@ -265,6 +270,10 @@ def _parity_at_scale(gs, fixture=None, statement_only=False):
     full = len(ref_w) >= MIN_ENSEMBLE
     sd_ref, sd_hip = statistics.stdev(ref_w), statistics.stdev(hip_w)
     mean_delta = statistics.mean(hip_w) - statistics.mean(ref_w)
+    mean_bar = 0.05
+    if chaotic:
+        assert full, "the chaotic case needs the reference ensemble"
+        mean_bar = 3.0 * sd_ref * math.sqrt(1.0 / len(ref_w) + 1.0 / len(hip_w))
     if full:
         bar_single = None  # the single pair is recorded, the ensembles are bounded
     else:
@@ -275,10 +284,12 @@ def _parity_at_scale(gs, fixture=None, statement_only=False):
                          "hip_window_db": hip_w,
                          "ref_mean_db": round(statistics.mean(ref_w), 4), "hip_mean_db": round(statistics.mean(hip_w), 4),
                          "mean_delta_db": round(mean_delta, 4), "ref_sd_db": round(sd_ref, 4),
-                         "hip_sd_db": round(sd_hip, 4), "mean_bar_db": 0.05},
+                         "hip_sd_db": round(sd_hip, 4), "mean_bar_db": round(mean_bar, 4),
+                         "mean_bar_kind": ("3 x the standard error of the difference from the reference sd" if chaotic
+                                           else "fixed")},
                final_iterate={"ref_db": ref["final_db"], "hip_db": round(fin_gpu, 4),
                               "delta_db": round(fin_gpu - ref["final_db"], 4)},
-               bar_db=(0.05 if full else round(bar_single, 4)),
+               bar_db=(round(mean_bar, 4) if full else round(bar_single, 4)),
                bar_source=("ensemble means within 0.05 dB; HIP sd <= 3 x the reference sd + 0.01 dB; the unperturbed "
                            "pair recorded" if full else "single reference draw: 2 x its 1e-6 floor (0.05 dB at least)"),
                single_pair_vs_ref_ensemble_sd=(round((win_gpu - ref["window_db"]) / sd_ref, 2) if sd_ref > 0 else None),
@@ -294,10 +305,8 @@ def _parity_at_scale(gs, fixture=None, statement_only=False):
     # identical parameters at the first step: the chains agree before any divergence
     assert abs(loss_gpu[0] - ref["loss_first"]) <= 1e-5 + 1e-4 * abs(ref["loss_first"]), res
     assert ref["window_db"] > gold["psnr_init_db"] + 5.0 and win_gpu > gold["psnr_init_db"] + 5.0  # both fits fit
-    if statement_only:  # a chaotic chain: the delta is recorded against the spreads, not bounded
-        return
     if full:
-        assert abs(mean_delta) <= 0.05, res
+        assert abs(mean_delta) <= mean_bar, res
         assert sd_hip <= 3.0 * sd_ref + 0.01, res
     else:
         assert abs(win_gpu - ref["window_db"]) <= bar_single, res
@@ -322,11 +331,11 @@ def test_psnr_parity_at_scale_3dgs_lr03():
 
 
 @pytest.mark.slow
-def test_psnr_at_scale_3dgs_unscaled_floor_statement():
-    """The unscaled fine-stage learning rates: the 3DGS chain is chaotic (a 1e-6 perturbation
-    of the reference chain's initialisation moves its window PSNR by 0.43 dB, its final iterate
-    by 1.4 dB), so no PSNR bar is meaningful here: the test records the HIP-vs-reference delta
-    and the HIP chain's spread over the same perturbation seeds (gpurun_out/psnr_scale_lr1_3dgs.json)
-    and checks only the first-step loss and that both chains fit.  Parity is bounded by the 0.1x
-    and 0.3x fixtures."""
-    _parity_at_scale("3d", "psnr_scale_3d_lr1", statement_only=True)
+def test_psnr_parity_at_scale_3dgs_unscaled():
+    """The unscaled fine-stage learning rates: the 3DGS chain is chaotic -- the reference
+    chain's 8-member ensemble (unperturbed + 1e-6 perturbations, seeds 5-11) spreads 0.97 dB sd
+    in window PSNR and 2.0 dB in the final iterate -- so the ensemble means are compared at 3
+    standard errors of their difference (from the reference sd: ~1.4 dB with 8 + 8 members) and
+    the HIP spread must stay within 3x the reference's + 0.01 dB (gpurun_out/psnr_scale_lr1_3dgs.json).
+    The tight fixed 0.05 dB bar is on the 0.1x and 0.3x fixtures, where the chains are not chaotic."""
+    _parity_at_scale("3d", "psnr_scale_3d_lr1", chaotic=True)
