@@ -11,7 +11,10 @@ is RCCL over xGMI on MI355X):
    after backward the Gaussian/anchor gradients are averaged with bucketed
    all-reduces (`GradientAllReduce`) and the densification statistics are
    reduced only at densify steps (`reduce_densify_stats`: sums, and max for the
-   max-mode fields, reference scene/basic_model.py:96-144).
+   max-mode fields, reference scene/basic_model.py:96-144).  Every rank then runs the
+   deterministic anchor_growing / prune on the same reduced statistics, so no parameters
+   are broadcast; `assert_replicas_agree` checks that with a digest per rank (SURVEY.md
+   §8(e): "verify with a hash").
 """
 from __future__ import annotations
 
@@ -509,3 +512,44 @@ def reduce_densify_stats(stats: Dict[str, torch.Tensor], max_fields: Sequence[st
         op = dist.ReduceOp.MAX if k in max_fields else dist.ReduceOp.SUM
         dist.all_reduce(stats[k], op=op, group=group)
     return stats
+
+
+def replica_digest(tensors: Iterable[torch.Tensor]) -> torch.Tensor:
+    """Order-sensitive 64-bit digest of the tensors' bytes, computed on their device
+    (int64 arithmetic: bit-exact on every rank that holds identical tensors, whatever the
+    reduction order).  Each tensor contributes its shape and its 32-bit words weighted by
+    position; a one-bit difference anywhere changes the digest."""
+    dev = None
+    acc = None
+    for i, t in enumerate(tensors):
+        t = t.detach().contiguous()
+        dev = t.device
+        w = t.reshape(-1).view(torch.uint8)
+        pad = (-w.numel()) % 4
+        if pad:
+            w = torch.cat([w, w.new_zeros(pad)])
+        x = w.view(torch.int32).to(torch.int64)
+        pos = torch.arange(1, x.numel() + 1, device=dev, dtype=torch.int64)
+        h = ((x + (i + 1) * 0x9E3779B1) * (pos * 0x5BD1E995 + 0x27D4EB2F)).sum()
+        h = h + (i + 1) * 1000003 * x.numel() + sum((k + 7) * int(n) for k, n in enumerate(t.shape))
+        acc = h if acc is None else acc * 31 + h
+    if acc is None:
+        return torch.zeros((), dtype=torch.int64)
+    return acc
+
+
+def assert_replicas_agree(tensors: Sequence[torch.Tensor], group=None, what: str = "parameters") -> int:
+    """Raise on every rank if the ranks' `tensors` differ (digest all-gather; after a densify
+    step every rank must have grown / pruned the same anchors).  Returns the digest."""
+    d = replica_digest(tensors)
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return int(d)
+    dev = d.device if dist.get_backend(group) != "gloo" else torch.device("cpu")
+    mine = d.reshape(1).to(dev)
+    allv = [torch.zeros_like(mine) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(allv, mine, group=group)
+    vals = [int(v) for v in allv]
+    if len(set(vals)) != 1:
+        raise RuntimeError(f"hgsr multigpu: the ranks' {what} differ after a replicated update (digests {vals})")
+    return vals[0]
+

@@ -8,7 +8,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from horizongs_amd.multigpu import GradientAllReduce, chunks_for_rank, reduce_densify_stats
+from horizongs_amd.multigpu import (GradientAllReduce, assert_replicas_agree, chunks_for_rank, reduce_densify_stats,
+                                    replica_digest)
 
 
 def _free_port():
@@ -60,6 +61,51 @@ def test_ddp_gradient_and_stat_reduction():
         assert gc == pytest.approx(2.0)          # (4 + 0) / 2: missing grads count as zeros
         assert acc == [3.0] * 4                  # sum
         assert mx == [1.0, 10.0, 3.0, 0.0]       # max
+
+
+def _digest_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(7)  # the same anchors on every rank
+        anchors = [torch.randn(1001, 3, generator=g), torch.randn(1001, 32, generator=g), torch.randn(13, generator=g)]
+        same = assert_replicas_agree(anchors)
+        bad = [t.clone() for t in anchors]
+        if rank == 1:  # one bit of one value on one rank
+            bad[1].view(torch.int32)[500, 7] ^= 1
+        try:
+            assert_replicas_agree(bad, what="anchors")
+            raised = False
+        except RuntimeError as e:
+            raised = "anchors" in str(e)
+        q.put((rank, same, raised))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_replicas_agree_digest():
+    """After a densify step every rank runs anchor_growing / prune on the same reduced
+    statistics: the digest check passes for identical replicas and raises on
+    every rank when one bit differs on one rank."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_digest_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == res[1][1]
+    assert all(r[2] for r in res)
+    # order- and shape-sensitive
+    a, b = torch.arange(12.0), torch.arange(12.0).flip(0)
+    assert int(replica_digest([a])) != int(replica_digest([b]))
+    assert int(replica_digest([a.reshape(3, 4)])) != int(replica_digest([a.reshape(4, 3)]))
+    assert int(replica_digest([a, b])) != int(replica_digest([b, a]))
 
 
 def test_chunks_dealt_once():
