@@ -206,3 +206,15 @@ def test_sharded_adam_one_rank_rccl_matches_adam(monkeypatch):
             assert torch.equal(a.detach(), b.detach()), (i, float((a - b).abs().max()))
     finally:
         dist.destroy_process_group()
+
+
+def test_replica_digest_device_independent():
+    """multigpu.replica_digest (the post-densification replica check) gives the same value for
+    the same bytes on the device and on the host, and changes with one flipped bit."""
+    from horizongs_amd.multigpu import replica_digest
+    g = torch.Generator().manual_seed(11)
+    host = [torch.randn(50_001, 32, generator=g), torch.randn(7, generator=g), torch.randint(0, 9, (333,), generator=g)]
+    dev = [t.to(DEV) for t in host]
+    assert int(replica_digest(host)) == int(replica_digest(dev))
+    dev[0].view(torch.int32)[25_000, 3] ^= 1
+    assert int(replica_digest(host)) != int(replica_digest(dev))
