@@ -117,7 +117,8 @@ CONFIGS = {
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # 32 = two cycles of the 16-view camera set: every view weighs the same in the mean
+    ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
                     help="workload of the headline line (default c2; the flags below override it)")
@@ -707,7 +708,8 @@ def secondary(args, rank, world, dev):
     returns the lines), measured after the headline workload is freed."""
     out = []
     for name in secondary_names(args, world):
-        a = parse(["--config", name, "--steps", str(min(args.steps, 10)), "--warmup", str(min(args.warmup, 3)),
+        # 16 timed steps = one full cycle of the camera set (10 covered views 3-12 only: a biased mean)
+        a = parse(["--config", name, "--steps", str(min(args.steps, 16)), "--warmup", str(min(args.warmup, 3)),
                    "--width", str(args.width), "--height", str(args.height)] + (["--no-timing"] if args.no_timing else []))
         a = resolve(a, world)
         r = measure(a, rank, world, dev)
