@@ -21,10 +21,13 @@ Multi-GPU: one process per GPU.  `--gpus N` with no WORLD_SIZE in the environmen
 N ranks itself (a torch.distributed.run child process, before this process touches the
 GPU); under torchrun it is one rank.  At N > 1 the headline c2 line trains ONE scene
 data-parallel over views (each rank renders its own camera; the Gaussian gradients are
-averaged with bucketed RCCL all-reduces launched from gradient hooks while the backward
-runs, multigpu.GradientAllReduce), and the secondary lines are c4 (per chunk: each rank
-trains its own chunk, no collectives -- reference preprocess/generate_chunks_config.py,
-merge.py) and c5 (DDP over views).  At N = 1 the DDP modes are the single-GPU step.
+reduce-scattered in buckets launched from gradient hooks while the backward runs, each rank
+steps Adam on its shard and the parameters are all-gathered, the colours' all-gather left in
+flight until the next rasterization reads them: multigpu.ShardedAdamDDP), and the secondary
+lines are c2-chunks (the same workload under the per-chunk mapping: each rank trains its own
+scene, no collectives), c4 (per chunk -- reference preprocess/generate_chunks_config.py,
+merge.py) and c5 (DDP over views, bucketed all-reduce: multigpu.GradientAllReduce).  At N = 1
+the DDP modes are the single-GPU step.
 
 Prints ONE JSON line (rank 0) with the metric, a roofline object for the dominant
 kernel (HIP-event timed live over the timed region), a CPU baseline (the C oracle on all
@@ -105,6 +108,9 @@ CONFIGS = {
                        anchors=500_000, sh_degree=None, view_dim=3, mode=None),
     "c3": dict(label="configs[2] Block_small fine: 2DGS surfels, depth + normal outputs, 1080p", gs="2d", anchors=0,
                sh_degree=None, mode=None),
+    "c2-chunks": dict(label=("c2 under the per-chunk mapping (north_star's first way: each rank trains its own "
+                             "2M-Gaussian chunk, seed = rank, no collectives); the headline c2 line at N > 1 is DDP "
+                             "over views"), gs="3d", anchors=0, sh_degree=None, mode="chunk"),
     "c4": dict(label=("configs[3] MatrixCity Block_A per-chunk fine: 500k-anchor SH2 chunk (view_dim 0, 10 offsets, "
                       "colour head [32,270]), one chunk per GPU, no collectives"), gs="3d", anchors=500_000,
                sh_degree=2, view_dim=0, mode="chunk"),
@@ -130,7 +136,7 @@ def parse(argv=None):
                     help="auto: the config's own mapping (c4 per chunk, c5 DDP; c2 / c3 DDP over views at N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the secondary config lines (N = 1: c2-anchors, c3, c4, c5; N > 1: c4, c5)")
+                    help="skip the secondary config lines (N = 1: c2-fixed, c2-anchors, c3, c4, c5; N > 1: c2-chunks, c4, c5)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events (rocprof runs)")
     ap.add_argument("--no-quality", action="store_true", help="skip the live PSNR-parity measurement (N = 1)")
     ap.add_argument("--freeze", action="store_true",
@@ -699,7 +705,7 @@ def parallelism(args, world):
 
 
 def secondary_names(args, world):
-    names = ["c4", "c5"] if world > 1 else ["c2-fixed", "c2-anchors", "c3", "c4", "c5"]
+    names = ["c2-chunks", "c4", "c5"] if world > 1 else ["c2-fixed", "c2-anchors", "c3", "c4", "c5"]
     return [n for n in names if n != args.config]
 
 

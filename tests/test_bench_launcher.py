@@ -88,7 +88,10 @@ def test_secondary_lines_per_world(bench):
     a = bench.resolve(bench.parse([]), 1)
     assert bench.secondary_names(a, 1) == ["c2-fixed", "c2-anchors", "c3", "c4", "c5"]
     assert a.cameras == 16 and bench.resolve(bench.parse(["--config", "c2-fixed"]), 1).cameras == 1
-    assert bench.secondary_names(bench.resolve(bench.parse([]), 8), 8) == ["c4", "c5"]
+    assert bench.secondary_names(bench.resolve(bench.parse([]), 8), 8) == ["c2-chunks", "c4", "c5"]
+    # c2 at N > 1: the headline is DDP over views, the per-chunk mapping of the same workload a secondary
+    assert bench.resolve(bench.parse([]), 8).mode == "ddp"
+    assert bench.resolve(bench.parse(["--config", "c2-chunks"]), 8).mode == "chunk"
     assert "c4" not in bench.secondary_names(bench.resolve(bench.parse(["--config", "c4"]), 2), 2)
 
 
