@@ -215,11 +215,13 @@ class Workload:
         # Adam on this rank's 1/N -> all-gather, multigpu.ShardedAdamDDP)
         self.sharded = None
         if not args.anchors:
-            # buckets in the order the backward finishes their gradients; the colours' all-gather is
-            # left in flight by finish() and waited for inside the next rasterization() just before
+            # buckets in the order the backward finishes their gradients: the colours' (the raster
+            # backward's) reduce-scatter runs under the projection and activation backwards, the
+            # means / quats' under the activation backward.  The colours' all-gather is left in flight
+            # by finish() (stepped last) and waited for inside the next rasterization() just before
             # it reads them (gsplat_api parameter-ready hook), under the projection and binning
-            self.sharded = ShardedAdamDDP(self.optimizer, order=[[self.means, self.quats],
-                                                                 [self.log_scales, self.opac_logit], [self.colors]],
+            self.sharded = ShardedAdamDDP(self.optimizer, order=[[self.colors], [self.means, self.quats],
+                                                                 [self.log_scales, self.opac_logit]],
                                           defer=[self.colors])
             G.register_param_ready_hook(self.sharded.wait_deferred)
 

@@ -462,7 +462,11 @@ class ShardedAdamDDP:
     def finish(self) -> None:
         """Launch what the backward left, then per bucket: wait for its reduce-scatter, Adam on
         this rank's shard, launch the all-gather of the updated shard (which overlaps the later
-        buckets); finally the current stream waits for every all-gather."""
+        buckets); finally the current stream waits for every all-gather but the deferred ones.
+        The deferred buckets are stepped and gathered last, whatever their place in `order`: the
+        collectives of one group run in issue order, so an all-gather left in flight must not sit
+        in front of one that is waited for (a deferred bucket may still come first in `order`, so
+        that its reduce-scatter starts while the backward is still running)."""
         if not self._active():
             self.opt.step()
             return
@@ -472,7 +476,8 @@ class ShardedAdamDDP:
             self._next += 1
         gathers = []
         lo = self.rank
-        for b in self.buckets:
+        deferred = [id(b["members"][0][0]) in self.defer_ids for b in self.buckets]
+        for b in [b for b, d in zip(self.buckets, deferred) if not d] + [b for b, d in zip(self.buckets, deferred) if d]:
             b["work"].wait()
             L = b["L"]
             s0, s1 = lo * L, lo * L + L

@@ -190,7 +190,7 @@ def test_sharded_adam_one_rank_rccl_matches_adam(monkeypatch):
         pb = [b.to(DEV).clone().requires_grad_(True) for b in base]
         oa = Adam([{"params": [p], "lr": 1e-3 * (i + 1)} for i, p in enumerate(pa)], lr=0.0, eps=1e-15)
         ob = Adam([{"params": [p], "lr": 1e-3 * (i + 1)} for i, p in enumerate(pb)], lr=0.0, eps=1e-15)
-        red = MG.ShardedAdamDDP(ob, order=[[pb[0], pb[1]], [pb[2]]], defer=[pb[2]])
+        red = MG.ShardedAdamDDP(ob, order=[[pb[2]], [pb[0], pb[1]]], defer=[pb[2]])  # deferred first: stepped last
         for _ in range(3):
             w = [torch.randn(sh, generator=g).to(DEV) for sh in shapes]
             oa.zero_grad(set_to_none=True)

@@ -470,7 +470,11 @@ def _sharded_worker(rank, world, port, q, defer=False):
         from horizongs_amd.multigpu import ShardedAdamDDP
         params = _sharded_params()
         opt = torch.optim.Adam([{"params": [p], "lr": 0.01 * (i + 1)} for i, p in enumerate(params)], eps=1e-15)
-        if defer:  # explicit buckets, the last one's all-gather left in flight until the next use
+        if defer == "first":  # the deferred bucket first in order (its reduce-scatter launches first):
+            # finish() still steps and gathers it last
+            red = ShardedAdamDDP(opt, adam_fn=_cpu_adam, order=[[params[2]], [params[0]], [params[1]]],
+                                 defer=[params[2]])
+        elif defer:  # explicit buckets, the last one's all-gather left in flight until the next use
             red = ShardedAdamDDP(opt, adam_fn=_cpu_adam, order=[[params[0]], [params[1]], [params[2]]],
                                  defer=[params[2]])
         else:
@@ -494,7 +498,7 @@ def _sharded_worker(rank, world, port, q, defer=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,defer", [(2, False), (3, False), (2, True)])
+@pytest.mark.parametrize("world,defer", [(2, False), (3, False), (2, True), (2, "first")])
 def test_sharded_adam_matches_one_rank_two_views(world, defer):
     """N ranks x 1 view with the sharded optimizer == 1 process x N views averaged with
     torch.optim.Adam (reference train.py:274-277 over the batch), parameters identical on
