@@ -220,6 +220,10 @@ class Workload:
             # means / quats' under the activation backward.  The colours' all-gather is left in flight
             # by finish() (stepped last) and waited for inside the next rasterization() just before
             # it reads them (gsplat_api parameter-ready hook), under the projection and binning
+            # (one bucket per parameter would spare the gradients' copy into the flat buffers, but
+            # each collective's fixed cost is larger: c2 1.716 -> 1.821 ms in the one-GPU rehearsal
+            # with five buckets, gpurun_out/r05s32; the colours' one-parameter bucket reduces
+            # autograd's tensor in place)
             self.sharded = ShardedAdamDDP(self.optimizer, order=[[self.colors], [self.means, self.quats],
                                                                  [self.log_scales, self.opac_logit]],
                                           defer=[self.colors])

@@ -410,8 +410,13 @@ class ShardedAdamDDP:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
                 offs.append(o)
                 o += nk
+            # a one-parameter bucket whose size divides by the world reduce-scatters the gradient
+            # tensor autograd produced, in place of a scaled copy into gflat (the 1/N goes onto
+            # this rank's shard after the reduction: exact for power-of-two worlds)
+            direct = len(members) == 1 and n == world * L
             self.buckets.append({"members": members, "offs": offs, "n": n, "L": L, "pflat": pflat,
-                                 "gflat": torch.zeros(world * L, dtype=dt, device=dev),
+                                 "direct": direct, "gsrc": None,
+                                 "gflat": None if direct else torch.zeros(world * L, dtype=dt, device=dev),
                                  "gshard": torch.empty(L, dtype=dt, device=dev), "m": m, "v": v, "steps": steps,
                                  "ready": [False] * len(members), "work": None, "launched": False})
         self.rank, self.world = rank, world
@@ -431,7 +436,7 @@ class ShardedAdamDDP:
         self._next = 0
         for b in self.buckets:
             b["ready"] = [False] * len(b["members"])
-            b["work"], b["launched"] = None, False
+            b["work"], b["launched"], b["gsrc"] = None, False, None
         self._in_step = True
 
     def _on_grad(self, p) -> None:
@@ -443,7 +448,14 @@ class ShardedAdamDDP:
             raise RuntimeError("hgsr ShardedAdamDDP: a second gradient arrived for a parameter in this step; "
                                "exactly one backward is allowed between begin() and finish()")
         o, n = b["offs"][k], p.numel()
-        torch.mul(p.grad.reshape(-1), 1.0 / self.world, out=b["gflat"][o:o + n])
+        g = p.grad
+        if b["direct"] and g.is_contiguous() and g.dtype == b["pflat"].dtype:
+            b["gsrc"] = g.reshape(-1)  # held until the reduce-scatter is waited for
+        else:
+            if b["gflat"] is None:
+                b["gflat"] = torch.zeros(self.world * b["L"], dtype=b["pflat"].dtype, device=b["pflat"].device)
+            torch.mul(g.reshape(-1), 1.0 / self.world, out=b["gflat"][o:o + n])
+            b["gsrc"] = None
         p.grad = None  # the reduced gradient exists only as this rank's shard
         b["ready"][k] = True
         while self._next < len(self.buckets) and all(self.buckets[self._next]["ready"]):
@@ -455,7 +467,8 @@ class ShardedAdamDDP:
             miss = [tuple(p.shape) for (p, _), r in zip(b["members"], b["ready"]) if not r]
             raise RuntimeError(f"hgsr ShardedAdamDDP: no gradient this step for parameters {miss}; every rank must "
                                "produce every gradient (use GradientAllReduce for partial graphs)")
-        b["work"] = dist.reduce_scatter_tensor(b["gshard"], b["gflat"], op=dist.ReduceOp.SUM, group=self.group,
+        src = b["gsrc"] if b["gsrc"] is not None else b["gflat"]
+        b["work"] = dist.reduce_scatter_tensor(b["gshard"], src, op=dist.ReduceOp.SUM, group=self.group,
                                                async_op=True)
         b["launched"] = True
 
@@ -479,6 +492,10 @@ class ShardedAdamDDP:
         deferred = [id(b["members"][0][0]) in self.defer_ids for b in self.buckets]
         for b in [b for b, d in zip(self.buckets, deferred) if not d] + [b for b, d in zip(self.buckets, deferred) if d]:
             b["work"].wait()
+            if b["gsrc"] is not None:  # reduced unscaled: the mean over ranks on the shard only
+                b["gsrc"] = None
+                if self.world > 1:
+                    b["gshard"].mul_(1.0 / self.world)
             L = b["L"]
             s0, s1 = lo * L, lo * L + L
             descs = {}
