@@ -1,0 +1,137 @@
+"""The explicit-Gaussian DDP step with two ranks on ONE GPU (gloo carries the collectives on
+device tensors; the driver's N > 1 runs use RCCL across GPUs): each rank renders its own view
+through gsplat_api.rasterization + the fused loss, multigpu.ShardedAdamDDP reduce-scatters the
+gradients from the autograd hooks, steps the HIP Adam on its shard (offsets != 0, the colours'
+bucket reduced in place) and all-gathers, the colours' gather left in flight until the next
+rasterization's parameter-ready hook.  Against one process rendering both views per step and
+stepping hgsr's Adam on the averaged gradient (reference train.py:206,274-277 over a batch of two
+views).
+
+Tolerance: the two runs' raster backwards sum with float atomics in different orders (run-to-run
+spread <= 4.4e-7 of each gradient's scale, profiles/r05_run_to_run_*.json), and Adam with
+eps = 1e-15 turns a sign flip of a near-zero gradient into a 2 lr step: so the parameters must
+agree within 1e-3 lr except for at most 0.2 % of the elements, and within 2 lr x steps everywhere.
+The ranks' parameters must be bit-identical."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+N, W, H, V, STEPS = 20_000, 160, 96, 4, 3
+LRS = [1.6e-4, 1e-3, 5e-3, 5e-2, 2.5e-3]  # means, quats, log-scales, opacity logits, colours (bench.py)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _setup(dev):
+    from horizongs_amd.synthetic import camera_set, make_scene
+    sc = make_scene(N, W, H, seed=0)
+    cams = camera_set(V).to(dev)
+    ps = [sc.means, sc.quats, torch.log(sc.scales), torch.logit(sc.opacities), sc.colors]
+    ps = [p.to(dev).clone().requires_grad_(True) for p in ps]
+    targets = [torch.rand(3, H, W, generator=torch.Generator().manual_seed(100 + v)).to(dev) for v in range(V)]
+    return sc.Ks.to(dev), cams, ps, targets
+
+
+def _view_loss(ps, Ks, cams, targets, view):
+    from horizongs_amd import gsplat_api as G
+    from horizongs_amd.activations import activate
+    from horizongs_amd.loss import fused_loss
+    means, quats, log_scales, opac_logit, colors = ps
+    scales, opac = activate(log_scales, opac_logit)
+    out, alpha, _ = G.rasterization(means, quats, scales, opac, colors, cams[view][None], Ks, W, H, packed=False,
+                                    backgrounds=torch.zeros(1, 3, device=means.device), render_mode="RGB+ED")
+    img = out.reshape(H, W, -1).permute(2, 0, 1)
+    return fused_loss(img, targets[view], None, 0.2, alpha.reshape(H, W), 0.05, 0.05, scales, 0.01)[0]
+
+
+def _optimizer(ps):
+    from horizongs_amd.optim import Adam
+    return Adam([{"params": [p], "lr": lr} for p, lr in zip(ps, LRS)], lr=0.0, eps=1e-15)
+
+
+def _rank(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from horizongs_amd import gsplat_api as G
+        from horizongs_amd.multigpu import ShardedAdamDDP
+        dev = "cuda"
+        Ks, cams, ps, targets = _setup(dev)
+        means, quats, log_scales, opac_logit, colors = ps
+        red = ShardedAdamDDP(_optimizer(ps), order=[[colors], [means, quats], [log_scales, opac_logit]],
+                             defer=[colors])
+        remove = G.register_param_ready_hook(red.wait_deferred)
+        try:
+            for s in range(STEPS):
+                loss = _view_loss(ps, Ks, cams, targets, (s * world + rank) % V)
+                red.begin()
+                loss.backward()
+                red.finish()
+            red.wait_deferred()
+            torch.cuda.synchronize()
+            direct = [b["direct"] for b in red.buckets]
+            q.put((rank, [p.detach().cpu().numpy() for p in ps], direct, None))
+        finally:
+            remove()
+    except Exception as e:  # noqa: BLE001  (reported to the parent, which fails the test)
+        q.put((rank, None, None, f"{type(e).__name__}: {e}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_ddp_two_ranks_one_gpu_matches_two_view_batch():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[3] is None for r in res), [r[3] for r in res]
+    assert all(p.exitcode == 0 for p in procs)
+    assert res[0][2] == [True, False, False]  # the colours' bucket took the in-place path
+    # the reference: one process, both views of each step, averaged, one Adam step
+    Ks, cams, ps, targets = _setup("cuda")
+    init = [p.detach().cpu().numpy().copy() for p in ps]
+    opt = _optimizer(ps)
+    for s in range(STEPS):
+        opt.zero_grad(set_to_none=True)
+        loss = sum(_view_loss(ps, Ks, cams, targets, (s * world + r) % V) for r in range(world)) / world
+        loss.backward()
+        opt.step()
+    torch.cuda.synchronize()
+    stats = {}
+    for k, (p, lr) in enumerate(zip(ps, LRS)):
+        d = np.abs(res[0][1][k] - p.detach().cpu().numpy())
+        stats[k] = {"lr": lr, "max_abs_diff": float(d.max()), "frac_above_1e-3_lr": float((d > 1e-3 * lr).mean()),
+                    "frac_moved": float((np.abs(p.detach().cpu().numpy() - init[k]) > 0).mean())}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "ddp_two_ranks.json"), "w") as f:
+        json.dump(stats, f)
+    for k, (p, lr) in enumerate(zip(ps, LRS)):
+        ref = p.detach().cpu().numpy()
+        a, b = res[0][1][k], res[1][1][k]
+        assert np.array_equal(a, b), f"param {k}: the ranks' all-gathered parameters differ"
+        d = np.abs(a - ref)
+        assert d.max() <= 2 * lr * STEPS + 1e-6, (k, float(d.max()))
+        assert (d > 1e-3 * lr).mean() <= 2e-3, (k, float((d > 1e-3 * lr).mean()))
+        assert (np.abs(ref - init[k]) > 0).mean() > 0.05  # the steps moved the parameters
