@@ -750,9 +750,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     args = resolve(parse(), world)
+    # HGSR_BENCH_SHARE_GPU=1 (rehearsal only): the ranks share the visible GPUs round-robin and the
+    # collectives go over gloo on device tensors -- the N > 1 code paths on a one-GPU box.  The
+    # measured lines are RCCL with one GPU per rank.
+    share = os.environ.get("HGSR_BENCH_SHARE_GPU", "0") != "0"
+    if share:
+        local = local % max(1, torch.cuda.device_count())
     if world > 1 or (os.environ.get("HGSR_DDP_FORCE", "0") != "0" and "WORLD_SIZE" in os.environ):
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     res = measure(args, rank, world, dev)
     wl, dt = res["wl"], res["dt"]
