@@ -214,6 +214,7 @@ class Workload:
         # nothing is densified, so the optimizer is sharded instead (ZeRO-1: reduce-scatter ->
         # Adam on this rank's 1/N -> all-gather, multigpu.ShardedAdamDDP)
         self.sharded = None
+        self._unhook = None
         if not args.anchors:
             # buckets in the order the backward finishes their gradients: the colours' (the raster
             # backward's) reduce-scatter runs under the projection and activation backwards, the
@@ -227,7 +228,19 @@ class Workload:
             self.sharded = ShardedAdamDDP(self.optimizer, order=[[self.colors], [self.means, self.quats],
                                                                  [self.log_scales, self.opac_logit]],
                                           defer=[self.colors])
-            G.register_param_ready_hook(self.sharded.wait_deferred)
+            self._unhook = G.register_param_ready_hook(self.sharded.wait_deferred)
+
+    def flush(self):
+        """Every parameter whole (the sharded optimizer's deferred colours all-gather waited for)."""
+        if self.sharded is not None:
+            self.sharded.flush()
+
+    def close(self):
+        """Drop the parameter-ready hook (it holds this workload's optimizer and buffers alive)."""
+        self.flush()
+        if self._unhook is not None:
+            self._unhook()
+            self._unhook = None
 
     def _init_anchors(self, args, seed, dev):
         """SURVEY 8(d) decode-inclusive c2: anchors placed like the c2 Gaussians, feat ~ N(0, 0.1),
@@ -559,8 +572,21 @@ def measure(args, rank, world, dev):
     # before the warmup: no generation-2 pass inside the timed steps, and no idle GPU between
     # the warmup and the timed steps (a collection there left the first timed steps ~10 % slower)
     gc.collect()
-    for _ in range(args.warmup):
+    # at N > 1 a progress line on stderr at most once a second (a slow but live run -- a first
+    # RCCL collective's setup, gloo in a rehearsal -- is never silent long enough to look hung)
+    last = [time.perf_counter()]
+
+    def progress(what, i, n):
+        if world > 1:
+            now = time.perf_counter()
+            if now - last[0] >= 1.0 or i + 1 == n:
+                last[0] = now
+                print(f"bench rank {rank}: {args.config} {what} step {i + 1}/{n}", file=sys.stderr, flush=True)
+
+    for i in range(args.warmup):
         wl.step()
+        progress("warmup", i, args.warmup)
+    wl.flush()
     torch.cuda.synchronize(dev)
     # the optimizer moves the scene: intersections before / after the timed steps show the drift
     isects_before = wl.meta["flatten_ids"].numel() if args.warmup else None
@@ -573,10 +599,12 @@ def measure(args, rank, world, dev):
     t0 = time.perf_counter()
     step_t = [] if os.environ.get("HGSR_BENCH_STEP_TIMES") else None  # (diagnostic: host time per step)
     seg0 = torch.cuda.memory_stats(dev).get("segment.all.allocated") if step_t is not None else None
-    for _ in range(args.steps):
+    for i in range(args.steps):
         wl.step()
+        progress("timed", i, args.steps)
         if step_t is not None:
             step_t.append(time.perf_counter())
+    wl.flush()  # the last step's deferred all-gather is part of the timed work
     torch.cuda.synchronize(dev)
     if step_t is not None:
         ms = torch.cuda.memory_stats(dev)
@@ -611,6 +639,7 @@ def measure(args, rank, world, dev):
         log1 = len(wl.view_log)
         for _ in range(min(args.steps, 10)):
             wl.step()
+        wl.flush()
         torch.cuda.synchronize(dev)
         NAT.call("hgsr_timing_enable", 0)
         res["isects_breakdown"] = float(np.mean([n for _, n in wl.view_log[log1:]]))
@@ -740,6 +769,7 @@ def secondary(args, rank, world, dev):
                                   "figure (pairs the per-quadrant culling skips included) is a note only")),
                         "decode_mfma": decode_mfma(r["wl"], r["kernels"]) if a.anchors else None,
                         "kernels": r["kernels"]})
+        r["wl"].close()
         del r
         torch.cuda.empty_cache()
     return out
@@ -786,6 +816,7 @@ def main():
             "kernels_source": "HIP events of every kernel over a separate pass after the timed region",
             "hbm_kernels": hbm_kernels(wl, res["kernels"], res.get("isects_breakdown")),
         }
+    wl.close()
     del res, wl
     torch.cuda.empty_cache()
     if not args.no_secondary:

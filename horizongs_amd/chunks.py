@@ -61,34 +61,43 @@ def run_chunks(chunks: Sequence[str], devices: Sequence[str], command: Callable[
                 return
             rec = {"device": dev, "returncodes": {}, "seconds": 0.0}
             t0 = time.time()
-            for st in stages:
-                e = dict(base)
-                e["HIP_VISIBLE_DEVICES"] = str(dev)
-                out = open(os.path.join(log_dir, f"{c}_{st}.log"), "w") if log_dir else subprocess.DEVNULL
-                try:
-                    rc = subprocess.call(command(c, st), env=e, stdout=out, stderr=subprocess.STDOUT,
-                                         timeout=timeout)
-                except subprocess.TimeoutExpired:
-                    rc = -9
-                finally:
-                    if log_dir:
-                        out.close()
-                rec["returncodes"][st] = rc
-                if rc != 0:
-                    break
-            rec["seconds"] = round(time.time() - t0, 3)
-            with lock:
-                results[c] = rec
+            try:
+                for st in stages:
+                    e = dict(base)
+                    e["HIP_VISIBLE_DEVICES"] = str(dev)
+                    try:
+                        out = open(os.path.join(log_dir, f"{c}_{st}.log"), "w") if log_dir else subprocess.DEVNULL
+                        try:
+                            rc = subprocess.call(command(c, st), env=e, stdout=out, stderr=subprocess.STDOUT,
+                                                 timeout=timeout)
+                        finally:
+                            if log_dir:
+                                out.close()
+                    except subprocess.TimeoutExpired:
+                        rc = -9
+                    except Exception as ex:  # a command() error, a missing executable, an unwritable log
+                        rc = -1
+                        rec["error"] = f"{st}: {type(ex).__name__}: {ex}"
+                    rec["returncodes"][st] = rc
+                    if rc != 0:
+                        break
+            finally:
+                # recorded whatever happened, so a chunk never silently drops out of the results
+                rec["seconds"] = round(time.time() - t0, 3)
+                with lock:
+                    results[c] = rec
 
     threads = [threading.Thread(target=slot, args=(d,), daemon=True) for d in devices]
     for t in threads:
         t.start()
     for t in threads:
         t.join()
+    missing = [c for c in chunks if c not in results]
     failed = [c for c, r in results.items() if any(v != 0 for v in r["returncodes"].values())
               or len(r["returncodes"]) < len(stages)]
-    if failed:
-        raise RuntimeError(f"run_chunks: chunks failed: {sorted(failed)} ({ {c: results[c] for c in failed} })")
+    if failed or missing:
+        raise RuntimeError(f"run_chunks: chunks failed: {sorted(failed)}, never run: {sorted(missing)} "
+                           f"({ {c: results[c] for c in failed} })")
     return results
 
 

@@ -152,6 +152,99 @@ int launch_tile_order(int64_t n_bins, const int32_t* offsets, int64_t n_isects, 
 #define HGSR_BWD_ORDER 1
 #endif
 
+// Gradient slots of the raster backwards (isect.hip): (camera, Gaussian) o owns the slots
+// [seg[o], seg[o + 1]), one per tile of its rectangle in row-major order; its slot at tile (x, y)
+// is slot[o].x + y slot[o].y + x.  Each slot e has kSlotWaves partial rows (one per wave of the
+// tile's workgroup) and flags[kSlotWaves e + w] != 0 iff wave w wrote row (e, w) in this launch
+// (both raster backwards).
+constexpr int kSlotWaves = 4;
+struct GradSlots {
+    int32_t* seg;  // [C N + 1]
+    int2* slot;    // [C N]
+};
+// bytes of launch_grad_slots' buffer (from_lists: the rectangles are found from the lists)
+size_t grad_slot_bytes(int64_t CN, bool from_lists);
+// radii != nullptr: rectangles from means2d / radii (isect_tiles'); else from the sorted lists
+int launch_grad_slots(int C, int N, const float* means2d, const int32_t* radii, int tile_size, int tw, int th,
+                      const int32_t* offsets, const int32_t* flatten_ids, int64_t n_isects, void* buf,
+                      hipStream_t s, GradSlots& out);
+// the flags and partial rows of a backward workspace: flags first, so a forward that only
+// knows the intersection capacity can clear them (hgsr_raster{3,2}d_fwd_packed bwd_ws)
+inline size_t slot_flag_bytes(int64_t n_isects, int ways) { return ((size_t)n_isects * ways + 255) & ~(size_t)255; }
+
+// LDS ordering between the lanes of ONE wave (a wave's LDS operations complete in issue order;
+// this keeps the compiler from moving LDS accesses across it)
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// The splits' fixed-order sum of gradient slots, for one wave owning the nloc (1..64)
+// (camera, Gaussian) entries [ib, ib + nloc): the wave walks their contiguous slot range 64 slots
+// at a time.  Each slot has WAYS partial rows of ROWF floats (the first NV used, R4 float4) and
+// WAYS flag bytes; LPR consecutive lanes read one row (one coalesced request per row, 64 / LPR
+// rows per load instruction, all of a chunk's loads issued before any is summed), sum the slot's
+// flagged rows in way order and park the sums in the wave's LDS area; then each entry's lane adds
+// its own slots' sums in slot order, the next chunk's flags already in flight.  No atomics: the
+// result depends only on the inputs.
+template <int NV, int R4, int ROWF, int WAYS>
+__device__ __forceinline__ void reduce_slots(const float* __restrict__ rows, const uint8_t* __restrict__ flags,
+                                             const int32_t* __restrict__ seg, int64_t ib, int nloc,
+                                             float (*s_v)[65], float (&out)[NV]) {
+    static_assert(WAYS == 1 || WAYS == 4, "slot ways");
+    static_assert(R4 <= 8 && NV <= 4 * R4, "row shape");
+    constexpr int LPR = R4 <= 4 ? 4 : 8;  // lanes per row
+    constexpr int SPI = 64 / LPR;         // slots per load instruction
+    constexpr int G = LPR;                // slot groups per 64-slot chunk
+    constexpr int GB = 4;                 // slot groups whose loads are issued together
+    const int lane = threadIdx.x & 63;
+    const int q = lane & (LPR - 1), sl = lane / LPR;
+    const bool live = lane < nloc;
+    const int32_t lo_e = live ? seg[ib + lane] : 0, hi_e = live ? seg[ib + lane + 1] : 0;
+    const int32_t E0 = __builtin_amdgcn_readfirstlane(lo_e), E1 = seg[ib + nloc];
+    auto fl = [&](int32_t e) -> uint32_t {
+        if (e >= E1) return 0u;
+        return WAYS == 4 ? reinterpret_cast<const uint32_t*>(flags)[e] : (uint32_t)flags[e];
+    };
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[k] = 0.f;
+    uint32_t fc = fl(E0 + lane);  // flags of slot cs + lane
+    for (int32_t cs = E0; cs < E1; cs += 64) {
+        const uint32_t fcur = fc;
+        fc = fl(cs + 64 + lane);  // the next chunk's, in flight while this one is summed
+#pragma unroll
+        for (int g0 = 0; g0 < G; g0 += GB) {
+            float4 x[GB][WAYS];
+#pragma unroll
+            for (int gb = 0; gb < GB; ++gb) {
+                const int s = (g0 + gb) * SPI + sl;
+                const uint32_t f = (uint32_t)__shfl((int)fcur, s);
+#pragma unroll
+                for (int w = 0; w < WAYS; ++w) {
+                    x[gb][w] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (q < R4 && ((f >> (8 * w)) & 0xffu))
+                        x[gb][w] = reinterpret_cast<const float4*>(rows + ((int64_t)(cs + s) * WAYS + w) * ROWF)[q];
+                }
+            }
+#pragma unroll
+            for (int gb = 0; gb < GB; ++gb) {
+                float4 a = x[gb][0];
+#pragma unroll
+                for (int w = 1; w < WAYS; ++w)
+                    a = make_float4(a.x + x[gb][w].x, a.y + x[gb][w].y, a.z + x[gb][w].z, a.w + x[gb][w].w);
+                const int s = (g0 + gb) * SPI + sl;
+                const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (q < R4 && 4 * q + c < NV) s_v[4 * q + c][s] = av[c];
+            }
+        }
+        wave_lds_sync();
+        const int32_t lo = max(lo_e, cs), hi = min(hi_e, cs + 64);
+        for (int32_t y = lo; y < hi; ++y)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) out[k] += s_v[k][y - cs];
+        wave_lds_sync();
+    }
+}
+
 // count floats from src to LDS dst (16-B aligned) as float4 runs when src allows
 __device__ __forceinline__ void stage_floats(const float* __restrict__ src, int count, float* dst) {
     int done = 0;

@@ -459,9 +459,7 @@ __global__ __launch_bounds__(256) void decode_fwd_kernel(DecodeDims d, MlpPtrs m
     }
 }
 
-// wave-level LDS ordering point: all of this wave's LDS operations have completed and the
-// compiler may not move memory operations across it (no workgroup barrier)
-__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// (wave_lds_sync, common.h: the wave-level LDS ordering point; no workgroup barrier)
 
 // Colour head alone, for models whose second layer exceeds the 128-row plan (SH colour
 // heads: 27 x 10 outputs).  With every head's W2 in LDS the fused forward fits one workgroup

@@ -25,7 +25,9 @@
 
 namespace hgsr {
 
-constexpr int kLdsBins = 15360;   // <= 60 KiB of LDS per block for the histogram / cursors (+ the 4-KiB BigQ)
+// the histogram / cursors take <= 60 KiB of LDS per block, plus the 4,104-B BigQ: 65,544 B at most
+// (isect_lds_bytes), above 64 KiB -- gfx950 allows 160 KiB per workgroup (static_assert below)
+constexpr int kLdsBins = 15360;
 constexpr int kSortCap = 2048;    // keys sorted entirely in LDS by one 256-lane workgroup
 constexpr int kIsectBatch = 8;    // Gaussians per lane whose loads are issued together (count / emit)
 
@@ -88,6 +90,7 @@ struct BigQ {
 __host__ __device__ inline size_t isect_lds_bytes(int n_bins) {
     return (((size_t)n_bins * 4 + 15) & ~(size_t)15) + sizeof(BigQ);
 }
+static_assert(((size_t)kLdsBins * 4 + 15) / 16 * 16 + sizeof(BigQ) <= 160 * 1024, "count / emit LDS over gfx950's 160 KiB");
 __device__ __forceinline__ BigQ* bigq_of(int* s, int n_bins) {
     return reinterpret_cast<BigQ*>(reinterpret_cast<char*>(s) + (((size_t)n_bins * 4 + 15) & ~(size_t)15));
 }
@@ -979,11 +982,222 @@ __global__ void copy_i32_kernel(int n, const int32_t* __restrict__ a, int32_t* _
     if (i < n) b[i] = a[i];
 }
 
+// ---------------------------------------------------------------- gradient slots
+// The raster backwards give every (tile-list entry, wave) partial sum its own slot row instead
+// of adding it into a per-Gaussian row with float atomics (whose order -- hence whose last bits
+// -- changes from launch to launch); the splits then sum each Gaussian's slots in one fixed
+// order, so two launches give bit-identical gradients.  Slot e of flattened (camera, Gaussian)
+// o's tile (x, y) is seg[o] + (y - y0) w + (x - x0): the tile's rank in o's rectangle in
+// gsplat's emission order (row-major over the rectangle, isect_tiles), seg = the exclusive
+// prefix of the rectangles' areas (tiles_per_gauss).  A Gaussian's slots are contiguous and
+// slot[o] = {seg[o] - y0 w - x0, w} gives e = slot.x + y slot.y + x in one multiply-add.
+// The rectangles come from means2d / radii (the same tile_rect the emission ran), or -- for
+// rasterize_to_pixels called on bare lists -- from each Gaussian's first and last tile in the
+// lists (a rectangle's corners are its smallest and largest row-major tile index).
+constexpr int kSlotPer = 2048;  // (camera, Gaussian) entries per scan block: 256 threads x 8
+
+struct RectFromRadii {
+    const float2* m;
+    const int32_t* r;
+    int ts, tw, th;
+    __device__ __forceinline__ int operator()(int64_t o, int& x0, int& y0, int& w) const {
+        const int32_t rad = r[o];
+        if (rad <= 0) {
+            x0 = y0 = w = 0;
+            return 0;
+        }
+        const float2 mm = m[o];
+        int x1, y1;
+        tile_rect(mm.x, mm.y, rad, ts, tw, th, x0, y0, x1, y1);
+        w = x1 - x0;
+        return (y1 - y0) * w;
+    }
+};
+
+struct RectFromTiles {
+    const int32_t* tmin;  // per-camera row-major tile index, INT32_MAX when o has no entry
+    const int32_t* tmax;
+    int tw;
+    __device__ __forceinline__ int operator()(int64_t o, int& x0, int& y0, int& w) const {
+        const int32_t a = tmin[o], b = tmax[o];
+        if (a > b) {
+            x0 = y0 = w = 0;
+            return 0;
+        }
+        y0 = a / tw;
+        x0 = a - y0 * tw;
+        const int y1 = b / tw + 1, x1 = b - (y1 - 1) * tw + 1;
+        w = x1 - x0;
+        return (y1 - y0) * w;
+    }
+};
+
+// stage A: the area total of each block of kSlotPer entries (entry o0 + 256 k + tid: coalesced)
+template <typename R>
+__global__ __launch_bounds__(256) void slot_sum_kernel(int64_t CN, R rect, int32_t* __restrict__ bsum) {
+    const int64_t o0 = (int64_t)blockIdx.x * kSlotPer + threadIdx.x;
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int x0, y0, w;
+        if (o0 + 256 * k < CN) s += rect(o0 + 256 * k, x0, y0, w);
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) s += __shfl_xor(s, d);
+    __shared__ int ws[4];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) bsum[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// stage B: one workgroup, exclusive scan of the block totals in place; seg[CN] = the total
+__global__ __launch_bounds__(1024) void slot_scan_kernel(int nb, int32_t* __restrict__ bsum,
+                                                         int32_t* __restrict__ seg_end) {
+    __shared__ int32_t s_w[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int per = (nb + 1023) / 1024;
+    const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
+    int32_t local = 0;
+    for (int i = b0; i < b1; ++i) local += bsum[i];
+    int32_t inc = local;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int32_t o = __shfl_up(inc, d);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    int32_t pre = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+        pre += w < wave ? s_w[w] : 0;
+        total += s_w[w];
+    }
+    int32_t run = pre + inc - local;
+    for (int i = b0; i < b1; ++i) {
+        const int32_t v = bsum[i];
+        bsum[i] = run;
+        run += v;
+    }
+    if (tid == 0) *seg_end = total;
+}
+
+// stage C: per block, the exclusive prefix of the areas (eight block-wide scans over the
+// coalesced rows o0 + 256 k + tid, k = 0..7) plus the block's offset -> seg and slot of every entry
+template <typename R>
+__global__ __launch_bounds__(256) void slot_write_kernel(int64_t CN, R rect, const int32_t* __restrict__ bpre,
+                                                         int32_t* __restrict__ seg, int2* __restrict__ slot) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t o0 = (int64_t)blockIdx.x * kSlotPer + tid;
+    int a[8], x0[8], y0[8], w[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = o0 + 256 * k < CN ? rect(o0 + 256 * k, x0[k], y0[k], w[k]) : 0;
+    __shared__ int s_w[8][4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int inc = a[k];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(inc, d);
+            if (lane >= d) inc += o;
+        }
+        if (lane == 63) s_w[k][wave] = inc;
+        a[k] = inc - a[k];  // exclusive within the wave
+    }
+    __syncthreads();
+    int run = bpre[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int pre = run;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            pre += v < wave ? s_w[k][v] : 0;
+            run += s_w[k][v];
+        }
+        const int64_t o = o0 + 256 * k;
+        if (o < CN) {
+            const int e = pre + a[k];
+            seg[o] = e;
+            slot[o] = make_int2(e - y0[k] * w[k] - x0[k], w[k]);
+        }
+    }
+}
+
+// bare lists: each entry's first and last tile (row-major index within its camera)
+__global__ __launch_bounds__(256) void slot_minmax_kernel(int n_tiles, const int32_t* __restrict__ offsets,
+                                                          int64_t n_isects, int n_bins,
+                                                          const int32_t* __restrict__ flatten_ids,
+                                                          int32_t* __restrict__ tmin, int32_t* __restrict__ tmax) {
+    const int bin = blockIdx.x;
+    const int32_t start = offsets[bin];
+    const int32_t end = bin == n_bins - 1 ? (int32_t)n_isects : offsets[bin + 1];
+    const int tile = bin % n_tiles;
+    for (int32_t p = start + threadIdx.x; p < end; p += 256) {
+        const int32_t o = flatten_ids[p];
+        atomicMin(&tmin[o], tile);
+        atomicMax(&tmax[o], tile);
+    }
+}
+
+__global__ void fill_i32_kernel(int64_t n, int32_t* __restrict__ p, int32_t v) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
 }  // namespace hgsr
+
+static size_t align256_(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t hgsr::grad_slot_bytes(int64_t CN, bool from_lists) {
+    const int64_t nb = (CN + kSlotPer - 1) / kSlotPer;
+    size_t b = align256_((size_t)(CN + 1) * 4) + align256_((size_t)CN * 8) + align256_((size_t)(nb + 1) * 4);
+    if (from_lists) b += 2 * align256_((size_t)CN * 4);
+    return b;
+}
+
+int hgsr::launch_grad_slots(int C, int N, const float* means2d, const int32_t* radii, int tile_size, int tw, int th,
+                            const int32_t* offsets, const int32_t* flatten_ids, int64_t n_isects, void* buf,
+                            hipStream_t s, GradSlots& out) {
+    const int64_t CN = (int64_t)C * N;
+    const int64_t nb = (CN + kSlotPer - 1) / kSlotPer;
+    char* p = (char*)buf;
+    out.seg = (int32_t*)p;
+    p += align256_((size_t)(CN + 1) * 4);
+    out.slot = (int2*)p;
+    p += align256_((size_t)CN * 8);
+    int32_t* bsum = (int32_t*)p;
+    p += align256_((size_t)(nb + 1) * 4);
+    HGSR_REQUIRE(nb < (1ll << 31), "too many Gaussians for the gradient slots");
+    if (CN == 0) return memset_async(out.seg, 4, s, "grad_slots");
+    const dim3 grid((unsigned)nb);
+    if (radii) {
+        HGSR_REQUIRE(means2d, "null pointer");
+        const RectFromRadii r{reinterpret_cast<const float2*>(means2d), radii, tile_size, tw, th};
+        hipLaunchKernelGGL(slot_sum_kernel<RectFromRadii>, grid, dim3(256), 0, s, CN, r, bsum);
+        hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bsum, out.seg + CN);
+        hipLaunchKernelGGL(slot_write_kernel<RectFromRadii>, grid, dim3(256), 0, s, CN, r, bsum, out.seg, out.slot);
+    } else {
+        HGSR_REQUIRE(offsets && (n_isects == 0 || flatten_ids), "null pointer");
+        int32_t* tmin = (int32_t*)p;
+        int32_t* tmax = (int32_t*)(p + align256_((size_t)CN * 4));
+        const dim3 g1((unsigned)((CN + 255) / 256));
+        hipLaunchKernelGGL(fill_i32_kernel, g1, dim3(256), 0, s, CN, tmin, (int32_t)0x7fffffff);
+        hipLaunchKernelGGL(fill_i32_kernel, g1, dim3(256), 0, s, CN, tmax, (int32_t)-1);
+        const int n_bins = C * tw * th;
+        if (n_isects > 0)
+            hipLaunchKernelGGL(slot_minmax_kernel, dim3(n_bins), dim3(256), 0, s, tw * th, offsets, n_isects, n_bins,
+                               flatten_ids, tmin, tmax);
+        const RectFromTiles r{tmin, tmax, tw};
+        hipLaunchKernelGGL(slot_sum_kernel<RectFromTiles>, grid, dim3(256), 0, s, CN, r, bsum);
+        hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bsum, out.seg + CN);
+        hipLaunchKernelGGL(slot_write_kernel<RectFromTiles>, grid, dim3(256), 0, s, CN, r, bsum, out.seg, out.slot);
+    }
+    return check_launch("grad_slots");
+}
 
 using namespace hgsr;
 
-static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+static size_t align256(size_t x) { return align256_(x); }
 
 extern "C" size_t hgsr_isect_ws1_bytes(int C, int N, int tile_w, int tile_h) {
     const IsectGeom g = isect_geom(C, N, tile_w, tile_h);

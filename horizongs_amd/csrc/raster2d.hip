@@ -2,8 +2,10 @@
 // rasterize_to_pixels_2dgs semantics, reached from reference
 // gaussian_renderer/render.py:62-76).  Same CDNA4 structure as raster3d.hip:
 // a 256-lane workgroup per 16x16 tile (four 8x8 wave quadrants), LDS-staged
-// surfel batches, workgroup early-out vote, wave-ballot skips and one packed
-// atomic record per (surfel, tile) in the backward.
+// surfel batches, workgroup early-out vote, wave-ballot skips and, in the
+// backward, each wave's partial of a (tile, surfel) pair stored as one 80-B row of
+// the pair's gradient slot (plain stores; split2 sums a surfel's slots in a fixed
+// order: bit-reproducible).
 //
 // Per pair: h_u = px*w - u, h_v = py*w - v (rows u,v,w of the ray transform),
 // x = h_u x h_v, s = x.xy / x.z, G = min(|s|^2, 2|mean2d - p|^2), alpha =
@@ -19,12 +21,10 @@ namespace hgsr {
 // raster2d_fwd 0.682 -> 0.633 ms at c3 against 128 (25 KB, 6 waves)
 constexpr int kFwd2Batch = HGSR_FWD2_BATCH;
 constexpr int kBwd2Batch = 64;
-#ifndef HGSR_REC2
-#define HGSR_REC2 24
-#endif
-// floats per accumulator row (96 B): 15 + D colour + 2 abs xy <= 21 used; HGSR_REC2 = 32 aligns
-// every row to one 128-B line (A/B build)
-constexpr int kRec2 = HGSR_REC2;
+// floats per gradient-slot row (80 B, 16-B aligned): accumulator value idx at idx -- v_xy 0-1,
+// (p - m)x v_c 2-4, (p - m)y v_c 5-7, v_c 8-10, opacity 11, normal 12-14, colour 15 + k (19 used
+// at D = 4; a row is written only where koff says, the reader takes the first 15 + D)
+constexpr int kRow2 = 20;
 
 struct Tile2 {
     int cam, tile, i, j;
@@ -436,8 +436,8 @@ __device__ __forceinline__ int32_t wave_max2(int32_t v) {
 // re-evaluates the hit of that step's surfel at those 4 pixels (the same float operations as
 // pass 1: identical values), forms the 19 accumulator terms (v_xy, (p - m) x v_c, v_c, the
 // opacity sum, fac x normal / colour upstream) summed over its 4 pixels, and a 16-lane
-// transpose-reduce (4 DPP levels, the value set halved at each) leaves 2 of the 19 sums per lane
-// for two global float atomics per 4 steps into the surfel's accumulator row (no LDS partials).
+// transpose-reduce (4 DPP levels, the value set halved at each) leaves 2 of the 19 sums per lane,
+// stored as one float2 per lane into the wave's row of the (tile, surfel) pair's gradient slot.
 #ifndef HGSR_BWD2TP_WAVES
 #define HGSR_BWD2TP_WAVES 5
 #endif
@@ -467,7 +467,8 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
                        int64_t n_isects, const int32_t* __restrict__ flatten_ids,
                        const float* __restrict__ render_alphas, const int32_t* __restrict__ last_ids,
                        const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
-                       const float* __restrict__ v_render_normals, float* __restrict__ acc_rows,
+                       const float* __restrict__ v_render_normals, float* __restrict__ rows,
+                       uint8_t* __restrict__ flags, const int2* __restrict__ slot, int64_t n_slots,
                        unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask,
                        int64_t qstride, const float* __restrict__ normal_rot,
                        const float* __restrict__ v_depth_extra, const int32_t* __restrict__ order) {
@@ -476,7 +477,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
     __shared__ struct {
         float4 r0[2][NB], r1[2][NB], r2[2][NB], col[2][NB], r4[2][NB], box[2][NB];
     } sr;
-    __shared__ int32_t s_id[2][NB];
+    __shared__ int32_t s_e[2][NB];  // the batch's records' gradient slots (-1: none)
     __shared__ __attribute__((aligned(16))) uint8_t s_list[4][NB];
     __shared__ int32_t s_last[4];
     __shared__ __attribute__((aligned(16))) float s_tp[4][4 * 16 * 4 * 2];
@@ -485,6 +486,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
+    const int tile_y = tc.tile / tw, tile_x = tc.tile - tile_y * tw;
     // per-pixel upstream terms of pixel (i, j), as raster2d_bwd_kernel: colour (ED divided, the
     // depth channel plus the depth->normal gradient), normal (back to the camera frame), the
     // alpha / background term; returns T_final
@@ -556,6 +558,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
         atomicAdd(pair_slot(pair_counter, 0), (unsigned long long)(end - tc.start) * kTilePixels);
     float4* const stage_arr[6] = {&sr.r0[0][0], &sr.r1[0][0], &sr.r2[0][0], &sr.col[0][0], &sr.r4[0][0], &sr.box[0][0]};
     int32_t cid = 0, nid = 0;
+    int2 csl = make_int2(-1, 0);  // slot base of cid (raster3d_bwd_kernel)
     const bool loader = tid < NB;
     auto dma_batch = [&](int buf, int32_t id) {
         const float4* r = reinterpret_cast<const float4*>(rec + id);
@@ -565,6 +568,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
     if (nb > 0 && loader) {
         cid = flatten_ids[max(end - 1 - tid, tc.start)];
         dma_batch(0, cid);
+        csl = slot[cid];
         nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
     }
     uint8_t* my_list = s_list[wave];
@@ -580,16 +584,20 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
         qw[1] = qp[1];
     };
     if (qmask && nb > 0) qfetch(0);
-    const int slot = lane >> 4;
+    const int gsl = lane >> 4;  // pass-2 queue entry of this lane
     for (int b = 0; b < nb; ++b) {
         const int cur = b & 1, prv = cur ^ 1;
         const int32_t batch_end = end - 1 - b * NB;
         const int bsz = min(NB, batch_end + 1 - tc.start);
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): batch b's DMA has landed
-        if (tid < bsz) s_id[cur][tid] = cid;
+        if (tid < bsz) {
+            const int64_t e = (int64_t)csl.x + (int64_t)tile_y * csl.y + tile_x;
+            s_e[cur][tid] = (e >= 0 && e < n_slots) ? (int32_t)e : -1;
+        }
         if (b + 1 < nb && loader) {
             cid = nid;
             dma_batch(prv, cid);
+            csl = slot[cid];
             nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
         lds_barrier();
@@ -620,19 +628,19 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
         if (n_mine > 0) {
             const uint32_t lstp = reinterpret_cast<const uint32_t*>(my_list)[lane < NB / 4 ? lane : 0];
             float* const tp = s_tp[wave];
-            // pass 2 over the 4 queued steps (packed record indices, NB = empty slot): step `slot`'s
-            // surfel at this lane's 4 pixels, the 16-lane transpose-reduce, two float atomics
+            // pass 2 over the 4 queued steps (packed record indices, NB = empty entry): step `gsl`'s
+            // surfel at this lane's 4 pixels, the 16-lane transpose-reduce, the sums stored
             auto pass2 = [&](const uint32_t qpk) {
-                const int t = (int)__builtin_amdgcn_ubfe(qpk, 8 * slot, 8);
+                const int t = (int)__builtin_amdgcn_ubfe(qpk, 8 * gsl, 8);
                 const int tt = t < NB ? t : 0;
+                const int se = s_e[cur][tt];
                 const float4 r0 = sr.r0[cur][tt], r1 = sr.r1[cur][tt], r2 = sr.r2[cur][tt];
-                const int sid = s_id[cur][tt];
                 float g[20];
 #pragma unroll
                 for (int k = 0; k < 20; ++k) g[k] = 0.f;
 #pragma unroll HGSR_BWD2TP_U2
                 for (int mq = 0; mq < 4; ++mq) {
-                    const float2 fv = *reinterpret_cast<const float2*>(tp + 128 * mq + 32 * slot + 2 * r16);
+                    const float2 fv = *reinterpret_cast<const float2*>(tp + 128 * mq + 32 * gsl + 2 * r16);
                     // pixel (y0 + 2 mq) * 8 + cx = r16 + 16 mq
                     const float4 po = *reinterpret_cast<const float4*>(pv + 128 * mq + 4 * r16);
                     const float4 pn = *reinterpret_cast<const float4*>(pv + 128 * mq + 64 + 4 * r16);
@@ -671,14 +679,13 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
                 }
 #pragma unroll
                 for (int q = 0; q < 2; ++q) asm volatile("" : "+v"(w4[q]));
-                if (t < NB) {
+                if (t < NB && se >= 0) {  // this wave's row of the (tile, surfel) pair's slot
+                    const int64_t rw = (int64_t)se * kSlotWaves + wave;
+                    float* const row = rows + rw * kRow2;
 #pragma unroll
                     for (int q = 0; q < 2; ++q)
-#if HGSR_PROBE_NOATOM2  // (probe build: the sums are formed but never added -- wrong results)
-                        if (koff[q] >= 0 && w4[q] == 1234.5f) atomicAdd(acc_rows + (int64_t)sid * kRec2 + koff[q], w4[q]);
-#else
-                        if (koff[q] >= 0 && w4[q] != 0.f) atomicAdd(acc_rows + (int64_t)sid * kRec2 + koff[q], w4[q]);
-#endif
+                        if (koff[q] >= 0) row[koff[q]] = w4[q];
+                    if (r16 == 0) flags[rw] = 1;
                 }
             };
             // pass 1, one step at a time; a step with a valid pixel is queued -- its (F, V) go to
@@ -740,24 +747,26 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
 // d(a x b).g = da.(b x g) + db.(g x a):
 //   v_u = gB x w + v x gC,  v_v = w x gA + gC x u,  v_w = gA x v + u x gB;
 // the densification proxy (d loss / d screen translation) is v_xy - (A.gC, B.gC).
-template <int D, bool ABS>
+template <int D>
 __global__ __launch_bounds__(256) void split2_kernel(int C, int N, const float* __restrict__ rows,
-                                                     const float* __restrict__ rt, const float2* __restrict__ means2d,
-                                                     float2* __restrict__ v_means2d, float* __restrict__ v_rt,
-                                                     ChanDst cd, float* __restrict__ v_normals,
-                                                     float2* __restrict__ v_densify, float2* __restrict__ v_abs) {
-    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (g >= N) return;
+                                                    const uint8_t* __restrict__ flags, const int32_t* __restrict__ seg,
+                                                    const float* __restrict__ rt, const float2* __restrict__ means2d,
+                                                    float2* __restrict__ v_means2d, float* __restrict__ v_rt,
+                                                    ChanDst cd, float* __restrict__ v_normals,
+                                                    float2* __restrict__ v_densify) {
+    constexpr int KV = 15 + D;
+    __shared__ float s_v[4][KV][65];  // per wave (each wave owns 64 surfels)
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t g0 = ((int64_t)blockIdx.x * 4 + wave) * 64, g = g0 + lane;
+    if (g0 >= N) return;  // wave-uniform; the waves never synchronise with each other
+    const int nloc = (int)min((int64_t)64, (int64_t)N - g0);
+    const bool live = lane < nloc;
     float col_sum[4] = {0.f, 0.f, 0.f, 0.f}, op_sum = 0.f;
     for (int c = 0; c < C; ++c) {
         const int64_t i = (int64_t)c * N + g;
-        const float4* r4 = reinterpret_cast<const float4*>(rows + i * kRec2);
-        float r[24];
-#pragma unroll
-        for (int q = 0; q < (15 + D + 2 + 3) / 4; ++q) {
-            const float4 v = r4[q];
-            r[q * 4] = v.x; r[q * 4 + 1] = v.y; r[q * 4 + 2] = v.z; r[q * 4 + 3] = v.w;
-        }
+        float r[KV];
+        reduce_slots<KV, (KV + 3) / 4, kRow2, kSlotWaves>(rows, flags, seg, (int64_t)c * N + g0, nloc, s_v[wave], r);
+        if (!live) continue;
         double u[3], v[3], w[3], gA[3], gB[3], gC[3];
         const float2 mm = means2d[i];
 #pragma unroll
@@ -803,8 +812,8 @@ __global__ __launch_bounds__(256) void split2_kernel(int C, int N, const float* 
                 cd.depths[i] = r[15 + k];
             }
         }
-        if (ABS) v_abs[i] = make_float2(r[15 + D], r[16 + D]);
     }
+    if (!live) return;
     if (cd.op_shared) cd.opac[g] = op_sum;
     if (cd.col_shared)
 #pragma unroll
@@ -985,21 +994,27 @@ extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, in
     HGSR_REQUIRE(n_isects == 0 || (flatten_ids && records), "null pointer");
     HGSR_REQUIRE(!qmask || qmask_bytes >= hgsr_raster3d_qmask_bytes(C, tile_w, tile_h, n_isects),
                  "raster2d_fwd_packed: quadrant-mask buffer too small");
-    // bwd_ws (nullable): the backward's workspace, whose accumulator rows this launch clears
-    const size_t rows_b = (size_t)C * N * kRec2 * sizeof(float);
-    HGSR_REQUIRE(!bwd_ws || (bwd_ws_bytes >= rows_b && (reinterpret_cast<uintptr_t>(bwd_ws) & 15) == 0),
+    // bwd_ws (nullable): the backward's workspace, whose gradient-slot flags this launch clears
+    const size_t flags_b = slot_flag_bytes(n_isects, kSlotWaves);
+    HGSR_REQUIRE(!bwd_ws || (bwd_ws_bytes >= flags_b && (reinterpret_cast<uintptr_t>(bwd_ws) & 15) == 0),
                  "raster2d_fwd_packed: bwd_ws too small or not 16-B aligned");
     return raster2d_fwd_launch(C, D, (const Rec2*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
                                tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
                                render_normals, render_distort, render_median, last_ids, median_ids,
-                               as_stream(stream), qmask, qmask_bytes, (float*)bwd_ws, bwd_ws ? rows_b : 0, isect_info,
+                               as_stream(stream), qmask, qmask_bytes, (float*)bwd_ws, bwd_ws ? flags_b : 0, isect_info,
                                normal_rot);
 }
 
-extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
+// backward workspace: [slot flags (cleared by a forward given it)][slot rows][slot index (seg,
+// slot) + its scan scratch][the packed records unless the forward's are reused]
+static size_t rows2_bytes(int64_t n_isects) {
+    return ((size_t)n_isects * kSlotWaves * kRow2 * sizeof(float) + 255) & ~(size_t)255;
+}
+
+extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int64_t n_isects, int reuse_fwd) {
     (void)D;
-    const size_t rows_b = ((size_t)C * N * kRec2 * sizeof(float) + 255) & ~(size_t)255;
-    return rows_b + (reuse_fwd ? 0 : rec2_bytes(C, N));
+    return slot_flag_bytes(n_isects, kSlotWaves) + rows2_bytes(n_isects) + grad_slot_bytes((int64_t)C * N, true) +
+           (reuse_fwd ? 0 : rec2_bytes(C, N));
 }
 
 static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const float* rt, const ChanSrc& cs,
@@ -1010,10 +1025,10 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* v_render_alphas, const float* v_render_normals, float* v_means2d,
                              float* v_rt, const ChanDst& cd, float* v_normals, float* v_densify,
                              const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream, const void* qbuf = nullptr,
-                             size_t qmask_bytes = 0, bool rows_zeroed = false, const float* normal_rot = nullptr,
-                             const float* v_depth_extra = nullptr) {
+                             size_t qmask_bytes = 0, bool flags_zeroed = false, const float* normal_rot = nullptr,
+                             const float* v_depth_extra = nullptr, const int32_t* radii = nullptr) {
     if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
-    HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
+    HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_bwd_ws_bytes(C, N, D, n_isects, fwd_ws != nullptr),
                  "raster2d_bwd workspace too small");
     HGSR_REQUIRE(ed_ch < 0 || render_colors, "expected-depth backward needs render_colors");
     if (N == 0) return HGSR_OK;
@@ -1037,14 +1052,19 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     HGSR_REQUIRE(means2d && rt && normals && isect_offsets && flatten_ids && render_alphas && last_ids &&
                      v_render_colors && v_render_alphas && v_render_normals && ws,
                  "null pointer");
-    const size_t rows_b = ((size_t)C * N * kRec2 * sizeof(float) + 255) & ~(size_t)255;
-    float* rows = (float*)ws;
+    uint8_t* const flags = (uint8_t*)ws;
+    float* const rows = (float*)((char*)ws + slot_flag_bytes(n_isects, kSlotWaves));
+    char* const sbuf = (char*)rows + rows2_bytes(n_isects);
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
-    if (!rows_zeroed)  // else hgsr_raster2d_fwd_packed cleared them (bwd_ws)
-        if (int st = memset_async(rows, (size_t)C * N * kRec2 * sizeof(float), s, "raster2d_bwd")) return st;
+    if (!flags_zeroed)  // else hgsr_raster2d_fwd_packed cleared them (bwd_ws)
+        if (int st = memset_async(flags, slot_flag_bytes(n_isects, kSlotWaves), s, "raster2d_bwd")) return st;
+    GradSlots gs;  // each (camera, surfel)'s gradient slots (raster3d_bwd_impl)
+    if (int st = launch_grad_slots(C, N, means2d, radii, tile_size, tile_w, tile_h, isect_offsets, flatten_ids,
+                                   n_isects, sbuf, s, gs))
+        return st;
     const Rec2* rec = (const Rec2*)fwd_ws;
     if (!rec) {
-        Rec2* own = (Rec2*)((char*)ws + rows_b);
+        Rec2* own = (Rec2*)(sbuf + grad_slot_bytes(n, true));
         if (int st = pack2(C, N, D, means2d, rt, cs, normals, own, s)) return st;
         rec = own;
     }
@@ -1066,11 +1086,11 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         hipLaunchKernelGGL((raster2d_bwd_tp_kernel<DD>), grid, dim3(256), 0, s, C, width, height, tile_w, tile_h,  \
                            rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects, flatten_ids,    \
                            render_alphas, last_ids, v_render_colors, v_render_alphas, v_render_normals, rows,      \
-                           pairs, qmask, qstride, normal_rot, v_depth_extra, order);                              \
+                           flags, gs.slot, n_isects, pairs, qmask, qstride, normal_rot, v_depth_extra, order);     \
     }                                                                                                             \
-    hipLaunchKernelGGL((split2_kernel<DD, false>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s,   \
-                       C, N, rows, rt, m2, reinterpret_cast<float2*>(v_means2d), v_rt, cd, v_normals,             \
-                       reinterpret_cast<float2*>(v_densify), nullptr)
+    hipLaunchKernelGGL((split2_kernel<DD>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, N,    \
+                       rows, flags, gs.seg, rt, m2,                                                                \
+                       reinterpret_cast<float2*>(v_means2d), v_rt, cd, v_normals, reinterpret_cast<float2*>(v_densify))
     switch (D) {
         case 1: LAUNCH_B2(1); break;
         case 2: LAUNCH_B2(2); break;
@@ -1110,7 +1130,7 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                                        float* v_colors, float* v_depths, float* v_opacities, float* v_normals,
                                        float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
                                        const void* qmask, size_t qmask_bytes, int ws_zeroed,
-                                       const float* normal_rot, const float* v_depth_extra,
+                                       const float* normal_rot, const float* v_depth_extra, const int32_t* radii,
                                        hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !depths), "expected_depth needs depths");
@@ -1128,5 +1148,5 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                              isect_offsets, n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
                              v_render_alphas, v_render_normals, v_means2d, v_ray_transforms, cd, v_normals,
                              v_densify, fwd_ws, ws, ws_bytes, stream, qmask, qmask_bytes,
-                             ws_zeroed != 0, normal_rot, v_depth_extra);
+                             ws_zeroed != 0, normal_rot, v_depth_extra, radii);
 }

@@ -16,22 +16,18 @@
 //  * backward: replay back-to-front bounded by the tile's latest contributor,
 //    wave-ballot skip of Gaussians no lane sees, all gradient components
 //    reduced across the wave together (step-major DPP, no hazard stalls), and
-//    each wave's sums go straight to the Gaussian's 48-byte accumulator row as
-//    one float-atomic instruction per 4 steps (the waves' partials meet in L2).
+//    each wave's sums stored as one 64-B row in the (tile, Gaussian) pair's own
+//    gradient slot (one plain store per 4 steps, no atomics); split3 sums each
+//    Gaussian's slots in a fixed order, so the gradients are bit-reproducible.
 #include "rec3.h"
 
 namespace hgsr {
 
 constexpr int kFwdBatch = 256;
 constexpr int kBwdBatch = 128;
-#ifndef HGSR_REC3
-#define HGSR_REC3 16
-#endif
-// floats per accumulator row: sigma moments(5) S0(1) color(D<=4) absxy(2) = 12 used, padded to
-// 64 B so no row's atomics straddle two cache lines (raster3d_bwd 0.556 -> 0.542 ms at c2,
-// gpurun_out/r05s8/ab_rec; 2DGS's 96-B rows padded to 128 B gained nothing and stay)
-constexpr int kRec3 = HGSR_REC3;
-constexpr int kRec3Used = 12;
+// floats per gradient-slot row (64 B, one full sector per store): sigma moments Sx Sy Sxx Sxy Syy
+// at 0-4, S0 = sum v_sigma at 5, colour channel k at 6 + k, |v_xy| at 10-11 (absgrad), 12-15 zero
+constexpr int kRow3 = 16;
 
 struct TileCtx {
     int cam, tile, i, j;
@@ -167,29 +163,6 @@ __device__ __forceinline__ void fwd_step(const float4 g0, const float4 g1, const
     cur = ok ? idx : cur;
 }
 
-// HGSR_PROBE_WGTIME (diagnostic build): each workgroup of the raster kernels records its start /
-// end on the 100-MHz real-time counter and its bin (scripts/wg_time.py reads them)
-#ifndef HGSR_PROBE_WGTIME
-#define HGSR_PROBE_WGTIME 0
-#endif
-#if HGSR_PROBE_WGTIME
-constexpr int kWgtSlots = 16384;
-__device__ unsigned long long g_wgtime[2][kWgtSlots][3];
-#define WGT_START const unsigned long long wgt0 = __builtin_amdgcn_s_memrealtime()
-#define WGT_END(k, bin)                                                                   \
-    do {                                                                                  \
-        __syncthreads();                                                                  \
-        if (threadIdx.x == 0 && blockIdx.x < kWgtSlots) {                                 \
-            g_wgtime[k][blockIdx.x][0] = wgt0;                                            \
-            g_wgtime[k][blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();                \
-            g_wgtime[k][blockIdx.x][2] = (unsigned long long)(bin);                       \
-        }                                                                                 \
-    } while (0)
-#else
-#define WGT_START
-#define WGT_END(k, bin)
-#endif
-
 template <int D>
 __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
@@ -207,7 +180,6 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     // keeps the offset, rebased once per batch
     __shared__ uint32_t s_list[4][kFwdBatch + 4];
     __shared__ int s_vote[2][4];
-    WGT_START;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects, isect_info, order);
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;   // centre of this wave's quadrant
@@ -317,7 +289,6 @@ __global__ __launch_bounds__(256) void raster3d_fwd_kernel(
     // the backward's accumulator rows, cleared here (after the last load: no wait covers
     // these stores) instead of by a memset on the step's critical path
     zero_share(zero_rows, zero_n4);
-    WGT_END(0, (int64_t)tc.cam * (tw * th) + tc.tile);
 }
 
 __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
@@ -363,9 +334,9 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     int bg_ch, int ed_ch, const float* __restrict__ render_colors, const int32_t* __restrict__ offsets,
     int64_t n_isects, const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
     const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
-    const float* __restrict__ v_render_alphas, float* __restrict__ acc_rows,
-    unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask, int64_t qstride,
-    const int32_t* __restrict__ order) {
+    const float* __restrict__ v_render_alphas, float* __restrict__ rows, uint8_t* __restrict__ flags,
+    const int2* __restrict__ slot, int64_t n_slots, unsigned long long* __restrict__ pair_counter,
+    const uint64_t* __restrict__ qmask, int64_t qstride, const int32_t* __restrict__ order) {
     constexpr int NB = kBwdBatch;
     // double-buffered staging: batch b+1 is loaded while batch b is composited (two
     // barriers per batch); slot NB is a zero-opacity dummy
@@ -374,16 +345,16 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     __shared__ struct {
         float4 g0[2][NB + 1], g1[2][NB + 1], col[2][NB + 1];
     } sr;
-    __shared__ int32_t s_id[2][NB];
+    __shared__ int32_t s_e[2][NB];  // the batch's records' gradient slots (-1: none)
     __shared__ __attribute__((aligned(16))) uint8_t s_list[4][NB];  // read back as 32-bit words
     __shared__ int32_t s_last[4];
     // pass-1 -> pass-2 transpose through LDS: [step s][column lane r][pixel m][F, V]
     __shared__ __attribute__((aligned(16))) float s_tp[4][4 * 16 * 4 * 2];
-    WGT_START;
     const TileCtx tc = tile_ctx(C, W, H, tw, th, offsets, n_isects, nullptr, order);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float qx = (float)(tc.j - (lane & 7)) + 4.0f;
     const float qy = (float)(tc.i - (lane >> 3)) + 4.0f;
+    const int tile_y = tc.tile / tw, tile_x = tc.tile - tile_y * tw;
     // per-pixel upstream terms of pixel (i, j); the ED channel is divided by max(alpha, 1e-10)
     auto pixel_terms = [&](int i, int j, float (&v)[4], float& vterm) {
         const bool in = i < H && j < W;
@@ -457,8 +428,10 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         atomicAdd(pair_slot(pair_counter, 0), (unsigned long long)(end - tc.start) * kTilePixels);
     // records are staged with LDS-DMA (global_load_lds_dwordx4: per-lane source, LDS
     // destination wave base + 16 B x lane) one batch ahead; ids two batches ahead in a
-    // register; lanes < NB (waves 0, 1) load one Gaussian each, clamped indices
+    // register; lanes < NB (waves 0, 1) load one Gaussian each, clamped indices; with each id its
+    // slot base {seg - y0 w - x0, w} (isect.hip), so the record's gradient slot is base + y w + x
     int32_t cid = 0, nid = 0;
+    int2 csl = make_int2(-1, 0);
     const bool loader = tid < NB;
     auto dma_batch = [&](int buf, int32_t id) {
         const float4* r = reinterpret_cast<const float4*>(rec + id);
@@ -470,12 +443,12 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     if (nb > 0 && loader) {
         cid = flatten_ids[max(end - 1 - tid, tc.start)];
         dma_batch(0, cid);
+        csl = slot[cid];
         nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
     }
     uint8_t* my_list = s_list[wave];
     uint32_t stepped = 0;  // compacted list entries this wave stepped (bench roofline only)
-    const int slot = lane >> 4;  // pass-2 Gaussian slot of this lane
-    const int slot8 = 8 * slot;
+    const int gsl = lane >> 4;  // pass-2 Gaussian (list entry of the 4-step group) of this lane
     // pass-2 output lane roles: after the 16-lane tree every lane of a row holds the six
     // sigma sums (and |v_xy|) and each quad one colour channel; lane r16 = 4 q + 3 adds its
     // quad's channel, lanes 0-2 / 4-6 the sums 0-2 / 3-5, lanes 8 / 9 the |v_xy| pair (ABS)
@@ -483,8 +456,11 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     const bool qb2 = (r16 >> 2) & 1, qsel1 = qlo == 1, qsel2 = qlo == 2, qcol = qlo == 3;
     const int koff = qlo == 3 ? 6 + ((r16 >> 3) | ((r16 >> 1) & 2))
                    : r16 < 8  ? qlo + (qb2 ? 3 : 0)
-                   : (ABS && r16 == 8) ? 6 + D
-                   : (ABS && r16 == 9) ? 7 + D : -1;
+                   : (ABS && r16 == 8) ? 10
+                   : (ABS && r16 == 9) ? 11 : -1;
+    // the row position lane r16 stores: koff, the unused lanes 8-10 (without ABS 8, 9) and 12-14
+    // on 10-15, so the 16 lanes of a Gaussian write one whole 64-B row
+    const int spos = (int)((0x9FED7CBA85436210ull >> (4 * r16)) & 15);
     // quadrant-mask words of batch bb: wave-uniform index, so they are scalar loads
     uint64_t qw[3] = {0, 0, 0};
     auto qfetch = [&](int bb) {
@@ -506,10 +482,14 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         // before the barrier below publishes it; then DMA batch b+1 into the other buffer
         // (its previous records were last read before the previous barrier)
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-        if (tid < bsz) s_id[cur][tid] = cid;
+        if (tid < bsz) {
+            const int64_t e = (int64_t)csl.x + (int64_t)tile_y * csl.y + tile_x;
+            s_e[cur][tid] = (e >= 0 && e < n_slots) ? (int32_t)e : -1;  // (inconsistent lists: no store)
+        }
         if (b + 1 < nb && loader) {
             cid = nid;
             dma_batch(prv, cid);
+            csl = slot[cid];
             nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
         lds_barrier();
@@ -590,10 +570,10 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
             };
             // pass 2 over 4 composited steps (records ts[0..3], values F/V in pass-1 layout)
             auto pass2 = [&](const uint32_t packed, float (&F)[4], float (&V)[4]) {
-                // this lane's Gaussian (step `slot`), extracted from the group's packed list
+                // this lane's Gaussian (step `gsl`), extracted from the group's packed list
                 // entries: its position and id reads are independent and go out before the
                 // transpose
-                const int t = (int)__builtin_amdgcn_ubfe(packed, slot8, 8);
+                const int t = (int)__builtin_amdgcn_ubfe(packed, 8 * gsl, 8);
                 float4 g0;
                 if (ABS) {
                     g0 = sr.g0[cur][t];
@@ -602,7 +582,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                     g0 = make_float4(xy.x, xy.y, 0.f, 0.f);
                 }
                 const float g1x = ABS ? sr.g1[cur][t].x : 0.f;
-                const int sid = s_id[cur][t < NB ? t : 0];
+                const int se = s_e[cur][t < NB ? t : 0];
                 {
                     // lane L = pixel r + 16 m writes (F[s], V[s]) at float 128 s + 64 (m >> 1) + 4 r +
                     // 2 (m & 1); lane 16 s + r reads its step's column as two 16-B chunks, pixels
@@ -616,12 +596,12 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                     for (int q = 0; q < 4; ++q)
                         *reinterpret_cast<float2*>(tp + 128 * q + 64 * (mm >> 1) + 4 * rr + 2 * (mm & 1)) =
                             make_float2(F[q], V[q]);
-                    const float4 lo = *reinterpret_cast<const float4*>(tp + 128 * slot + 4 * rr);
-                    const float4 hi = *reinterpret_cast<const float4*>(tp + 128 * slot + 64 + 4 * rr);
+                    const float4 lo = *reinterpret_cast<const float4*>(tp + 128 * gsl + 4 * rr);
+                    const float4 hi = *reinterpret_cast<const float4*>(tp + 128 * gsl + 64 + 4 * rr);
                     F[0] = lo.x; V[0] = lo.y; F[1] = lo.z; V[1] = lo.w;
                     F[2] = hi.x; V[2] = hi.y; F[3] = hi.z; V[3] = hi.w;
                 }
-                // now F[m], V[m]: step `slot`, pixel (column cx, row y0 + 2m)
+                // now F[m], V[m]: step `gsl`, pixel (column cx, row y0 + 2m)
                 const float dx = g0.x - p2.pxc, dy0 = g0.y - p2.py0c;
                 float S0, Sy, Syy, P[4], A0 = 0.f, A1 = 0.f;
                 float ax = 0.f, ay = 0.f, bx = 0.f, c2 = 0.f;
@@ -692,19 +672,19 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
 #pragma unroll
                 for (int k = 0; k < 7; ++k) asm volatile("" : "+v"(g[k]));
                 {
-                    // one float atomic per value straight into the Gaussian's accumulator row:
-                    // the four waves' partials meet in L2 (no LDS staging, no per-batch combine)
+                    // the wave's partial of this (tile, Gaussian) pair goes to its own row of the
+                    // pair's gradient slot: one plain 64-B store per Gaussian, no atomics
                     constexpr float kLn2 = 0.6931471805599453f;
                     const float a = qb2 ? g[3] : g[0], b = qb2 ? g[4] : g[1], c = qb2 ? g[5] : g[2];
                     float v = qsel1 ? b : a;
                     v = qsel2 ? c : v;
                     v = qcol ? g[6] : v;
                     if (ABS) v = r16 == 8 ? kLn2 * A0 : r16 == 9 ? kLn2 * A1 : v;
-#if HGSR_PROBE_NOATOM3  // (probe build: the sums are formed but never added -- wrong results)
-                    if (koff >= 0 && t < NB && v == 1234.5f) atomicAdd(acc_rows + (int64_t)sid * kRec3 + koff, v);
-#else
-                    if (koff >= 0 && t < NB && v != 0.f) atomicAdd(acc_rows + (int64_t)sid * kRec3 + koff, v);
-#endif
+                    if (t < NB && se >= 0) {
+                        const int64_t rw = (int64_t)se * kSlotWaves + wave;
+                        rows[rw * kRow3 + spos] = koff >= 0 ? v : 0.f;
+                        if (r16 == 0) flags[rw] = 1;
+                    }
                 }
             };
             for (int i = 0; i < n_mine; i += 4) {
@@ -720,31 +700,31 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     }
     if (pair_counter && lane == 0 && stepped)  // measurement only: lane-pairs stepped
         atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
-    WGT_END(1, (int64_t)tc.cam * (tw * th) + tc.tile);
 }
 
-// scatter accumulator rows into gsplat's separate gradient tensors (overwrite);
-// one lane per Gaussian, looping cameras in order (deterministic sums).  The rows
-// hold sigma moments (Sx, Sy, Sxx, Sxy, Syy) = sum_p v_sigma (dx, dy, dx^2, dx dy, dy^2):
-// v_means2d = Q (Sx, Sy) with Q the conic, v_conic = (Sxx / 2, Sxy, Syy / 2); slot 5
-// holds S0 = sum_p v_sigma, and v_opacity = sum_p vis v_alpha = -S0 / opacity.
+// Gradient slots -> gsplat's separate gradient tensors (overwrite): each (camera, Gaussian)'s
+// slot rows summed in a fixed order (reduce_slots), cameras in order per Gaussian.  The sums are
+// sigma moments (Sx, Sy, Sxx, Sxy, Syy) = sum_p v_sigma (dx, dy, dx^2, dx dy, dy^2):
+// v_means2d = Q (Sx, Sy) with Q the conic, v_conic = (Sxx / 2, Sxy, Syy / 2); value 5 is
+// S0 = sum_p v_sigma, and v_opacity = sum_p vis v_alpha = -S0 / opacity.
 template <int D, bool ABS>
 __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* __restrict__ rows,
+                                                     const uint8_t* __restrict__ flags, const int32_t* __restrict__ seg,
                                                      const Rec3* __restrict__ rec, const float* __restrict__ conics,
                                                      float2* __restrict__ v_means2d, float* __restrict__ v_conics,
                                                      ChanDst cd, float2* __restrict__ v_abs) {
-    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (g >= N) return;
+    __shared__ float s_v[4][12][65];  // per wave (each wave owns 64 Gaussians)
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t g0 = ((int64_t)blockIdx.x * 4 + wave) * 64, g = g0 + lane;
+    if (g0 >= N) return;  // wave-uniform; the waves never synchronise with each other
+    const int nloc = (int)min((int64_t)64, (int64_t)N - g0);
+    const bool live = lane < nloc;
     float col_sum[4] = {0.f, 0.f, 0.f, 0.f}, op_sum = 0.f;
     for (int c = 0; c < C; ++c) {
         const int64_t i = (int64_t)c * N + g;
-        const float4* r4 = reinterpret_cast<const float4*>(rows + i * kRec3);
-        float r[kRec3Used];
-#pragma unroll
-        for (int q = 0; q < kRec3Used / 4; ++q) {
-            const float4 v = r4[q];
-            r[q * 4] = v.x; r[q * 4 + 1] = v.y; r[q * 4 + 2] = v.z; r[q * 4 + 3] = v.w;
-        }
+        float r[12];
+        reduce_slots<12, 3, kRow3, kSlotWaves>(rows, flags, seg, (int64_t)c * N + g0, nloc, s_v[wave], r);
+        if (!live) continue;
         const float qa = conics[i * 3], qb = conics[i * 3 + 1], qc = conics[i * 3 + 2];
         v_means2d[i] = make_float2(qa * r[0] + qb * r[1], qb * r[0] + qc * r[1]);
         v_conics[i * 3] = 0.5f * r[2];
@@ -763,8 +743,9 @@ __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* 
                 cd.depths[i] = r[6 + k];
             }
         }
-        if (ABS) v_abs[i] = make_float2(r[6 + D], r[7 + D]);
+        if (ABS) v_abs[i] = make_float2(r[10], r[11]);
     }
+    if (!live) return;
     if (cd.op_shared) cd.opac[g] = op_sum;
     if (cd.col_shared)
 #pragma unroll
@@ -931,22 +912,28 @@ extern "C" int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, in
     HGSR_REQUIRE(n_isects == 0 || (flatten_ids && records), "null pointer");
     HGSR_REQUIRE(!qmask || qmask_bytes >= hgsr_raster3d_qmask_bytes(C, tile_w, tile_h, n_isects),
                  "raster3d_fwd_packed: quadrant-mask buffer too small");
-    // bwd_ws (nullable): the backward's workspace, whose accumulator rows this launch clears
-    const size_t rows_b = (size_t)C * N * kRec3 * sizeof(float);
-    HGSR_REQUIRE(!bwd_ws || (bwd_ws_bytes >= rows_b && (reinterpret_cast<uintptr_t>(bwd_ws) & 15) == 0),
+    // bwd_ws (nullable): the backward's workspace, whose gradient-slot flags this launch clears
+    const size_t flags_b = slot_flag_bytes(n_isects, kSlotWaves);
+    HGSR_REQUIRE(!bwd_ws || (bwd_ws_bytes >= flags_b && (reinterpret_cast<uintptr_t>(bwd_ws) & 15) == 0),
                  "raster3d_fwd_packed: bwd_ws too small or not 16-B aligned");
     // the quadrant-mask stride follows the buffer (sized for the capacity of a deferred count;
     // the backward, given the same buffer, derives the same stride)
     return raster3d_fwd_launch(C, D, (const Rec3*)records, backgrounds, Dc, expected_depth ? Dc : -1, width, height,
                                tile_w, tile_h, isect_offsets, n_isects, flatten_ids, render_colors, render_alphas,
-                               last_ids, as_stream(stream), qmask, qmask_bytes, (float*)bwd_ws, bwd_ws ? rows_b : 0,
+                               last_ids, as_stream(stream), qmask, qmask_bytes, (float*)bwd_ws, bwd_ws ? flags_b : 0,
                                isect_info);
 }
 
-extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd) {
+// backward workspace: [slot flags (cleared by a forward given it)][slot rows][slot index (seg,
+// slot) + its scan scratch][the packed records unless the forward's are reused]
+static size_t rows3_bytes(int64_t n_isects) {
+    return ((size_t)n_isects * kSlotWaves * kRow3 * sizeof(float) + 255) & ~(size_t)255;
+}
+
+extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int64_t n_isects, int reuse_fwd) {
     (void)D;
-    const size_t rows_b = ((size_t)C * N * kRec3 * sizeof(float) + 255) & ~(size_t)255;
-    return rows_b + (reuse_fwd ? 0 : rec_bytes(C, N));
+    return slot_flag_bytes(n_isects, kSlotWaves) + rows3_bytes(n_isects) + grad_slot_bytes((int64_t)C * N, true) +
+           (reuse_fwd ? 0 : rec_bytes(C, N));
 }
 
 static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const float* conics, const ChanSrc& cs,
@@ -957,9 +944,9 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* v_render_alphas, float* v_means2d, float* v_conics, const ChanDst& cd,
                              float* v_means2d_abs, const void* fwd_ws, void* ws, size_t ws_bytes,
                              hgsr_stream_t stream, const void* qbuf = nullptr, size_t qmask_bytes = 0,
-                             bool rows_zeroed = false) {
+                             bool flags_zeroed = false, const int32_t* radii = nullptr) {
     if (int st = check_raster(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
-    HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_bwd_ws_bytes(C, N, D, fwd_ws != nullptr),
+    HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_bwd_ws_bytes(C, N, D, n_isects, fwd_ws != nullptr),
                  "raster3d_bwd workspace too small");
     HGSR_REQUIRE(ed_ch < 0 || render_colors, "expected-depth backward needs render_colors");
     if (N == 0) return HGSR_OK;
@@ -982,14 +969,21 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     HGSR_REQUIRE(means2d && conics && isect_offsets && flatten_ids && render_alphas && last_ids && v_render_colors &&
                      v_render_alphas && ws,
                  "null pointer");
-    const size_t rows_b = ((size_t)C * N * kRec3 * sizeof(float) + 255) & ~(size_t)255;
-    float* rows = (float*)ws;
-    if (!rows_zeroed)  // else hgsr_raster3d_fwd_packed cleared them (bwd_ws)
-        if (int st = memset_async(rows, (size_t)C * N * kRec3 * sizeof(float), s, "raster3d_bwd")) return st;
+    uint8_t* const flags = (uint8_t*)ws;
+    float* const rows = (float*)((char*)ws + slot_flag_bytes(n_isects, kSlotWaves));
+    char* const sbuf = (char*)rows + rows3_bytes(n_isects);
+    if (!flags_zeroed)  // else hgsr_raster3d_fwd_packed cleared them (bwd_ws)
+        if (int st = memset_async(flags, slot_flag_bytes(n_isects, kSlotWaves), s, "raster3d_bwd")) return st;
+    // each (camera, Gaussian)'s gradient slots: from its tile rectangle (radii given), else
+    // from the lists
+    GradSlots gs;
+    if (int st = launch_grad_slots(C, N, means2d, radii, tile_size, tile_w, tile_h, isect_offsets, flatten_ids,
+                                   n_isects, sbuf, s, gs))
+        return st;
     // the forward's packed records when the caller kept them, else pack again
     const Rec3* rec = (const Rec3*)fwd_ws;
     if (!rec) {
-        Rec3* own = (Rec3*)((char*)ws + rows_b);
+        Rec3* own = (Rec3*)(sbuf + grad_slot_bytes(n, true));
         if (int st = pack3(C, N, D, means2d, conics, cs, own, s)) return st;
         rec = own;
     }
@@ -1014,12 +1008,12 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         KernelTimer kt("raster3d_bwd", s);                                                                     \
         hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
                            tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,       \
-                           flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, pairs,  \
-                           qmask, qstride, order);                                                             \
+                           flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, flags,  \
+                           gs.slot, n_isects, pairs, qmask, qstride, order);                                   \
     }                                                                                                          \
     hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, \
-                       N, rows, rec, conics, reinterpret_cast<float2*>(v_means2d), v_conics, cd,                     \
-                       reinterpret_cast<float2*>(v_means2d_abs))
+                       N, rows, flags, gs.seg, rec, conics,                                                        \
+                       reinterpret_cast<float2*>(v_means2d), v_conics, cd, reinterpret_cast<float2*>(v_means2d_abs))
     switch (D * 2 + (abs ? 1 : 0)) {
         case 2: LAUNCH_B(1, false); break;
         case 3: LAUNCH_B(1, true); break;
@@ -1061,7 +1055,7 @@ extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2
                                        float* v_means2d, float* v_conics, float* v_colors, float* v_depths,
                                        float* v_opacities, float* v_means2d_abs, const void* fwd_ws, void* ws,
                                        size_t ws_bytes, const void* qmask, size_t qmask_bytes, int ws_zeroed,
-                                       hgsr_stream_t stream) {
+                                       const int32_t* radii, hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!qmask || qmask_bytes >= hgsr_raster3d_qmask_bytes(C, tile_w, tile_h, n_isects),
                  "raster3d_bwd_fused: quadrant-mask buffer too small");
@@ -1076,12 +1070,5 @@ extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2
                              render_colors, width, height, tile_size, tile_w, tile_h, isect_offsets, n_isects,
                              flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, v_means2d,
                              v_conics, cd, v_means2d_abs, fwd_ws, ws, ws_bytes, stream, qmask, qmask_bytes,
-                             ws_zeroed != 0);
+                             ws_zeroed != 0, radii);
 }
-
-#if HGSR_PROBE_WGTIME
-// diagnostic build only: [fwd, bwd][workgroup][start, end, bin] of the last launches
-extern "C" int hgsr_debug_wgtime(void* dst) {
-    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(hgsr::g_wgtime), sizeof(hgsr::g_wgtime)) == hipSuccess ? 0 : -1;
-}
-#endif

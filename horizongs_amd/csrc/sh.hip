@@ -312,6 +312,8 @@ extern "C" int hgsr_sh_rgb_fwd(int degree, int C, int N, int K, const float* mea
     HGSR_REQUIRE(degree >= 0 && degree <= 3, "sh degree %d unsupported (0..3)", degree);
     HGSR_REQUIRE(K >= (degree + 1) * (degree + 1), "K=%d too small for degree %d", K, degree);
     HGSR_REQUIRE(C >= 1 && N >= 0, "bad dims C=%d N=%d", C, N);
+    // the backward stages K coefficient rows in LDS: refuse here, not one step later in it
+    HGSR_REQUIRE(K <= kShMaxK, "sh_rgb: K=%d coefficients per Gaussian (at most %d)", K, kShMaxK);
     if (N == 0) return HGSR_OK;
     HGSR_REQUIRE(means && campos && coeffs && radii && colors, "null pointer");
     dim3 grid((unsigned)((N + 255) / 256));

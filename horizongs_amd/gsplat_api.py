@@ -531,7 +531,7 @@ class _Raster3D(torch.autograd.Function):
         v_opac = torch.empty_like(opacities)
         v_abs = torch.empty_like(means2d) if absgrad else None
         fwd_ws = ctx.fwd_ws
-        ws_b = N.size_query("hgsr_raster3d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
+        ws_b = N.size_query("hgsr_raster3d_bwd_ws_bytes", C, Ng, D, flatten_ids.numel(), int(fwd_ws is not None))
         ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
         v_rc = _f32(v_rc)
         v_ra = _f32(v_ra)
@@ -548,23 +548,24 @@ class _Raster3D(torch.autograd.Function):
         return v_means2d, v_conics, v_colors, v_opac, v_bg, None, None, None, None, None, None
 
 
-def _bwd_ws(size_fn, ctx, C, Ng, D, dev, grad_mode):
+def _bwd_ws(size_fn, ctx, C, Ng, D, n_isects, dev, grad_mode):
     """The raster backward's workspace (records reused), allocated by the forward when a
-    backward can follow: the forward kernel clears its accumulator rows while it composites,
-    so the backward needs no memset (hgsr_raster{3,2}d_fwd_packed bwd_ws).  grad_mode is the
+    backward can follow: the forward kernel clears its gradient-slot flags while it composites,
+    so the backward needs no memset (hgsr_raster{3,2}d_fwd_packed bwd_ws).  n_isects: the
+    intersection arrays' size (a deferred count's capacity).  grad_mode is the
     CALLER's torch.is_grad_enabled() (inside forward() grad mode is always off, and
     needs_input_grad follows requires_grad only): an evaluation render under no_grad()
     allocates and clears nothing."""
     ctx.bwd_ws = None
     if not grad_mode or not any(ctx.needs_input_grad):
         return None
-    ws_b = N.size_query(size_fn, C, Ng, D, 1)
+    ws_b = N.size_query(size_fn, C, Ng, D, n_isects, 1)
     ctx.bwd_ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
     return ctx.bwd_ws
 
 
 def _take_bwd_ws(ctx, ws_b, dev):
-    """(workspace, rows already zero) for the backward: the forward's pre-cleared one once,
+    """(workspace, slot flags already zero) for the backward: the forward's pre-cleared one once,
     else a fresh one the backward clears itself (a second backward through the same graph)."""
     ws = getattr(ctx, "bwd_ws", None)
     ctx.bwd_ws = None
@@ -595,8 +596,11 @@ class _Raster3DFused(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means2d, conics, colors, depths, opacities, backgrounds, width, height, tile_size,
-                isect_offsets, flatten_ids, expected_depth, absgrad, records=None, grad_mode=True, deferred=None):
-        """deferred (_Deferred): flatten_ids is its capacity-sized array, the count device-resident."""
+                isect_offsets, flatten_ids, expected_depth, absgrad, records=None, grad_mode=True, deferred=None,
+                radii=None):
+        """deferred (_Deferred): flatten_ids is its capacity-sized array, the count device-resident.
+        radii: the projection's radii the lists were emitted from (the backward's gradient slots
+        follow their tile rectangles; without them the backward finds the rectangles in the lists)."""
         C, Ng = means2d.shape[:2]
         Dc = 0 if colors is None else colors.shape[-1]
         D = Dc + (0 if depths is None else 1)
@@ -613,8 +617,8 @@ class _Raster3DFused(torch.autograd.Function):
             # the forward's per-quadrant culling bits, read back by the backward
             q_b = N.size_query("hgsr_raster3d_qmask_bytes", C, tw, th, flatten_ids.numel())
             qmask = torch.empty(q_b, dtype=torch.uint8, device=dev)
-            # the backward's workspace, its accumulator rows cleared by this forward launch
-            bwd_ws = _bwd_ws("hgsr_raster3d_bwd_ws_bytes", ctx, C, Ng, D, dev, grad_mode)
+            # the backward's workspace, its gradient-slot flags cleared by this forward launch
+            bwd_ws = _bwd_ws("hgsr_raster3d_bwd_ws_bytes", ctx, C, Ng, D, flatten_ids.numel(), dev, grad_mode)
             N.call("hgsr_raster3d_fwd_packed", C, Ng, Dc, int(depths is not None), int(expected_depth),
                    ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
                    ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(last), ptr(ws),
@@ -634,6 +638,7 @@ class _Raster3DFused(torch.autograd.Function):
         ctx.fwd_ws = ws  # packed raster records, reused by the backward
         ctx.qmask = qmask
         ctx.deferred = deferred
+        ctx.radii = None if radii is None else radii.detach().contiguous()
         return rc, ra
 
     @staticmethod
@@ -651,22 +656,23 @@ class _Raster3DFused(torch.autograd.Function):
         v_opac = torch.empty_like(opacities)
         v_abs = torch.empty_like(means2d) if absgrad else None
         fwd_ws = ctx.fwd_ws
-        ws_b = N.size_query("hgsr_raster3d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
+        n_is = flatten_ids.numel() if ctx.deferred is None else ctx.deferred.n  # exact once resolved
+        ws_b = N.size_query("hgsr_raster3d_bwd_ws_bytes", C, Ng, D, n_is, int(fwd_ws is not None))
         ws, zeroed = _take_bwd_ws(ctx, ws_b, dev)
         v_rc, v_ra = _f32(v_rc), _f32(v_ra)
-        n_is = flatten_ids.numel() if ctx.deferred is None else ctx.deferred.n  # exact once resolved
         N.call("hgsr_raster3d_bwd_fused", C, Ng, Dc, ptr(means2d), ptr(conics), ptr(colors), int(col_shared),
                ptr(depths), int(expected_depth), ptr(opacities), int(op_shared), ptr(backgrounds), width, height,
                tile_size, tw, th, ptr(offsets), n_is, ptr(flatten_ids) if n_is else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_means2d), ptr(v_conics), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_abs), ptr(fwd_ws),
-               ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(), zeroed, N.stream(dev))
+               ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(), zeroed,
+               ptr(ctx.radii), N.stream(dev))
         if absgrad:
             means2d.absgrad = v_abs
         v_bg = None
         if backgrounds is not None and ctx.needs_input_grad[5]:
             v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))
         return (v_means2d, v_conics, v_colors, v_depths, v_opac, v_bg, None, None, None, None, None, None, None,
-                None, None, None)
+                None, None, None, None)
 
 
 def rasterize_to_pixels(means2d, conics, colors, opacities, image_width, image_height, tile_size, isect_offsets,
@@ -742,7 +748,7 @@ class _Raster2D(torch.autograd.Function):
         v_normals = torch.empty_like(normals)
         v_dens = torch.empty_like(means2d)
         fwd_ws = ctx.fwd_ws
-        ws_b = N.size_query("hgsr_raster2d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
+        ws_b = N.size_query("hgsr_raster2d_bwd_ws_bytes", C, Ng, D, flatten_ids.numel(), int(fwd_ws is not None))
         ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
         v_rc, v_ra, v_rn = (_f32(g if g is not None else torch.zeros(sh, dtype=torch.float32, device=dev))
                             for g, sh in zip((v_rc, v_ra, v_rn), ctx.out_shapes))
@@ -777,7 +783,7 @@ class _Raster2DFused(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means2d, rt, colors, depths, opacities, normals, densify, backgrounds, width, height,
                 tile_size, isect_offsets, flatten_ids, expected_depth, records=None, grad_mode=True, deferred=None,
-                frame=None):
+                frame=None, radii=None):
         """frame = (viewmats [C,4,4], Ks [C,3,3], normals_from_depth) with records: render_normals
         come out in world frame (the kernels apply R^T) and, with normals_from_depth, K13 runs on
         the depth channel here and is a sixth output whose gradient the raster backward adds to
@@ -802,8 +808,8 @@ class _Raster2DFused(torch.autograd.Function):
             # the forward's per-quadrant culling bits, read back by the backward
             q_b = N.size_query("hgsr_raster3d_qmask_bytes", C, tw, th, flatten_ids.numel())
             qmask = torch.empty(q_b, dtype=torch.uint8, device=dev)
-            # the backward's workspace, its accumulator rows cleared by this forward launch
-            bwd_ws = _bwd_ws("hgsr_raster2d_bwd_ws_bytes", ctx, C, Ng, D, dev, grad_mode)
+            # the backward's workspace, its gradient-slot flags cleared by this forward launch
+            bwd_ws = _bwd_ws("hgsr_raster2d_bwd_ws_bytes", ctx, C, Ng, D, flatten_ids.numel(), dev, grad_mode)
             N.call("hgsr_raster2d_fwd_packed", C, Ng, Dc, int(depths is not None), int(expected_depth),
                    ptr(backgrounds), width, height, tile_size, tw, th, ptr(isect_offsets), flatten_ids.numel(),
                    ptr(flatten_ids) if flatten_ids.numel() else None, ptr(rc), ptr(ra), ptr(rn), ptr(rd), ptr(rm),
@@ -826,6 +832,7 @@ class _Raster2DFused(torch.autograd.Function):
         ctx.qmask = qmask  # the forward's quadrant culling bits, reused by the backward
         ctx.deferred = deferred
         ctx.frame = frame
+        ctx.radii = None if radii is None else radii.detach().contiguous()
         nfd = None
         if frame is not None and frame[2] and depths is not None:
             # K13 on the rendered depth channel (read in place through its strides), world frame
@@ -856,11 +863,11 @@ class _Raster2DFused(torch.autograd.Function):
         v_normals = torch.empty_like(normals)
         v_dens = torch.empty_like(means2d)
         fwd_ws = ctx.fwd_ws
-        ws_b = N.size_query("hgsr_raster2d_bwd_ws_bytes", C, Ng, D, int(fwd_ws is not None))
+        n_is = flatten_ids.numel() if ctx.deferred is None else ctx.deferred.n  # exact once resolved
+        ws_b = N.size_query("hgsr_raster2d_bwd_ws_bytes", C, Ng, D, n_is, int(fwd_ws is not None))
         ws, zeroed = _take_bwd_ws(ctx, ws_b, dev)
         v_rc, v_ra, v_rn = (_f32(g if g is not None else torch.zeros(sh, dtype=torch.float32, device=dev))
                             for g, sh in zip((v_rc, v_ra, v_rn), ctx.out_shapes))
-        n_is = flatten_ids.numel() if ctx.deferred is None else ctx.deferred.n  # exact once resolved
         frame, v_dep = ctx.frame, None
         if v_nfd is not None:  # K13 backward: its depth gradient goes into the raster backward
             dch = rc[..., D - 1]
@@ -873,12 +880,12 @@ class _Raster2DFused(torch.autograd.Function):
                width, height, tile_size, tw, th, ptr(offsets), n_is, ptr(flatten_ids) if n_is else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_rn), ptr(v_means2d), ptr(v_rt), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_normals),
                ptr(v_dens), ptr(fwd_ws), ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(),
-               zeroed, None if frame is None else ptr(frame[0]), ptr(v_dep), N.stream(dev))
+               zeroed, None if frame is None else ptr(frame[0]), ptr(v_dep), ptr(ctx.radii), N.stream(dev))
         v_bg = None
         if backgrounds is not None and ctx.needs_input_grad[7]:
             v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))
         return (v_means2d, v_rt, v_colors, v_depths, v_opac, v_normals, v_dens, v_bg, None, None, None, None, None,
-                None, None, None, None, None)
+                None, None, None, None, None, None)
 
 
 def rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals, densify, image_width,
@@ -994,7 +1001,7 @@ def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, 
         d = _isect_emit_deferred(isect_state)
         if d is not None:  # emission, sort and forward queued; then the count is read
             render_colors, render_alphas = _Raster3DFused.apply(*r_in, *args, isect_offsets, d.flat, ed, absgrad,
-                                                                records, grad_mode, d)
+                                                                records, grad_mode, d, radii)
             if _isect_resolve(isect_state, d):
                 isect_ids, flatten_ids = d.ids[:d.n], d.flat[:d.n]
             else:
@@ -1002,7 +1009,7 @@ def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, 
         if d is None:
             tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
             render_colors, render_alphas = _Raster3DFused.apply(*r_in, *args, isect_offsets, flatten_ids, ed,
-                                                                absgrad, records, grad_mode)
+                                                                absgrad, records, grad_mode, None, radii)
         opac = opacities.expand(C, -1)
     else:
         tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
@@ -1138,14 +1145,15 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
         tpg, isect_offsets = isect_state[3], isect_state[4]
         d = _isect_emit_deferred(isect_state)
         if d is not None:  # emission, sort and forward queued; then the count is read
-            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, d.flat, ed, records, grad_mode, d, frame)
+            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, d.flat, ed, records, grad_mode, d, frame, radii)
             if _isect_resolve(isect_state, d):
                 isect_ids, flatten_ids = d.ids[:d.n], d.flat[:d.n]
             else:
                 d = None  # over capacity: redo at the exact size
         if d is None:
             tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
-            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, flatten_ids, ed, records, grad_mode, None, frame)
+            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, flatten_ids, ed, records, grad_mode, None, frame,
+                                        radii)
         render_colors, render_alphas, render_normals, render_distort, render_median, nfd_fused = outs
         fused_frame = frame is not None
     else:

@@ -428,6 +428,14 @@ class ShardedAdamDDP:
         for w in works:
             w.wait()
 
+    def flush(self) -> None:
+        """Make every parameter whole again: wait for the deferred all-gathers.  finish() returns
+        with the colours' all-gather still writing p.data (rasterization()'s parameter-ready hook
+        and the next begin() wait for it); call this before any other read of the parameters --
+        a checkpoint or PLY save, replica_digest / assert_replicas_agree, an evaluation render
+        outside gsplat_api."""
+        self.wait_deferred()
+
     def begin(self) -> None:
         if not self._active():
             return

@@ -170,8 +170,13 @@ int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, const float* co
  * v_opacities [C*N]; v_means2d_abs nullable (gsplat absgrad).  fwd_ws: the
  * workspace hgsr_raster3d_fwd filled for the same inputs (its packed records
  * are reused), or NULL to pack again.  ws: caller scratch of
- * hgsr_raster3d_bwd_ws_bytes(C, N, D, fwd_ws != NULL). */
-size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd);
+ * hgsr_raster3d_bwd_ws_bytes(C, N, D, n_isects, fwd_ws != NULL).
+ * Deterministic: every (tile, Gaussian) pair's per-wave partial sums go to the pair's own
+ * gradient slot and each Gaussian's slots are summed in one fixed order (no float atomics),
+ * so the same inputs give bit-identical gradients on every launch.  The slots follow each
+ * Gaussian's tile rectangle in isect_tiles order; this entry finds the rectangles from the
+ * lists (flatten_ids must come from isect_tiles: every Gaussian's tiles a full rectangle). */
+size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int64_t n_isects, int reuse_fwd);
 int hgsr_raster3d_bwd(int C, int N, int D, const float* means2d, const float* conics,
                       const float* colors, const float* opacities, const float* backgrounds,
                       int width, int height, int tile_size, int tile_w, int tile_h,
@@ -210,9 +215,10 @@ int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * buffer starts with the tiles' heaviest-first dispatch order and each tile's latest
  * contributor + 1, which the forward writes; the backward re-sorts the order by the ranges it
  * walks (placement only: no result depends on it).
- * bwd_ws (nullable, 16-B aligned, >= hgsr_raster3d_bwd_ws_bytes(C, N, D, 1)): the workspace
- * the backward will get; the forward clears its accumulator rows while it composites (HBM
- * is idle there), so hgsr_raster3d_bwd_fused given it with ws_zeroed = 1 skips its memset.
+ * bwd_ws (nullable, 16-B aligned, >= hgsr_raster3d_bwd_ws_bytes(C, N, D, n_isects, 1)): the
+ * workspace the backward will get; the forward clears its gradient-slot flags while it
+ * composites (HBM is idle there), so hgsr_raster3d_bwd_fused given it with ws_zeroed = 1 skips
+ * its memset.
  * isect_info (nullable): the deferred count of hgsr_isect_emit_sorted (n_isects is then the
  * capacity the intersection arrays and qmask were sized for); the quadrant-mask stride is
  * derived from qmask_bytes, so the backward must get the same buffer and size. */
@@ -231,7 +237,11 @@ int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_
 /* vjp of hgsr_raster3d_fwd_fused: v_colors in the colours' layout (shared colours
  * summed over cameras in camera order), v_depths [C,N] (when depths), v_opacities
  * in the opacities' layout; render_colors is the forward output (needed for ED);
- * qmask (nullable): the buffer hgsr_raster3d_fwd_packed filled for the same lists. */
+ * qmask (nullable): the buffer hgsr_raster3d_fwd_packed filled for the same lists.
+ * radii (nullable, [C,N] int32): the projection's radii the lists were emitted from
+ * (isect_tiles(means2d, radii, ...)); given, the gradient slots come from the tile rectangles
+ * directly instead of from a pass over the lists.  ws: hgsr_raster3d_bwd_ws_bytes(C, N,
+ * Dc + (depths ? 1 : 0), n_isects, fwd_ws != NULL). */
 int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* conics,
                             const float* colors, int colors_shared, const float* depths,
                             int expected_depth, const float* opacities, int opacities_shared,
@@ -243,7 +253,7 @@ int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             float* v_means2d, float* v_conics, float* v_colors, float* v_depths,
                             float* v_opacities, float* v_means2d_abs, const void* fwd_ws, void* ws,
                             size_t ws_bytes, const void* qmask, size_t qmask_bytes, int ws_zeroed,
-                            hgsr_stream_t stream);
+                            const int32_t* radii, hgsr_stream_t stream);
 
 /* ---- K11/K12: 2DGS surfel rasterization -----------------------------------
  * replaces gsplat rasterize_to_pixels_2dgs.  The LAST colour channel is the
@@ -262,8 +272,9 @@ int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, const float* ra
                       hgsr_stream_t stream);
 /* writes (overwrites) v_means2d [C*N,2], v_ray_transforms [C*N,9], v_colors [C*N,D],
  * v_opacities [C*N], v_normals [C*N,3], v_densify [C*N,2] (d loss / d screen
- * translation; nullable). */
-size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int reuse_fwd);
+ * translation; nullable).  Deterministic gradient slots as hgsr_raster3d_bwd; ws:
+ * hgsr_raster2d_bwd_ws_bytes(C, N, D, n_isects, fwd_ws != NULL). */
+size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int64_t n_isects, int reuse_fwd);
 int hgsr_raster2d_bwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
                       const float* colors, const float* opacities, const float* normals,
                       const float* backgrounds, int width, int height, int tile_size,
@@ -293,7 +304,7 @@ int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * qmask (nullable; size hgsr_raster3d_qmask_bytes, the same layout): the forward's
  * per-quadrant culling bits, read by hgsr_raster2d_bwd_fused instead of repeating the tests.
  * bwd_ws / ws_zeroed / isect_info: as hgsr_raster3d_fwd_packed (size
- * hgsr_raster2d_bwd_ws_bytes(C, N, D, 1)).
+ * hgsr_raster2d_bwd_ws_bytes(C, N, D, n_isects, 1)).
  * normal_rot (nullable, the viewmats [C,4,4]): render_normals are written in world frame,
  * R^T n (rasterization_2dgs' frame), and hgsr_raster2d_bwd_fused given the same matrices
  * takes world-frame v_render_normals.  v_depth_extra (nullable, [C,H,W]): a second gradient
@@ -324,7 +335,8 @@ int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             float* v_colors, float* v_depths, float* v_opacities, float* v_normals,
                             float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
                             const void* qmask, size_t qmask_bytes, int ws_zeroed,
-                            const float* normal_rot, const float* v_depth_extra, hgsr_stream_t stream);
+                            const float* normal_rot, const float* v_depth_extra, const int32_t* radii,
+                            hgsr_stream_t stream);
 
 /* ---- K14: anchor -> neural-Gaussian decode --------------
  * replaces scene/lod_model.py:286-290 set_anchor_mask (LoD mask, dist2level

@@ -58,9 +58,12 @@ def test_pure_host_entry_points(lib):
     assert _native.size_query("hgsr_isect_ws1_bytes", 1, 2_000_000, 120, 68) > 0
     assert _native.size_query("hgsr_isect_ws2_bytes", 1000, 10) >= 8000
     assert _native.size_query("hgsr_isect_ws2_bytes", 1000, 5000) >= 16000
-    assert _native.size_query("hgsr_raster3d_bwd_ws_bytes", 1, 100, 4, 0) >= 100 * 12 * 4 + 100 * 48
-    assert _native.size_query("hgsr_raster3d_bwd_ws_bytes", 1, 100, 4, 1) >= 100 * 12 * 4
-    assert _native.size_query("hgsr_raster2d_bwd_ws_bytes", 1, 100, 4, 0) >= 100 * 24 * 4 + 100 * 96
+    # raster backwards' gradient slots: 3DGS 4 flags + 4 partial rows of 64 B per intersection,
+    # 2DGS (waves merged in LDS) 1 flag + one 80-B row; per Gaussian the slot index (seg, base)
+    # and, unless reused, the packed record
+    assert _native.size_query("hgsr_raster3d_bwd_ws_bytes", 1, 100, 4, 500, 0) >= 500 * 4 * (1 + 64) + 100 * (12 + 48)
+    assert _native.size_query("hgsr_raster3d_bwd_ws_bytes", 1, 100, 4, 500, 1) >= 500 * 4 * (1 + 64) + 100 * 12
+    assert _native.size_query("hgsr_raster2d_bwd_ws_bytes", 1, 100, 4, 500, 0) >= 500 * (1 + 80) + 100 * (12 + 96)
 
 
 def test_invalid_args_return_status(lib):

@@ -91,3 +91,24 @@ def test_failed_stage_stops_its_chunk(tmp_path):
         run_chunks(chunk_ids(1, 2), ["0", "0"], cmd, env=env, timeout=300)
     assert os.path.exists(os.path.join(out, "0_0", "fine", "point_cloud_explicit.ply"))
     assert not os.path.exists(os.path.join(out, "0_1", "fine"))
+
+
+def test_launch_errors_fail_their_chunk(tmp_path):
+    """A stage whose executable does not exist, or whose command() raises, is a failed stage
+    (ADVICE r05): the launcher still runs the other chunks and raises naming the chunks, instead
+    of losing them with the slot thread."""
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    out = str(tmp_path / "o")
+
+    def cmd(c, st):
+        if c == "0_0":
+            return [str(tmp_path / "no_such_binary")]
+        if c == "0_1":
+            raise ValueError("bad chunk config")
+        return _cmd(out, ["--dry"])(c, st)
+
+    with pytest.raises(RuntimeError) as ei:
+        run_chunks(chunk_ids(1, 3), ["0"], cmd, env=env, timeout=300)
+    msg = str(ei.value)
+    assert "0_0" in msg and "0_1" in msg and "bad chunk config" in msg and "0_2" not in msg.split("never run")[0]
+    assert os.path.exists(os.path.join(out, "0_2", "fine", "point_cloud_explicit.ply"))
