@@ -158,12 +158,31 @@ int launch_tile_order(int64_t n_bins, const int32_t* offsets, int64_t n_isects, 
 // tile's workgroup) and flags[kSlotWaves e + w] != 0 iff wave w wrote row (e, w) in this launch
 // (both raster backwards).
 constexpr int kSlotWaves = 4;
+// A (camera, Gaussian) with more than kBigSlots slots (a footprint over kBigSlots tiles: close
+// views put Gaussians over the whole screen, 8,160 tiles at 1080p) is reduced in pieces of
+// kPieceSlots slots, one wave each (reduce_pieces), instead of by the wave that owns it: a wave
+// walking 8,160 slots alone held the whole reduction's tail (split3 0.28 ms at c2).
+constexpr int kBigSlots = 32;
+constexpr int kPieceSlots = 128;
+constexpr int kPieceFloats = 20;  // floats per piece partial (>= the rows' used values, 16-B aligned)
 struct GradSlots {
-    int32_t* seg;  // [C N + 1]
-    int2* slot;    // [C N]
+    int32_t* seg;     // [C N + 1]
+    int2* slot;       // [C N]
+    int32_t* pbase;   // [C N]: first piece of a big entry, -1 for the others
+    int32_t* pieces;  // [piece capacity]: the entry of each piece (order of no consequence)
+    int32_t* npieces; // [1]: pieces listed
+    float* partial;   // [piece capacity][kPieceFloats]: each piece's fixed-order sum
+    int64_t cap;      // piece capacity
 };
+// piece capacity for n_isects slots: sum over big entries of ceil(slots / kPieceSlots)
+inline int64_t piece_capacity(int64_t n_isects) { return n_isects / kPieceSlots + n_isects / (kBigSlots + 1) + 4; }
+// reduce_pieces_kernel's grid: 4 waves per workgroup striding over the device-side piece count
+inline unsigned piece_grid(const GradSlots& g) {
+    const int64_t w = (g.cap + 3) / 4;
+    return (unsigned)(w < 2048 ? (w > 0 ? w : 1) : 2048);
+}
 // bytes of launch_grad_slots' buffer (from_lists: the rectangles are found from the lists)
-size_t grad_slot_bytes(int64_t CN, bool from_lists);
+size_t grad_slot_bytes(int64_t CN, bool from_lists, int64_t n_isects);
 // radii != nullptr: rectangles from means2d / radii (isect_tiles'); else from the sorted lists
 int launch_grad_slots(int C, int N, const float* means2d, const int32_t* radii, int tile_size, int tw, int th,
                       const int32_t* offsets, const int32_t* flatten_ids, int64_t n_isects, void* buf,
@@ -177,64 +196,110 @@ inline size_t slot_flag_bytes(int64_t n_isects, int ways) { return ((size_t)n_is
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // The splits' fixed-order sum of gradient slots, for one wave owning the nloc (1..64)
-// (camera, Gaussian) entries [ib, ib + nloc): the wave walks their contiguous slot range 64 slots
-// at a time.  Each slot has WAYS partial rows of ROWF floats (the first NV used, R4 float4) and
-// WAYS flag bytes; LPR consecutive lanes read one row (one coalesced request per row, 64 / LPR
-// rows per load instruction, all of a chunk's loads issued before any is summed), sum the slot's
-// flagged rows in way order and park the sums in the wave's LDS area; then each entry's lane adds
-// its own slots' sums in slot order, the next chunk's flags already in flight.  No atomics: the
-// result depends only on the inputs.
-template <int NV, int R4, int ROWF, int WAYS>
+// (camera, Gaussian) entries [ib, ib + nloc), whose slots [E0, E1) are contiguous.  Each slot has
+// WAYS partial rows of ROWF floats (the first NV used, R4 float4) and WAYS flag bytes (row (e, w)
+// written iff flags[WAYS e + w] != 0).  The wave walks [E0, E1) 64 slots at a time:
+//   * the chunk's flagged rows are listed way-major in LDS (one ballot per way);
+//   * R4 consecutive lanes load one listed row (64 / R4 rows per load instruction, every lane
+//     useful whatever fraction of rows is flagged), up to kSlotCap rows per round, all issued
+//     before any is used, the next chunk's flags behind them; the rows are parked in LDS;
+//   * lane s sums slot s's rows in way order (the list is way-major, so rounds keep that order);
+//   * each entry's lane then adds its own slots' sums in slot order.
+// No atomics anywhere: the result depends only on the inputs.  LDS per wave: s_list (256 B) and
+// reduce_slots_floats() floats of scratch (the parked rows, then the slot sums).
+template <int NV, int R4, int CAP>
+constexpr int reduce_slots_floats() {
+    return CAP * R4 * 4 > NV * 65 ? CAP * R4 * 4 : NV * 65;
+}
+__device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v = min(v, __shfl_xor(v, d));
+    return v;
+}
+template <int NV, int R4, int ROWF, int WAYS, int CAP>
 __device__ __forceinline__ void reduce_slots(const float* __restrict__ rows, const uint8_t* __restrict__ flags,
-                                             const int32_t* __restrict__ seg, int64_t ib, int nloc,
-                                             float (*s_v)[65], float (&out)[NV]) {
-    static_assert(WAYS == 1 || WAYS == 4, "slot ways");
-    static_assert(R4 <= 8 && NV <= 4 * R4, "row shape");
-    constexpr int LPR = R4 <= 4 ? 4 : 8;  // lanes per row
-    constexpr int SPI = 64 / LPR;         // slots per load instruction
-    constexpr int G = LPR;                // slot groups per 64-slot chunk
-    constexpr int GB = 4;                 // slot groups whose loads are issued together
+                                             const int32_t* __restrict__ seg, const int32_t* __restrict__ pbase,
+                                             const float* __restrict__ partial, int64_t ib, int nloc,
+                                             uint8_t* s_list, float* s_scr, float (&out)[NV]) {
+    static_assert(WAYS >= 1 && WAYS <= 4 && NV <= 4 * R4 && R4 <= 8, "slot rows");
+    constexpr int RPI = 64 / R4;                  // rows per load instruction
+    constexpr int MAXI = (CAP + RPI - 1) / RPI;   // load instructions per round
+    float4* const s_rows = reinterpret_cast<float4*>(s_scr);  // [CAP][R4] during the rounds
+    float(*const s_v)[65] = reinterpret_cast<float(*)[65]>(s_scr);  // [NV][65] after them
     const int lane = threadIdx.x & 63;
-    const int q = lane & (LPR - 1), sl = lane / LPR;
+    const int q = lane % R4, jl = lane / R4;
     const bool live = lane < nloc;
-    const int32_t lo_e = live ? seg[ib + lane] : 0, hi_e = live ? seg[ib + lane + 1] : 0;
-    const int32_t E0 = __builtin_amdgcn_readfirstlane(lo_e), E1 = seg[ib + nloc];
+    const int32_t pb = live ? pbase[ib + lane] : -1;
+    // a big entry's slots are reduced in pieces: the walker skips them
+    const int32_t lo_e = (live && pb < 0) ? seg[ib + lane] : 0, hi_e = (live && pb < 0) ? seg[ib + lane + 1] : 0;
+    const int32_t E1 = seg[ib + nloc];
     auto fl = [&](int32_t e) -> uint32_t {
         if (e >= E1) return 0u;
         return WAYS == 4 ? reinterpret_cast<const uint32_t*>(flags)[e] : (uint32_t)flags[e];
     };
 #pragma unroll
     for (int k = 0; k < NV; ++k) out[k] = 0.f;
-    uint32_t fc = fl(E0 + lane);  // flags of slot cs + lane
-    for (int32_t cs = E0; cs < E1; cs += 64) {
-        const uint32_t fcur = fc;
-        fc = fl(cs + 64 + lane);  // the next chunk's, in flight while this one is summed
+    constexpr int32_t kNone = 0x7fffffff;
+    // the chunks walked: 64 slots from the first small entry's first slot, then from the next
+    // slot any small entry still needs (entries' slot ranges are ascending and disjoint)
+    int32_t cs = wave_min_i32(lo_e < hi_e ? lo_e : kNone);
+    uint32_t fc = cs != kNone ? fl(cs + lane) : 0u;  // flags of slot cs + lane
+    while (cs != kNone) {
+        const int32_t cn = wave_min_i32(hi_e > cs + 64 ? max(lo_e, cs + 64) : kNone);  // the next chunk
+        const uint32_t f = fc;
+        // way-major list of the chunk's flagged rows: entry = slot | way << 6
+        int n = 0, pos[WAYS];
 #pragma unroll
-        for (int g0 = 0; g0 < G; g0 += GB) {
-            float4 x[GB][WAYS];
+        for (int w = 0; w < WAYS; ++w) {
+            const bool has = (f >> (8 * w)) & 0xffu;
+            const uint64_t bw = __ballot(has);
+            pos[w] = has ? n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bw >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bw, 0))
+                         : -1;
+            if (has) s_list[pos[w]] = (uint8_t)(lane | (w << 6));
+            n += __popcll(bw);
+        }
+        wave_lds_sync();
+        float4 acc[R4];
 #pragma unroll
-            for (int gb = 0; gb < GB; ++gb) {
-                const int s = (g0 + gb) * SPI + sl;
-                const uint32_t f = (uint32_t)__shfl((int)fcur, s);
+        for (int r = 0; r < R4; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int base = 0; base < n; base += CAP) {
+            const int cnt = min(CAP, n - base);
+            float4 x[MAXI];
 #pragma unroll
-                for (int w = 0; w < WAYS; ++w) {
-                    x[gb][w] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (q < R4 && ((f >> (8 * w)) & 0xffu))
-                        x[gb][w] = reinterpret_cast<const float4*>(rows + ((int64_t)(cs + s) * WAYS + w) * ROWF)[q];
+            for (int i = 0; i < MAXI; ++i) {
+                const int j = i * RPI + jl;
+                x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (jl < RPI && j < cnt) {
+                    const int ent = s_list[base + j];
+                    x[i] = reinterpret_cast<const float4*>(
+                        rows + ((int64_t)(cs + (ent & 63)) * WAYS + (ent >> 6)) * ROWF)[q];
                 }
             }
+            if (base == 0 && cn != kNone) fc = fl(cn + lane);  // the next chunk's flags, behind this round's rows
 #pragma unroll
-            for (int gb = 0; gb < GB; ++gb) {
-                float4 a = x[gb][0];
-#pragma unroll
-                for (int w = 1; w < WAYS; ++w)
-                    a = make_float4(a.x + x[gb][w].x, a.y + x[gb][w].y, a.z + x[gb][w].z, a.w + x[gb][w].w);
-                const int s = (g0 + gb) * SPI + sl;
-                const float av[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (q < R4 && 4 * q + c < NV) s_v[4 * q + c][s] = av[c];
+            for (int i = 0; i < MAXI; ++i) {
+                const int j = i * RPI + jl;
+                if (jl < RPI && j < cnt) s_rows[j * R4 + q] = x[i];
             }
+            wave_lds_sync();
+#pragma unroll
+            for (int w = 0; w < WAYS; ++w)
+                if (pos[w] >= base && pos[w] < base + cnt)
+#pragma unroll
+                    for (int r = 0; r < R4; ++r) {
+                        const float4 y = s_rows[(pos[w] - base) * R4 + r];
+                        acc[r] = make_float4(acc[r].x + y.x, acc[r].y + y.y, acc[r].z + y.z, acc[r].w + y.w);
+                    }
+            wave_lds_sync();
+        }
+        if (n == 0 && cn != kNone) fc = fl(cn + lane);
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+            const float a4[4] = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (4 * r + c < NV) s_v[4 * r + c][lane] = a4[c];
         }
         wave_lds_sync();
         const int32_t lo = max(lo_e, cs), hi = min(hi_e, cs + 64);
@@ -242,6 +307,74 @@ __device__ __forceinline__ void reduce_slots(const float* __restrict__ rows, con
 #pragma unroll
             for (int k = 0; k < NV; ++k) out[k] += s_v[k][y - cs];
         wave_lds_sync();
+        cs = cn;
+    }
+    if (pb >= 0) {  // a big entry: its pieces' partials in piece order
+        const int32_t np = (seg[ib + lane + 1] - seg[ib + lane] + kPieceSlots - 1) / kPieceSlots;
+        for (int32_t j = 0; j < np; ++j) {
+            const float4* pp = reinterpret_cast<const float4*>(partial + (int64_t)(pb + j) * kPieceFloats);
+#pragma unroll
+            for (int r = 0; r < (NV + 3) / 4; ++r) {
+                const float4 y = pp[r];
+                const float y4[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (4 * r + c < NV) out[4 * r + c] += y4[c];
+            }
+        }
+    }
+}
+
+// One wave per piece of a big entry's slots (listed by launch_grad_slots): lane l sums slots
+// s0 + l and s0 + 64 + l (each slot's flagged rows in way order), then a fixed DPP tree over the
+// 64 lanes; partial[k] = the piece's NV sums.  Grid-stride over the device-side piece count.
+template <int NV, int R4, int ROWF, int WAYS>
+__global__ __launch_bounds__(256) void reduce_pieces_kernel(const float* __restrict__ rows,
+                                                            const uint8_t* __restrict__ flags,
+                                                            const int32_t* __restrict__ seg,
+                                                            const int32_t* __restrict__ pbase,
+                                                            const int32_t* __restrict__ pieces,
+                                                            const int32_t* __restrict__ npieces,
+                                                            float* __restrict__ partial) {
+    static_assert(kPieceSlots == 128 && NV <= kPieceFloats, "piece shape");
+    const int lane = threadIdx.x & 63;
+    const int n = *npieces;
+    const int nw = gridDim.x * 4;
+    for (int k = blockIdx.x * 4 + (threadIdx.x >> 6); k < n; k += nw) {
+        const int32_t o = pieces[k];
+        const int32_t j = k - pbase[o];
+        const int32_t s0 = seg[o] + j * kPieceSlots, s1 = min(seg[o + 1], s0 + kPieceSlots);
+        float4 acc[R4];
+#pragma unroll
+        for (int r = 0; r < R4; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const int32_t e = s0 + 64 * m + lane;
+            const uint32_t f = e < s1 ? (WAYS == 4 ? reinterpret_cast<const uint32_t*>(flags)[e] : (uint32_t)flags[e]) : 0u;
+#pragma unroll
+            for (int w = 0; w < WAYS; ++w)
+                if ((f >> (8 * w)) & 0xffu) {
+                    const float4* rp = reinterpret_cast<const float4*>(rows + ((int64_t)e * WAYS + w) * ROWF);
+#pragma unroll
+                    for (int r = 0; r < R4; ++r) {
+                        const float4 y = rp[r];
+                        acc[r] = make_float4(acc[r].x + y.x, acc[r].y + y.y, acc[r].z + y.z, acc[r].w + y.w);
+                    }
+                }
+        }
+        float v[4 * R4];
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+            v[4 * r] = wave_sum_to_lane63(acc[r].x);
+            v[4 * r + 1] = wave_sum_to_lane63(acc[r].y);
+            v[4 * r + 2] = wave_sum_to_lane63(acc[r].z);
+            v[4 * r + 3] = wave_sum_to_lane63(acc[r].w);
+        }
+        if (lane == 63) {
+            float4* pp = reinterpret_cast<float4*>(partial + (int64_t)k * kPieceFloats);
+#pragma unroll
+            for (int r = 0; r < R4; ++r) pp[r] = make_float4(v[4 * r], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
+        }
     }
 }
 

@@ -1050,9 +1050,10 @@ __global__ __launch_bounds__(256) void slot_sum_kernel(int64_t CN, R rect, int32
     if (threadIdx.x == 0) bsum[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// stage B: one workgroup, exclusive scan of the block totals in place; seg[CN] = the total
+// stage B: one workgroup, exclusive scan of the block totals in place; seg[CN] = the total; the
+// piece count cleared for stage C
 __global__ __launch_bounds__(1024) void slot_scan_kernel(int nb, int32_t* __restrict__ bsum,
-                                                         int32_t* __restrict__ seg_end) {
+                                                         int32_t* __restrict__ seg_end, int32_t* __restrict__ npieces) {
     __shared__ int32_t s_w[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int per = (nb + 1023) / 1024;
@@ -1079,30 +1080,35 @@ __global__ __launch_bounds__(1024) void slot_scan_kernel(int nb, int32_t* __rest
         bsum[i] = run;
         run += v;
     }
-    if (tid == 0) *seg_end = total;
+    if (tid == 0) {
+        *seg_end = total;
+        *npieces = 0;
+    }
 }
 
 // stage C: per block, the exclusive prefix of the areas (eight block-wide scans over the
 // coalesced rows o0 + 256 k + tid, k = 0..7) plus the block's offset -> seg and slot of every entry
 template <typename R>
 __global__ __launch_bounds__(256) void slot_write_kernel(int64_t CN, R rect, const int32_t* __restrict__ bpre,
-                                                         int32_t* __restrict__ seg, int2* __restrict__ slot) {
+                                                         int32_t* __restrict__ seg, int2* __restrict__ slot,
+                                                         int32_t* __restrict__ pbase, int32_t* __restrict__ pieces,
+                                                         int32_t* __restrict__ npieces, int64_t piece_cap) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t o0 = (int64_t)blockIdx.x * kSlotPer + tid;
-    int a[8], x0[8], y0[8], w[8];
+    int area[8], sa[8], x0[8], y0[8], w[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] = o0 + 256 * k < CN ? rect(o0 + 256 * k, x0[k], y0[k], w[k]) : 0;
+    for (int k = 0; k < 8; ++k) area[k] = o0 + 256 * k < CN ? rect(o0 + 256 * k, x0[k], y0[k], w[k]) : 0;
     __shared__ int s_w[8][4];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        int inc = a[k];
+        int inc = area[k];
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const int o = __shfl_up(inc, d);
             if (lane >= d) inc += o;
         }
         if (lane == 63) s_w[k][wave] = inc;
-        a[k] = inc - a[k];  // exclusive within the wave
+        sa[k] = inc - area[k];  // exclusive within the wave
     }
     __syncthreads();
     int run = bpre[blockIdx.x];
@@ -1116,9 +1122,21 @@ __global__ __launch_bounds__(256) void slot_write_kernel(int64_t CN, R rect, con
         }
         const int64_t o = o0 + 256 * k;
         if (o < CN) {
-            const int e = pre + a[k];
+            const int e = pre + sa[k];
             seg[o] = e;
             slot[o] = make_int2(e - y0[k] * w[k] - x0[k], w[k]);
+            // a big entry lists its pieces (where in the list is of no consequence: each piece is
+            // reduced on its own and the pieces are summed in piece order)
+            int32_t pb = -1;
+            if (area[k] > kBigSlots) {
+                const int np = (area[k] + kPieceSlots - 1) / kPieceSlots;
+                pb = atomicAdd(npieces, np);
+                if (pb + np <= piece_cap)
+                    for (int j = 0; j < np; ++j) pieces[pb + j] = (int32_t)o;
+                else
+                    pb = -1;  // (cannot happen within piece_capacity; the walker then takes it)
+            }
+            pbase[o] = pb;
         }
     }
 }
@@ -1148,9 +1166,10 @@ __global__ void fill_i32_kernel(int64_t n, int32_t* __restrict__ p, int32_t v) {
 
 static size_t align256_(size_t x) { return (x + 255) & ~(size_t)255; }
 
-size_t hgsr::grad_slot_bytes(int64_t CN, bool from_lists) {
-    const int64_t nb = (CN + kSlotPer - 1) / kSlotPer;
+size_t hgsr::grad_slot_bytes(int64_t CN, bool from_lists, int64_t n_isects) {
+    const int64_t nb = (CN + kSlotPer - 1) / kSlotPer, pc = piece_capacity(n_isects);
     size_t b = align256_((size_t)(CN + 1) * 4) + align256_((size_t)CN * 8) + align256_((size_t)(nb + 1) * 4);
+    b += align256_((size_t)CN * 4) + align256_((size_t)pc * 4) + 256 + align256_((size_t)pc * kPieceFloats * 4);
     if (from_lists) b += 2 * align256_((size_t)CN * 4);
     return b;
 }
@@ -1167,15 +1186,28 @@ int hgsr::launch_grad_slots(int C, int N, const float* means2d, const int32_t* r
     p += align256_((size_t)CN * 8);
     int32_t* bsum = (int32_t*)p;
     p += align256_((size_t)(nb + 1) * 4);
+    out.cap = piece_capacity(n_isects);
+    out.pbase = (int32_t*)p;
+    p += align256_((size_t)CN * 4);
+    out.pieces = (int32_t*)p;
+    p += align256_((size_t)out.cap * 4);
+    out.npieces = (int32_t*)p;
+    p += 256;
+    out.partial = (float*)p;
+    p += align256_((size_t)out.cap * kPieceFloats * 4);
     HGSR_REQUIRE(nb < (1ll << 31), "too many Gaussians for the gradient slots");
-    if (CN == 0) return memset_async(out.seg, 4, s, "grad_slots");
+    if (CN == 0) {
+        if (int st = memset_async(out.npieces, 4, s, "grad_slots")) return st;
+        return memset_async(out.seg, 4, s, "grad_slots");
+    }
     const dim3 grid((unsigned)nb);
     if (radii) {
         HGSR_REQUIRE(means2d, "null pointer");
         const RectFromRadii r{reinterpret_cast<const float2*>(means2d), radii, tile_size, tw, th};
         hipLaunchKernelGGL(slot_sum_kernel<RectFromRadii>, grid, dim3(256), 0, s, CN, r, bsum);
-        hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bsum, out.seg + CN);
-        hipLaunchKernelGGL(slot_write_kernel<RectFromRadii>, grid, dim3(256), 0, s, CN, r, bsum, out.seg, out.slot);
+        hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bsum, out.seg + CN, out.npieces);
+        hipLaunchKernelGGL(slot_write_kernel<RectFromRadii>, grid, dim3(256), 0, s, CN, r, bsum, out.seg, out.slot,
+                           out.pbase, out.pieces, out.npieces, out.cap);
     } else {
         HGSR_REQUIRE(offsets && (n_isects == 0 || flatten_ids), "null pointer");
         int32_t* tmin = (int32_t*)p;
@@ -1189,8 +1221,9 @@ int hgsr::launch_grad_slots(int C, int N, const float* means2d, const int32_t* r
                                flatten_ids, tmin, tmax);
         const RectFromTiles r{tmin, tmax, tw};
         hipLaunchKernelGGL(slot_sum_kernel<RectFromTiles>, grid, dim3(256), 0, s, CN, r, bsum);
-        hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bsum, out.seg + CN);
-        hipLaunchKernelGGL(slot_write_kernel<RectFromTiles>, grid, dim3(256), 0, s, CN, r, bsum, out.seg, out.slot);
+        hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bsum, out.seg + CN, out.npieces);
+        hipLaunchKernelGGL(slot_write_kernel<RectFromTiles>, grid, dim3(256), 0, s, CN, r, bsum, out.seg, out.slot,
+                           out.pbase, out.pieces, out.npieces, out.cap);
     }
     return check_launch("grad_slots");
 }

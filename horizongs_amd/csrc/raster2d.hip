@@ -750,12 +750,15 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
 template <int D>
 __global__ __launch_bounds__(256) void split2_kernel(int C, int N, const float* __restrict__ rows,
                                                     const uint8_t* __restrict__ flags, const int32_t* __restrict__ seg,
+                                                     const int32_t* __restrict__ pbase, const float* __restrict__ partial,
                                                     const float* __restrict__ rt, const float2* __restrict__ means2d,
                                                     float2* __restrict__ v_means2d, float* __restrict__ v_rt,
                                                     ChanDst cd, float* __restrict__ v_normals,
                                                     float2* __restrict__ v_densify) {
     constexpr int KV = 15 + D;
-    __shared__ float s_v[4][KV][65];  // per wave (each wave owns 64 surfels)
+    constexpr int kCap = 64, kScr = reduce_slots_floats<KV, (KV + 3) / 4, kCap>();
+    __shared__ uint8_t s_list[4][256];  // per wave (each wave owns 64 surfels)
+    __shared__ __attribute__((aligned(16))) float s_scr[4][kScr];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t g0 = ((int64_t)blockIdx.x * 4 + wave) * 64, g = g0 + lane;
     if (g0 >= N) return;  // wave-uniform; the waves never synchronise with each other
@@ -765,7 +768,8 @@ __global__ __launch_bounds__(256) void split2_kernel(int C, int N, const float* 
     for (int c = 0; c < C; ++c) {
         const int64_t i = (int64_t)c * N + g;
         float r[KV];
-        reduce_slots<KV, (KV + 3) / 4, kRow2, kSlotWaves>(rows, flags, seg, (int64_t)c * N + g0, nloc, s_v[wave], r);
+        reduce_slots<KV, (KV + 3) / 4, kRow2, kSlotWaves, kCap>(rows, flags, seg, pbase, partial, (int64_t)c * N + g0, nloc,
+                                                                s_list[wave], s_scr[wave], r);
         if (!live) continue;
         double u[3], v[3], w[3], gA[3], gB[3], gC[3];
         const float2 mm = means2d[i];
@@ -1013,7 +1017,7 @@ static size_t rows2_bytes(int64_t n_isects) {
 
 extern "C" size_t hgsr_raster2d_bwd_ws_bytes(int C, int N, int D, int64_t n_isects, int reuse_fwd) {
     (void)D;
-    return slot_flag_bytes(n_isects, kSlotWaves) + rows2_bytes(n_isects) + grad_slot_bytes((int64_t)C * N, true) +
+    return slot_flag_bytes(n_isects, kSlotWaves) + rows2_bytes(n_isects) + grad_slot_bytes((int64_t)C * N, true, n_isects) +
            (reuse_fwd ? 0 : rec2_bytes(C, N));
 }
 
@@ -1064,7 +1068,7 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         return st;
     const Rec2* rec = (const Rec2*)fwd_ws;
     if (!rec) {
-        Rec2* own = (Rec2*)(sbuf + grad_slot_bytes(n, true));
+        Rec2* own = (Rec2*)(sbuf + grad_slot_bytes(n, true, n_isects));
         if (int st = pack2(C, N, D, means2d, rt, cs, normals, own, s)) return st;
         rec = own;
     }
@@ -1088,8 +1092,10 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                            render_alphas, last_ids, v_render_colors, v_render_alphas, v_render_normals, rows,      \
                            flags, gs.slot, n_isects, pairs, qmask, qstride, normal_rot, v_depth_extra, order);     \
     }                                                                                                             \
+    hipLaunchKernelGGL((reduce_pieces_kernel<15 + DD, (15 + DD + 3) / 4, kRow2, kSlotWaves>), dim3(piece_grid(gs)), \
+                       dim3(256), 0, s, rows, flags, gs.seg, gs.pbase, gs.pieces, gs.npieces, gs.partial);          \
     hipLaunchKernelGGL((split2_kernel<DD>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, N,    \
-                       rows, flags, gs.seg, rt, m2,                                                                \
+                       rows, flags, gs.seg, gs.pbase, gs.partial, rt, m2,                                          \
                        reinterpret_cast<float2*>(v_means2d), v_rt, cd, v_normals, reinterpret_cast<float2*>(v_densify))
     switch (D) {
         case 1: LAUNCH_B2(1); break;

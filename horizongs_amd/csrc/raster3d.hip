@@ -710,10 +710,14 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
 template <int D, bool ABS>
 __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* __restrict__ rows,
                                                      const uint8_t* __restrict__ flags, const int32_t* __restrict__ seg,
-                                                     const Rec3* __restrict__ rec, const float* __restrict__ conics,
+                                                     const int32_t* __restrict__ pbase, const float* __restrict__ partial,
+                                                     const float* __restrict__ opac, int64_t op_cstride,
+                                                     const float* __restrict__ conics,
                                                      float2* __restrict__ v_means2d, float* __restrict__ v_conics,
                                                      ChanDst cd, float2* __restrict__ v_abs) {
-    __shared__ float s_v[4][12][65];  // per wave (each wave owns 64 Gaussians)
+    constexpr int kCap = 128, kScr = reduce_slots_floats<12, 3, kCap>();
+    __shared__ uint8_t s_list[4][256];  // per wave (each wave owns 64 Gaussians)
+    __shared__ __attribute__((aligned(16))) float s_scr[4][kScr];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t g0 = ((int64_t)blockIdx.x * 4 + wave) * 64, g = g0 + lane;
     if (g0 >= N) return;  // wave-uniform; the waves never synchronise with each other
@@ -723,7 +727,8 @@ __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* 
     for (int c = 0; c < C; ++c) {
         const int64_t i = (int64_t)c * N + g;
         float r[12];
-        reduce_slots<12, 3, kRow3, kSlotWaves>(rows, flags, seg, (int64_t)c * N + g0, nloc, s_v[wave], r);
+        reduce_slots<12, 3, kRow3, kSlotWaves, kCap>(rows, flags, seg, pbase, partial, (int64_t)c * N + g0, nloc, s_list[wave],
+                                                     s_scr[wave], r);
         if (!live) continue;
         const float qa = conics[i * 3], qb = conics[i * 3 + 1], qc = conics[i * 3 + 2];
         v_means2d[i] = make_float2(qa * r[0] + qb * r[1], qb * r[0] + qc * r[1]);
@@ -731,7 +736,8 @@ __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* 
         v_conics[i * 3 + 1] = r[3];
         v_conics[i * 3 + 2] = 0.5f * r[4];
         // S0 != 0 only if the Gaussian composited somewhere, i.e. opacity >= 1/255
-        const float v_op = r[5] != 0.f ? -r[5] / rec[i].g1.y : 0.f;
+        // (the records' opacity, read from its coalesced source instead of a 48-B record each)
+        const float v_op = r[5] != 0.f ? -r[5] / opac[c * op_cstride + g] : 0.f;
         if (cd.op_shared) op_sum += v_op;
         else cd.opac[i] = v_op;
 #pragma unroll
@@ -932,7 +938,7 @@ static size_t rows3_bytes(int64_t n_isects) {
 
 extern "C" size_t hgsr_raster3d_bwd_ws_bytes(int C, int N, int D, int64_t n_isects, int reuse_fwd) {
     (void)D;
-    return slot_flag_bytes(n_isects, kSlotWaves) + rows3_bytes(n_isects) + grad_slot_bytes((int64_t)C * N, true) +
+    return slot_flag_bytes(n_isects, kSlotWaves) + rows3_bytes(n_isects) + grad_slot_bytes((int64_t)C * N, true, n_isects) +
            (reuse_fwd ? 0 : rec_bytes(C, N));
 }
 
@@ -983,7 +989,7 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     // the forward's packed records when the caller kept them, else pack again
     const Rec3* rec = (const Rec3*)fwd_ws;
     if (!rec) {
-        Rec3* own = (Rec3*)(sbuf + grad_slot_bytes(n, true));
+        Rec3* own = (Rec3*)(sbuf + grad_slot_bytes(n, true, n_isects));
         if (int st = pack3(C, N, D, means2d, conics, cs, own, s)) return st;
         rec = own;
     }
@@ -1011,8 +1017,10 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                            flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, flags,  \
                            gs.slot, n_isects, pairs, qmask, qstride, order);                                   \
     }                                                                                                          \
+    hipLaunchKernelGGL((reduce_pieces_kernel<12, 3, kRow3, kSlotWaves>), dim3(piece_grid(gs)), dim3(256), 0, s,   \
+                       rows, flags, gs.seg, gs.pbase, gs.pieces, gs.npieces, gs.partial);                          \
     hipLaunchKernelGGL((split3_kernel<DD, AA>), dim3((unsigned)(((int64_t)N + 255) / 256)), dim3(256), 0, s, C, \
-                       N, rows, flags, gs.seg, rec, conics,                                                        \
+                       N, rows, flags, gs.seg, gs.pbase, gs.partial, cs.opac, cs.op_cstride, conics,               \
                        reinterpret_cast<float2*>(v_means2d), v_conics, cd, reinterpret_cast<float2*>(v_means2d_abs))
     switch (D * 2 + (abs ? 1 : 0)) {
         case 2: LAUNCH_B(1, false); break;

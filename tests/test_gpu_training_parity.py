@@ -302,14 +302,18 @@ def _parity_at_scale(gs, fixture=None, chaotic=False):
     with open(os.path.join("gpurun_out", f"{fixture}_{gs}gs.json".replace(f"psnr_scale_{gs}_", "psnr_scale_")), "w") as f:
         json.dump(res, f)
     print(res)
+    # the first line of every failure states the numbers and the bars (the driver keeps a tail)
+    head = (f"{fixture}: mean delta {mean_delta:+.4f} dB (bar {mean_bar:.4f}); sd hip {sd_hip:.4f} dB (bar "
+            f"{3.0 * sd_ref + 0.01:.4f} = 3 x sd ref {sd_ref:.4f} + 0.01); single pair {win_gpu - ref['window_db']:+.4f} dB"
+            f"{'' if full else f' (bar {bar_single:.4f})'}; first loss {loss_gpu[0]:.6f} vs {ref['loss_first']:.6f}\n")
     # identical parameters at the first step: the chains agree before any divergence
-    assert abs(loss_gpu[0] - ref["loss_first"]) <= 1e-5 + 1e-4 * abs(ref["loss_first"]), res
-    assert ref["window_db"] > gold["psnr_init_db"] + 5.0 and win_gpu > gold["psnr_init_db"] + 5.0  # both fits fit
+    assert abs(loss_gpu[0] - ref["loss_first"]) <= 1e-5 + 1e-4 * abs(ref["loss_first"]), head + str(res)
+    assert ref["window_db"] > gold["psnr_init_db"] + 5.0 and win_gpu > gold["psnr_init_db"] + 5.0, head  # both fit
     if full:
-        assert abs(mean_delta) <= mean_bar, res
-        assert sd_hip <= 3.0 * sd_ref + 0.01, res
+        assert abs(mean_delta) <= mean_bar, head + str(res)
+        assert sd_hip <= 3.0 * sd_ref + 0.01, head + str(res)
     else:
-        assert abs(win_gpu - ref["window_db"]) <= bar_single, res
+        assert abs(win_gpu - ref["window_db"]) <= bar_single, head + str(res)
 
 
 @pytest.mark.slow
