@@ -76,6 +76,11 @@ __device__ __forceinline__ int raster_bin(const int32_t* __restrict__ order) {
     return order ? order[slot] : slot;
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {  // lane-shuffled copy of x (bound_ctrl: 0 for invalid)
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
 // Full 64-lane sum with DPP row ops; the total lands in lane 63.
 __device__ __forceinline__ float wave_sum_to_lane63(float v) {
     int x;
@@ -196,132 +201,162 @@ inline size_t slot_flag_bytes(int64_t n_isects, int ways) { return ((size_t)n_is
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // The splits' fixed-order sum of gradient slots, for one wave owning the nloc (1..64)
-// (camera, Gaussian) entries [ib, ib + nloc), whose slots [E0, E1) are contiguous.  Each slot has
-// WAYS partial rows of ROWF floats (the first NV used, R4 float4) and WAYS flag bytes (row (e, w)
-// written iff flags[WAYS e + w] != 0).  The wave walks [E0, E1) 64 slots at a time:
-//   * the chunk's flagged rows are listed way-major in LDS (one ballot per way);
-//   * R4 consecutive lanes load one listed row (64 / R4 rows per load instruction, every lane
-//     useful whatever fraction of rows is flagged), up to kSlotCap rows per round, all issued
-//     before any is used, the next chunk's flags behind them; the rows are parked in LDS;
-//   * lane s sums slot s's rows in way order (the list is way-major, so rounds keep that order);
-//   * each entry's lane then adds its own slots' sums in slot order.
-// No atomics anywhere: the result depends only on the inputs.  LDS per wave: s_list (256 B) and
-// reduce_slots_floats() floats of scratch (the parked rows, then the slot sums).
-template <int NV, int R4, int CAP>
+// (camera, Gaussian) entries [ib, ib + nloc), whose slots are contiguous and ascending.  Each slot
+// has WAYS partial rows of ROWF floats (the first NV used, R4 float4) and WAYS flag bytes (row
+// (e, w) written iff flags[WAYS e + w] != 0).  Entries over kBigSlots slots were reduced in pieces
+// (reduce_pieces_kernel, pbase >= 0); the wave walks the other entries' slots 64 at a time:
+//   * lane s takes slot cs + s: its flagged rows, loaded together through a range-checked buffer
+//     descriptor (an unflagged way passes an out-of-range offset and reads zero without touching
+//     memory; the loads are never skipped, so the compiler's wait counts stay exact) and summed
+//     in way order in registers -- the next chunk's flags already in flight;
+//   * the slot sums are parked in LDS ([slot][NV], float4 runs) and each entry's lane adds its
+//     own slots' sums in slot order.
+// (Measured against this at c2, split3 0.130 ms: a compacted-list variant -- ballot per way, every
+// lane loading a useful quarter row -- 0.147 ms, its list and parking costing more than the loads
+// it coalesced (gpurun_out/r06probe); four lanes per row with the ways summed by DPP row shifts
+// 0.172 ms at 166 VGPRs (gpurun_out/r06probe3).)  No atomics anywhere: the result depends only on the inputs.
+// LDS per wave: reduce_slots_floats() floats.
+template <int NV>
 constexpr int reduce_slots_floats() {
-    return CAP * R4 * 4 > NV * 65 ? CAP * R4 * 4 : NV * 65;
+    return 64 * 4 * ((NV + 3) / 4);
 }
+// wave-wide minimum, returned as a scalar (readfirstlane: the compiler then knows it is uniform)
 __device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) v = min(v, __shfl_xor(v, d));
-    return v;
+    return __builtin_amdgcn_readfirstlane(v);
 }
-template <int NV, int R4, int ROWF, int WAYS, int CAP>
+#ifndef HGSR_PROBE_SPLIT
+#define HGSR_PROBE_SPLIT 0
+#endif
+constexpr int kBufWord3 = 0x00020000;  // gfx9 raw buffer descriptor word 3 (32-bit data, range-checked)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    // (an explicitly typed result: through `auto` and v[k] the compiler kept one dword of four)
+    const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+template <int NV, int R4, int ROWF, int WAYS, int UNR>
 __device__ __forceinline__ void reduce_slots(const float* __restrict__ rows, const uint8_t* __restrict__ flags,
                                              const int32_t* __restrict__ seg, const int32_t* __restrict__ pbase,
-                                             const float* __restrict__ partial, int64_t ib, int nloc,
-                                             uint8_t* s_list, float* s_scr, float (&out)[NV]) {
+                                             const float* __restrict__ partial, int64_t ib, int nloc, float* s_scr,
+                                             float (&out)[NV]) {
     static_assert(WAYS >= 1 && WAYS <= 4 && NV <= 4 * R4 && R4 <= 8, "slot rows");
-    constexpr int RPI = 64 / R4;                  // rows per load instruction
-    constexpr int MAXI = (CAP + RPI - 1) / RPI;   // load instructions per round
-    float4* const s_rows = reinterpret_cast<float4*>(s_scr);  // [CAP][R4] during the rounds
-    float(*const s_v)[65] = reinterpret_cast<float(*)[65]>(s_scr);  // [NV][65] after them
+    constexpr int V4 = (NV + 3) / 4;      // float4 per parked slot sum
+    constexpr uint32_t kOOB = 0x7fffffffu;  // out-of-range buffer offset: reads zero
+    float4* const s_sum = reinterpret_cast<float4*>(s_scr);  // [64 slots][V4]
     const int lane = threadIdx.x & 63;
-    const int q = lane % R4, jl = lane / R4;
     const bool live = lane < nloc;
     const int32_t pb = live ? pbase[ib + lane] : -1;
-    // a big entry's slots are reduced in pieces: the walker skips them
-    const int32_t lo_e = (live && pb < 0) ? seg[ib + lane] : 0, hi_e = (live && pb < 0) ? seg[ib + lane + 1] : 0;
-    const int32_t E1 = seg[ib + nloc];
-    auto fl = [&](int32_t e) -> uint32_t {
-        if (e >= E1) return 0u;
-        return WAYS == 4 ? reinterpret_cast<const uint32_t*>(flags)[e] : (uint32_t)flags[e];
+    const int32_t sl = live ? seg[ib + lane] : 0, sh = live ? seg[ib + lane + 1] : 0;
+    // a big entry's slots were reduced in pieces: the walker skips them
+    const int32_t lo_e = pb < 0 ? sl : 0, hi_e = pb < 0 ? sh : 0;
+    const int32_t E1 = __builtin_amdgcn_readfirstlane(seg[ib + nloc]);
+    constexpr int32_t kNone = 0x7fffffff;
+    // flags of slots [0, E1) through a range-checked descriptor: beyond E1 (or no chunk) reads zero
+    const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(flags), (short)0, (int)(E1 * WAYS), kBufWord3);
+    auto fl = [&](int32_t cs) -> uint32_t {
+        const uint32_t off = cs != kNone ? (uint32_t)(cs + lane) * WAYS : kOOB;
+        return WAYS == 4 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(frs, (int)off, 0, 0)
+                         : (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(frs, (int)off, 0, 0);
+    };
+    // the next chunk: 64 slots from the next slot any entry of this wave still needs.  The
+    // entries' slot ranges ascend with the lane, so that is the first lane still needing one
+    // (a ballot and a readlane: no cross-lane reduction)
+    auto first_from = [&](uint64_t m, int32_t floor_cs) -> int32_t {
+        if (m == 0) return kNone;
+        const int l = (int)__builtin_ctzll(m);
+        return max(__builtin_amdgcn_readlane(lo_e, l), floor_cs);
     };
 #pragma unroll
     for (int k = 0; k < NV; ++k) out[k] = 0.f;
-    constexpr int32_t kNone = 0x7fffffff;
-    // the chunks walked: 64 slots from the first small entry's first slot, then from the next
-    // slot any small entry still needs (entries' slot ranges are ascending and disjoint)
-    int32_t cs = wave_min_i32(lo_e < hi_e ? lo_e : kNone);
-    uint32_t fc = cs != kNone ? fl(cs + lane) : 0u;  // flags of slot cs + lane
+#if HGSR_PROBE_SPLIT == 1  // (probe build, wrong results: no slot reduction at all)
+    if (E1 != 1234567) return;
+#endif
+    int32_t cs = first_from(__ballot(lo_e < hi_e), 0);
+    uint32_t f = cs != kNone ? fl(cs) : 0u;
     while (cs != kNone) {
-        const int32_t cn = wave_min_i32(hi_e > cs + 64 ? max(lo_e, cs + 64) : kNone);  // the next chunk
-        const uint32_t f = fc;
-        // way-major list of the chunk's flagged rows: entry = slot | way << 6
-        int n = 0, pos[WAYS];
+        const int32_t cn = first_from(__ballot(hi_e > cs + 64), cs + 64);
+        const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(rows) + (int64_t)cs * WAYS * ROWF, (short)0, 64 * WAYS * ROWF * 4, kBufWord3);
+        // slot cs + lane: its flagged rows in way order
+        float4 x[WAYS][V4];
 #pragma unroll
         for (int w = 0; w < WAYS; ++w) {
             const bool has = (f >> (8 * w)) & 0xffu;
-            const uint64_t bw = __ballot(has);
-            pos[w] = has ? n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bw >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bw, 0))
-                         : -1;
-            if (has) s_list[pos[w]] = (uint8_t)(lane | (w << 6));
-            n += __popcll(bw);
+#pragma unroll
+            for (int r = 0; r < V4; ++r) {
+                const uint32_t off = has ? (uint32_t)(((lane * WAYS + w) * ROWF + 4 * r) * 4) : kOOB;
+#if HGSR_PROBE_SPLIT == 2  // (probe build, wrong results: no row loads)
+                x[w][r] = make_float4((float)off, 0.f, 0.f, 0.f);
+#else
+                x[w][r] = buf_load4(rrs, off);
+#endif
+            }
+        }
+        f = cn != kNone ? fl(cn) : 0u;  // the next chunk's flags, behind this chunk's rows
+#pragma unroll
+        for (int r = 0; r < V4; ++r) {
+            float4 a = x[0][r];
+#pragma unroll
+            for (int w = 1; w < WAYS; ++w)
+                a = make_float4(a.x + x[w][r].x, a.y + x[w][r].y, a.z + x[w][r].z, a.w + x[w][r].w);
+            s_sum[lane * V4 + r] = a;
         }
         wave_lds_sync();
-        float4 acc[R4];
+        // this entry's slots of the chunk, in order; UNR slots' reads issued together
+        const int32_t lo = max(lo_e, cs) - cs, hi = (HGSR_PROBE_SPLIT == 3 ? lo : min(hi_e, cs + 64) - cs);
+        for (int32_t y = lo; y < hi; y += UNR) {
+            float4 t[UNR][V4];
 #pragma unroll
-        for (int r = 0; r < R4; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int base = 0; base < n; base += CAP) {
-            const int cnt = min(CAP, n - base);
-            float4 x[MAXI];
+            for (int u = 0; u < UNR; ++u)
 #pragma unroll
-            for (int i = 0; i < MAXI; ++i) {
-                const int j = i * RPI + jl;
-                x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (jl < RPI && j < cnt) {
-                    const int ent = s_list[base + j];
-                    x[i] = reinterpret_cast<const float4*>(
-                        rows + ((int64_t)(cs + (ent & 63)) * WAYS + (ent >> 6)) * ROWF)[q];
-                }
-            }
-            if (base == 0 && cn != kNone) fc = fl(cn + lane);  // the next chunk's flags, behind this round's rows
+                for (int r = 0; r < V4; ++r)
+                    t[u][r] = y + u < hi ? s_sum[(y + u) * V4 + r] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-            for (int i = 0; i < MAXI; ++i) {
-                const int j = i * RPI + jl;
-                if (jl < RPI && j < cnt) s_rows[j * R4 + q] = x[i];
-            }
-            wave_lds_sync();
+            for (int u = 0; u < UNR; ++u)
+                if (y + u < hi)
 #pragma unroll
-            for (int w = 0; w < WAYS; ++w)
-                if (pos[w] >= base && pos[w] < base + cnt)
+                    for (int r = 0; r < V4; ++r) {
+                        const float t4[4] = {t[u][r].x, t[u][r].y, t[u][r].z, t[u][r].w};
 #pragma unroll
-                    for (int r = 0; r < R4; ++r) {
-                        const float4 y = s_rows[(pos[w] - base) * R4 + r];
-                        acc[r] = make_float4(acc[r].x + y.x, acc[r].y + y.y, acc[r].z + y.z, acc[r].w + y.w);
+                        for (int c = 0; c < 4; ++c)
+                            if (4 * r + c < NV) out[4 * r + c] += t4[c];
                     }
-            wave_lds_sync();
         }
-        if (n == 0 && cn != kNone) fc = fl(cn + lane);
-#pragma unroll
-        for (int r = 0; r < R4; ++r) {
-            const float a4[4] = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (4 * r + c < NV) s_v[4 * r + c][lane] = a4[c];
-        }
-        wave_lds_sync();
-        const int32_t lo = max(lo_e, cs), hi = min(hi_e, cs + 64);
-        for (int32_t y = lo; y < hi; ++y)
-#pragma unroll
-            for (int k = 0; k < NV; ++k) out[k] += s_v[k][y - cs];
         wave_lds_sync();
         cs = cn;
     }
-    if (pb >= 0) {  // a big entry: its pieces' partials in piece order
-        const int32_t np = (seg[ib + lane + 1] - seg[ib + lane] + kPieceSlots - 1) / kPieceSlots;
-        for (int32_t j = 0; j < np; ++j) {
-            const float4* pp = reinterpret_cast<const float4*>(partial + (int64_t)(pb + j) * kPieceFloats);
+    // the big entries (a few per wave at most): the whole wave sums each one's piece partials,
+    // lane j taking piece j (64 per round, one load latency each), with the fixed DPP tree; a lane
+    // walking an 8,160-tile entry's 64 pieces alone held the kernel's tail
+    uint64_t bigm = __ballot(pb >= 0);
+    while (bigm) {
+        const int l = (int)__builtin_ctzll(bigm);
+        bigm &= bigm - 1;
+        const int32_t pbl = __builtin_amdgcn_readlane(pb, l);
+        const int32_t e0 = __builtin_amdgcn_readlane(sl, l), e1 = __builtin_amdgcn_readlane(sh, l);
+        const int32_t np = (e1 - e0 + kPieceSlots - 1) / kPieceSlots;
+        float tot[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) tot[k] = 0.f;
+        for (int32_t j0 = 0; j0 < np; j0 += 64) {
+            const int32_t j = j0 + lane;
+            float v[4 * ((NV + 3) / 4)];
 #pragma unroll
             for (int r = 0; r < (NV + 3) / 4; ++r) {
-                const float4 y = pp[r];
-                const float y4[4] = {y.x, y.y, y.z, y.w};
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (4 * r + c < NV) out[4 * r + c] += y4[c];
+                const float4 y = j < np ? reinterpret_cast<const float4*>(partial + (int64_t)(pbl + j) * kPieceFloats)[r]
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[4 * r] = y.x; v[4 * r + 1] = y.y; v[4 * r + 2] = y.z; v[4 * r + 3] = y.w;
             }
+#pragma unroll
+            for (int k = 0; k < NV; ++k)
+                tot[k] += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wave_sum_to_lane63(v[k])), 63));
         }
+        if (lane == l)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) out[k] = tot[k];
     }
 }
 
@@ -440,10 +475,6 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <int CTRL>
-__device__ __forceinline__ float dpp(float x) {  // lane-shuffled copy of x (bound_ctrl: 0 for invalid)
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
-}
 
 // Where a raster call's channels come from.  gsplat's rasterize_to_pixels takes
 // colors [C,N,D] and opacities [C,N]; rasterization() itself concatenates the depth

@@ -1110,7 +1110,32 @@ __global__ __launch_bounds__(256) void slot_write_kernel(int64_t CN, R rect, con
         if (lane == 63) s_w[k][wave] = inc;
         sa[k] = inc - area[k];  // exclusive within the wave
     }
+    // the block's big entries' pieces: one list reservation per block (where in the list is of no
+    // consequence: each piece is reduced on its own and an entry sums its pieces in piece order)
+    int npk[8], tnp = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        npk[k] = area[k] > kBigSlots ? (area[k] + kPieceSlots - 1) / kPieceSlots : 0;
+        tnp += npk[k];
+    }
+    int pinc = tnp;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(pinc, d);
+        if (lane >= d) pinc += o;
+    }
+    __shared__ int s_p[4], s_pbase;
+    if (lane == 63) s_p[wave] = pinc;
     __syncthreads();
+    const int ptot = s_p[0] + s_p[1] + s_p[2] + s_p[3];
+    if (tid == 0 && ptot > 0) s_pbase = atomicAdd(npieces, ptot);
+    __syncthreads();
+    int pnext = 0;
+    if (ptot > 0) {
+        pnext = s_pbase + pinc - tnp;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) pnext += v < wave ? s_p[v] : 0;
+    }
     int run = bpre[blockIdx.x];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -1125,14 +1150,12 @@ __global__ __launch_bounds__(256) void slot_write_kernel(int64_t CN, R rect, con
             const int e = pre + sa[k];
             seg[o] = e;
             slot[o] = make_int2(e - y0[k] * w[k] - x0[k], w[k]);
-            // a big entry lists its pieces (where in the list is of no consequence: each piece is
-            // reduced on its own and the pieces are summed in piece order)
             int32_t pb = -1;
-            if (area[k] > kBigSlots) {
-                const int np = (area[k] + kPieceSlots - 1) / kPieceSlots;
-                pb = atomicAdd(npieces, np);
-                if (pb + np <= piece_cap)
-                    for (int j = 0; j < np; ++j) pieces[pb + j] = (int32_t)o;
+            if (npk[k] > 0) {
+                pb = pnext;
+                pnext += npk[k];
+                if (pb + npk[k] <= piece_cap)
+                    for (int j = 0; j < npk[k]; ++j) pieces[pb + j] = (int32_t)o;
                 else
                     pb = -1;  // (cannot happen within piece_capacity; the walker then takes it)
             }

@@ -756,9 +756,8 @@ __global__ __launch_bounds__(256) void split2_kernel(int C, int N, const float* 
                                                     ChanDst cd, float* __restrict__ v_normals,
                                                     float2* __restrict__ v_densify) {
     constexpr int KV = 15 + D;
-    constexpr int kCap = 64, kScr = reduce_slots_floats<KV, (KV + 3) / 4, kCap>();
-    __shared__ uint8_t s_list[4][256];  // per wave (each wave owns 64 surfels)
-    __shared__ __attribute__((aligned(16))) float s_scr[4][kScr];
+    constexpr int kScr = reduce_slots_floats<KV>();
+    __shared__ __attribute__((aligned(16))) float s_scr[4][kScr];  // per wave (each wave owns 64 surfels)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t g0 = ((int64_t)blockIdx.x * 4 + wave) * 64, g = g0 + lane;
     if (g0 >= N) return;  // wave-uniform; the waves never synchronise with each other
@@ -768,8 +767,7 @@ __global__ __launch_bounds__(256) void split2_kernel(int C, int N, const float* 
     for (int c = 0; c < C; ++c) {
         const int64_t i = (int64_t)c * N + g;
         float r[KV];
-        reduce_slots<KV, (KV + 3) / 4, kRow2, kSlotWaves, kCap>(rows, flags, seg, pbase, partial, (int64_t)c * N + g0, nloc,
-                                                                s_list[wave], s_scr[wave], r);
+        reduce_slots<KV, (KV + 3) / 4, kRow2, kSlotWaves, 2>(rows, flags, seg, pbase, partial, (int64_t)c * N + g0, nloc, s_scr[wave], r);
         if (!live) continue;
         double u[3], v[3], w[3], gA[3], gB[3], gC[3];
         const float2 mm = means2d[i];

@@ -715,9 +715,8 @@ __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* 
                                                      const float* __restrict__ conics,
                                                      float2* __restrict__ v_means2d, float* __restrict__ v_conics,
                                                      ChanDst cd, float2* __restrict__ v_abs) {
-    constexpr int kCap = 128, kScr = reduce_slots_floats<12, 3, kCap>();
-    __shared__ uint8_t s_list[4][256];  // per wave (each wave owns 64 Gaussians)
-    __shared__ __attribute__((aligned(16))) float s_scr[4][kScr];
+    constexpr int kScr = reduce_slots_floats<12>();
+    __shared__ __attribute__((aligned(16))) float s_scr[4][kScr];  // per wave (each wave owns 64 Gaussians)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t g0 = ((int64_t)blockIdx.x * 4 + wave) * 64, g = g0 + lane;
     if (g0 >= N) return;  // wave-uniform; the waves never synchronise with each other
@@ -727,8 +726,7 @@ __global__ __launch_bounds__(256) void split3_kernel(int C, int N, const float* 
     for (int c = 0; c < C; ++c) {
         const int64_t i = (int64_t)c * N + g;
         float r[12];
-        reduce_slots<12, 3, kRow3, kSlotWaves, kCap>(rows, flags, seg, pbase, partial, (int64_t)c * N + g0, nloc, s_list[wave],
-                                                     s_scr[wave], r);
+        reduce_slots<12, 3, kRow3, kSlotWaves, 2>(rows, flags, seg, pbase, partial, (int64_t)c * N + g0, nloc, s_scr[wave], r);
         if (!live) continue;
         const float qa = conics[i * 3], qb = conics[i * 3 + 1], qc = conics[i * 3 + 2];
         v_means2d[i] = make_float2(qa * r[0] + qb * r[1], qb * r[0] + qc * r[1]);
