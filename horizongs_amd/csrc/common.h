@@ -167,7 +167,10 @@ constexpr int kSlotWaves = 4;
 // views put Gaussians over the whole screen, 8,160 tiles at 1080p) is reduced in pieces of
 // kPieceSlots slots, one wave each (reduce_pieces), instead of by the wave that owns it: a wave
 // walking 8,160 slots alone held the whole reduction's tail (split3 0.28 ms at c2).
-constexpr int kBigSlots = 32;
+#ifndef HGSR_BIG_SLOTS
+#define HGSR_BIG_SLOTS 32
+#endif
+constexpr int kBigSlots = HGSR_BIG_SLOTS;
 constexpr int kPieceSlots = 128;
 constexpr int kPieceFloats = 20;  // floats per piece partial (>= the rows' used values, 16-B aligned)
 struct GradSlots {
