@@ -409,7 +409,7 @@ def decode_mfma(wl, kernels):
     T = [1, 5, (wl.color_dim * 10 + 15) // 16]  # opacity 10, cov 70, colour color_dim x 10 rows
     fwd = 3 * 2 * KS + 8 * sum(T) + (2 * KS + 8)
     bwd = 0
-    col_one = os.environ.get("HGSR_DEC_COLBWD", "1") != "0" and 5 < T[2] <= 20
+    col_one = NAT.lib().hgsr_decode_set_color_bwd(-1) != 0 and 5 < T[2] <= 20
     for h in range(3):
         if h == 2 and col_one:
             bwd += 2 * KS + 8 * T[2] + 32 * ((T[2] + 3) // 4) + 16 * kt

@@ -73,6 +73,7 @@ _SIGS = {
     "hgsr_decode_count": (I, [I, I, I, I, I, P, P, P, P, P, P, SZ, P, P, P]),
     "hgsr_decode_fwd": (I, [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P]),
     "hgsr_decode_bwd_ws_bytes": (SZ, [I]),
+    "hgsr_decode_set_color_bwd": (I, [I]),
     "hgsr_decode_bwd": (I, [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, SZ, P]),
     "hgsr_loss_ws_bytes": (SZ, [I, I, I]),
     "hgsr_training_statis": (I, [I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),

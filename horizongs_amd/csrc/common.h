@@ -216,7 +216,7 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 //     own slots' sums in slot order.
 // (Measured against this at c2, split3 0.130 ms: a compacted-list variant -- ballot per way, every
 // lane loading a useful quarter row -- 0.147 ms, its list and parking costing more than the loads
-// it coalesced (gpurun_out/r06probe); four lanes per row with the ways summed by DPP row shifts
+// it coalesced (gpurun_out/r06probe, probe builds since removed); four lanes per row with the ways summed by DPP row shifts
 // 0.172 ms at 166 VGPRs (gpurun_out/r06probe3).)  No atomics anywhere: the result depends only on the inputs.
 // LDS per wave: reduce_slots_floats() floats.
 template <int NV>
@@ -229,9 +229,6 @@ __device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
     for (int d = 1; d < 64; d <<= 1) v = min(v, __shfl_xor(v, d));
     return __builtin_amdgcn_readfirstlane(v);
 }
-#ifndef HGSR_PROBE_SPLIT
-#define HGSR_PROBE_SPLIT 0
-#endif
 constexpr int kBufWord3 = 0x00020000;  // gfx9 raw buffer descriptor word 3 (32-bit data, range-checked)
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
@@ -274,9 +271,6 @@ __device__ __forceinline__ void reduce_slots(const float* __restrict__ rows, con
     };
 #pragma unroll
     for (int k = 0; k < NV; ++k) out[k] = 0.f;
-#if HGSR_PROBE_SPLIT == 1  // (probe build, wrong results: no slot reduction at all)
-    if (E1 != 1234567) return;
-#endif
     int32_t cs = first_from(__ballot(lo_e < hi_e), 0);
     uint32_t f = cs != kNone ? fl(cs) : 0u;
     while (cs != kNone) {
@@ -291,11 +285,7 @@ __device__ __forceinline__ void reduce_slots(const float* __restrict__ rows, con
 #pragma unroll
             for (int r = 0; r < V4; ++r) {
                 const uint32_t off = has ? (uint32_t)(((lane * WAYS + w) * ROWF + 4 * r) * 4) : kOOB;
-#if HGSR_PROBE_SPLIT == 2  // (probe build, wrong results: no row loads)
-                x[w][r] = make_float4((float)off, 0.f, 0.f, 0.f);
-#else
                 x[w][r] = buf_load4(rrs, off);
-#endif
             }
         }
         f = cn != kNone ? fl(cn) : 0u;  // the next chunk's flags, behind this chunk's rows
@@ -309,7 +299,7 @@ __device__ __forceinline__ void reduce_slots(const float* __restrict__ rows, con
         }
         wave_lds_sync();
         // this entry's slots of the chunk, in order; UNR slots' reads issued together
-        const int32_t lo = max(lo_e, cs) - cs, hi = (HGSR_PROBE_SPLIT == 3 ? lo : min(hi_e, cs + 64) - cs);
+        const int32_t lo = max(lo_e, cs) - cs, hi = min(hi_e, cs + 64) - cs;
         for (int32_t y = lo; y < hi; y += UNR) {
             float4 t[UNR][V4];
 #pragma unroll

@@ -1485,6 +1485,15 @@ extern "C" size_t hgsr_decode_bwd_ws_bytes(int Av) {
     return parts + (size_t)kRedGroups * pf * sizeof(double);
 }
 
+// the SH colour head's backward form: 1 (default) one launch (decode_bwd_color_kernel), 0 the
+// chunked launches it replaced (kept for the tests that compare the two); returns the previous
+static int g_color_one = 1;
+extern "C" int hgsr_decode_set_color_bwd(int one) {
+    const int old = g_color_one;
+    if (one >= 0) g_color_one = one != 0;
+    return old;
+}
+
 extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim, const int32_t* vis_idx,
                                const float* anchor, const float* feat, const float* offset, const float* scaling_raw,
                                const float* cam_center, const float* const* mlp, const int32_t* slot_row,
@@ -1507,9 +1516,8 @@ extern "C" int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int c
     float* partials = (float*)ws;
     double* level2 = (double*)((char*)ws + (((size_t)grid * bwd_part_floats_max() * sizeof(float) + 255) & ~(size_t)255));
     // an SH colour head (more tiles than one chunked launch holds) in one launch:
-    // decode_bwd_color_kernel; HGSR_DEC_COLBWD=0 keeps the chunked launches (A/B)
-    const char* col_env = getenv("HGSR_DEC_COLBWD");  // read per call: the tests switch it
-    const bool col_one = col_env ? atoi(col_env) != 0 : true;
+    // decode_bwd_color_kernel; hgsr_decode_set_color_bwd(0) keeps the chunked launches (tests)
+    const bool col_one = g_color_one != 0;
     const int K1 = kDecF + view_dim;
     KernelTimer kt("decode_bwd", s);
     // the cov head first: after it d_offset, d_scaling and the cov weights are final, so a

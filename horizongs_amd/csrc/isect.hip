@@ -394,15 +394,8 @@ __global__ __launch_bounds__(256) void isect_emit_lds_kernel(
                 const int base = cam_of(o, N) * n_tiles;
                 for (int y = y0; y < y1; ++y)
                     for (int x = rx0[k]; x < rx1[k]; ++x) {
-#if HGSR_PROBE_EMIT == 1  // (probe build: cursor atomics, no key stores)
-                        const int pos = atomicAdd(&s_cur[base + y * tw + x], 1);
-                        if (pos == -7) keys[0] = key;
-#elif HGSR_PROBE_EMIT == 2  // (probe build: key stores to the slice start, no atomics)
-                        keys[s_cur[base + y * tw + x]] = key;
-#else
                         const int pos = atomicAdd(&s_cur[base + y * tw + x], 1);
                         keys[pos] = key;
-#endif
                     }
             }
         }

@@ -386,6 +386,9 @@ int hgsr_decode_fwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
  * caller runs {cov}, launches their all-reduce, then {opacity, colour} (the other
  * accumulations continue).  ws: hgsr_decode_bwd_ws_bytes(Av). */
 size_t hgsr_decode_bwd_ws_bytes(int Av);
+/* the SH colour head's backward form for later hgsr_decode_bwd calls: 1 (default) one launch,
+ * 0 the chunked launches (the tests compare both); -1 only queries.  Returns the previous form. */
+int hgsr_decode_set_color_bwd(int one);
 int hgsr_decode_bwd(int Av, int F, int view_dim, int n_offsets, int color_dim,
                     const int32_t* vis_idx, const float* anchor, const float* feat,
                     const float* offset, const float* scaling_raw, const float* cam_center,

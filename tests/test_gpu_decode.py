@@ -82,12 +82,14 @@ def _random_model(n_anchor, view_dim, color_dim, seed, n_off=10):
     # SH colour heads: the one-launch colour backward (17 / 9 / 15 tiles, view_dim 0 / 3) and
     # the chunked launches it replaces
     (0, 27, 5003, 10, 1), (3, 27, 1500, 10, 1), (0, 27, 900, 5, 1), (3, 48, 777, 5, 1), (0, 27, 700, 10, 0)])
-def test_decode_backward(view_dim, color_dim, n_anchor, n_off, col_one, monkeypatch):
+def test_decode_backward(view_dim, color_dim, n_anchor, n_off, col_one, request):
     """All input and weight gradients vs fp64 / fp32 autograd of the oracle restatement.
     n_offsets 5 is the Block_A chunk setting (config/ours/large_scene/block_A/config.yaml:11),
     11 the largest the kernels take."""
     from horizongs_amd import decode as HD
-    monkeypatch.setenv("HGSR_DEC_COLBWD", str(col_one))
+    from horizongs_amd import _native as NAT
+    old = NAT.lib().hgsr_decode_set_color_bwd(col_one)
+    request.addfinalizer(lambda: NAT.lib().hgsr_decode_set_color_bwd(old))
     inputs, mlps = _random_model(n_anchor, view_dim, color_dim, seed=5 + n_anchor, n_off=n_off)
     gen = torch.Generator().manual_seed(77)
     vis = torch.rand(n_anchor, generator=gen) < 0.8
