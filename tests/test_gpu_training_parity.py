@@ -352,9 +352,9 @@ def test_psnr_parity_at_scale_2dgs():
 
 @pytest.mark.slow
 def test_psnr_parity_at_scale_3dgs_lr03():
-    """The 3DGS chain at 0.3x the fine-stage learning rates: the reference chain's own 1e-6
-    perturbation moves its window PSNR by 0.11 dB there, so without an ensemble the bar is
-    twice that single draw (never the HIP chain's own draw); the 0.1x fixture is the tight one."""
+    """The 3DGS chain at 0.3x the fine-stage learning rates, against a 9-member reference ensemble
+    (unperturbed + 1e-6 perturbations, seeds 5-12: window sd 0.053 dB, scripts/psnr_ensemble_lr03.sh)
+    with the full-ensemble bars of _parity_at_scale."""
     _parity_at_scale("3d", "psnr_scale_3d_lr03")
 
 
