@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 
 from . import _native as N
+from . import gradbuf
 from ._native import ptr
 
 
@@ -22,14 +23,16 @@ class _Activate(torch.autograd.Function):
         N.call("hgsr_activate_fwd", n, ptr(log_scales), ptr(logits), ptr(scales), ptr(opac),
                N.stream(log_scales.device))
         ctx.save_for_backward(scales, opac)
+        ctx.keys = (gradbuf.key(log_scales), gradbuf.key(logits))
         return scales, opac
 
     @staticmethod
     def backward(ctx, v_scales, v_opac):
         scales, opac = ctx.saved_tensors
         n = scales.shape[0]
-        v_ls = torch.empty_like(scales) if ctx.needs_input_grad[0] else None
-        v_lg = torch.empty_like(opac) if ctx.needs_input_grad[1] else None
+        # in place in a DDP bucket when one is registered for the parameters (gradbuf)
+        v_ls = gradbuf.alloc_key(ctx.keys[0], scales) if ctx.needs_input_grad[0] else None
+        v_lg = gradbuf.alloc_key(ctx.keys[1], opac) if ctx.needs_input_grad[1] else None
         # contiguous copies held in locals until the launch is enqueued: a temporary freed
         # inside the call could hand its block to the next temporary (aliased inputs)
         vs = None if v_scales is None else v_scales.contiguous()

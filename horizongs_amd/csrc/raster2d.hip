@@ -1075,7 +1075,8 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     unsigned long long* const pairs = timing_pair_counter("raster2d_bwd");
     const uint64_t* const qmask = qmask_words(qbuf, n_bins);
     const int64_t qstride = qbuf ? qmask_stride_of(qmask_bytes, n_bins) : 0;
-    const int32_t* const order = (qbuf && HGSR_TILE_ORDER) ? tile_order_of(qbuf) : nullptr;
+    // the forward writes the order only for a non-empty view
+    const int32_t* const order = (qbuf && HGSR_TILE_ORDER && n_isects > 0) ? tile_order_of(qbuf) : nullptr;
     if (HGSR_BWD_ORDER && order) {  // tiles by the ranges the backward walks (raster3d_bwd_impl)
         void* const qb = const_cast<void*>(qbuf);
         if (int st = launch_tile_order(n_bins, isect_offsets, n_isects, nullptr, tile_order_of(qb), s,

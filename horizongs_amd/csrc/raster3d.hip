@@ -997,7 +997,8 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     // the mask buffer of the forward: its quadrant bits and its heaviest-first tile order
     const uint64_t* const qmask = qmask_words(qbuf, n_bins);
     const int64_t qstride = qbuf ? qmask_stride_of(qmask_bytes, n_bins) : 0;
-    const int32_t* const order = (qbuf && HGSR_TILE_ORDER) ? tile_order_of(qbuf) : nullptr;
+    // the forward writes the order only for a non-empty view
+    const int32_t* const order = (qbuf && HGSR_TILE_ORDER && n_isects > 0) ? tile_order_of(qbuf) : nullptr;
     if (HGSR_BWD_ORDER && order) {
         // re-sort the tiles by the ranges the backward walks (up to each tile's latest contributor,
         // written by the forward) instead of by their whole bins

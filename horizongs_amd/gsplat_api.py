@@ -30,6 +30,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
+from . import gradbuf
 from ._native import ptr
 
 _MAX_CH = 4  # channels per raster kernel call
@@ -149,8 +150,8 @@ class _Project3D(torch.autograd.Function):
         means, quats, scales, viewmats, Ks, radii, conics = ctx.saved_tensors
         width, height, eps2d = ctx.cfg
         C, Ng = viewmats.shape[0], means.shape[0]
-        v_means = torch.empty_like(means)
-        v_quats = torch.empty_like(quats)
+        v_means = gradbuf.alloc(means)  # in place in a DDP bucket when one is registered
+        v_quats = gradbuf.alloc(quats)
         v_scales = torch.empty_like(scales)
         v_means2d, v_depths, v_conics = (_f32(g) for g in _grads_or_zeros((v_means2d, v_depths, v_conics), (C, Ng),
                                                                            (2, None, 3), means))
@@ -208,8 +209,8 @@ class _Project2D(torch.autograd.Function):
         means, quats, scales, viewmats, Ks, radii, rt = ctx.saved_tensors
         width, height = ctx.cfg
         C, Ng = viewmats.shape[0], means.shape[0]
-        v_means = torch.empty_like(means)
-        v_quats = torch.empty_like(quats)
+        v_means = gradbuf.alloc(means)  # in place in a DDP bucket when one is registered
+        v_quats = gradbuf.alloc(quats)
         v_scales = torch.empty_like(scales)
         v_means2d, v_depths, v_rt, v_normals = (_f32(g) for g in _grads_or_zeros(
             (v_means2d, v_depths, v_rt, v_normals), (C, Ng), (2, None, (3, 3), 3), means))

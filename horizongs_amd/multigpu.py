@@ -24,6 +24,8 @@ from typing import Dict, Iterable, List, Sequence
 import torch
 import torch.distributed as dist
 
+from . import gradbuf
+
 
 def chunks_for_rank(chunks: Sequence[str], rank: int, world: int) -> List[str]:
     """Round-robin deal of chunk ids (e.g. '0_0'..'3_1' for Block_A) to ranks."""
@@ -310,9 +312,13 @@ class ShardedAdamDDP:
       (the order a backward produces gradients); every parameter of a bucket becomes a view into
       the bucket's flat parameter buffer (its values copied in), so the all-gather writes the
       parameters in place.  Bucket data is padded to a multiple of the world size.
-    * A post-accumulate-grad hook copies each gradient, pre-scaled by 1/world, into its bucket
-      and drops it; a complete bucket's reduce-scatter is launched during the backward, buckets in
-      bucket order on every rank.
+    * Each gradient lands in its bucket's flat gradient buffer: begin() registers the buffer's
+      slices as the parameters' gradient destinations (gradbuf), so the projection and
+      activation backwards write into them and autograd adopts them as `.grad` without a copy;
+      a gradient produced elsewhere is copied in by the post-accumulate-grad hook, which then
+      drops `.grad`.  A complete bucket's reduce-scatter is launched during the backward,
+      buckets in bucket order on every rank, and the 1/world of the mean is applied to the
+      reduced shard (exact for power-of-two worlds).
     * Every rank must produce a gradient for every parameter in every step (the explicit
       Gaussians' step always does): a missing one raises instead of desynchronising the
       collectives.  Densification (new Parameter objects) is not supported under the sharded
@@ -445,6 +451,9 @@ class ShardedAdamDDP:
         for b in self.buckets:
             b["ready"] = [False] * len(b["members"])
             b["work"], b["launched"], b["gsrc"] = None, False, None
+            if not b["direct"]:  # the producing backward writes straight into the flat buffer
+                for (p, _), o in zip(b["members"], b["offs"]):
+                    gradbuf.set_dest(p, b["gflat"][o:o + p.numel()].view_as(p))
         self._in_step = True
 
     def _on_grad(self, p) -> None:
@@ -462,7 +471,9 @@ class ShardedAdamDDP:
         else:
             if b["gflat"] is None:
                 b["gflat"] = torch.zeros(self.world * b["L"], dtype=b["pflat"].dtype, device=b["pflat"].device)
-            torch.mul(g.reshape(-1), 1.0 / self.world, out=b["gflat"][o:o + n])
+            dst = b["gflat"][o:o + n]
+            if g.data_ptr() != dst.data_ptr() or not g.is_contiguous():  # produced elsewhere: copy it in
+                dst.copy_(g.reshape(-1))
             b["gsrc"] = None
         p.grad = None  # the reduced gradient exists only as this rank's shard
         b["ready"][k] = True
@@ -498,12 +509,12 @@ class ShardedAdamDDP:
         gathers = []
         lo = self.rank
         deferred = [id(b["members"][0][0]) in self.defer_ids for b in self.buckets]
+        gradbuf.clear()  # destinations no backward took
         for b in [b for b, d in zip(self.buckets, deferred) if not d] + [b for b, d in zip(self.buckets, deferred) if d]:
             b["work"].wait()
-            if b["gsrc"] is not None:  # reduced unscaled: the mean over ranks on the shard only
-                b["gsrc"] = None
-                if self.world > 1:
-                    b["gshard"].mul_(1.0 / self.world)
+            b["gsrc"] = None
+            if self.world > 1:  # reduced unscaled: the mean over ranks on the shard only
+                b["gshard"].mul_(1.0 / self.world)
             L = b["L"]
             s0, s1 = lo * L, lo * L + L
             descs = {}

@@ -256,7 +256,11 @@ def _parity_at_scale(gs, fixture=None, chaotic=False):
     window PSNR by ~1 dB): a fixed 0.05 dB bar on the medians is below what 8 draws of either
     chain can resolve, so the medians must agree within 3 standard errors of the difference
     computed from the REFERENCE ensemble's sd (3 x 1.2533 sd_ref sqrt(1/n_ref + 1/n_hip), the
-    median's standard error); the HIP spread bound is the same as above and no outlier count
+    median's standard error); the spreads are compared by the two-sided 1% F-test of equal
+    variances on the classical sds (sd_hip / sd_ref <= sqrt(F_0.995(n_hip - 1, n_ref - 1)), 2.98 at
+    8 + 8 members), since the draws there are a wide distribution, not a narrow one with rare
+    spikes, and the median-absolute-deviation spread of 8 such draws is too noisy an estimate
+    for a 3x bar (the reference's own: 0.57 dB robust vs 0.97 dB classical); no outlier count
     applies (draws 1 dB apart are that chain's nature)."""
     import statistics
 
@@ -287,9 +291,13 @@ def _parity_at_scale(gs, fixture=None, chaotic=False):
     rsd_hip = 1.4826 * statistics.median([abs(x - med_hip) for x in hip_w])
     n_low = sum(1 for x in hip_w if x < med_ref - 0.3)
     mean_bar = 0.05
+    spread, spread_bar, spread_kind = rsd_hip, 3.0 * rsd_ref + 0.01, "robust sd hip"
     if chaotic:
+        from scipy.stats import f as fdist
         assert full, "the chaotic case needs the reference ensemble"
         mean_bar = 3.0 * 1.2533 * sd_ref * math.sqrt(1.0 / len(ref_w) + 1.0 / len(hip_w))
+        spread, spread_kind = sd_hip / sd_ref, "sd ratio hip / ref (F-test 1%)"
+        spread_bar = math.sqrt(fdist.ppf(0.995, len(hip_w) - 1, len(ref_w) - 1))
     if full:
         bar_single = None  # the single pair is recorded, the ensembles are bounded
     else:
@@ -305,11 +313,15 @@ def _parity_at_scale(gs, fixture=None, chaotic=False):
                          "ref_robust_sd_db": round(rsd_ref, 4), "hip_robust_sd_db": round(rsd_hip, 4),
                          "hip_draws_0p3_below_ref_median": n_low, "median_bar_db": round(mean_bar, 4),
                          "median_bar_kind": ("3 x the median's standard error of the difference from the reference sd"
-                                             if chaotic else "fixed")},
+                                             if chaotic else "fixed"),
+                         "spread_kind": spread_kind, "spread": round(spread, 4), "spread_bar": round(spread_bar, 4)},
                final_iterate={"ref_db": ref["final_db"], "hip_db": round(fin_gpu, 4),
                               "delta_db": round(fin_gpu - ref["final_db"], 4)},
                bar_db=(round(mean_bar, 4) if full else round(bar_single, 4)),
-               bar_source=("ensemble medians within 0.05 dB; HIP robust sd <= 3 x the reference's + 0.01 dB; <= 1 HIP "
+               bar_source=(("ensemble medians within 3 standard errors of their difference; sd_hip / sd_ref within "
+                            "the two-sided 1% F-test bound; means / robust sds and the unperturbed pair recorded")
+                           if chaotic else
+                           "ensemble medians within 0.05 dB; HIP robust sd <= 3 x the reference's + 0.01 dB; <= 1 HIP "
                            "draw 0.3 dB below the reference median; means / sds and the unperturbed pair recorded"
                            if full else "single reference draw: 2 x its 1e-6 floor (0.05 dB at least)"),
                single_pair_vs_ref_ensemble_sd=(round((win_gpu - ref["window_db"]) / sd_ref, 2) if sd_ref > 0 else None),
@@ -323,8 +335,8 @@ def _parity_at_scale(gs, fixture=None, chaotic=False):
         json.dump(res, f)
     print(res)
     # the first line of every failure states the numbers and the bars (the driver keeps a tail)
-    head = (f"{fixture}: median delta {med_delta:+.4f} dB (bar {mean_bar:.4f}); robust sd hip {rsd_hip:.4f} dB (bar "
-            f"{3.0 * rsd_ref + 0.01:.4f} = 3 x ref {rsd_ref:.4f} + 0.01); hip draws 0.3 dB low {n_low} (bar 1); mean "
+    head = (f"{fixture}: median delta {med_delta:+.4f} dB (bar {mean_bar:.4f}); {spread_kind} {spread:.4f} (bar "
+            f"{spread_bar:.4f}; robust sd ref {rsd_ref:.4f}); hip draws 0.3 dB low {n_low} (bar {'-' if chaotic else 1}); mean "
             f"delta {mean_delta:+.4f}, sd hip / ref {sd_hip:.4f} / {sd_ref:.4f}; single pair "
             f"{win_gpu - ref['window_db']:+.4f} dB{'' if full else f' (bar {bar_single:.4f})'}; first loss "
             f"{loss_gpu[0]:.6f} vs {ref['loss_first']:.6f}\n")
@@ -333,7 +345,7 @@ def _parity_at_scale(gs, fixture=None, chaotic=False):
     assert ref["window_db"] > gold["psnr_init_db"] + 5.0 and win_gpu > gold["psnr_init_db"] + 5.0, head  # both fit
     if full:
         assert abs(med_delta) <= mean_bar, head + str(res)
-        assert rsd_hip <= 3.0 * rsd_ref + 0.01, head + str(res)
+        assert spread <= spread_bar, head + str(res)
         if not chaotic:
             assert n_low <= 1, head + str(res)
     else:
@@ -363,7 +375,9 @@ def test_psnr_parity_at_scale_3dgs_unscaled():
     """The unscaled fine-stage learning rates: the 3DGS chain is chaotic -- the reference
     chain's 8-member ensemble (unperturbed + 1e-6 perturbations, seeds 5-11) spreads 0.97 dB sd
     in window PSNR and 2.0 dB in the final iterate -- so the ensemble means are compared at 3
-    standard errors of their difference (from the reference sd: ~1.4 dB with 8 + 8 members) and
-    the HIP spread must stay within 3x the reference's + 0.01 dB (gpurun_out/psnr_scale_lr1_3dgs.json).
+    standard errors of their difference (from the reference sd: ~1.8 dB with 8 + 8 members) and
+    the spreads by the two-sided 1% F-test (sd ratio <= 2.98; gpurun_out/psnr_scale_lr1_3dgs.json:
+    medians 42.985 / 42.968 dB, sds 1.82 / 0.97 dB, the HIP chain being bit-reproducible these
+    are fixed numbers of the code).
     The tight fixed 0.05 dB bar is on the 0.1x and 0.3x fixtures, where the chains are not chaotic."""
     _parity_at_scale("3d", "psnr_scale_3d_lr1", chaotic=True)
