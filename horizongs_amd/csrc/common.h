@@ -175,7 +175,8 @@ constexpr int kPieceSlots = 128;
 constexpr int kPieceFloats = 20;  // floats per piece partial (>= the rows' used values, 16-B aligned)
 struct GradSlots {
     int32_t* seg;     // [C N + 1]
-    int2* slot;       // [C N]
+    int2* slot;       // [C N] with element stride sstride (the dense array, or the 3DGS records' slot quads)
+    int64_t sstride;
     int32_t* pbase;   // [C N]: first piece of a big entry, -1 for the others
     int32_t* pieces;  // [piece capacity]: the entry of each piece (order of no consequence)
     int32_t* npieces; // [1]: pieces listed
@@ -189,12 +190,66 @@ inline unsigned piece_grid(const GradSlots& g) {
     const int64_t w = (g.cap + 3) / 4;
     return (unsigned)(w < 2048 ? (w > 0 ? w : 1) : 2048);
 }
+// gsplat isect_tiles rectangle; identical float ops to oracle/hgsr_oracle.c tile_rect.  For a
+// power-of-two tile size (gsplat's 16) x / tile_size is x times the exact reciprocal, bit for
+// bit, so the correctly rounded division sequence is only run for other sizes.
+__device__ __forceinline__ void tile_rect(float mx, float my, int32_t radius, int tile_size, int tw,
+                                          int th, int& x0, int& y0, int& x1, int& y1) {
+#pragma clang fp contract(off)
+    const float ts = (float)tile_size;
+    float tr, tx, ty;
+    if ((tile_size & (tile_size - 1)) == 0) {
+        const float inv = __int_as_float(0x7F000000 - __float_as_int(ts));  // 2^-k exactly
+        tr = (float)radius * inv;
+        tx = mx * inv;
+        ty = my * inv;
+    } else {
+        tr = (float)radius / ts;
+        tx = mx / ts;
+        ty = my / ts;
+    }
+    const float fx0 = floorf(tx - tr), fy0 = floorf(ty - tr), fx1 = ceilf(tx + tr), fy1 = ceilf(ty + tr);
+    x0 = fx0 <= 0.f ? 0 : (fx0 >= (float)tw ? tw : (int)fx0);
+    y0 = fy0 <= 0.f ? 0 : (fy0 >= (float)th ? th : (int)fy0);
+    x1 = fx1 <= 0.f ? 0 : (fx1 >= (float)tw ? tw : (int)fx1);
+    y1 = fy1 <= 0.f ? 0 : (fy1 >= (float)th ? th : (int)fy1);
+}
+
+// a (camera, Gaussian)'s tile rectangle from its projection (isect_tiles'): its area, corner and width
+struct RectFromRadii {
+    const float2* m;
+    const int32_t* r;
+    int ts, tw, th;
+    __device__ __forceinline__ int operator()(int64_t o, int& x0, int& y0, int& w) const {
+        const int32_t rad = r[o];
+        if (rad <= 0) {
+            x0 = y0 = w = 0;
+            return 0;
+        }
+        const float2 mm = m[o];
+        int x1, y1;
+        tile_rect(mm.x, mm.y, rad, ts, tw, th, x0, y0, x1, y1);
+        w = x1 - x0;
+        return (y1 - y0) * w;
+    }
+};
+
+constexpr int kSlotRow = 256;  // entries per element of the slot-area prefix (one workgroup row)
+// the forward's slot prefix (hgsr_raster3d_pack_fused with radii): seg [CN + 1] then the row
+// prefix [CN / kSlotRow + 1]
+size_t slot_prefix_bytes(int64_t CN);
+// row area sums + their exclusive scan into buf (seg[CN] = the total); pack3 finishes seg
+int launch_slot_prefix(int64_t CN, const RectFromRadii& r, void* buf, hipStream_t s);
+// the big entries' piece list from a finished seg (launch_grad_slots' buffer layout in buf)
+int launch_grad_pieces(int64_t CN, const int32_t* seg, int64_t n_isects, void* buf, hipStream_t s, GradSlots& out);
 // bytes of launch_grad_slots' buffer (from_lists: the rectangles are found from the lists)
 size_t grad_slot_bytes(int64_t CN, bool from_lists, int64_t n_isects);
-// radii != nullptr: rectangles from means2d / radii (isect_tiles'); else from the sorted lists
+// radii != nullptr: rectangles from means2d / radii (isect_tiles'); else from the sorted lists.
+// slot_dst (nullable): where the slot bases go, element o at slot_dst[o * sstride] (the 3DGS
+// records' slot quads); else the dense array in buf
 int launch_grad_slots(int C, int N, const float* means2d, const int32_t* radii, int tile_size, int tw, int th,
                       const int32_t* offsets, const int32_t* flatten_ids, int64_t n_isects, void* buf,
-                      hipStream_t s, GradSlots& out);
+                      hipStream_t s, GradSlots& out, int2* slot_dst = nullptr, int64_t sstride = 1);
 // the flags and partial rows of a backward workspace: flags first, so a forward that only
 // knows the intersection capacity can clear them (hgsr_raster{3,2}d_fwd_packed bwd_ws)
 inline size_t slot_flag_bytes(int64_t n_isects, int ways) { return ((size_t)n_isects * ways + 255) & ~(size_t)255; }

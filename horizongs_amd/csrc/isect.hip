@@ -37,31 +37,6 @@ __host__ __device__ inline int nbits64(int64_t v) {
     return b;
 }
 
-// gsplat isect_tiles rectangle; identical float ops to oracle/hgsr_oracle.c tile_rect.  For a
-// power-of-two tile size (gsplat's 16) x / tile_size is x times the exact reciprocal, bit for
-// bit, so the correctly rounded division sequence is only run for other sizes.
-__device__ __forceinline__ void tile_rect(float mx, float my, int32_t radius, int tile_size, int tw,
-                                          int th, int& x0, int& y0, int& x1, int& y1) {
-#pragma clang fp contract(off)
-    const float ts = (float)tile_size;
-    float tr, tx, ty;
-    if ((tile_size & (tile_size - 1)) == 0) {
-        const float inv = __int_as_float(0x7F000000 - __float_as_int(ts));  // 2^-k exactly
-        tr = (float)radius * inv;
-        tx = mx * inv;
-        ty = my * inv;
-    } else {
-        tr = (float)radius / ts;
-        tx = mx / ts;
-        ty = my / ts;
-    }
-    const float fx0 = floorf(tx - tr), fy0 = floorf(ty - tr), fx1 = ceilf(tx + tr), fy1 = ceilf(ty + tr);
-    x0 = fx0 <= 0.f ? 0 : (fx0 >= (float)tw ? tw : (int)fx0);
-    y0 = fy0 <= 0.f ? 0 : (fy0 >= (float)th ? th : (int)fy0);
-    x1 = fx1 <= 0.f ? 0 : (fx1 >= (float)tw ? tw : (int)fx1);
-    y1 = fy1 <= 0.f ? 0 : (fy1 >= (float)th ? th : (int)fy1);
-}
-
 // camera of flattened index o (< 2^31 by the entry checks): 32-bit division, none for o < N
 __device__ __forceinline__ int cam_of(int64_t o, int N) {
     return o < N ? 0 : (int)((uint32_t)o / (uint32_t)N);
@@ -987,25 +962,7 @@ __global__ void copy_i32_kernel(int n, const int32_t* __restrict__ a, int32_t* _
 // The rectangles come from means2d / radii (the same tile_rect the emission ran), or -- for
 // rasterize_to_pixels called on bare lists -- from each Gaussian's first and last tile in the
 // lists (a rectangle's corners are its smallest and largest row-major tile index).
-constexpr int kSlotPer = 2048;  // (camera, Gaussian) entries per scan block: 256 threads x 8
-
-struct RectFromRadii {
-    const float2* m;
-    const int32_t* r;
-    int ts, tw, th;
-    __device__ __forceinline__ int operator()(int64_t o, int& x0, int& y0, int& w) const {
-        const int32_t rad = r[o];
-        if (rad <= 0) {
-            x0 = y0 = w = 0;
-            return 0;
-        }
-        const float2 mm = m[o];
-        int x1, y1;
-        tile_rect(mm.x, mm.y, rad, ts, tw, th, x0, y0, x1, y1);
-        w = x1 - x0;
-        return (y1 - y0) * w;
-    }
-};
+constexpr int kSlotPer = 2048;  // (camera, Gaussian) entries per slot_write block: 256 threads x 8 rows
 
 struct RectFromTiles {
     const int32_t* tmin;  // per-camera row-major tile index, INT32_MAX when o has no entry
@@ -1025,15 +982,14 @@ struct RectFromTiles {
     }
 };
 
-// stage A: the area total of each block of kSlotPer entries (entry o0 + 256 k + tid: coalesced)
+// stage A: the area total of each row of kSlotRow entries
 template <typename R>
 __global__ __launch_bounds__(256) void slot_sum_kernel(int64_t CN, R rect, int32_t* __restrict__ bsum) {
-    const int64_t o0 = (int64_t)blockIdx.x * kSlotPer + threadIdx.x;
+    const int64_t o = (int64_t)blockIdx.x * kSlotRow + threadIdx.x;
     int s = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    {
         int x0, y0, w;
-        if (o0 + 256 * k < CN) s += rect(o0 + 256 * k, x0, y0, w);
+        if (o < CN) s = rect(o, x0, y0, w);
     }
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) s += __shfl_xor(s, d);
@@ -1043,16 +999,27 @@ __global__ __launch_bounds__(256) void slot_sum_kernel(int64_t CN, R rect, int32
     if (threadIdx.x == 0) bsum[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// stage B: one workgroup, exclusive scan of the block totals in place; seg[CN] = the total; the
-// piece count cleared for stage C
+// stage B: one workgroup, exclusive scan of the row totals in place; seg[CN] = the total; the
+// piece count cleared for stage C (nullable)
 __global__ __launch_bounds__(1024) void slot_scan_kernel(int nb, int32_t* __restrict__ bsum,
                                                          int32_t* __restrict__ seg_end, int32_t* __restrict__ npieces) {
     __shared__ int32_t s_w[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int per = (nb + 1023) / 1024;
     const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
+    // up to 8 rows per thread (8,192 rows = 2M entries) held in registers: their loads issued
+    // together, one memory round trip instead of one per row
+    constexpr int kR = 8;
+    int32_t r[kR];
     int32_t local = 0;
-    for (int i = b0; i < b1; ++i) local += bsum[i];
+    if (per <= kR) {
+#pragma unroll
+        for (int k = 0; k < kR; ++k) r[k] = b0 + k < b1 ? bsum[b0 + k] : 0;
+#pragma unroll
+        for (int k = 0; k < kR; ++k) local += r[k];
+    } else {
+        for (int i = b0; i < b1; ++i) local += bsum[i];
+    }
     int32_t inc = local;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -1068,29 +1035,49 @@ __global__ __launch_bounds__(1024) void slot_scan_kernel(int nb, int32_t* __rest
         total += s_w[w];
     }
     int32_t run = pre + inc - local;
-    for (int i = b0; i < b1; ++i) {
-        const int32_t v = bsum[i];
-        bsum[i] = run;
-        run += v;
+    if (per <= kR) {
+#pragma unroll
+        for (int k = 0; k < kR; ++k)
+            if (b0 + k < b1) {
+                bsum[b0 + k] = run;
+                run += r[k];
+            }
+    } else {
+        for (int i = b0; i < b1; ++i) {
+            const int32_t v = bsum[i];
+            bsum[i] = run;
+            run += v;
+        }
     }
     if (tid == 0) {
         *seg_end = total;
-        *npieces = 0;
+        if (npieces) *npieces = 0;
     }
 }
 
-// stage C: per block, the exclusive prefix of the areas (eight block-wide scans over the
-// coalesced rows o0 + 256 k + tid, k = 0..7) plus the block's offset -> seg and slot of every entry
-template <typename R>
+// stage C: per block of eight rows, the exclusive prefix of the areas (a block-wide scan over
+// each coalesced row o0 + 256 k + tid) plus the row's offset -> seg and slot of every entry, and
+// the big entries' piece list.  FROM_SEG: the areas are seg's differences (seg written by
+// pack3's slot pass) and only the piece list is made
+template <typename R, bool FROM_SEG>
 __global__ __launch_bounds__(256) void slot_write_kernel(int64_t CN, R rect, const int32_t* __restrict__ bpre,
                                                          int32_t* __restrict__ seg, int2* __restrict__ slot,
-                                                         int32_t* __restrict__ pbase, int32_t* __restrict__ pieces,
+                                                         int64_t sstride, int32_t* __restrict__ pbase,
+                                                         int32_t* __restrict__ pieces,
                                                          int32_t* __restrict__ npieces, int64_t piece_cap) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t o0 = (int64_t)blockIdx.x * kSlotPer + tid;
     int area[8], sa[8], x0[8], y0[8], w[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) area[k] = o0 + 256 * k < CN ? rect(o0 + 256 * k, x0[k], y0[k], w[k]) : 0;
+    for (int k = 0; k < 8; ++k) {
+        const int64_t o = o0 + 256 * k;
+        if (FROM_SEG) {
+            x0[k] = y0[k] = w[k] = 0;
+            area[k] = o < CN ? seg[o + 1] - seg[o] : 0;
+        } else {
+            area[k] = o < CN ? rect(o, x0[k], y0[k], w[k]) : 0;
+        }
+    }
     __shared__ int s_w[8][4];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -1129,20 +1116,18 @@ __global__ __launch_bounds__(256) void slot_write_kernel(int64_t CN, R rect, con
 #pragma unroll
         for (int v = 0; v < 4; ++v) pnext += v < wave ? s_p[v] : 0;
     }
-    int run = bpre[blockIdx.x];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        int pre = run;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            pre += v < wave ? s_w[k][v] : 0;
-            run += s_w[k][v];
-        }
         const int64_t o = o0 + 256 * k;
-        if (o < CN) {
+        if (!FROM_SEG && o < CN) {
+            int pre = bpre[blockIdx.x * (kSlotPer / kSlotRow) + k];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) pre += v < wave ? s_w[k][v] : 0;
             const int e = pre + sa[k];
             seg[o] = e;
-            slot[o] = make_int2(e - y0[k] * w[k] - x0[k], w[k]);
+            slot[o * sstride] = make_int2(e - y0[k] * w[k] - x0[k], w[k]);
+        }
+        if (o < CN) {
             int32_t pb = -1;
             if (npk[k] > 0) {
                 pb = pnext;
@@ -1183,7 +1168,7 @@ __global__ void fill_i32_kernel(int64_t n, int32_t* __restrict__ p, int32_t v) {
 static size_t align256_(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t hgsr::grad_slot_bytes(int64_t CN, bool from_lists, int64_t n_isects) {
-    const int64_t nb = (CN + kSlotPer - 1) / kSlotPer, pc = piece_capacity(n_isects);
+    const int64_t nb = (CN + kSlotRow - 1) / kSlotRow, pc = piece_capacity(n_isects);
     size_t b = align256_((size_t)(CN + 1) * 4) + align256_((size_t)CN * 8) + align256_((size_t)(nb + 1) * 4);
     b += align256_((size_t)CN * 4) + align256_((size_t)pc * 4) + 256 + align256_((size_t)pc * kPieceFloats * 4);
     if (from_lists) b += 2 * align256_((size_t)CN * 4);
@@ -1192,13 +1177,15 @@ size_t hgsr::grad_slot_bytes(int64_t CN, bool from_lists, int64_t n_isects) {
 
 int hgsr::launch_grad_slots(int C, int N, const float* means2d, const int32_t* radii, int tile_size, int tw, int th,
                             const int32_t* offsets, const int32_t* flatten_ids, int64_t n_isects, void* buf,
-                            hipStream_t s, GradSlots& out) {
+                            hipStream_t s, GradSlots& out, int2* slot_dst, int64_t sstride) {
     const int64_t CN = (int64_t)C * N;
-    const int64_t nb = (CN + kSlotPer - 1) / kSlotPer;
+    const int64_t nb = (CN + kSlotRow - 1) / kSlotRow;  // rows of the area prefix
+    const int64_t nblk = (CN + kSlotPer - 1) / kSlotPer;  // slot_write blocks
     char* p = (char*)buf;
     out.seg = (int32_t*)p;
     p += align256_((size_t)(CN + 1) * 4);
-    out.slot = (int2*)p;
+    out.slot = slot_dst ? slot_dst : (int2*)p;
+    out.sstride = slot_dst ? sstride : 1;
     p += align256_((size_t)CN * 8);
     int32_t* bsum = (int32_t*)p;
     p += align256_((size_t)(nb + 1) * 4);
@@ -1216,14 +1203,14 @@ int hgsr::launch_grad_slots(int C, int N, const float* means2d, const int32_t* r
         if (int st = memset_async(out.npieces, 4, s, "grad_slots")) return st;
         return memset_async(out.seg, 4, s, "grad_slots");
     }
-    const dim3 grid((unsigned)nb);
+    const dim3 grid((unsigned)nblk), rows((unsigned)nb);
     if (radii) {
         HGSR_REQUIRE(means2d, "null pointer");
         const RectFromRadii r{reinterpret_cast<const float2*>(means2d), radii, tile_size, tw, th};
-        hipLaunchKernelGGL(slot_sum_kernel<RectFromRadii>, grid, dim3(256), 0, s, CN, r, bsum);
+        hipLaunchKernelGGL(slot_sum_kernel<RectFromRadii>, rows, dim3(256), 0, s, CN, r, bsum);
         hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bsum, out.seg + CN, out.npieces);
-        hipLaunchKernelGGL(slot_write_kernel<RectFromRadii>, grid, dim3(256), 0, s, CN, r, bsum, out.seg, out.slot,
-                           out.pbase, out.pieces, out.npieces, out.cap);
+        hipLaunchKernelGGL((slot_write_kernel<RectFromRadii, false>), grid, dim3(256), 0, s, CN, r, bsum, out.seg, out.slot,
+                           out.sstride, out.pbase, out.pieces, out.npieces, out.cap);
     } else {
         HGSR_REQUIRE(offsets && (n_isects == 0 || flatten_ids), "null pointer");
         int32_t* tmin = (int32_t*)p;
@@ -1236,12 +1223,53 @@ int hgsr::launch_grad_slots(int C, int N, const float* means2d, const int32_t* r
             hipLaunchKernelGGL(slot_minmax_kernel, dim3(n_bins), dim3(256), 0, s, tw * th, offsets, n_isects, n_bins,
                                flatten_ids, tmin, tmax);
         const RectFromTiles r{tmin, tmax, tw};
-        hipLaunchKernelGGL(slot_sum_kernel<RectFromTiles>, grid, dim3(256), 0, s, CN, r, bsum);
+        hipLaunchKernelGGL(slot_sum_kernel<RectFromTiles>, rows, dim3(256), 0, s, CN, r, bsum);
         hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bsum, out.seg + CN, out.npieces);
-        hipLaunchKernelGGL(slot_write_kernel<RectFromTiles>, grid, dim3(256), 0, s, CN, r, bsum, out.seg, out.slot,
-                           out.pbase, out.pieces, out.npieces, out.cap);
+        hipLaunchKernelGGL((slot_write_kernel<RectFromTiles, false>), grid, dim3(256), 0, s, CN, r, bsum, out.seg, out.slot,
+                           out.sstride, out.pbase, out.pieces, out.npieces, out.cap);
     }
     return check_launch("grad_slots");
+}
+
+size_t hgsr::slot_prefix_bytes(int64_t CN) {
+    return align256_((size_t)(CN + 1) * 4) + align256_((size_t)((CN + kSlotRow - 1) / kSlotRow + 1) * 4);
+}
+
+int hgsr::launch_slot_prefix(int64_t CN, const RectFromRadii& r, void* buf, hipStream_t s) {
+    int32_t* const seg = (int32_t*)buf;
+    int32_t* const bpre = (int32_t*)((char*)buf + align256_((size_t)(CN + 1) * 4));
+    const int64_t nb = (CN + kSlotRow - 1) / kSlotRow;
+    HGSR_REQUIRE(nb < (1ll << 31), "too many Gaussians for the gradient slots");
+    if (CN == 0) return memset_async(seg, 4, s, "slot_prefix");
+    hipLaunchKernelGGL(slot_sum_kernel<RectFromRadii>, dim3((unsigned)nb), dim3(256), 0, s, CN, r, bpre);
+    hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bpre, seg + CN, (int32_t*)nullptr);
+    return check_launch("slot_prefix");
+}
+
+int hgsr::launch_grad_pieces(int64_t CN, const int32_t* seg, int64_t n_isects, void* buf, hipStream_t s,
+                             GradSlots& out) {
+    // the layout of launch_grad_slots' buffer (grad_slot_bytes), seg and slot held elsewhere
+    const int64_t nb = (CN + kSlotRow - 1) / kSlotRow, nblk = (CN + kSlotPer - 1) / kSlotPer;
+    char* p = (char*)buf;
+    out.seg = const_cast<int32_t*>(seg);
+    out.slot = nullptr;
+    out.sstride = 0;
+    p += align256_((size_t)(CN + 1) * 4) + align256_((size_t)CN * 8) + align256_((size_t)(nb + 1) * 4);
+    out.cap = piece_capacity(n_isects);
+    out.pbase = (int32_t*)p;
+    p += align256_((size_t)CN * 4);
+    out.pieces = (int32_t*)p;
+    p += align256_((size_t)out.cap * 4);
+    out.npieces = (int32_t*)p;
+    p += 256;
+    out.partial = (float*)p;
+    if (int st = memset_async(out.npieces, 4, s, "grad_pieces")) return st;
+    if (CN == 0) return HGSR_OK;
+    const RectFromRadii none{nullptr, nullptr, 0, 0, 0};
+    hipLaunchKernelGGL((slot_write_kernel<RectFromRadii, true>), dim3((unsigned)nblk), dim3(256), 0, s, CN, none,
+                       (const int32_t*)nullptr, out.seg, (int2*)nullptr, (int64_t)0, out.pbase, out.pieces,
+                       out.npieces, out.cap);
+    return check_launch("grad_pieces");
 }
 
 using namespace hgsr;

@@ -71,21 +71,49 @@ __device__ __forceinline__ float sigma2(const float4 g0, const float4 g1, float 
 }
 
 // One workgroup packs 256 consecutive (camera, Gaussian) records; the conics (12 B each)
-// come in and the 48-B records leave as contiguous float4 runs through LDS (lane-strided
-// AoS loads / stores touch ~12-48 cache lines per instruction): 37.6 -> 29.3 us at c2.
-template <int D>
+// come in and the 64-B records leave as contiguous float4 runs through LDS (lane-strided
+// AoS loads / stores touch ~12-48 cache lines per instruction): 37.6 -> 29.3 us at c2 (48-B
+// records).  SLOTS (a forward a backward follows): the workgroup's 256 entries are one row of
+// the slot-area prefix (launch_slot_prefix summed and scanned the rows), so a block scan of the
+// rectangles' areas gives seg and each record's gradient-slot base here, written with the record
+// instead of scattered into the records by the backward (8 B into each 64-B record: 60 us at c2);
+// else the slot quad is zero.
+template <int D, bool SLOTS>
 __global__ __launch_bounds__(256) void pack3_kernel(int64_t n, int N, const float2* __restrict__ means2d,
                                                     const float* __restrict__ conics, ChanSrc cs,
-                                                    Rec3* __restrict__ rec) {
-    constexpr int kOP = 13;  // record pitch in LDS (12 floats + 1: conflict-free lane stride)
+                                                    Rec3* __restrict__ rec, RectFromRadii rr,
+                                                    const int32_t* __restrict__ bpre, int32_t* __restrict__ seg) {
+    constexpr int kOP = 17;  // record pitch in LDS (16 floats + 1: conflict-free lane stride)
     __shared__ __attribute__((aligned(16))) float s_buf[256 * kOP];
     const int64_t i0 = (int64_t)blockIdx.x * 256;
     const int nloc = (int)min((int64_t)256, n - i0);
     const int t = threadIdx.x;
     const int64_t i = i0 + t;
     stage_floats(conics + i0 * 3, nloc * 3, s_buf);
+    int4 sl = make_int4(0, 0, 0, 0);
+    int area = 0, inc = 0, x0 = 0, y0 = 0, w = 0;
+    __shared__ int s_ws[4];
+    if (SLOTS) {
+        static_assert(kSlotRow == 256, "one prefix row per workgroup");
+        if (t < nloc) area = rr(i, x0, y0, w);
+        inc = area;
+        const int lane = t & 63;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(inc, d);
+            if (lane >= d) inc += o;
+        }
+        if (lane == 63) s_ws[t >> 6] = inc;
+    }
     __syncthreads();
     const float a = s_buf[t * 3], b = s_buf[t * 3 + 1], cc = s_buf[t * 3 + 2];
+    if (SLOTS && t < nloc) {
+        int e = bpre[blockIdx.x] + inc - area;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) e += v < (t >> 6) ? s_ws[v] : 0;
+        seg[i] = e;
+        sl = make_int4(e - y0 * w - x0, w, 0, 0);
+    }
     __syncthreads();  // s_buf now holds the records
     if (t < nloc) {
         const int64_t c = i / N, g = i - c * N;
@@ -95,16 +123,18 @@ __global__ __launch_bounds__(256) void pack3_kernel(int64_t n, int N, const floa
         const float* src = cs.colors + c * cs.col_cstride + g * cs.dc;
 #pragma unroll
         for (int k = 0; k < D; ++k) col[k] = k < cs.dc ? src[k] : cs.depths[i];
-        const Rec3 r = make_rec3(m, a, b, cc, o, col);
-        const float v[12] = {r.g0.x, r.g0.y, r.g0.z, r.g0.w, r.g1.x, r.g1.y,
-                             r.g1.z, r.g1.w, r.col.x, r.col.y, r.col.z, r.col.w};
+        Rec3 r = make_rec3(m, a, b, cc, o, col);
+        r.sl = sl;
+        const float v[16] = {r.g0.x, r.g0.y, r.g0.z, r.g0.w, r.g1.x, r.g1.y, r.g1.z, r.g1.w,
+                             r.col.x, r.col.y, r.col.z, r.col.w, __int_as_float(r.sl.x), __int_as_float(r.sl.y),
+                             __int_as_float(r.sl.z), __int_as_float(r.sl.w)};
 #pragma unroll
-        for (int k = 0; k < 12; ++k) s_buf[t * kOP + k] = v[k];
+        for (int k = 0; k < 16; ++k) s_buf[t * kOP + k] = v[k];
     }
     __syncthreads();
     float4* dst = reinterpret_cast<float4*>(rec + i0);
-    for (int q = t; q < nloc * 3; q += 256) {
-        const int e = q / 3, f = q - e * 3;
+    for (int q = t; q < nloc * 4; q += 256) {
+        const int e = q >> 2, f = q & 3;
         const float* p = s_buf + e * kOP + 4 * f;
         dst[q] = make_float4(p[0], p[1], p[2], p[3]);
     }
@@ -335,7 +365,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     int64_t n_isects, const int32_t* __restrict__ flatten_ids, const float* __restrict__ render_alphas,
     const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
     const float* __restrict__ v_render_alphas, float* __restrict__ rows, uint8_t* __restrict__ flags,
-    const int2* __restrict__ slot, int64_t n_slots, unsigned long long* __restrict__ pair_counter,
+    int64_t n_slots, unsigned long long* __restrict__ pair_counter,
     const uint64_t* __restrict__ qmask, int64_t qstride, const int32_t* __restrict__ order) {
     constexpr int NB = kBwdBatch;
     // double-buffered staging: batch b+1 is loaded while batch b is composited (two
@@ -428,8 +458,9 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         atomicAdd(pair_slot(pair_counter, 0), (unsigned long long)(end - tc.start) * kTilePixels);
     // records are staged with LDS-DMA (global_load_lds_dwordx4: per-lane source, LDS
     // destination wave base + 16 B x lane) one batch ahead; ids two batches ahead in a
-    // register; lanes < NB (waves 0, 1) load one Gaussian each, clamped indices; with each id its
-    // slot base {seg - y0 w - x0, w} (isect.hip), so the record's gradient slot is base + y w + x
+    // register; lanes < NB (waves 0, 1) load one Gaussian each, clamped indices; with each record
+    // its slot base {seg - y0 w - x0, w} (Rec3::sl, the same 64-B sector as the DMA: an L2 hit),
+    // so the record's gradient slot is base + y w + x
     int32_t cid = 0, nid = 0;
     int2 csl = make_int2(-1, 0);
     const bool loader = tid < NB;
@@ -443,7 +474,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     if (nb > 0 && loader) {
         cid = flatten_ids[max(end - 1 - tid, tc.start)];
         dma_batch(0, cid);
-        csl = slot[cid];
+        csl = *reinterpret_cast<const int2*>(&rec[cid].sl);
         nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
     }
     uint8_t* my_list = s_list[wave];
@@ -489,7 +520,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         if (b + 1 < nb && loader) {
             cid = nid;
             dma_batch(prv, cid);
-            csl = slot[cid];
+            csl = *reinterpret_cast<const int2*>(&rec[cid].sl);
             nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
         lds_barrier();
@@ -772,13 +803,25 @@ static int check_raster(int C, int N, int D, int W, int H, int tile_size, int tw
 
 static size_t rec_bytes(int C, int N) { return ((size_t)C * N * sizeof(Rec3) + 255) & ~(size_t)255; }
 
+// slots (nullable): the rectangles, and the buffer launch_slot_prefix filled (seg, then the row
+// prefix), for records that carry their gradient slots
 static int pack3(int C, int N, int D, const float* means2d, const float* conics, const ChanSrc& cs, Rec3* rec,
-                 hipStream_t s) {
+                 hipStream_t s, const RectFromRadii* rr = nullptr, void* slots = nullptr) {
     const int64_t n = (int64_t)C * N;
     if (n == 0) return HGSR_OK;
     const dim3 grid((unsigned)((n + 255) / 256));
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
-#define LAUNCH_P(DD) hipLaunchKernelGGL(pack3_kernel<DD>, grid, dim3(256), 0, s, n, N, m2, conics, cs, rec)
+    int32_t* const seg = (int32_t*)slots;
+    const int32_t* const bpre = slots ? (const int32_t*)((char*)slots + (((size_t)(n + 1) * 4 + 255) & ~(size_t)255))
+                                      : nullptr;
+    const RectFromRadii none{nullptr, nullptr, 0, 0, 0};
+#define LAUNCH_P(DD)                                                                                            \
+    if (slots)                                                                                                  \
+        hipLaunchKernelGGL((pack3_kernel<DD, true>), grid, dim3(256), 0, s, n, N, m2, conics, cs, rec, *rr, bpre, \
+                           seg);                                                                                \
+    else                                                                                                        \
+        hipLaunchKernelGGL((pack3_kernel<DD, false>), grid, dim3(256), 0, s, n, N, m2, conics, cs, rec, none,    \
+                           (const int32_t*)nullptr, (int32_t*)nullptr)
     switch (D) {
         case 1: LAUNCH_P(1); break;
         case 2: LAUNCH_P(2); break;
@@ -795,9 +838,10 @@ extern "C" size_t hgsr_raster3d_qmask_bytes(int C, int tile_w, int tile_h, int64
     return tile_order_bytes(n_bins) + (size_t)(4 * qmask_stride(n_isects, n_bins)) * sizeof(uint64_t);
 }
 
+// the records, then the slot prefix a training forward fills (hgsr_raster3d_pack_fused with radii)
 extern "C" size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D) {
     (void)D;
-    return rec_bytes(C, N);
+    return rec_bytes(C, N) + slot_prefix_bytes((int64_t)C * N);
 }
 
 static int raster3d_fwd_launch(int C, int D, const Rec3* rec, const float* backgrounds, int bg_ch, int ed_ch,
@@ -887,7 +931,8 @@ extern "C" int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2
 
 extern "C" int hgsr_raster3d_pack_fused(int C, int N, int Dc, const float* means2d, const float* conics,
                                         const float* colors, int colors_shared, const float* depths,
-                                        const float* opacities, int opacities_shared, void* ws, size_t ws_bytes,
+                                        const float* opacities, int opacities_shared, const int32_t* radii,
+                                        int tile_size, int tile_w, int tile_h, void* ws, size_t ws_bytes,
                                         hgsr_stream_t stream) {
     HGSR_REQUIRE(C >= 1 && N >= 0, "bad dims");
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
@@ -897,7 +942,14 @@ extern "C" int hgsr_raster3d_pack_fused(int C, int N, int Dc, const float* means
     HGSR_REQUIRE(N == 0 || (means2d && conics && (colors || Dc == 0) && opacities && ws), "null pointer");
     const ChanSrc cs{colors, colors_shared ? 0 : (int64_t)N * Dc, Dc, depths, opacities,
                      opacities_shared ? 0 : (int64_t)N};
-    return pack3(C, N, D, means2d, conics, cs, (Rec3*)ws, as_stream(stream));
+    hipStream_t s = as_stream(stream);
+    if (!radii || N == 0) return pack3(C, N, D, means2d, conics, cs, (Rec3*)ws, s);
+    // a backward follows: the records carry their gradient slots (isect_tiles' rectangles)
+    HGSR_REQUIRE(tile_size > 0 && tile_w > 0 && tile_h > 0, "bad tile grid");
+    const RectFromRadii rr{reinterpret_cast<const float2*>(means2d), radii, tile_size, tile_w, tile_h};
+    void* const slots = (char*)ws + rec_bytes(C, N);
+    if (int st = launch_slot_prefix((int64_t)C * N, rr, slots, s)) return st;
+    return pack3(C, N, D, means2d, conics, cs, (Rec3*)ws, s, &rr, slots);
 }
 
 extern "C" int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_depth,
@@ -948,7 +1000,7 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              const float* v_render_alphas, float* v_means2d, float* v_conics, const ChanDst& cd,
                              float* v_means2d_abs, const void* fwd_ws, void* ws, size_t ws_bytes,
                              hgsr_stream_t stream, const void* qbuf = nullptr, size_t qmask_bytes = 0,
-                             bool flags_zeroed = false, const int32_t* radii = nullptr) {
+                             bool flags_zeroed = false, const int32_t* radii = nullptr, bool fwd_slots = false) {
     if (int st = check_raster(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster3d_bwd_ws_bytes(C, N, D, n_isects, fwd_ws != nullptr),
                  "raster3d_bwd workspace too small");
@@ -978,18 +1030,24 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     char* const sbuf = (char*)rows + rows3_bytes(n_isects);
     if (!flags_zeroed)  // else hgsr_raster3d_fwd_packed cleared them (bwd_ws)
         if (int st = memset_async(flags, slot_flag_bytes(n_isects, kSlotWaves), s, "raster3d_bwd")) return st;
-    // each (camera, Gaussian)'s gradient slots: from its tile rectangle (radii given), else
-    // from the lists
-    GradSlots gs;
-    if (int st = launch_grad_slots(C, N, means2d, radii, tile_size, tile_w, tile_h, isect_offsets, flatten_ids,
-                                   n_isects, sbuf, s, gs))
-        return st;
     // the forward's packed records when the caller kept them, else pack again
-    const Rec3* rec = (const Rec3*)fwd_ws;
+    Rec3* rec = (Rec3*)const_cast<void*>(fwd_ws);
     if (!rec) {
-        Rec3* own = (Rec3*)(sbuf + grad_slot_bytes(n, true, n_isects));
-        if (int st = pack3(C, N, D, means2d, conics, cs, own, s)) return st;
-        rec = own;
+        rec = (Rec3*)(sbuf + grad_slot_bytes(n, true, n_isects));
+        if (int st = pack3(C, N, D, means2d, conics, cs, rec, s)) return st;
+    }
+    // each (camera, Gaussian)'s gradient slots: the training forward packed them into the records
+    // (fwd_slots: seg follows the records in fwd_ws), and only the big entries' piece list is left;
+    // else from the tile rectangles (radii given) or the lists, the slot bases scattered into the
+    // records' slot quads (Rec3::sl)
+    GradSlots gs;
+    if (fwd_ws && fwd_slots) {
+        const int32_t* const seg = (const int32_t*)((const char*)fwd_ws + rec_bytes(C, N));
+        if (int st = launch_grad_pieces(n, seg, n_isects, sbuf, s, gs)) return st;
+    } else if (int st = launch_grad_slots(C, N, means2d, radii, tile_size, tile_w, tile_h, isect_offsets, flatten_ids,
+                                          n_isects, sbuf, s, gs, reinterpret_cast<int2*>(&rec->sl),
+                                          sizeof(Rec3) / sizeof(int2))) {
+        return st;
     }
     const int64_t n_bins = (int64_t)C * tile_w * tile_h;
     const dim3 grid((unsigned)n_bins);
@@ -1014,7 +1072,7 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
                            tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,       \
                            flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, flags,  \
-                           gs.slot, n_isects, pairs, qmask, qstride, order);                                   \
+                           n_isects, pairs, qmask, qstride, order);                                            \
     }                                                                                                          \
     hipLaunchKernelGGL((reduce_pieces_kernel<12, 3, kRow3, kSlotWaves>), dim3(piece_grid(gs)), dim3(256), 0, s,   \
                        rows, flags, gs.seg, gs.pbase, gs.pieces, gs.npieces, gs.partial);                          \
@@ -1062,7 +1120,7 @@ extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2
                                        float* v_means2d, float* v_conics, float* v_colors, float* v_depths,
                                        float* v_opacities, float* v_means2d_abs, const void* fwd_ws, void* ws,
                                        size_t ws_bytes, const void* qmask, size_t qmask_bytes, int ws_zeroed,
-                                       const int32_t* radii, hgsr_stream_t stream) {
+                                       const int32_t* radii, int fwd_slots, hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!qmask || qmask_bytes >= hgsr_raster3d_qmask_bytes(C, tile_w, tile_h, n_isects),
                  "raster3d_bwd_fused: quadrant-mask buffer too small");
@@ -1077,5 +1135,5 @@ extern "C" int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2
                              render_colors, width, height, tile_size, tile_w, tile_h, isect_offsets, n_isects,
                              flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, v_means2d,
                              v_conics, cd, v_means2d_abs, fwd_ws, ws, ws_bytes, stream, qmask, qmask_bytes,
-                             ws_zeroed != 0, radii);
+                             ws_zeroed != 0, radii, fwd_slots != 0);
 }

@@ -582,9 +582,11 @@ class _Raster3DFused(torch.autograd.Function):
     kernels instead of torch cat / repeat / divide (gsplat rendering.py does those in torch)."""
 
     @staticmethod
-    def pack(means2d, conics, colors, depths, opacities):
+    def pack(means2d, conics, colors, depths, opacities, radii=None, tiles=(0, 0, 0)):
         """Raster records for forward(records=...): launched before the intersection
-        count is read back, so the packing overlaps the host sync."""
+        count is read back, so the packing overlaps the host sync.  radii (when a backward will
+        follow; tiles = (tile_size, tile_width, tile_height)): the records also carry their
+        gradient slots -- pass the same radii to forward()."""
         C, Ng = means2d.shape[:2]
         Dc = 0 if colors is None else colors.shape[-1]
         D = Dc + (0 if depths is None else 1)
@@ -592,7 +594,7 @@ class _Raster3DFused(torch.autograd.Function):
         ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=means2d.device)
         N.call("hgsr_raster3d_pack_fused", C, Ng, Dc, ptr(means2d), ptr(conics), ptr(colors),
                int(colors is not None and colors.dim() == 2), ptr(depths), ptr(opacities), int(opacities.dim() == 1),
-               ptr(ws), ws_b, N.stream(means2d.device))
+               ptr(radii), *tiles, ptr(ws), ws_b, N.stream(means2d.device))
         return ws
 
     @staticmethod
@@ -601,7 +603,8 @@ class _Raster3DFused(torch.autograd.Function):
                 radii=None):
         """deferred (_Deferred): flatten_ids is its capacity-sized array, the count device-resident.
         radii: the projection's radii the lists were emitted from (the backward's gradient slots
-        follow their tile rectangles; without them the backward finds the rectangles in the lists)."""
+        follow their tile rectangles; without them the backward finds the rectangles in the lists);
+        records packed with the same radii carry the slots already."""
         C, Ng = means2d.shape[:2]
         Dc = 0 if colors is None else colors.shape[-1]
         D = Dc + (0 if depths is None else 1)
@@ -640,6 +643,7 @@ class _Raster3DFused(torch.autograd.Function):
         ctx.qmask = qmask
         ctx.deferred = deferred
         ctx.radii = None if radii is None else radii.detach().contiguous()
+        ctx.fwd_slots = records is not None and radii is not None  # pack(radii=...) filled the slots
         return rc, ra
 
     @staticmethod
@@ -666,7 +670,7 @@ class _Raster3DFused(torch.autograd.Function):
                tile_size, tw, th, ptr(offsets), n_is, ptr(flatten_ids) if n_is else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_means2d), ptr(v_conics), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_abs), ptr(fwd_ws),
                ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(), zeroed,
-               ptr(ctx.radii), N.stream(dev))
+               ptr(ctx.radii), int(ctx.fwd_slots), N.stream(dev))
         if absgrad:
             means2d.absgrad = v_abs
         v_bg = None
@@ -994,15 +998,19 @@ def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, 
         # records are packed while the host waits for the intersection count
         r_in = (_f32(means2d), _f32(conics), _f32(cols) if rgb else None, _f32(depths) if with_depth else None,
                 _f32(opacities))
-        records = _Raster3DFused.pack(*(t.detach() if t is not None else None for t in r_in))
+        ed, grad_mode = render_mode in ("ED", "RGB+ED"), torch.is_grad_enabled()
+        # a backward will follow: the records carry their gradient slots (the same radii go to
+        # the Function, whose backward then finds them there)
+        slot_radii = radii.contiguous() if grad_mode and any(t is not None and t.requires_grad for t in r_in) else None
+        records = _Raster3DFused.pack(*(t.detach() if t is not None else None for t in r_in), radii=slot_radii,
+                                      tiles=(int(tile_size), tw, th))
         bgs = None if (backgrounds is None or not rgb) else _f32(backgrounds)
         args = (bgs, int(width), int(height), int(tile_size))
-        ed, grad_mode = render_mode in ("ED", "RGB+ED"), torch.is_grad_enabled()
         tpg, isect_offsets = isect_state[3], isect_state[4]
         d = _isect_emit_deferred(isect_state)
         if d is not None:  # emission, sort and forward queued; then the count is read
             render_colors, render_alphas = _Raster3DFused.apply(*r_in, *args, isect_offsets, d.flat, ed, absgrad,
-                                                                records, grad_mode, d, radii)
+                                                                records, grad_mode, d, slot_radii)
             if _isect_resolve(isect_state, d):
                 isect_ids, flatten_ids = d.ids[:d.n], d.flat[:d.n]
             else:
@@ -1010,7 +1018,7 @@ def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, 
         if d is None:
             tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
             render_colors, render_alphas = _Raster3DFused.apply(*r_in, *args, isect_offsets, flatten_ids, ed,
-                                                                absgrad, records, grad_mode, None, radii)
+                                                                absgrad, records, grad_mode, None, slot_radii)
         opac = opacities.expand(C, -1)
     else:
         tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)

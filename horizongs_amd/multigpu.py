@@ -350,6 +350,7 @@ class ShardedAdamDDP:
         self._hooks = []
         self.buckets: List[dict] = []
         self._in_step = False
+        self.copies = 0
 
     def _active(self) -> bool:
         return dist.is_initialized() and (dist.get_world_size(self.group) > 1 or _FORCE)
@@ -448,6 +449,7 @@ class ShardedAdamDDP:
         self.wait_deferred()  # backstop: the next backward / Adam touch the deferred buffers
         self._bind()
         self._next = 0
+        self.copies = 0  # gradients of this step the hook had to copy into a bucket (0: all in place)
         for b in self.buckets:
             b["ready"] = [False] * len(b["members"])
             b["work"], b["launched"], b["gsrc"] = None, False, None
@@ -474,6 +476,7 @@ class ShardedAdamDDP:
             dst = b["gflat"][o:o + n]
             if g.data_ptr() != dst.data_ptr() or not g.is_contiguous():  # produced elsewhere: copy it in
                 dst.copy_(g.reshape(-1))
+                self.copies += 1
             b["gsrc"] = None
         p.grad = None  # the reduced gradient exists only as this rank's shard
         b["ready"][k] = True

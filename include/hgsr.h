@@ -158,7 +158,7 @@ int hgsr_isect_offset_encode(int64_t n_isects, const int64_t* isect_ids, int C, 
  * call; callers chunk wider channel counts).  colors [C*N, D], opacities [C*N],
  * backgrounds [C, D] nullable.  Outputs render_colors [C,H,W,D],
  * render_alphas [C,H,W,1], last_ids [C,H,W].  ws: caller scratch of
- * hgsr_raster3d_fwd_ws_bytes() (packed 48-B per-Gaussian raster records). */
+ * hgsr_raster3d_fwd_ws_bytes() (packed 64-B per-Gaussian raster records). */
 size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D);
 int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, const float* conics,
                       const float* colors, const float* opacities, const float* backgrounds,
@@ -169,7 +169,8 @@ int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, const float* co
 /* writes (overwrites) v_means2d [C*N,2], v_conics [C*N,3], v_colors [C*N,D],
  * v_opacities [C*N]; v_means2d_abs nullable (gsplat absgrad).  fwd_ws: the
  * workspace hgsr_raster3d_fwd filled for the same inputs (its packed records
- * are reused), or NULL to pack again.  ws: caller scratch of
+ * are reused; the backward writes each record's gradient-slot quad, a field the
+ * forward does not read), or NULL to pack again.  ws: caller scratch of
  * hgsr_raster3d_bwd_ws_bytes(C, N, D, n_isects, fwd_ws != NULL).
  * Deterministic: every (tile, Gaussian) pair's per-wave partial sums go to the pair's own
  * gradient slot and each Gaussian's slots are summed in one fixed order (no float atomics),
@@ -223,9 +224,13 @@ int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * capacity the intersection arrays and qmask were sized for); the quadrant-mask stride is
  * derived from qmask_bytes, so the backward must get the same buffer and size. */
 size_t hgsr_raster3d_qmask_bytes(int C, int tile_w, int tile_h, int64_t n_isects);
+/* radii (nullable, [C,N] int32, with the tile grid): a backward will follow; the records then
+ * carry each (camera, Gaussian)'s gradient-slot base (its isect_tiles rectangle in the grid) and
+ * ws the slots' prefix, which hgsr_raster3d_bwd_fused given fwd_slots = 1 uses as they are. */
 int hgsr_raster3d_pack_fused(int C, int N, int Dc, const float* means2d, const float* conics,
                              const float* colors, int colors_shared, const float* depths,
-                             const float* opacities, int opacities_shared, void* ws, size_t ws_bytes,
+                             const float* opacities, int opacities_shared, const int32_t* radii,
+                             int tile_size, int tile_w, int tile_h, void* ws, size_t ws_bytes,
                              hgsr_stream_t stream);
 int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_depth,
                              const float* backgrounds, int width, int height, int tile_size,
@@ -240,7 +245,9 @@ int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_
  * qmask (nullable): the buffer hgsr_raster3d_fwd_packed filled for the same lists.
  * radii (nullable, [C,N] int32): the projection's radii the lists were emitted from
  * (isect_tiles(means2d, radii, ...)); given, the gradient slots come from the tile rectangles
- * directly instead of from a pass over the lists.  ws: hgsr_raster3d_bwd_ws_bytes(C, N,
+ * directly instead of from a pass over the lists.  fwd_slots: fwd_ws came from
+ * hgsr_raster3d_pack_fused given these radii (its records carry the slots; only the big
+ * entries' piece list is made here).  ws: hgsr_raster3d_bwd_ws_bytes(C, N,
  * Dc + (depths ? 1 : 0), n_isects, fwd_ws != NULL). */
 int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2d, const float* conics,
                             const float* colors, int colors_shared, const float* depths,
@@ -253,7 +260,7 @@ int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             float* v_means2d, float* v_conics, float* v_colors, float* v_depths,
                             float* v_opacities, float* v_means2d_abs, const void* fwd_ws, void* ws,
                             size_t ws_bytes, const void* qmask, size_t qmask_bytes, int ws_zeroed,
-                            const int32_t* radii, hgsr_stream_t stream);
+                            const int32_t* radii, int fwd_slots, hgsr_stream_t stream);
 
 /* ---- K11/K12: 2DGS surfel rasterization -----------------------------------
  * replaces gsplat rasterize_to_pixels_2dgs.  The LAST colour channel is the
