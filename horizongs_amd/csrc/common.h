@@ -519,6 +519,35 @@ __device__ __forceinline__ void lds_dma16(const void* src, void* lds_dst) {
 #endif
 }
 
+// Wait-site attribution hooks (scripts/micro/wait_probe.py builds the library with
+// -DHGSR_PROBE_WAIT=1 into its own directory; in the product build they compile to nothing).
+// HGSR_WP_MARK(k) adds the shader-clock cycles since the previous mark to the wave's site k;
+// HGSR_WP_FLUSH() adds the wave's sites into the kernel's device-global sums (vector atomics).
+#ifndef HGSR_PROBE_WAIT
+#define HGSR_PROBE_WAIT 0
+#endif
+#if HGSR_PROBE_WAIT
+#define HGSR_WP_DECL(acc)                                   \
+    unsigned long long wp_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+    unsigned long long wp_t_ = __builtin_amdgcn_s_memtime();  \
+    unsigned long long* const wp_dst_ = (acc)
+#define HGSR_WP_MARK(k)                                               \
+    {                                                                 \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+        wp_acc_[k] += t_ - wp_t_;                                     \
+        wp_t_ = t_;                                                   \
+    }
+#define HGSR_WP_FLUSH()                                                                  \
+    if ((threadIdx.x & 63) == 0) {                                                       \
+        for (int k_ = 0; k_ < 8; ++k_) atomicAdd(wp_dst_ + k_, wp_acc_[k_]);              \
+        atomicAdd(wp_dst_ + 8, 1ull);                                                    \
+    }
+#else
+#define HGSR_WP_DECL(acc)
+#define HGSR_WP_MARK(k)
+#define HGSR_WP_FLUSH()
+#endif
+
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }

@@ -358,6 +358,20 @@ struct Pass2Lane {
     float vo[4][4];          // [m][slot]: upstream colour gradient of pixel m, lane-permuted channels
 };
 
+#if HGSR_PROBE_WAIT
+// raster3d_bwd's wait sites (scripts/micro/wait_probe.py): 0 setup, 1 batch-top vmcnt wait, 2 DMA /
+// slot issue, 3 first barrier, 4 compaction, 5 steps + pass 2, 6 second barrier, 7 tail; [8] waves
+__device__ unsigned long long g_wait_bwd3[16];
+extern "C" int hgsr_probe_wait_read(unsigned long long* host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wait_bwd3), sizeof(g_wait_bwd3)) != hipSuccess) return 1;
+    if (reset) {
+        static const unsigned long long zero[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_wait_bwd3), zero, sizeof(zero)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
+
 template <int D, bool ABS>
 __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     int C, int W, int H, int tw, int th, const Rec3* __restrict__ rec, const float* __restrict__ backgrounds,
@@ -366,8 +380,10 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
     const int32_t* __restrict__ last_ids, const float* __restrict__ v_render_colors,
     const float* __restrict__ v_render_alphas, float* __restrict__ rows, uint8_t* __restrict__ flags,
     int64_t n_slots, unsigned long long* __restrict__ pair_counter,
-    const uint64_t* __restrict__ qmask, int64_t qstride, const int32_t* __restrict__ order) {
+    const uint64_t* __restrict__ qmask, int64_t qstride, const int32_t* __restrict__ order,
+    const int32_t* __restrict__ tile_end) {
     constexpr int NB = kBwdBatch;
+    HGSR_WP_DECL(g_wait_bwd3);
     // double-buffered staging: batch b+1 is loaded while batch b is composited (two
     // barriers per batch); slot NB is a zero-opacity dummy
     // one LDS object, so every component of record t sits at a compile-time offset from one
@@ -441,16 +457,24 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         }
     }
     const int32_t bin_final = tc.inside ? last_ids[tc.pix] : -1;
-    const int32_t wave_final = wave_max_i32(bin_final);
-    if (lane == 0) s_last[wave] = wave_final;
     if (tid < 6) {
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
         sr.g0[tid >> 1][NB] = z;  // both buffers' dummy records: opacity 0, never composited
         sr.g1[tid >> 1][NB] = z;
-        sr.col[tid >> 1][NB] = z;
+        sr.col[tid >> 1][NB] = z;  // (published by the first batch's barrier)
     }
-    lds_barrier();
-    const int32_t blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
+    // the tile's latest contributor: the forward's tile_end when it kept one (a load issued with
+    // the tile's offsets, so the first ids and DMA do not wait for the pixels' last ids and a
+    // workgroup barrier), else the maximum of the pixels' last ids
+    int32_t blk_final;
+    if (tile_end) {
+        blk_final = __builtin_amdgcn_readfirstlane(tile_end[(int64_t)tc.cam * (tw * th) + tc.tile]) - 1;
+    } else {
+        const int32_t wf = wave_max_i32(bin_final);
+        if (lane == 0) s_last[wave] = wf;
+        lds_barrier();
+        blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
+    }
     // Gaussians after the block's last contributor are never reached
     const int32_t end = min(tc.end, blk_final + 1);
     const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
@@ -505,6 +529,9 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         qw[2] = qp[2];
     };
     if (qmask && nb > 0) qfetch(0);
+    // this quadrant's latest contributor (after the first batch's loads are out)
+    const int32_t wave_final = wave_max_i32(bin_final);
+    HGSR_WP_MARK(0);
     for (int b = 0; b < nb; ++b) {
         const int cur = b & 1, prv = cur ^ 1;
         const int32_t batch_end = end - 1 - b * NB;
@@ -513,6 +540,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         // before the barrier below publishes it; then DMA batch b+1 into the other buffer
         // (its previous records were last read before the previous barrier)
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+        HGSR_WP_MARK(1);
         if (tid < bsz) {
             const int64_t e = (int64_t)csl.x + (int64_t)tile_y * csl.y + tile_x;
             s_e[cur][tid] = (e >= 0 && e < n_slots) ? (int32_t)e : -1;  // (inconsistent lists: no store)
@@ -523,7 +551,9 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
             csl = *reinterpret_cast<const int2*>(&rec[cid].sl);
             nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
+        HGSR_WP_MARK(2);
         lds_barrier();
+        HGSR_WP_MARK(3);
         // phase 2: composite batch b, first the per-wave list of its records that reach this
         // quadrant and are not behind every pixel's last contributor (order-preserving)
         const int t0 = max(0, batch_end - wave_final);
@@ -567,6 +597,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         // padded with the dummy to a multiple of 4
         if (lane < 4 && n_mine + lane < NB) my_list[n_mine + lane] = (uint8_t)NB;
         stepped += (uint32_t)n_mine;
+        HGSR_WP_MARK(4);
         if (n_mine > 0) {
             // the list comes back into registers once per batch; the loop reads
             // entries with readlane so no LDS index read sits on the critical path
@@ -727,10 +758,14 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
                 pass2(packed, F, V);
             }
         }
+        HGSR_WP_MARK(5);
         lds_barrier();
+        HGSR_WP_MARK(6);
     }
     if (pair_counter && lane == 0 && stepped)  // measurement only: lane-pairs stepped
         atomicAdd(pair_slot(pair_counter, 1), (unsigned long long)stepped * 64ull);
+    HGSR_WP_MARK(7);
+    HGSR_WP_FLUSH();
 }
 
 // Gradient slots -> gsplat's separate gradient tensors (overwrite): each (camera, Gaussian)'s
@@ -1057,6 +1092,8 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     const int64_t qstride = qbuf ? qmask_stride_of(qmask_bytes, n_bins) : 0;
     // the forward writes the order only for a non-empty view
     const int32_t* const order = (qbuf && HGSR_TILE_ORDER && n_isects > 0) ? tile_order_of(qbuf) : nullptr;
+    // each tile's latest contributor + 1, written by the forward with the order
+    const int32_t* const tile_end = (HGSR_BWD_ORDER && order) ? tile_end_of(const_cast<void*>(qbuf), n_bins) : nullptr;
     if (HGSR_BWD_ORDER && order) {
         // re-sort the tiles by the ranges the backward walks (up to each tile's latest contributor,
         // written by the forward) instead of by their whole bins
@@ -1072,7 +1109,7 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         hipLaunchKernelGGL((raster3d_bwd_kernel<DD, AA>), grid, dim3(256), 0, s, C, width, height, tile_w,      \
                            tile_h, rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects,       \
                            flatten_ids, render_alphas, last_ids, v_render_colors, v_render_alphas, rows, flags,  \
-                           n_isects, pairs, qmask, qstride, order);                                            \
+                           n_isects, pairs, qmask, qstride, order, tile_end);                                  \
     }                                                                                                          \
     hipLaunchKernelGGL((reduce_pieces_kernel<12, 3, kRow3, kSlotWaves>), dim3(piece_grid(gs)), dim3(256), 0, s,   \
                        rows, flags, gs.seg, gs.pbase, gs.pieces, gs.npieces, gs.partial);                          \

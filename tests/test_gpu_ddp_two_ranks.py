@@ -141,3 +141,153 @@ def test_sharded_ddp_two_ranks_one_gpu_matches_two_view_batch():
         assert d.max() <= 2 * lr * STEPS + 1e-6, (k, float(d.max()))
         assert (d > 1e-3 * lr).mean() <= 2e-3, (k, float((d > 1e-3 * lr).mean()))
         assert (np.abs(ref - init[k]) > 0).mean() > 0.05  # the steps moved the parameters
+
+
+# ---------------------------------------------------------------------------------------
+# the anchor model (reference train.py:206,257-277): GradientAllReduce across a densify step
+# ---------------------------------------------------------------------------------------
+A_ANCHORS, A_STEPS, A_GROW_AT, A_K = 3000, 4, 1, 10
+
+
+def _anchor_workload(rank, world):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    args = bench.resolve(bench.parse(["--config", "c5", "--anchors", str(A_ANCHORS), "--width", "320", "--height",
+                                      "192", "--cameras", "4", "--mode", "ddp", "--no-cpu-baseline", "--no-secondary",
+                                      "--no-quality", "--no-timing"]), world)
+    return bench.Workload(args, rank, torch.device("cuda", 0), world)
+
+
+def _grow_anchors(wl):
+    """A densify step of the anchor model on statistics every rank holds identically (reduced
+    over the ranks when distributed): the most often visible anchors (offset_denom counts are
+    integers, so their sums are exact in any order -- the one-process reference accumulates the
+    views in another order than the ranks' reduction) grow a neighbour, and every anchor
+    Parameter is replaced by a longer one with zero-extended Adam state
+    (cat_tensors_to_optimizer, reference scene/lod_model.py:487-541) -- the reducer must rebuild
+    its buckets around the new objects."""
+    st = wl.stats
+    A = wl.anchor.shape[0]
+    cnt = st["offset_denom"].view(A, A_K).sum(1)
+    sel = torch.nonzero(cnt >= 0.5 * cnt.max()).squeeze(1)[:256]
+    add = {"anchor": wl.anchor.detach()[sel] + 0.01, "feat": wl.feat.detach()[sel],
+           "offset": torch.zeros(sel.numel(), A_K, 3, device=sel.device), "scaling_raw": wl.scaling_raw.detach()[sel]}
+    opt = wl.optimizer
+    for name, ext in add.items():
+        old = getattr(wl, name)
+        q = torch.nn.Parameter(torch.cat([old.detach(), ext], 0))
+        for g in opt.param_groups:
+            if g["params"][0] is old:
+                s = opt.state.pop(old, None)
+                if s:
+                    s["exp_avg"] = torch.cat([s["exp_avg"], torch.zeros_like(ext)], 0)
+                    s["exp_avg_sq"] = torch.cat([s["exp_avg_sq"], torch.zeros_like(ext)], 0)
+                    opt.state[q] = s
+                g["params"][0] = q
+        setattr(wl, name, q)
+    n = sel.numel()
+    mlp_ps = [p for m in wl.mlps for p in m.parameters()]
+    wl.params = [wl.anchor, wl.feat, wl.offset, wl.scaling_raw] + mlp_ps
+    wl.ddp_order = [wl.offset, wl.scaling_raw, *wl.mlps[1].parameters(), wl.feat, wl.anchor]
+    wl.allreduce.order = wl.ddp_order
+    for k, v in list(st.items()):  # the statistics restart after a densify (train.py:263-273)
+        per = v.shape[0] // A
+        st[k] = torch.zeros((A + n) * per, 1, device=v.device)
+    wl.stats_model = type("Stats", (), dict(n_offsets=A_K, **st))
+    wl.lod["level"] = torch.cat([wl.lod["level"], wl.lod["level"][sel]])
+    wl.lod["extra_level"] = torch.cat([wl.lod["extra_level"], wl.lod["extra_level"][sel]])
+    wl.anchor_quats = torch.cat([wl.anchor_quats, wl.anchor_quats[sel]])
+    return n
+
+
+def _anchor_rank(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from horizongs_amd.multigpu import assert_replicas_agree, reduce_densify_stats
+        wl = _anchor_workload(rank, world)
+        grown, buckets = 0, []
+        for s in range(A_STEPS):
+            wl.step()  # GradientAllReduce: early cov-head buckets, per-bucket HIP Adam
+            buckets.append(sum(b["n"] for b in wl.allreduce.buckets))
+            if s == A_GROW_AT:
+                reduce_densify_stats(wl.stats)
+                assert_replicas_agree(list(wl.stats.values()), what="densify statistics")
+                grown = _grow_anchors(wl)
+        torch.cuda.synchronize()
+        digest = assert_replicas_agree(wl.params, what="anchor parameters")
+        q.put((rank, [p.detach().cpu().numpy() for p in wl.params], grown, buckets, digest, None))
+    except Exception as e:  # noqa: BLE001  (reported to the parent, which fails the test)
+        q.put((rank, None, None, None, None, f"{type(e).__name__}: {e}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _anchor_reference(world):
+    """One process, the ranks' views of each step (rank r's view and target), gradients summed
+    and halved -- what the all-reduce of the 1/world-scaled gradients computes -- one Adam step."""
+    wl = _anchor_workload(0, 1)
+    targets = [wl.target]
+    g = torch.Generator().manual_seed(1000 + 1)
+    targets.append(torch.rand(3, wl.args.height, wl.args.width, generator=g).to(wl.dev))
+    wl.args.freeze = True  # step() leaves the gradients, the optimizer is stepped here
+    wl.world = world
+    grown = 0
+    for s in range(A_STEPS):
+        acc = None
+        for r in range(world):
+            wl.rank, wl.n_steps, wl.target = r, s, targets[r]
+            wl.step()
+            gs = [p.grad.clone() if p.grad is not None else None for p in wl.params]
+            acc = gs if acc is None else [a if b is None else (b if a is None else a + b) for a, b in zip(acc, gs)]
+        for p, a in zip(wl.params, acc):
+            p.grad = None if a is None else a * (1.0 / world)
+        wl.optimizer.step()
+        if s == A_GROW_AT:
+            grown = _grow_anchors(wl)
+    torch.cuda.synchronize()
+    return [p.detach().cpu().numpy() for p in wl.params], grown
+
+
+def test_anchor_ddp_two_ranks_across_densify():
+    """The anchor model's DDP step (multigpu.GradientAllReduce: buckets in gradient order, the
+    fused decode backward's early cov-head buckets, per-bucket HIP Adam) with two ranks on one GPU,
+    across a densify step: the statistics reduced over the ranks, every rank growing the same
+    anchors (replica digest), the buckets rebuilt around the new Parameters; after the steps the
+    ranks' parameters are bit-identical, and bit-identical to one process stepping the two views'
+    averaged gradient: every backward is deterministic, and halving before the sum (the hooks'
+    1/world) equals halving after it in fp32 (profiles/r06_ddp_anchor_two_ranks.json)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [ctx.Process(target=_anchor_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[5] is None for r in res), [r[5] for r in res]
+    assert all(p.exitcode == 0 for p in procs)
+    (_, p0, grown0, b0, d0, _), (_, p1, grown1, b1, d1, _) = res
+    assert grown0 == grown1 > 0 and d0 == d1
+    assert b0[A_GROW_AT + 1] > b0[A_GROW_AT], b0  # the buckets were rebuilt around the grown anchors
+    ref, grown_ref = _anchor_reference(world)
+    assert grown_ref == grown0
+    stats = {}
+    for k, (a, b, r) in enumerate(zip(p0, p1, ref)):
+        assert np.array_equal(a, b), f"param {k}: the ranks differ"
+        assert a.shape == r.shape, (k, a.shape, r.shape)
+        d = np.abs(a - r)
+        stats[k] = {"shape": list(a.shape), "max_abs_diff": float(d.max()), "frac_differing": float((d > 0).mean())}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "ddp_anchor_two_ranks.json"), "w") as f:
+        json.dump({"grown": grown0, "bucket_floats": b0, "params": stats}, f)
+    for k, st in stats.items():
+        assert st["max_abs_diff"] == 0.0, (k, st)
