@@ -44,7 +44,8 @@ raw = ["", "raw counters (per launch):"]
 P = 1920 * 1080
 for ptag, gs, name, occ, rows_mb, alg in (
         ("l3", "3dgs", "raster3d_bwd, c2 (2M Gaussians, 1080p)", "7 (72 VGPRs, 22 KB LDS)",
-         2e6 * (48 if tag == "r04" else 64) / 1e6, (44 * nis + 28 * P) / 1e6),
+         2e6 * (48 if tag == "r04" else 64) / 1e6, (44 * nis + 28 * P) / 1e6 if tag < "r06" else
+         (56 * nis + 28 * P + 65 * steps) / 1e6),
         ("l2", "2dgs", "raster2d_bwd (transposed inputs), c3", "5 (96 VGPRs, 29 KB LDS)", 2e6 * 96 / 1e6, None)):
     L, txt = counters(os.path.join(src, ptag))
     raw += txt.splitlines()
@@ -66,8 +67,16 @@ for ptag, gs, name, occ, rows_mb, alg in (
     lines.append(f"   HBM: 2 x FETCH_SIZE {2 * k['fetch_size_raw_bytes'] / 1e6:.1f} MB + WRITE_SIZE {k['write_size_bytes'] / 1e6:.1f} MB"
                  f" = {k['hbm_bytes_corrected'] / 1e6:.1f} MB / launch"
                  + (f" against {alg:.0f} MB algorithmic ({k['hbm_bytes_corrected'] / 1e6 / alg:.2f}x)" if alg else ""))
-    lines.append(f"   WRITE_SIZE {k['write_size_bytes'] / 1e6:.1f} MB vs {rows_mb:.0f} MB of accumulator rows "
-                 f"({k['write_size_bytes'] / 1e6 / rows_mb:.1f}x: float atomics of every (wave, Gaussian) group meet in L2)")
+    if tag < "r06":
+        lines.append(f"   WRITE_SIZE {k['write_size_bytes'] / 1e6:.1f} MB vs {rows_mb:.0f} MB of accumulator rows "
+                     f"({k['write_size_bytes'] / 1e6 / rows_mb:.1f}x: float atomics of every (wave, Gaussian) group meet in L2)")
+    elif gs == "3dgs":
+        # round 6: one plain 64-B gradient-slot row + a flag byte per wave-list entry (no atomics);
+        # algorithmic above = 56 B of each 64-B record per intersection + 28 B per pixel + those rows
+        lines.append(f"   WRITE_SIZE {k['write_size_bytes'] / 1e6:.1f} MB vs {65 * steps / 1e6:.0f} MB of gradient-slot rows "
+                     f"and flags ({k['write_size_bytes'] / 1e6 / (65 * steps / 1e6):.2f}x); reads "
+                     f"{2 * k['fetch_size_raw_bytes'] / 1e6:.0f} MB vs {(56 * nis + 28 * P) / 1e6:.0f} MB of records and pixels "
+                     f"({2 * k['fetch_size_raw_bytes'] / (56 * nis + 28 * P):.2f}x)")
     dpass = os.path.join(src, "d3" if gs == "3dgs" else "d2")
     if os.path.isdir(dpass):
         D, dtxt = counters(dpass)
