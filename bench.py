@@ -333,7 +333,11 @@ class Workload:
         red = (self.sharded or self.allreduce) if ddp else None
         if ddp:
             red.begin()  # gradient hooks launch the bucket collectives during the backward
-        loss.backward()
+        # the backward's seed dL/dL = 1, allocated once (loss.backward() fills a new one-element
+        # tensor with a kernel launch every step)
+        if getattr(self, "_seed", None) is None or self._seed.shape != loss.shape:
+            self._seed = torch.ones_like(loss)
+        loss.backward(self._seed)
         if self.args.anchors:  # densification statistics of this view (train.py:258-262)
             HDn.training_statis(self.stats_model, self.stats_opt,
                                 dict(selection_mask=sel, visible_mask=visible, viewspace_points=meta["means2d"],
