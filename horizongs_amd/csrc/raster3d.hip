@@ -476,13 +476,7 @@ __global__ __launch_bounds__(256) HGSR_BWD_WAVES void raster3d_bwd_kernel(
         blk_final = max(max(s_last[0], s_last[1]), max(s_last[2], s_last[3]));
     }
     // Gaussians after the block's last contributor are never reached
-#ifdef HGSR_PROBE_SETUP  // TEMPORARY experiment: HGSR_PROBE_SETUP dependent loads added to the setup chain
-    int32_t px_ = tc.start;
-    for (int k_ = 0; k_ < HGSR_PROBE_SETUP; ++k_) px_ = offsets[(uint32_t)px_ & 1023u];
-    const int32_t end = min(tc.end, blk_final + 1 + (px_ == (int32_t)0x80000000 ? 1 : 0));
-#else
     const int32_t end = min(tc.end, blk_final + 1);
-#endif
     const int nb = end > tc.start ? (end - tc.start + NB - 1) / NB : 0;
     if (pair_counter && threadIdx.x == 0 && end > tc.start)  // measurement only (bench roofline)
         atomicAdd(pair_slot(pair_counter, 0), (unsigned long long)(end - tc.start) * kTilePixels);

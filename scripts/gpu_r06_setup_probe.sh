@@ -1,4 +1,4 @@
-# Round 6 (temporary experiment): is raster3d_bwd's setup latency exposed?  The c2 line with the
+# Round 6 experiment (the probe block has since been removed from raster3d.hip): is raster3d_bwd's setup latency exposed?
 # product library and with 4 dependent loads added to every workgroup's setup chain.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
