@@ -235,13 +235,16 @@ struct RectFromRadii {
 };
 
 constexpr int kSlotRow = 256;  // entries per element of the slot-area prefix (one workgroup row)
-// the forward's slot prefix (hgsr_raster3d_pack_fused with radii): seg [CN + 1] then the row
-// prefix [CN / kSlotRow + 1]
+// the forward's slot prefix (hgsr_raster3d_pack_fused with radii): seg [CN + 1], the row prefix
+// [CN / kSlotRow + 1], then the backward's piece count (cleared by the forward's scan)
 size_t slot_prefix_bytes(int64_t CN);
+int32_t* slot_prefix_npieces(void* buf, int64_t CN);
 // row area sums + their exclusive scan into buf (seg[CN] = the total); pack3 finishes seg
 int launch_slot_prefix(int64_t CN, const RectFromRadii& r, void* buf, hipStream_t s);
 // the big entries' piece list from a finished seg (launch_grad_slots' buffer layout in buf)
-int launch_grad_pieces(int64_t CN, const int32_t* seg, int64_t n_isects, void* buf, hipStream_t s, GradSlots& out);
+// npieces (nullable): the piece count's location, already zero when npieces_zeroed (else cleared here)
+int launch_grad_pieces(int64_t CN, const int32_t* seg, int64_t n_isects, void* buf, hipStream_t s, GradSlots& out,
+                       int32_t* npieces = nullptr, bool npieces_zeroed = false);
 // bytes of launch_grad_slots' buffer (from_lists: the rectangles are found from the lists)
 size_t grad_slot_bytes(int64_t CN, bool from_lists, int64_t n_isects);
 // radii != nullptr: rectangles from means2d / radii (isect_tiles'); else from the sorted lists.

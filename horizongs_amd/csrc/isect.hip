@@ -1232,7 +1232,12 @@ int hgsr::launch_grad_slots(int C, int N, const float* means2d, const int32_t* r
 }
 
 size_t hgsr::slot_prefix_bytes(int64_t CN) {
-    return align256_((size_t)(CN + 1) * 4) + align256_((size_t)((CN + kSlotRow - 1) / kSlotRow + 1) * 4);
+    return align256_((size_t)(CN + 1) * 4) + align256_((size_t)((CN + kSlotRow - 1) / kSlotRow + 1) * 4) + 256;
+}
+
+int32_t* hgsr::slot_prefix_npieces(void* buf, int64_t CN) {
+    return (int32_t*)((char*)buf + align256_((size_t)(CN + 1) * 4) +
+                      align256_((size_t)((CN + kSlotRow - 1) / kSlotRow + 1) * 4));
 }
 
 int hgsr::launch_slot_prefix(int64_t CN, const RectFromRadii& r, void* buf, hipStream_t s) {
@@ -1242,12 +1247,14 @@ int hgsr::launch_slot_prefix(int64_t CN, const RectFromRadii& r, void* buf, hipS
     HGSR_REQUIRE(nb < (1ll << 31), "too many Gaussians for the gradient slots");
     if (CN == 0) return memset_async(seg, 4, s, "slot_prefix");
     hipLaunchKernelGGL(slot_sum_kernel<RectFromRadii>, dim3((unsigned)nb), dim3(256), 0, s, CN, r, bpre);
-    hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bpre, seg + CN, (int32_t*)nullptr);
+    // (the scan also clears the backward's piece count, kept here with the prefix)
+    hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bpre, seg + CN,
+                       slot_prefix_npieces(buf, CN));
     return check_launch("slot_prefix");
 }
 
 int hgsr::launch_grad_pieces(int64_t CN, const int32_t* seg, int64_t n_isects, void* buf, hipStream_t s,
-                             GradSlots& out) {
+                             GradSlots& out, int32_t* npieces, bool npieces_zeroed) {
     // the layout of launch_grad_slots' buffer (grad_slot_bytes), seg and slot held elsewhere
     const int64_t nb = (CN + kSlotRow - 1) / kSlotRow, nblk = (CN + kSlotPer - 1) / kSlotPer;
     char* p = (char*)buf;
@@ -1260,10 +1267,11 @@ int hgsr::launch_grad_pieces(int64_t CN, const int32_t* seg, int64_t n_isects, v
     p += align256_((size_t)CN * 4);
     out.pieces = (int32_t*)p;
     p += align256_((size_t)out.cap * 4);
-    out.npieces = (int32_t*)p;
+    out.npieces = npieces ? npieces : (int32_t*)p;
     p += 256;
     out.partial = (float*)p;
-    if (int st = memset_async(out.npieces, 4, s, "grad_pieces")) return st;
+    if (!(npieces && npieces_zeroed))
+        if (int st = memset_async(out.npieces, 4, s, "grad_pieces")) return st;
     if (CN == 0) return HGSR_OK;
     const RectFromRadii none{nullptr, nullptr, 0, 0, 0};
     hipLaunchKernelGGL((slot_write_kernel<RectFromRadii, true>), dim3((unsigned)nblk), dim3(256), 0, s, CN, none,

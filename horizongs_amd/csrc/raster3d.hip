@@ -1077,8 +1077,12 @@ static int raster3d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     // records' slot quads (Rec3::sl)
     GradSlots gs;
     if (fwd_ws && fwd_slots) {
-        const int32_t* const seg = (const int32_t*)((const char*)fwd_ws + rec_bytes(C, N));
-        if (int st = launch_grad_pieces(n, seg, n_isects, sbuf, s, gs)) return st;
+        void* const slots = (char*)const_cast<void*>(fwd_ws) + rec_bytes(C, N);
+        // the piece count the forward's scan cleared: zero for the first backward (the one the
+        // forward's workspace went to, flags_zeroed); a later backward clears it again
+        if (int st = launch_grad_pieces(n, (const int32_t*)slots, n_isects, sbuf, s, gs, slot_prefix_npieces(slots, n),
+                                        flags_zeroed))
+            return st;
     } else if (int st = launch_grad_slots(C, N, means2d, radii, tile_size, tile_w, tile_h, isect_offsets, flatten_ids,
                                           n_isects, sbuf, s, gs, reinterpret_cast<int2*>(&rec->sl),
                                           sizeof(Rec3) / sizeof(int2))) {
