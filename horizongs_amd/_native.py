@@ -58,7 +58,7 @@ _SIGS = {
                                      P, P]),
     "hgsr_raster2d_fwd_ws_bytes": (SZ, [I, I, I]),
     "hgsr_raster2d_fwd": (I, [I, I, I, P, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, SZ, P]),
-    "hgsr_raster2d_pack_fused": (I, [I, I, I, P, P, P, I, P, P, I, P, P, SZ, P]),
+    "hgsr_raster2d_pack_fused": (I, [I, I, I, P, P, P, I, P, P, I, P, P, I, I, I, P, SZ, P]),
     "hgsr_raster2d_fwd_packed": (I, [I, I, I, I, I, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, SZ, P, SZ,
                                      P, SZ, P, P, P]),
     "hgsr_raster2d_bwd_ws_bytes": (SZ, [I, I, I, I64, I]),
@@ -67,7 +67,7 @@ _SIGS = {
     "hgsr_raster2d_fwd_fused": (I, [I, I, I, P, P, P, I, P, I, P, I, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P,
                                     P, P, P, SZ, P]),
     "hgsr_raster2d_bwd_fused": (I, [I, I, I, P, P, P, I, P, I, P, I, P, P, I, I, I, I, I, P, I64, P, P, P, P, P,
-                                    P, P, P, P, P, P, P, P, P, P, P, SZ, P, SZ, I, P, P, P, P]),
+                                    P, P, P, P, P, P, P, P, P, P, P, SZ, P, SZ, I, P, P, P, I, P]),
     "hgsr_lod_mask": (I, [I, P, P, P, P, F, F, F, I, P, P]),
     "hgsr_decode_ws_bytes": (SZ, [I]),
     "hgsr_decode_count": (I, [I, I, I, I, I, P, P, P, P, P, P, SZ, P, P, P]),

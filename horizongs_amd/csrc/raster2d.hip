@@ -60,12 +60,15 @@ __device__ __forceinline__ Tile2 tile2_ctx(int C, int W, int H, int tw, int th,
     return t;
 }
 
-// 96-B raster record of one (camera, surfel).  With rows u, v, w of the ray
+// Raster record of one (camera, surfel).  With rows u, v, w of the ray
 // transform, h_u x h_v = (p_x w - u) x (p_y w - v) = p_x A + p_y B + C for
 // A = v x w, B = w x u, C = u x v.  Relative to the projected mean m this is
 // (p_x - m_x) A + (p_y - m_y) B + C' with C' = C + m_x A + m_y B (the hit at m), so
 // the kernels store A, B, C' (from f64) and evaluate the hit with six FMAs on
 // small offsets, keeping cancellation out of both passes.
+// 128 B: the seventh quad carries the pair's gradient-slot base (as Rec3::sl: written by a
+// training forward's pack, read by the backward from the sectors its record DMA fetched); a
+// 96-B record touched two 64-B sectors too, so the forward reads no more.
 struct Rec2 {
     float4 r0;  // A.x A.y A.z B.x
     float4 r1;  // B.y B.z C'.x C'.y
@@ -73,7 +76,10 @@ struct Rec2 {
     float4 col; // colour (D <= 4, zero padded; the last channel is the depth in RGB+ED)
     float4 r4;  // normal xyz, low-pass disk radius
     float4 box; // centre xy and half-extents of the surfel ellipse's screen bounding box
+    int4 sl;    // gradient-slot base, slot width, 0, 0
+    float4 pad;
 };
+static_assert(sizeof(Rec2) == 128, "Rec2 is two 64-B sectors");
 
 // Skip-test geometry.  alpha >= 1/255 needs sigma = min(|s|^2, 2|m-p|^2)/2 <= L =
 // ln(255 o), i.e. either the ray-plane hit s lies in the UV disk of radius
@@ -139,14 +145,16 @@ __device__ __forceinline__ void cross_abc(const float* M, float mx, float my, fl
 }
 
 // One workgroup packs 256 consecutive (camera, surfel) records.  The ray transforms (36 B
-// each) and normals (12 B) come in as contiguous float4 runs through LDS and the 96-B
+// each) and normals (12 B) come in as contiguous float4 runs through LDS and the 128-B
 // records leave the same way: lane-strided AoS loads / stores made every instruction touch
-// ~36 cache lines.
-template <int D>
+// ~36 cache lines.  SLOTS: the gradient slots with the records, as pack3_kernel.
+template <int D, bool SLOTS>
 __global__ __launch_bounds__(256) void pack2_kernel(int64_t n, int N, const float2* __restrict__ means2d,
                                                     const float* __restrict__ rt, ChanSrc cs,
-                                                    const float* __restrict__ normals, Rec2* __restrict__ rec) {
-    constexpr int kOP = 25;  // record pitch in LDS (24 floats + 1: conflict-free lane stride)
+                                                    const float* __restrict__ normals, Rec2* __restrict__ rec,
+                                                    RectFromRadii rr, const int32_t* __restrict__ bpre,
+                                                    int32_t* __restrict__ seg) {
+    constexpr int kOP = 33;  // record pitch in LDS (32 floats + 1: conflict-free lane stride)
     __shared__ __attribute__((aligned(16))) float s_buf[256 * kOP];
     const int64_t i0 = (int64_t)blockIdx.x * 256;
     const int nloc = (int)min((int64_t)256, n - i0);
@@ -154,7 +162,30 @@ __global__ __launch_bounds__(256) void pack2_kernel(int64_t n, int N, const floa
     const int64_t i = i0 + t;
     stage_floats(rt + i0 * 9, nloc * 9, s_buf);
     stage_floats(normals + i0 * 3, nloc * 3, s_buf + 256 * 9);
+    int area = 0, inc = 0, x0 = 0, y0 = 0, w = 0;
+    __shared__ int s_ws[4];
+    if (SLOTS) {
+        static_assert(kSlotRow == 256, "one prefix row per workgroup");
+        if (t < nloc) area = rr(i, x0, y0, w);
+        inc = area;
+        const int lane = t & 63;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(inc, d);
+            if (lane >= d) inc += o;
+        }
+        if (lane == 63) s_ws[t >> 6] = inc;
+    }
     __syncthreads();
+    int sl_x = 0, sl_w = 0;
+    if (SLOTS && t < nloc) {
+        int e = bpre[blockIdx.x] + inc - area;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) e += v < (t >> 6) ? s_ws[v] : 0;
+        seg[i] = e;
+        sl_x = e - y0 * w - x0;
+        sl_w = w;
+    }
     float M[9], nr[3];
 #pragma unroll
     for (int k = 0; k < 9; ++k) M[k] = s_buf[t * 9 + k];
@@ -174,16 +205,17 @@ __global__ __launch_bounds__(256) void pack2_kernel(int64_t n, int N, const floa
         const float* src = cs.colors + c * cs.col_cstride + g * cs.dc;
 #pragma unroll
         for (int k = 0; k < D; ++k) col[k] = k < cs.dc ? src[k] : cs.depths[i];
-        const float r[24] = {abc[0], abc[1], abc[2], abc[3], abc[4], abc[5], abc[6], abc[7],
+        const float r[32] = {abc[0], abc[1], abc[2], abc[3], abc[4], abc[5], abc[6], abc[7],
                              abc[8], m.x,    m.y,    o,      col[0], col[1], col[2], col[3],
-                             nr[0],  nr[1],  nr[2],  disk,   box.x,  box.y,  box.z,  box.w};
+                             nr[0],  nr[1],  nr[2],  disk,   box.x,  box.y,  box.z,  box.w,
+                             __int_as_float(sl_x), __int_as_float(sl_w), 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < 24; ++k) s_buf[t * kOP + k] = r[k];
+        for (int k = 0; k < 32; ++k) s_buf[t * kOP + k] = r[k];
     }
     __syncthreads();
     float4* dst = reinterpret_cast<float4*>(rec + i0);
-    for (int q = t; q < nloc * 6; q += 256) {
-        const int e = q / 6, f = q - e * 6;
+    for (int q = t; q < nloc * 8; q += 256) {
+        const int e = q >> 3, f = q & 7;
         const float* p = s_buf + e * kOP + 4 * f;
         dst[q] = make_float4(p[0], p[1], p[2], p[3]);
     }
@@ -468,7 +500,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
                        const float* __restrict__ render_alphas, const int32_t* __restrict__ last_ids,
                        const float* __restrict__ v_render_colors, const float* __restrict__ v_render_alphas,
                        const float* __restrict__ v_render_normals, float* __restrict__ rows,
-                       uint8_t* __restrict__ flags, const int2* __restrict__ slot, int64_t n_slots,
+                       uint8_t* __restrict__ flags, int64_t n_slots,
                        unsigned long long* __restrict__ pair_counter, const uint64_t* __restrict__ qmask,
                        int64_t qstride, const float* __restrict__ normal_rot,
                        const float* __restrict__ v_depth_extra, const int32_t* __restrict__ order) {
@@ -568,7 +600,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
     if (nb > 0 && loader) {
         cid = flatten_ids[max(end - 1 - tid, tc.start)];
         dma_batch(0, cid);
-        csl = slot[cid];
+        csl = *reinterpret_cast<const int2*>(&rec[cid].sl);
         nid = flatten_ids[max(end - 1 - NB - tid, tc.start)];
     }
     uint8_t* my_list = s_list[wave];
@@ -597,7 +629,7 @@ raster2d_bwd_tp_kernel(int C, int W, int H, int tw, int th, const Rec2* __restri
         if (b + 1 < nb && loader) {
             cid = nid;
             dma_batch(prv, cid);
-            csl = slot[cid];
+            csl = *reinterpret_cast<const int2*>(&rec[cid].sl);
             nid = flatten_ids[max(batch_end - 2 * NB - tid, tc.start)];
         }
         lds_barrier();
@@ -837,13 +869,25 @@ static int check_raster2(int C, int N, int D, int W, int H, int tile_size, int t
 
 static size_t rec2_bytes(int C, int N) { return ((size_t)C * N * sizeof(Rec2) + 255) & ~(size_t)255; }
 
+// slots (nullable): as pack3's (the rectangles and launch_slot_prefix's buffer)
 static int pack2(int C, int N, int D, const float* means2d, const float* rt, const ChanSrc& cs,
-                 const float* normals, Rec2* rec, hipStream_t s) {
+                 const float* normals, Rec2* rec, hipStream_t s, const RectFromRadii* rr = nullptr,
+                 void* slots = nullptr) {
     const int64_t n = (int64_t)C * N;
     if (n == 0) return HGSR_OK;
     const dim3 grid((unsigned)((n + 255) / 256));
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
-#define LAUNCH_P2(DD) hipLaunchKernelGGL(pack2_kernel<DD>, grid, dim3(256), 0, s, n, N, m2, rt, cs, normals, rec)
+    int32_t* const seg = (int32_t*)slots;
+    const int32_t* const bpre = slots ? (const int32_t*)((char*)slots + (((size_t)(n + 1) * 4 + 255) & ~(size_t)255))
+                                      : nullptr;
+    const RectFromRadii none{nullptr, nullptr, 0, 0, 0};
+#define LAUNCH_P2(DD)                                                                                           \
+    if (slots)                                                                                                  \
+        hipLaunchKernelGGL((pack2_kernel<DD, true>), grid, dim3(256), 0, s, n, N, m2, rt, cs, normals, rec, *rr, \
+                           bpre, seg);                                                                          \
+    else                                                                                                        \
+        hipLaunchKernelGGL((pack2_kernel<DD, false>), grid, dim3(256), 0, s, n, N, m2, rt, cs, normals, rec,    \
+                           none, (const int32_t*)nullptr, (int32_t*)nullptr)
     switch (D) {
         case 1: LAUNCH_P2(1); break;
         case 2: LAUNCH_P2(2); break;
@@ -854,9 +898,10 @@ static int pack2(int C, int N, int D, const float* means2d, const float* rt, con
     return check_launch("raster2d_pack");
 }
 
+// the records, then the slot prefix a training forward fills (hgsr_raster2d_pack_fused with radii)
 extern "C" size_t hgsr_raster2d_fwd_ws_bytes(int C, int N, int D) {
     (void)D;
-    return rec2_bytes(C, N);
+    return rec2_bytes(C, N) + slot_prefix_bytes((int64_t)C * N);
 }
 
 static int raster2d_fwd_launch(int C, int D, const Rec2* rec, const float* backgrounds, int bg_ch, int ed_ch,
@@ -962,7 +1007,8 @@ extern "C" int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2
 
 extern "C" int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                                         const float* colors, int colors_shared, const float* depths,
-                                        const float* opacities, int opacities_shared, const float* normals, void* ws,
+                                        const float* opacities, int opacities_shared, const float* normals,
+                                        const int32_t* radii, int tile_size, int tile_w, int tile_h, void* ws,
                                         size_t ws_bytes, hgsr_stream_t stream) {
     HGSR_REQUIRE(C >= 1 && N >= 0, "bad dims");
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
@@ -973,7 +1019,14 @@ extern "C" int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means
                  "null pointer");
     const ChanSrc cs{colors, colors_shared ? 0 : (int64_t)N * Dc, Dc, depths, opacities,
                      opacities_shared ? 0 : (int64_t)N};
-    return pack2(C, N, D, means2d, ray_transforms, cs, normals, (Rec2*)ws, as_stream(stream));
+    hipStream_t s = as_stream(stream);
+    if (!radii || N == 0) return pack2(C, N, D, means2d, ray_transforms, cs, normals, (Rec2*)ws, s);
+    // a backward follows: the records carry their gradient slots (pack3's scheme)
+    HGSR_REQUIRE(tile_size > 0 && tile_w > 0 && tile_h > 0, "bad tile grid");
+    const RectFromRadii rr{reinterpret_cast<const float2*>(means2d), radii, tile_size, tile_w, tile_h};
+    void* const slots = (char*)ws + rec2_bytes(C, N);
+    if (int st = launch_slot_prefix((int64_t)C * N, rr, slots, s)) return st;
+    return pack2(C, N, D, means2d, ray_transforms, cs, normals, (Rec2*)ws, s, &rr, slots);
 }
 
 extern "C" int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_depth,
@@ -1028,7 +1081,8 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
                              float* v_rt, const ChanDst& cd, float* v_normals, float* v_densify,
                              const void* fwd_ws, void* ws, size_t ws_bytes, hgsr_stream_t stream, const void* qbuf = nullptr,
                              size_t qmask_bytes = 0, bool flags_zeroed = false, const float* normal_rot = nullptr,
-                             const float* v_depth_extra = nullptr, const int32_t* radii = nullptr) {
+                             const float* v_depth_extra = nullptr, const int32_t* radii = nullptr,
+                             bool fwd_slots = false) {
     if (int st = check_raster2(C, N, D, width, height, tile_size, tile_w, tile_h)) return st;
     HGSR_REQUIRE(ws_bytes >= hgsr_raster2d_bwd_ws_bytes(C, N, D, n_isects, fwd_ws != nullptr),
                  "raster2d_bwd workspace too small");
@@ -1060,15 +1114,23 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
     const float2* m2 = reinterpret_cast<const float2*>(means2d);
     if (!flags_zeroed)  // else hgsr_raster2d_fwd_packed cleared them (bwd_ws)
         if (int st = memset_async(flags, slot_flag_bytes(n_isects, kSlotWaves), s, "raster2d_bwd")) return st;
-    GradSlots gs;  // each (camera, surfel)'s gradient slots (raster3d_bwd_impl)
-    if (int st = launch_grad_slots(C, N, means2d, radii, tile_size, tile_w, tile_h, isect_offsets, flatten_ids,
-                                   n_isects, sbuf, s, gs))
-        return st;
-    const Rec2* rec = (const Rec2*)fwd_ws;
+    // the forward's records when the caller kept them, else pack again; the gradient slots as in
+    // raster3d_bwd_impl (in the records from a training forward's pack, else made here)
+    Rec2* rec = (Rec2*)const_cast<void*>(fwd_ws);
     if (!rec) {
-        Rec2* own = (Rec2*)(sbuf + grad_slot_bytes(n, true, n_isects));
-        if (int st = pack2(C, N, D, means2d, rt, cs, normals, own, s)) return st;
-        rec = own;
+        rec = (Rec2*)(sbuf + grad_slot_bytes(n, true, n_isects));
+        if (int st = pack2(C, N, D, means2d, rt, cs, normals, rec, s)) return st;
+    }
+    GradSlots gs;
+    if (fwd_ws && fwd_slots) {
+        void* const slots = (char*)const_cast<void*>(fwd_ws) + rec2_bytes(C, N);
+        if (int st = launch_grad_pieces(n, (const int32_t*)slots, n_isects, sbuf, s, gs, slot_prefix_npieces(slots, n),
+                                        flags_zeroed))
+            return st;
+    } else if (int st = launch_grad_slots(C, N, means2d, radii, tile_size, tile_w, tile_h, isect_offsets, flatten_ids,
+                                          n_isects, sbuf, s, gs, reinterpret_cast<int2*>(&rec->sl),
+                                          sizeof(Rec2) / sizeof(int2))) {
+        return st;
     }
     const int64_t n_bins = (int64_t)C * tile_w * tile_h;
     const dim3 grid((unsigned)n_bins);
@@ -1089,7 +1151,7 @@ static int raster2d_bwd_impl(int C, int N, int D, const float* means2d, const fl
         hipLaunchKernelGGL((raster2d_bwd_tp_kernel<DD>), grid, dim3(256), 0, s, C, width, height, tile_w, tile_h,  \
                            rec, backgrounds, bg_ch, ed_ch, render_colors, isect_offsets, n_isects, flatten_ids,    \
                            render_alphas, last_ids, v_render_colors, v_render_alphas, v_render_normals, rows,      \
-                           flags, gs.slot, n_isects, pairs, qmask, qstride, normal_rot, v_depth_extra, order);     \
+                           flags, n_isects, pairs, qmask, qstride, normal_rot, v_depth_extra, order);              \
     }                                                                                                             \
     hipLaunchKernelGGL((reduce_pieces_kernel<15 + DD, (15 + DD + 3) / 4, kRow2, kSlotWaves>), dim3(piece_grid(gs)), \
                        dim3(256), 0, s, rows, flags, gs.seg, gs.pbase, gs.pieces, gs.npieces, gs.partial);          \
@@ -1136,7 +1198,7 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                                        float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
                                        const void* qmask, size_t qmask_bytes, int ws_zeroed,
                                        const float* normal_rot, const float* v_depth_extra, const int32_t* radii,
-                                       hgsr_stream_t stream) {
+                                       int fwd_slots, hgsr_stream_t stream) {
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
     HGSR_REQUIRE(!(expected_depth && !depths), "expected_depth needs depths");
     HGSR_REQUIRE(!depths || v_depths, "null pointer");
@@ -1153,5 +1215,5 @@ extern "C" int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2
                              isect_offsets, n_isects, flatten_ids, render_alphas, last_ids, v_render_colors,
                              v_render_alphas, v_render_normals, v_means2d, v_ray_transforms, cd, v_normals,
                              v_densify, fwd_ws, ws, ws_bytes, stream, qmask, qmask_bytes,
-                             ws_zeroed != 0, normal_rot, v_depth_extra, radii);
+                             ws_zeroed != 0, normal_rot, v_depth_extra, radii, fwd_slots != 0);
 }

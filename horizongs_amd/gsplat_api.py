@@ -773,8 +773,9 @@ class _Raster2DFused(torch.autograd.Function):
     native call each way (hgsr_raster2d_{fwd,bwd}_fused); see _Raster3DFused."""
 
     @staticmethod
-    def pack(means2d, rt, colors, depths, opacities, normals):
-        """Surfel records for forward(records=...), packed while the host reads the count."""
+    def pack(means2d, rt, colors, depths, opacities, normals, radii=None, tiles=(0, 0, 0)):
+        """Surfel records for forward(records=...), packed while the host reads the count; with
+        radii (a backward will follow) they carry their gradient slots (_Raster3DFused.pack)."""
         C, Ng = means2d.shape[:2]
         Dc = 0 if colors is None else colors.shape[-1]
         D = Dc + (0 if depths is None else 1)
@@ -782,7 +783,7 @@ class _Raster2DFused(torch.autograd.Function):
         ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=means2d.device)
         N.call("hgsr_raster2d_pack_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors),
                int(colors is not None and colors.dim() == 2), ptr(depths), ptr(opacities), int(opacities.dim() == 1),
-               ptr(normals), ptr(ws), ws_b, N.stream(means2d.device))
+               ptr(normals), ptr(radii), *tiles, ptr(ws), ws_b, N.stream(means2d.device))
         return ws
 
     @staticmethod
@@ -838,6 +839,7 @@ class _Raster2DFused(torch.autograd.Function):
         ctx.deferred = deferred
         ctx.frame = frame
         ctx.radii = None if radii is None else radii.detach().contiguous()
+        ctx.fwd_slots = records is not None and radii is not None  # pack(radii=...) filled the slots
         nfd = None
         if frame is not None and frame[2] and depths is not None:
             # K13 on the rendered depth channel (read in place through its strides), world frame
@@ -885,7 +887,8 @@ class _Raster2DFused(torch.autograd.Function):
                width, height, tile_size, tw, th, ptr(offsets), n_is, ptr(flatten_ids) if n_is else None, ptr(rc), ptr(ra), ptr(last), ptr(v_rc), ptr(v_ra),
                ptr(v_rn), ptr(v_means2d), ptr(v_rt), ptr(v_colors), ptr(v_depths), ptr(v_opac), ptr(v_normals),
                ptr(v_dens), ptr(fwd_ws), ptr(ws), ws_b, ptr(ctx.qmask), 0 if ctx.qmask is None else ctx.qmask.numel(),
-               zeroed, None if frame is None else ptr(frame[0]), ptr(v_dep), ptr(ctx.radii), N.stream(dev))
+               zeroed, None if frame is None else ptr(frame[0]), ptr(v_dep), ptr(ctx.radii), int(ctx.fwd_slots),
+               N.stream(dev))
         v_bg = None
         if backgrounds is not None and ctx.needs_input_grad[7]:
             v_bg = (v_rc[..., :Dc] * (1.0 - ra)).sum(dim=(1, 2))
@@ -1142,11 +1145,15 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
         # records are packed while the host waits for the intersection count
         r_in = (_f32(means2d), _f32(ray_transforms.reshape(C, Ng, 9)), _f32(cols) if rgb else None,
                 _f32(depths) if with_depth else None, _f32(opacities), _f32(normals))
-        records = _Raster2DFused.pack(*(t.detach() if t is not None else None for t in r_in))
+        ed, grad_mode = render_mode in ("ED", "RGB+ED"), torch.is_grad_enabled()
+        # a backward will follow: the records carry their gradient slots (same radii to the Function)
+        slot_radii = radii.contiguous() if grad_mode and (densifications.requires_grad or any(
+            t is not None and t.requires_grad for t in r_in)) else None
+        records = _Raster2DFused.pack(*(t.detach() if t is not None else None for t in r_in), radii=slot_radii,
+                                      tiles=(int(tile_size), tw, th))
         bgs = None if (backgrounds is None or not rgb) else _f32(backgrounds)
         opac = opacities.expand(C, -1)
         args = (densifications, bgs, int(width), int(height), int(tile_size))
-        ed, grad_mode = render_mode in ("ED", "RGB+ED"), torch.is_grad_enabled()
         # world-frame normals and (expected / raw depth channel) K13 inside the fused Function
         _unsupported(viewmats.requires_grad or Ks.requires_grad, "rasterization_2dgs gradients w.r.t. the cameras")
         frame = (_f32(viewmats.detach()), _f32(Ks.detach()),
@@ -1154,7 +1161,8 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
         tpg, isect_offsets = isect_state[3], isect_state[4]
         d = _isect_emit_deferred(isect_state)
         if d is not None:  # emission, sort and forward queued; then the count is read
-            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, d.flat, ed, records, grad_mode, d, frame, radii)
+            outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, d.flat, ed, records, grad_mode, d, frame,
+                                        slot_radii)
             if _isect_resolve(isect_state, d):
                 isect_ids, flatten_ids = d.ids[:d.n], d.flat[:d.n]
             else:
@@ -1162,7 +1170,7 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
         if d is None:
             tpg, isect_ids, flatten_ids, isect_offsets = _isect_finish(isect_state)
             outs = _Raster2DFused.apply(*r_in, *args, isect_offsets, flatten_ids, ed, records, grad_mode, None, frame,
-                                        radii)
+                                        slot_radii)
         render_colors, render_alphas, render_normals, render_distort, render_median, nfd_fused = outs
         fused_frame = frame is not None
     else:

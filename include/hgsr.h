@@ -317,9 +317,12 @@ int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * takes world-frame v_render_normals.  v_depth_extra (nullable, [C,H,W]): a second gradient
  * of the depth channel (K13's, the normals from the rendered depth), added per pixel by the
  * backward kernel instead of by a separate sum. */
+/* radii (nullable, with the tile grid): the records carry their gradient slots, as
+ * hgsr_raster3d_pack_fused's (hgsr_raster2d_bwd_fused then gets fwd_slots = 1). */
 int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                              const float* colors, int colors_shared, const float* depths,
-                             const float* opacities, int opacities_shared, const float* normals, void* ws,
+                             const float* opacities, int opacities_shared, const float* normals,
+                             const int32_t* radii, int tile_size, int tile_w, int tile_h, void* ws,
                              size_t ws_bytes, hgsr_stream_t stream);
 int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_depth,
                              const float* backgrounds, int width, int height, int tile_size, int tile_w,
@@ -343,7 +346,7 @@ int hgsr_raster2d_bwd_fused(int C, int N, int Dc, const float* means2d, const fl
                             float* v_densify, const void* fwd_ws, void* ws, size_t ws_bytes,
                             const void* qmask, size_t qmask_bytes, int ws_zeroed,
                             const float* normal_rot, const float* v_depth_extra, const int32_t* radii,
-                            hgsr_stream_t stream);
+                            int fwd_slots, hgsr_stream_t stream);
 
 /* ---- K14: anchor -> neural-Gaussian decode --------------
  * replaces scene/lod_model.py:286-290 set_anchor_mask (LoD mask, dist2level
