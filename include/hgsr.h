@@ -158,7 +158,8 @@ int hgsr_isect_offset_encode(int64_t n_isects, const int64_t* isect_ids, int C, 
  * call; callers chunk wider channel counts).  colors [C*N, D], opacities [C*N],
  * backgrounds [C, D] nullable.  Outputs render_colors [C,H,W,D],
  * render_alphas [C,H,W,1], last_ids [C,H,W].  ws: caller scratch of
- * hgsr_raster3d_fwd_ws_bytes() (packed 64-B per-Gaussian raster records). */
+ * hgsr_raster3d_fwd_ws_bytes() (packed 64-B per-Gaussian raster records, then room for
+ * the gradient slots' prefix a training pack writes: 4 B per (camera, Gaussian) + 1 KB). */
 size_t hgsr_raster3d_fwd_ws_bytes(int C, int N, int D);
 int hgsr_raster3d_fwd(int C, int N, int D, const float* means2d, const float* conics,
                       const float* colors, const float* opacities, const float* backgrounds,
@@ -267,7 +268,8 @@ int hgsr_raster3d_bwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * depth (render_mode RGB+ED / RGB+D) used for the median depth and distortion.
  * Outputs colors [C,H,W,D], alphas [C,H,W,1], normals [C,H,W,3],
  * distort [C,H,W,1], median [C,H,W,1], last_ids, median_ids [C,H,W].
- * ws (hgsr_raster2d_fwd_ws_bytes) receives the packed 96-B surfel records. */
+ * ws (hgsr_raster2d_fwd_ws_bytes) receives the packed 128-B surfel records (and, for a
+ * training pack, the gradient slots' prefix). */
 size_t hgsr_raster2d_fwd_ws_bytes(int C, int N, int D);
 int hgsr_raster2d_fwd(int C, int N, int D, const float* means2d, const float* ray_transforms,
                       const float* colors, const float* opacities, const float* normals,
