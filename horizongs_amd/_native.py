@@ -35,8 +35,8 @@ _SIGS = {
     "hgsr_project2d_bwd": (I, [I, I, P, P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P]),
     "hgsr_sh_fwd": (I, [I, I, I64, P, P, P, P, P]),
     "hgsr_sh_bwd": (I, [I, I, I64, P, P, P, P, P, P, P]),
-    "hgsr_sh_rgb_fwd": (I, [I, I, I, I, P, P, P, I, P, P, P]),
-    "hgsr_sh_rgb_bwd": (I, [I, I, I, I, P, P, P, I, P, P, P, P, P]),
+    "hgsr_sh_rgb_fwd": (I, [I, I, I, I, P, P, P, P, I, P, P, P]),
+    "hgsr_sh_rgb_bwd": (I, [I, I, I, I, P, P, P, P, I, P, P, P, P, P]),
     "hgsr_isect_ws1_bytes": (SZ, [I, I, I, I]),
     "hgsr_isect_ws2_bytes": (SZ, [I64, I64]),
     "hgsr_isect_count": (I, [I, I, P, P, I, I, I, P, P, P, P, SZ, P]),

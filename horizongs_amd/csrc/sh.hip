@@ -166,9 +166,25 @@ __device__ __forceinline__ bool sh_rgb_eval(int K, const float* __restrict__ m, 
     return true;
 }
 
+// camera c's centre: campos[c] given, else -R^T t of the world-to-camera view matrix
+// viewmats[c] (row-major 4x4): the renderer's camera centres without a batched GEMM + negation in
+// torch per view
+__device__ __forceinline__ void cam_center(const float* __restrict__ campos, const float* __restrict__ viewmats,
+                                           int c, float (&cp)[3]) {
+    if (viewmats) {
+        const float* v = viewmats + c * 16;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) cp[j] = -(v[j] * v[3] + v[4 + j] * v[7] + v[8 + j] * v[11]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) cp[j] = campos[c * 3 + j];
+    }
+}
+
 template <int DEG>
 __global__ __launch_bounds__(256) void sh_rgb_fwd_kernel(int C, int N, int K, const float* __restrict__ means,
                                                          const float* __restrict__ campos,
+                                                         const float* __restrict__ viewmats,
                                                          const float* __restrict__ coeffs, int shared,
                                                          const int32_t* __restrict__ radii,
                                                          float* __restrict__ colors) {
@@ -178,8 +194,9 @@ __global__ __launch_bounds__(256) void sh_rgb_fwd_kernel(int C, int N, int K, co
     if (g >= N) return;
     for (int c = 0; c < C; ++c) {
         const int64_t i = (int64_t)c * N + g;
-        float u[3], inv, b[NB], r[3];
-        sh_rgb_eval<DEG>(K, means + (int64_t)g * 3, campos + c * 3, coeffs + (shared ? g : i) * K * 3,
+        float u[3], inv, b[NB], r[3], cp[3];
+        cam_center(campos, viewmats, c, cp);
+        sh_rgb_eval<DEG>(K, means + (int64_t)g * 3, cp, coeffs + (shared ? g : i) * K * 3,
                          radii[i] > 0, u, inv, b, r);
 #pragma unroll
         for (int q = 0; q < 3; ++q) colors[i * 3 + q] = fmaxf(r[q] + 0.5f, 0.0f);
@@ -189,6 +206,7 @@ __global__ __launch_bounds__(256) void sh_rgb_fwd_kernel(int C, int N, int K, co
 template <int DEG>
 __global__ __launch_bounds__(256) void sh_rgb_bwd_kernel(int C, int N, int K, const float* __restrict__ means,
                                                          const float* __restrict__ campos,
+                                                         const float* __restrict__ viewmats,
                                                          const float* __restrict__ coeffs, int shared,
                                                          const int32_t* __restrict__ radii,
                                                          const float* __restrict__ v_colors,
@@ -211,8 +229,9 @@ __global__ __launch_bounds__(256) void sh_rgb_bwd_kernel(int C, int N, int K, co
         }
         if (t < nloc) {
             const int64_t i = (int64_t)c * N + g;
-            float u[3], inv, b[NB], r[3];
-            const bool on = sh_rgb_eval<DEG>(K, means + (int64_t)g * 3, campos + c * 3, my, radii[i] > 0, u, inv, b, r);
+            float u[3], inv, b[NB], r[3], cp[3];
+            cam_center(campos, viewmats, c, cp);
+            const bool on = sh_rgb_eval<DEG>(K, means + (int64_t)g * 3, cp, my, radii[i] > 0, u, inv, b, r);
             // clamp_min backward: the gradient passes where colour + 0.5 >= 0
             float gq[3];
 #pragma unroll
@@ -307,20 +326,20 @@ extern "C" int hgsr_sh_bwd(int degree, int K, int64_t n, const float* dirs, cons
 }
 
 extern "C" int hgsr_sh_rgb_fwd(int degree, int C, int N, int K, const float* means, const float* campos,
-                               const float* coeffs, int shared, const int32_t* radii, float* colors,
-                               hgsr_stream_t stream) {
+                               const float* viewmats, const float* coeffs, int shared, const int32_t* radii,
+                               float* colors, hgsr_stream_t stream) {
     HGSR_REQUIRE(degree >= 0 && degree <= 3, "sh degree %d unsupported (0..3)", degree);
     HGSR_REQUIRE(K >= (degree + 1) * (degree + 1), "K=%d too small for degree %d", K, degree);
     HGSR_REQUIRE(C >= 1 && N >= 0, "bad dims C=%d N=%d", C, N);
     // the backward stages K coefficient rows in LDS: refuse here, not one step later in it
     HGSR_REQUIRE(K <= kShMaxK, "sh_rgb: K=%d coefficients per Gaussian (at most %d)", K, kShMaxK);
     if (N == 0) return HGSR_OK;
-    HGSR_REQUIRE(means && campos && coeffs && radii && colors, "null pointer");
+    HGSR_REQUIRE(means && (campos || viewmats) && coeffs && radii && colors, "null pointer");
     dim3 grid((unsigned)((N + 255) / 256));
     hipStream_t s = as_stream(stream);
     KernelTimer kt("sh_fwd", s);
-#define SH_RGB_F(D) hipLaunchKernelGGL(sh_rgb_fwd_kernel<D>, grid, dim3(256), 0, s, C, N, K, means, campos, coeffs, \
-                                       shared, radii, colors)
+#define SH_RGB_F(D) hipLaunchKernelGGL(sh_rgb_fwd_kernel<D>, grid, dim3(256), 0, s, C, N, K, means, campos, \
+                                       viewmats, coeffs, shared, radii, colors)
     switch (degree) {
         case 0: SH_RGB_F(0); break;
         case 1: SH_RGB_F(1); break;
@@ -332,20 +351,20 @@ extern "C" int hgsr_sh_rgb_fwd(int degree, int C, int N, int K, const float* mea
 }
 
 extern "C" int hgsr_sh_rgb_bwd(int degree, int C, int N, int K, const float* means, const float* campos,
-                               const float* coeffs, int shared, const int32_t* radii, const float* v_colors,
-                               float* v_coeffs, float* v_means, hgsr_stream_t stream) {
+                               const float* viewmats, const float* coeffs, int shared, const int32_t* radii,
+                               const float* v_colors, float* v_coeffs, float* v_means, hgsr_stream_t stream) {
     HGSR_REQUIRE(degree >= 0 && degree <= 3, "sh degree %d unsupported (0..3)", degree);
     HGSR_REQUIRE(K >= (degree + 1) * (degree + 1), "K=%d too small for degree %d", K, degree);
     HGSR_REQUIRE(C >= 1 && N >= 0, "bad dims C=%d N=%d", C, N);
     HGSR_REQUIRE(K <= kShMaxK, "sh_rgb: K=%d coefficients per Gaussian (at most %d)", K, kShMaxK);
     if (N == 0) return HGSR_OK;
-    HGSR_REQUIRE(means && campos && coeffs && radii && v_colors && v_coeffs, "null pointer");
+    HGSR_REQUIRE(means && (campos || viewmats) && coeffs && radii && v_colors && v_coeffs, "null pointer");
     dim3 grid((unsigned)((N + 255) / 256));
     hipStream_t s = as_stream(stream);
     KernelTimer kt("sh_bwd", s);
     const size_t lds = (size_t)256 * K * 3 * sizeof(float);
-#define SH_RGB_B(D) hipLaunchKernelGGL(sh_rgb_bwd_kernel<D>, grid, dim3(256), lds, s, C, N, K, means, campos, coeffs, \
-                                       shared, radii, v_colors, v_coeffs, v_means)
+#define SH_RGB_B(D) hipLaunchKernelGGL(sh_rgb_bwd_kernel<D>, grid, dim3(256), lds, s, C, N, K, means, campos,   \
+                                       viewmats, coeffs, shared, radii, v_colors, v_coeffs, v_means)
     switch (degree) {
         case 0: SH_RGB_B(0); break;
         case 1: SH_RGB_B(1); break;

@@ -267,30 +267,32 @@ class _SH(torch.autograd.Function):
 
 class _SHColors(torch.autograd.Function):
     """rasterization()'s SH colour path (dirs = means - campos, masked SH evaluation,
-    clamp_min(+0.5, 0)) as one native call each way: hgsr_sh_rgb_{fwd,bwd}."""
+    clamp_min(+0.5, 0)) as one native call each way: hgsr_sh_rgb_{fwd,bwd}.  viewmats (instead
+    of campos): the kernels compute the camera centres -R^T t themselves."""
 
     @staticmethod
-    def forward(ctx, degree, means, campos, coeffs, radii):
+    def forward(ctx, degree, means, campos, coeffs, radii, viewmats=None):
         C, Ng = radii.shape
         K = coeffs.shape[-2]
         shared = coeffs.dim() == 3
         colors = torch.empty((C, Ng, 3), dtype=torch.float32, device=means.device)
-        N.call("hgsr_sh_rgb_fwd", degree, C, Ng, K, ptr(means), ptr(campos), ptr(coeffs), int(shared), ptr(radii),
-               ptr(colors), N.stream(means.device))
-        ctx.save_for_backward(means, campos, coeffs, radii)
+        N.call("hgsr_sh_rgb_fwd", degree, C, Ng, K, ptr(means), ptr(campos), ptr(viewmats), ptr(coeffs), int(shared),
+               ptr(radii), ptr(colors), N.stream(means.device))
+        ctx.save_for_backward(means, campos, coeffs, radii, viewmats)
         ctx.degree = degree
         return colors
 
     @staticmethod
     def backward(ctx, v_colors):
-        means, campos, coeffs, radii = ctx.saved_tensors
+        means, campos, coeffs, radii, viewmats = ctx.saved_tensors
         C, Ng = radii.shape
         v_coeffs = torch.empty_like(coeffs)
         v_means = torch.empty_like(means) if ctx.needs_input_grad[1] else None
         vc = _f32(v_colors)
-        N.call("hgsr_sh_rgb_bwd", ctx.degree, C, Ng, coeffs.shape[-2], ptr(means), ptr(campos), ptr(coeffs),
-               int(coeffs.dim() == 3), ptr(radii), ptr(vc), ptr(v_coeffs), ptr(v_means), N.stream(means.device))
-        return None, v_means, None, v_coeffs, None
+        N.call("hgsr_sh_rgb_bwd", ctx.degree, C, Ng, coeffs.shape[-2], ptr(means), ptr(campos), ptr(viewmats),
+               ptr(coeffs), int(coeffs.dim() == 3), ptr(radii), ptr(vc), ptr(v_coeffs), ptr(v_means),
+               N.stream(means.device))
+        return None, v_means, None, v_coeffs, None, None
 
 
 def spherical_harmonics(degrees_to_use: int, dirs: torch.Tensor, coeffs: torch.Tensor,
@@ -924,13 +926,6 @@ def rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals
 # =========================================================================
 # high-level entry points
 # =========================================================================
-def _camera_centers(viewmats):
-    # c2w translation of a rigid world->camera transform: -R^T t
-    R = viewmats[:, :3, :3]
-    t = viewmats[:, :3, 3]
-    return -(R.transpose(1, 2) @ t[..., None])[..., 0]
-
-
 def _colors_for_raster(means, colors, viewmats, radii, sh_degree, C):
     """Colours per raster call: [N,D] (shared over cameras) or [C,N,D]."""
     if sh_degree is None:
@@ -940,8 +935,9 @@ def _colors_for_raster(means, colors, viewmats, radii, sh_degree, C):
     _check_cuda(means, colors, viewmats)
     K = colors.shape[-2]
     assert colors.shape[-1] == 3 and colors.dim() in (3, 4) and (sh_degree + 1) ** 2 <= K, "bad SH coefficients"
-    campos = _f32(_camera_centers(viewmats.detach()))
-    return _SHColors.apply(int(sh_degree), _f32(means), campos, _f32(colors), radii.contiguous())
+    # the camera centres -R^T t are computed in the SH kernels from the view matrices
+    return _SHColors.apply(int(sh_degree), _f32(means), None, _f32(colors), radii.contiguous(),
+                           _f32(viewmats.detach().reshape(-1, 4, 4)))
 
 
 def _with_depth(colors, backgrounds, depths, render_mode, C):

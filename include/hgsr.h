@@ -104,13 +104,15 @@ int hgsr_sh_bwd(int degree, int K, int64_t n, const float* dirs, const float* co
  * coeffs [N,K,3] (shared = 1) or [C,N,K,3], radii [C,N] -> colors [C,N,3] (written).
  * The backward writes v_coeffs (summed over cameras when shared) and v_means [N,3]
  * (nullable; overwritten, = the gradient through dirs).  The backward takes K <= 16
- * (degree <= 3 coefficient rows, staged through LDS); HGSR_EINVAL otherwise. */
+ * (degree <= 3 coefficient rows, staged through LDS); HGSR_EINVAL otherwise.  viewmats
+ * (nullable, [C,4,4] world-to-camera, row-major): the camera centres -R^T t are computed in
+ * the kernels from them instead of read from campos (which may then be NULL). */
 int hgsr_sh_rgb_fwd(int degree, int C, int N, int K, const float* means, const float* campos,
-                    const float* coeffs, int shared, const int32_t* radii, float* colors,
-                    hgsr_stream_t stream);
+                    const float* viewmats, const float* coeffs, int shared, const int32_t* radii,
+                    float* colors, hgsr_stream_t stream);
 int hgsr_sh_rgb_bwd(int degree, int C, int N, int K, const float* means, const float* campos,
-                    const float* coeffs, int shared, const int32_t* radii, const float* v_colors,
-                    float* v_coeffs, float* v_means, hgsr_stream_t stream);
+                    const float* viewmats, const float* coeffs, int shared, const int32_t* radii,
+                    const float* v_colors, float* v_coeffs, float* v_means, hgsr_stream_t stream);
 
 /* ---- K5/K6/K7: tile intersection, sort, tile offsets ---------------------
  * Replaces gsplat isect_tiles(sort=True) + cub DeviceRadixSort + isect_offset_encode

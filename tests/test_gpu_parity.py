@@ -138,13 +138,27 @@ def test_sh_fwd_bwd(deg):
     grad_close(d.grad.cpu().numpy(), vd_ref, "v_dirs")
 
 
+def _viewmats_for(campos, g):
+    """World-to-camera rigid transforms whose centres -R^T t are `campos` (random rotations)."""
+    vms = []
+    for c in range(campos.shape[0]):
+        q, _ = torch.linalg.qr(torch.randn(3, 3, generator=g, dtype=torch.float64))
+        vm = torch.eye(4, dtype=torch.float64)
+        vm[:3, :3] = q
+        vm[:3, 3] = -(q @ campos[c].double())
+        vms.append(vm)
+    return torch.stack(vms).float()
+
+
 @pytest.mark.parametrize("deg", [0, 1, 2, 3])
 @pytest.mark.parametrize("C,shared", [(1, True), (2, True), (2, False)])
-def test_sh_rgb_fused(deg, C, shared):
+@pytest.mark.parametrize("from_viewmats", [False, True])
+def test_sh_rgb_fused(deg, C, shared, from_viewmats):
     """rasterization()'s fused SH colour step (hgsr_sh_rgb_fwd/bwd) against the C oracle's SH
     on dirs = means - campos per camera, masks = radii > 0, then clamp_min(+0.5, 0) and its
     gradient mask (gsplat rendering as render.py calls it); shared coefficients sum their
-    gradient over the cameras, v_means sums v_dirs over the cameras."""
+    gradient over the cameras, v_means sums v_dirs over the cameras.  from_viewmats: the kernels
+    compute the camera centres from world-to-camera matrices (rasterization()'s path)."""
     g = torch.Generator().manual_seed(10 * deg + C + int(shared))
     n, K = 4000, 16
     means = torch.randn(n, 3, generator=g) * 2.0
@@ -155,7 +169,10 @@ def test_sh_rgb_fused(deg, C, shared):
     m, cf = to_dev(means, coeffs)
     m.requires_grad_(True)
     cf.requires_grad_(True)
-    cols = G._SHColors.apply(deg, m, campos.to(DEV), cf, radii.to(DEV))
+    if from_viewmats:
+        cols = G._SHColors.apply(deg, m, None, cf, radii.to(DEV), _viewmats_for(campos, g).to(DEV))
+    else:
+        cols = G._SHColors.apply(deg, m, campos.to(DEV), cf, radii.to(DEV))
     (cols * vo.to(DEV)).sum().backward()
     ref, vc_ref, vm_ref = [], [], np.zeros((n, 3), np.float32)
     for c in range(C):
