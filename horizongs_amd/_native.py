@@ -30,7 +30,7 @@ _SIGS = {
     "hgsr_version": (I, []),
     "hgsr_last_error": (ct.c_char_p, []),
     "hgsr_project3d_fwd": (I, [I, I, P, P, P, P, P, I, I, F, F, F, F, P, P, P, P, P]),
-    "hgsr_project3d_bwd": (I, [I, I, P, P, P, P, P, I, I, F, P, P, P, P, P, P, P, P, P, P]),
+    "hgsr_project3d_bwd": (I, [I, I, P, P, P, P, P, I, I, F, P, P, P, P, P, P, P, P, P, P, P]),
     "hgsr_project2d_fwd": (I, [I, I, P, P, P, P, P, I, I, F, F, F, P, P, P, P, P, P]),
     "hgsr_project2d_bwd": (I, [I, I, P, P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P]),
     "hgsr_sh_fwd": (I, [I, I, I64, P, P, P, P, P]),

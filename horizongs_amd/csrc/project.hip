@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
     const float* __restrict__ conics, const float2* __restrict__ v_means2d,
     const float* __restrict__ v_depths, const float* __restrict__ v_conics,
     float* __restrict__ v_means, float4* __restrict__ v_quats, float* __restrict__ v_scales,
-    const float* __restrict__ v_scales_in) {
+    const float* __restrict__ v_scales_in, const float* __restrict__ v_means_in) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= N) return;
     const float m[3] = {means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2]};
@@ -292,9 +292,10 @@ __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
     // the other consumer's scale gradient travels with the first round trip (loaded after the
     // camera loop it costs one more exposed memory latency per lane at 3 waves / SIMD)
     const float3 vsi = v_scales_in ? ld3(v_scales_in + (int64_t)g * 3) : make_float3(0.f, 0.f, 0.f);
+    const float3 vmi = v_means_in ? ld3(v_means_in + (int64_t)g * 3) : make_float3(0.f, 0.f, 0.f);
     HGSR_CAM_READY;
     asm volatile("" ::"v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w), "v"(s3.x),
-                 "v"(s3.y), "v"(s3.z), "v"(vsi.x), "v"(vsi.y), "v"(vsi.z));
+                 "v"(s3.y), "v"(s3.z), "v"(vsi.x), "v"(vsi.y), "v"(vsi.z), "v"(vmi.x), "v"(vmi.y), "v"(vmi.z));
     Mat3 Rq;
     const Mat3 cov = covar_from_qs(q, s3, Rq);
     for (int c = 0; c < C; ++c) {
@@ -399,11 +400,12 @@ __global__ __launch_bounds__(256, 3) void project3d_bwd_kernel(
         vq_acc.z += live ? vq.z : 0.f;
         vq_acc.w += live ? vq.w : 0.f;
     }
-    // overwrite semantics: a Gaussian culled in every camera gets zeros; v_scales_in (another
-    // consumer's gradient of the scales) is added here instead of by a separate sum
+    // overwrite semantics: a Gaussian culled in every camera gets zeros; v_scales_in / v_means_in
+    // (another consumer's gradient of the scales / means) are added here instead of by a
+    // separate sum -- one fp32 add of two terms, the same value autograd's sum gives
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        v_means[(int64_t)g * 3 + j] = vm_acc[j];
+        v_means[(int64_t)g * 3 + j] = v_means_in ? vm_acc[j] + (j == 0 ? vmi.x : (j == 1 ? vmi.y : vmi.z)) : vm_acc[j];
         v_scales[(int64_t)g * 3 + j] = v_scales_in ? vs_acc[j] + (j == 0 ? vsi.x : (j == 1 ? vsi.y : vsi.z)) : vs_acc[j];
     }
     v_quats[g] = vq_acc;
@@ -635,7 +637,7 @@ extern "C" int hgsr_project3d_bwd(int C, int N, const float* means, const float*
                                   const float* conics, const float* v_means2d,
                                   const float* v_depths, const float* v_conics, float* v_means,
                                   float* v_quats, float* v_scales, const float* v_scales_in,
-                                  hgsr_stream_t stream) {
+                                  const float* v_means_in, hgsr_stream_t stream) {
     (void)eps2d;
     int st = check_common(C, N, means, quats, scales, viewmats, Ks, width, height);
     if (st) return st;
@@ -646,7 +648,7 @@ extern "C" int hgsr_project3d_bwd(int C, int N, const float* means, const float*
     hipLaunchKernelGGL(project3d_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, as_stream(stream), C, N,
                        means, reinterpret_cast<const float4*>(quats), scales, viewmats, Ks, width,
                        height, radii, conics, reinterpret_cast<const float2*>(v_means2d), v_depths,
-                       v_conics, v_means, reinterpret_cast<float4*>(v_quats), v_scales, v_scales_in);
+                       v_conics, v_means, reinterpret_cast<float4*>(v_quats), v_scales, v_scales_in, v_means_in);
     return check_launch("project3d_bwd");
 }
 

@@ -128,7 +128,7 @@ def _sink_grad(ctx, like):
 class _Project3D(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means, quats, scales, viewmats, Ks, width, height, eps2d, near_plane, far_plane,
-                radius_clip, grad_mode=False):
+                radius_clip, grad_mode=False, means_sink=None):
         C, Ng = viewmats.shape[0], means.shape[0]
         dev = means.device
         radii = torch.empty((C, Ng), dtype=torch.int32, device=dev)
@@ -141,6 +141,9 @@ class _Project3D(torch.autograd.Function):
         ctx.save_for_backward(means, quats, scales, viewmats, Ks, radii, conics)
         ctx.cfg = (width, height, eps2d)
         _attach_sink(ctx, scales, grad_mode, 2)
+        # the SH colour step's means gradient, handed over by _SHColors' backward (which runs
+        # first: it is later in the graph) and added in this backward's kernel (v_means_in)
+        ctx.msink = means_sink if ctx.needs_input_grad[0] else None
         ctx.mark_non_differentiable(radii)
         ctx.set_materialize_grads(False)  # no zero-filled int grad for radii per step
         return radii, means2d, depths, conics
@@ -156,18 +159,26 @@ class _Project3D(torch.autograd.Function):
         v_means2d, v_depths, v_conics = (_f32(g) for g in _grads_or_zeros((v_means2d, v_depths, v_conics), (C, Ng),
                                                                            (2, None, 3), means))
         v_in = _sink_grad(ctx, scales)
+        vm_in = None if ctx.msink is None else ctx.msink.take()
+        vm_in = None if vm_in is None else _f32(vm_in.reshape(means.shape))
         N.call("hgsr_project3d_bwd", C, Ng, ptr(means), ptr(quats), ptr(scales), ptr(viewmats), ptr(Ks), width,
                height, eps2d, ptr(radii), ptr(conics), ptr(v_means2d), ptr(v_depths), ptr(v_conics), ptr(v_means),
-               ptr(v_quats), ptr(v_scales), ptr(v_in), N.stream(means.device))
+               ptr(v_quats), ptr(v_scales), ptr(v_in), ptr(vm_in), N.stream(means.device))
         if ctx.needs_input_grad[3]:
             raise NotImplementedError("hgsr: gradients w.r.t. viewmats are not supported")
-        return v_means, v_quats, v_scales, None, None, None, None, None, None, None, None, None
+        return v_means, v_quats, v_scales, None, None, None, None, None, None, None, None, None, None
 
 
 def fully_fused_projection(means, covars, quats, scales, viewmats, Ks, width, height, eps2d=0.3,
                            packed=False, near_plane=0.01, far_plane=1e10, radius_clip=0.0,
                            sparse_grad=False, calc_compensations=False, camera_model="pinhole"):
     """gsplat.cuda._wrapper.fully_fused_projection -> (radii, means2d, depths, conics, compensations)."""
+    return _projection(means, covars, quats, scales, viewmats, Ks, width, height, eps2d, packed, near_plane,
+                       far_plane, radius_clip, sparse_grad, calc_compensations, camera_model)
+
+
+def _projection(means, covars, quats, scales, viewmats, Ks, width, height, eps2d, packed, near_plane, far_plane,
+                radius_clip, sparse_grad, calc_compensations, camera_model, means_sink=None):
     _unsupported(covars is not None, "covars input")
     _unsupported(packed, "packed=True")
     _unsupported(sparse_grad, "sparse_grad")
@@ -179,7 +190,7 @@ def fully_fused_projection(means, covars, quats, scales, viewmats, Ks, width, he
     assert viewmats.dim() == 3 and viewmats.shape[1:] == (4, 4) and Ks.shape == (viewmats.shape[0], 3, 3)
     radii, means2d, depths, conics = _Project3D.apply(
         _f32(means), _f32(quats), _f32(scales), _f32(viewmats), _f32(Ks), int(width), int(height),
-        float(eps2d), float(near_plane), float(far_plane), float(radius_clip), torch.is_grad_enabled())
+        float(eps2d), float(near_plane), float(far_plane), float(radius_clip), torch.is_grad_enabled(), means_sink)
     return radii, means2d, depths, conics, None
 
 
@@ -271,7 +282,7 @@ class _SHColors(torch.autograd.Function):
     of campos): the kernels compute the camera centres -R^T t themselves."""
 
     @staticmethod
-    def forward(ctx, degree, means, campos, coeffs, radii, viewmats=None):
+    def forward(ctx, degree, means, campos, coeffs, radii, viewmats=None, means_sink=None):
         C, Ng = radii.shape
         K = coeffs.shape[-2]
         shared = coeffs.dim() == 3
@@ -280,6 +291,7 @@ class _SHColors(torch.autograd.Function):
                ptr(radii), ptr(colors), N.stream(means.device))
         ctx.save_for_backward(means, campos, coeffs, radii, viewmats)
         ctx.degree = degree
+        ctx.msink = means_sink
         return colors
 
     @staticmethod
@@ -292,7 +304,9 @@ class _SHColors(torch.autograd.Function):
         N.call("hgsr_sh_rgb_bwd", ctx.degree, C, Ng, coeffs.shape[-2], ptr(means), ptr(campos), ptr(viewmats),
                ptr(coeffs), int(coeffs.dim() == 3), ptr(radii), ptr(vc), ptr(v_coeffs), ptr(v_means),
                N.stream(means.device))
-        return None, v_means, None, v_coeffs, None, None
+        if v_means is not None and ctx.msink is not None and ctx.msink.put(v_means):
+            v_means = None  # added by the projection backward (refused once it has run: autograd sums)
+        return None, v_means, None, v_coeffs, None, None, None
 
 
 def spherical_harmonics(degrees_to_use: int, dirs: torch.Tensor, coeffs: torch.Tensor,
@@ -926,7 +940,7 @@ def rasterize_to_pixels_2dgs(means2d, ray_transforms, colors, opacities, normals
 # =========================================================================
 # high-level entry points
 # =========================================================================
-def _colors_for_raster(means, colors, viewmats, radii, sh_degree, C):
+def _colors_for_raster(means, colors, viewmats, radii, sh_degree, C, means_sink=None):
     """Colours per raster call: [N,D] (shared over cameras) or [C,N,D]."""
     if sh_degree is None:
         return colors
@@ -937,7 +951,7 @@ def _colors_for_raster(means, colors, viewmats, radii, sh_degree, C):
     assert colors.shape[-1] == 3 and colors.dim() in (3, 4) and (sh_degree + 1) ** 2 <= K, "bad SH coefficients"
     # the camera centres -R^T t are computed in the SH kernels from the view matrices
     return _SHColors.apply(int(sh_degree), _f32(means), None, _f32(colors), radii.contiguous(),
-                           _f32(viewmats.detach().reshape(-1, 4, 4)))
+                           _f32(viewmats.detach().reshape(-1, 4, 4)), means_sink)
 
 
 def _with_depth(colors, backgrounds, depths, render_mode, C):
@@ -981,14 +995,16 @@ def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, 
     _unsupported(rasterize_mode != "classic", f"rasterize_mode={rasterize_mode}")
     _unsupported(distributed, "distributed=True")
     C = viewmats.shape[0]
-    radii, means2d, depths, conics, _ = fully_fused_projection(
-        means, covars, quats, scales, viewmats, Ks, width, height, eps2d=eps2d, packed=False,
-        near_plane=near_plane, far_plane=far_plane, radius_clip=radius_clip, sparse_grad=sparse_grad,
-        calc_compensations=False, camera_model=camera_model)
+    # SH colours: their means gradient goes to the projection backward's kernel (GradSink)
+    msink = (GradSink() if _GRAD_SINK and sh_degree is not None and torch.is_grad_enabled() and means.requires_grad
+             else None)
+    radii, means2d, depths, conics, _ = _projection(
+        means, covars, quats, scales, viewmats, Ks, width, height, eps2d, False, near_plane, far_plane, radius_clip,
+        sparse_grad, False, camera_model, msink)
     tw, th = _tile_grid(width, height, tile_size)
     isect_state = _isect_count(means2d, radii, int(tile_size), tw, th, depths)
     _params_ready(colors)
-    cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C)
+    cols = _colors_for_raster(means, colors, viewmats, radii, sh_degree, C, msink)
     with_depth = render_mode in ("RGB+D", "RGB+ED", "D", "ED")
     rgb = render_mode in ("RGB", "RGB+D", "RGB+ED")
     Dc = cols.shape[-1] if rgb else 0

@@ -57,13 +57,14 @@ int hgsr_project3d_fwd(int C, int N, const float* means, const float* quats,
 
 /* vjp of the above: writes (overwrites) v_means [N,3], v_quats [N,4], v_scales [N,3];
  * v_scales_in (nullable [N,3]): another consumer's gradient of the same scales (the loss
- * head's scale regulariser), added into v_scales in the same pass. */
+ * head's scale regulariser), added into v_scales in the same pass; v_means_in (nullable
+ * [N,3]): likewise for the means (the SH colour step's view directions, hgsr_sh_rgb_bwd). */
 int hgsr_project3d_bwd(int C, int N, const float* means, const float* quats,
                        const float* scales, const float* viewmats, const float* Ks,
                        int width, int height, float eps2d, const int32_t* radii,
                        const float* conics, const float* v_means2d, const float* v_depths,
                        const float* v_conics, float* v_means, float* v_quats, float* v_scales,
-                       const float* v_scales_in, hgsr_stream_t stream);
+                       const float* v_scales_in, const float* v_means_in, hgsr_stream_t stream);
 
 /* ---- K1'/K10: 2DGS surfel projection -------------------------------------
  * replaces fully_fused_projection_2dgs (render.py:171-186 and inside

@@ -8,7 +8,9 @@ composition it replaces:
 * rasterization_2dgs' world-frame normals and K13 (render_normals_from_depth) inside the fused
   raster Function, their gradients entering its backward kernel, instead of separate rotate /
   depth_to_normal launches and the slice-backward fill + copy + sum of the depth channel
-  (reference gaussian_renderer/render.py:62-76, train.py:180-188)."""
+  (reference gaussian_renderer/render.py:62-76, train.py:180-188);
+* rasterization()'s SH colour step: its means gradient (dirs = means - campos) handed to the
+  projection backward's kernel in the same way (v_means_in)."""
 import numpy as np
 import pytest
 import torch
@@ -72,6 +74,41 @@ def test_scale_reg_grad_sink_matches_autograd_sum(gs, monkeypatch):
     for i in (0, 1, 3, 4):
         assert np.array_equal(got[i], got[5 + i]), f"grad {i}: the second backward differs"
     assert np.abs(got[2]).max() > 0
+
+
+def _sh_step(sc, twice=False):
+    means, quats, scales, opac, coeffs = (t.to(DEV).clone().requires_grad_(True) for t in (
+        sc.means, sc.quats, sc.scales, sc.opacities, sc.colors))
+    out, alpha, _ = G.rasterization(means, quats, scales, opac, coeffs, sc.viewmats.to(DEV), sc.Ks.to(DEV),
+                                    sc.width, sc.height, packed=False, sh_degree=2, render_mode="RGB+ED")
+    g = torch.Generator().manual_seed(9)
+    ups = [torch.randn(t.shape, generator=g).to(DEV) for t in (out, alpha)]
+    loss = (out * ups[0]).sum() + (alpha * ups[1]).sum()
+    loss.backward(retain_graph=twice)
+    ts = (means, quats, scales, opac, coeffs)
+    grads = [t.grad.clone() for t in ts]
+    if twice:  # the sink is closed: the SH means gradient returns through autograd's sum
+        for t in ts:
+            t.grad = None
+        loss.backward()
+        grads += [t.grad.clone() for t in ts]
+    torch.cuda.synchronize()
+    return [x.cpu().numpy() for x in grads]
+
+
+def test_sh_means_grad_sink_matches_autograd_sum(monkeypatch):
+    """The SH colour step's means gradient (view directions) handed to the projection backward
+    (v_means_in) instead of autograd's add: the same single f32 addition of the same two terms,
+    so every gradient -- the means' included -- is bit-identical, in both backwards."""
+    sc = make_scene(6000, 160, 120, seed=31, scale_range=(0.01, 0.05), depth_range=(2.0, 6.0), sh_degree=2)
+    monkeypatch.setattr(G, "_GRAD_SINK", False)
+    ref = _sh_step(sc)
+    monkeypatch.setattr(G, "_GRAD_SINK", True)
+    got = _sh_step(sc, twice=True)
+    for i in range(5):
+        assert np.array_equal(got[i], ref[i]), f"grad {i}"
+        assert np.array_equal(got[5 + i], ref[i]), f"2nd grad {i}"
+    assert np.abs(got[0]).max() > 0
 
 
 def _render_2dgs(sc, seed):
