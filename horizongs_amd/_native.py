@@ -53,12 +53,12 @@ _SIGS = {
     "hgsr_raster3d_bwd_fused": (I, [I, I, I, P, P, P, I, P, I, P, I, P, I, I, I, I, I, P, I64, P, P, P, P, P, P,
                                     P, P, P, P, P, P, P, P, SZ, P, SZ, I, P, I, P]),
     "hgsr_raster3d_qmask_bytes": (SZ, [I, I, I, I64]),
-    "hgsr_raster3d_pack_fused": (I, [I, I, I, P, P, P, I, P, P, I, P, I, I, I, P, SZ, P]),
+    "hgsr_raster3d_pack_fused": (I, [I, I, I, P, P, P, I, P, P, I, P, P, I, I, I, P, SZ, P]),
     "hgsr_raster3d_fwd_packed": (I, [I, I, I, I, I, P, I, I, I, I, I, P, I64, P, P, P, P, P, SZ, P, SZ, P, SZ,
                                      P, P]),
     "hgsr_raster2d_fwd_ws_bytes": (SZ, [I, I, I]),
     "hgsr_raster2d_fwd": (I, [I, I, I, P, P, P, P, P, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, SZ, P]),
-    "hgsr_raster2d_pack_fused": (I, [I, I, I, P, P, P, I, P, P, I, P, P, I, I, I, P, SZ, P]),
+    "hgsr_raster2d_pack_fused": (I, [I, I, I, P, P, P, I, P, P, I, P, P, P, I, I, I, P, SZ, P]),
     "hgsr_raster2d_fwd_packed": (I, [I, I, I, I, I, P, I, I, I, I, I, P, I64, P, P, P, P, P, P, P, P, P, SZ, P, SZ,
                                      P, SZ, P, P, P]),
     "hgsr_raster2d_bwd_ws_bytes": (SZ, [I, I, I, I64, I]),

@@ -234,13 +234,24 @@ struct RectFromRadii {
     }
 };
 
+// the same areas, already counted by hgsr_isect_count (its tiles_per_gauss): 4 B an entry read
+// instead of 12 B and a rectangle (the slot prefix's row sums; the corner is not needed there)
+struct AreaFromCounts {
+    const int32_t* a;
+    __device__ __forceinline__ int operator()(int64_t o, int& x0, int& y0, int& w) const {
+        x0 = y0 = w = 0;
+        return a[o];
+    }
+};
+
 constexpr int kSlotRow = 256;  // entries per element of the slot-area prefix (one workgroup row)
 // the forward's slot prefix (hgsr_raster3d_pack_fused with radii): seg [CN + 1], the row prefix
 // [CN / kSlotRow + 1], then the backward's piece count (cleared by the forward's scan)
 size_t slot_prefix_bytes(int64_t CN);
 int32_t* slot_prefix_npieces(void* buf, int64_t CN);
-// row area sums + their exclusive scan into buf (seg[CN] = the total); pack3 finishes seg
-int launch_slot_prefix(int64_t CN, const RectFromRadii& r, void* buf, hipStream_t s);
+// row area sums + their exclusive scan into buf (seg[CN] = the total); pack3 finishes seg.
+// areas (nullable): the entries' areas as hgsr_isect_count counted them (else from r)
+int launch_slot_prefix(int64_t CN, const RectFromRadii& r, void* buf, hipStream_t s, const int32_t* areas = nullptr);
 // the big entries' piece list from a finished seg (launch_grad_slots' buffer layout in buf)
 // npieces (nullable): the piece count's location, already zero when npieces_zeroed (else cleared here)
 int launch_grad_pieces(int64_t CN, const int32_t* seg, int64_t n_isects, void* buf, hipStream_t s, GradSlots& out,

@@ -1240,13 +1240,17 @@ int32_t* hgsr::slot_prefix_npieces(void* buf, int64_t CN) {
                       align256_((size_t)((CN + kSlotRow - 1) / kSlotRow + 1) * 4));
 }
 
-int hgsr::launch_slot_prefix(int64_t CN, const RectFromRadii& r, void* buf, hipStream_t s) {
+int hgsr::launch_slot_prefix(int64_t CN, const RectFromRadii& r, void* buf, hipStream_t s, const int32_t* areas) {
     int32_t* const seg = (int32_t*)buf;
     int32_t* const bpre = (int32_t*)((char*)buf + align256_((size_t)(CN + 1) * 4));
     const int64_t nb = (CN + kSlotRow - 1) / kSlotRow;
     HGSR_REQUIRE(nb < (1ll << 31), "too many Gaussians for the gradient slots");
     if (CN == 0) return memset_async(seg, 4, s, "slot_prefix");
-    hipLaunchKernelGGL(slot_sum_kernel<RectFromRadii>, dim3((unsigned)nb), dim3(256), 0, s, CN, r, bpre);
+    if (areas)
+        hipLaunchKernelGGL(slot_sum_kernel<AreaFromCounts>, dim3((unsigned)nb), dim3(256), 0, s, CN,
+                           AreaFromCounts{areas}, bpre);
+    else
+        hipLaunchKernelGGL(slot_sum_kernel<RectFromRadii>, dim3((unsigned)nb), dim3(256), 0, s, CN, r, bpre);
     // (the scan also clears the backward's piece count, kept here with the prefix)
     hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(1024), 0, s, (int)nb, bpre, seg + CN,
                        slot_prefix_npieces(buf, CN));

@@ -1008,8 +1008,8 @@ extern "C" int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2
 extern "C" int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                                         const float* colors, int colors_shared, const float* depths,
                                         const float* opacities, int opacities_shared, const float* normals,
-                                        const int32_t* radii, int tile_size, int tile_w, int tile_h, void* ws,
-                                        size_t ws_bytes, hgsr_stream_t stream) {
+                                        const int32_t* radii, const int32_t* tiles_per_gauss, int tile_size,
+                                        int tile_w, int tile_h, void* ws, size_t ws_bytes, hgsr_stream_t stream) {
     HGSR_REQUIRE(C >= 1 && N >= 0, "bad dims");
     HGSR_REQUIRE(Dc >= 0 && Dc <= 4 && (Dc > 0 || depths), "fused raster: 0..4 colour channels (got %d)", Dc);
     const int D = Dc + (depths ? 1 : 0);
@@ -1025,7 +1025,7 @@ extern "C" int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means
     HGSR_REQUIRE(tile_size > 0 && tile_w > 0 && tile_h > 0, "bad tile grid");
     const RectFromRadii rr{reinterpret_cast<const float2*>(means2d), radii, tile_size, tile_w, tile_h};
     void* const slots = (char*)ws + rec2_bytes(C, N);
-    if (int st = launch_slot_prefix((int64_t)C * N, rr, slots, s)) return st;
+    if (int st = launch_slot_prefix((int64_t)C * N, rr, slots, s, tiles_per_gauss)) return st;
     return pack2(C, N, D, means2d, ray_transforms, cs, normals, (Rec2*)ws, s, &rr, slots);
 }
 

@@ -598,11 +598,12 @@ class _Raster3DFused(torch.autograd.Function):
     kernels instead of torch cat / repeat / divide (gsplat rendering.py does those in torch)."""
 
     @staticmethod
-    def pack(means2d, conics, colors, depths, opacities, radii=None, tiles=(0, 0, 0)):
+    def pack(means2d, conics, colors, depths, opacities, radii=None, tiles=(0, 0, 0), areas=None):
         """Raster records for forward(records=...): launched before the intersection
         count is read back, so the packing overlaps the host sync.  radii (when a backward will
         follow; tiles = (tile_size, tile_width, tile_height)): the records also carry their
-        gradient slots -- pass the same radii to forward()."""
+        gradient slots -- pass the same radii to forward().  areas (optional): tiles_per_gauss of
+        the intersection count of these radii, read by the slot prefix's row sums."""
         C, Ng = means2d.shape[:2]
         Dc = 0 if colors is None else colors.shape[-1]
         D = Dc + (0 if depths is None else 1)
@@ -610,7 +611,7 @@ class _Raster3DFused(torch.autograd.Function):
         ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=means2d.device)
         N.call("hgsr_raster3d_pack_fused", C, Ng, Dc, ptr(means2d), ptr(conics), ptr(colors),
                int(colors is not None and colors.dim() == 2), ptr(depths), ptr(opacities), int(opacities.dim() == 1),
-               ptr(radii), *tiles, ptr(ws), ws_b, N.stream(means2d.device))
+               ptr(radii), ptr(areas), *tiles, ptr(ws), ws_b, N.stream(means2d.device))
         return ws
 
     @staticmethod
@@ -789,7 +790,7 @@ class _Raster2DFused(torch.autograd.Function):
     native call each way (hgsr_raster2d_{fwd,bwd}_fused); see _Raster3DFused."""
 
     @staticmethod
-    def pack(means2d, rt, colors, depths, opacities, normals, radii=None, tiles=(0, 0, 0)):
+    def pack(means2d, rt, colors, depths, opacities, normals, radii=None, tiles=(0, 0, 0), areas=None):
         """Surfel records for forward(records=...), packed while the host reads the count; with
         radii (a backward will follow) they carry their gradient slots (_Raster3DFused.pack)."""
         C, Ng = means2d.shape[:2]
@@ -799,7 +800,7 @@ class _Raster2DFused(torch.autograd.Function):
         ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=means2d.device)
         N.call("hgsr_raster2d_pack_fused", C, Ng, Dc, ptr(means2d), ptr(rt), ptr(colors),
                int(colors is not None and colors.dim() == 2), ptr(depths), ptr(opacities), int(opacities.dim() == 1),
-               ptr(normals), ptr(radii), *tiles, ptr(ws), ws_b, N.stream(means2d.device))
+               ptr(normals), ptr(radii), ptr(areas), *tiles, ptr(ws), ws_b, N.stream(means2d.device))
         return ws
 
     @staticmethod
@@ -1018,7 +1019,7 @@ def rasterization(means, quats, scales, opacities, colors, viewmats, Ks, width, 
         # the Function, whose backward then finds them there)
         slot_radii = radii.contiguous() if grad_mode and any(t is not None and t.requires_grad for t in r_in) else None
         records = _Raster3DFused.pack(*(t.detach() if t is not None else None for t in r_in), radii=slot_radii,
-                                      tiles=(int(tile_size), tw, th))
+                                      tiles=(int(tile_size), tw, th), areas=isect_state[3])
         bgs = None if (backgrounds is None or not rgb) else _f32(backgrounds)
         args = (bgs, int(width), int(height), int(tile_size))
         tpg, isect_offsets = isect_state[3], isect_state[4]
@@ -1162,7 +1163,7 @@ def rasterization_2dgs(means, quats, scales, opacities, colors, viewmats, Ks, wi
         slot_radii = radii.contiguous() if grad_mode and (densifications.requires_grad or any(
             t is not None and t.requires_grad for t in r_in)) else None
         records = _Raster2DFused.pack(*(t.detach() if t is not None else None for t in r_in), radii=slot_radii,
-                                      tiles=(int(tile_size), tw, th))
+                                      tiles=(int(tile_size), tw, th), areas=isect_state[3])
         bgs = None if (backgrounds is None or not rgb) else _f32(backgrounds)
         opac = opacities.expand(C, -1)
         args = (densifications, bgs, int(width), int(height), int(tile_size))

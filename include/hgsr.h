@@ -230,12 +230,14 @@ int hgsr_raster3d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
 size_t hgsr_raster3d_qmask_bytes(int C, int tile_w, int tile_h, int64_t n_isects);
 /* radii (nullable, [C,N] int32, with the tile grid): a backward will follow; the records then
  * carry each (camera, Gaussian)'s gradient-slot base (its isect_tiles rectangle in the grid) and
- * ws the slots' prefix, which hgsr_raster3d_bwd_fused given fwd_slots = 1 uses as they are. */
+ * ws the slots' prefix, which hgsr_raster3d_bwd_fused given fwd_slots = 1 uses as they are.
+ * tiles_per_gauss (nullable, [C,N] int32): the same rectangles' areas as hgsr_isect_count wrote
+ * them for these radii -- the prefix's row sums read them instead of re-deriving the areas. */
 int hgsr_raster3d_pack_fused(int C, int N, int Dc, const float* means2d, const float* conics,
                              const float* colors, int colors_shared, const float* depths,
                              const float* opacities, int opacities_shared, const int32_t* radii,
-                             int tile_size, int tile_w, int tile_h, void* ws, size_t ws_bytes,
-                             hgsr_stream_t stream);
+                             const int32_t* tiles_per_gauss, int tile_size, int tile_w, int tile_h,
+                             void* ws, size_t ws_bytes, hgsr_stream_t stream);
 int hgsr_raster3d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_depth,
                              const float* backgrounds, int width, int height, int tile_size,
                              int tile_w, int tile_h, const int32_t* isect_offsets, int64_t n_isects,
@@ -322,13 +324,13 @@ int hgsr_raster2d_fwd_fused(int C, int N, int Dc, const float* means2d, const fl
  * takes world-frame v_render_normals.  v_depth_extra (nullable, [C,H,W]): a second gradient
  * of the depth channel (K13's, the normals from the rendered depth), added per pixel by the
  * backward kernel instead of by a separate sum. */
-/* radii (nullable, with the tile grid): the records carry their gradient slots, as
- * hgsr_raster3d_pack_fused's (hgsr_raster2d_bwd_fused then gets fwd_slots = 1). */
+/* radii (nullable, with the tile grid) and tiles_per_gauss (nullable): the records carry their
+ * gradient slots, as hgsr_raster3d_pack_fused's (hgsr_raster2d_bwd_fused then gets fwd_slots = 1). */
 int hgsr_raster2d_pack_fused(int C, int N, int Dc, const float* means2d, const float* ray_transforms,
                              const float* colors, int colors_shared, const float* depths,
                              const float* opacities, int opacities_shared, const float* normals,
-                             const int32_t* radii, int tile_size, int tile_w, int tile_h, void* ws,
-                             size_t ws_bytes, hgsr_stream_t stream);
+                             const int32_t* radii, const int32_t* tiles_per_gauss, int tile_size, int tile_w,
+                             int tile_h, void* ws, size_t ws_bytes, hgsr_stream_t stream);
 int hgsr_raster2d_fwd_packed(int C, int N, int Dc, int with_depth, int expected_depth,
                              const float* backgrounds, int width, int height, int tile_size, int tile_w,
                              int tile_h, const int32_t* isect_offsets, int64_t n_isects,
